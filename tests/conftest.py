@@ -1,0 +1,84 @@
+"""Shared fixtures.  `-m "not gpu"` runs here (no GPU); `-m gpu` runs on an MI355X box."""
+from __future__ import annotations
+
+import gzip
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+TESTS = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(TESTS)
+PKG = os.path.join(REPO, "shredword-trainer_amd")
+GOLDEN = os.path.join(TESTS, "golden")
+ORACLE = os.path.join(REPO, "oracle")
+for p in (TESTS, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import corpora  # noqa: E402
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI library)")
+    config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+def golden_cases():
+    return sorted(d for d in os.listdir(GOLDEN) if os.path.isfile(os.path.join(GOLDEN, d, "case.json")))
+
+
+def load_case(name):
+    d = os.path.join(GOLDEN, name)
+    with open(os.path.join(d, "case.json")) as f:
+        case = json.load(f)
+    with open(os.path.join(d, "model.bin"), "rb") as f:
+        case["model_bytes"] = f.read()
+    with open(os.path.join(d, "vocab.txt"), "rb") as f:
+        case["vocab_bytes"] = f.read()
+    with gzip.open(os.path.join(d, "trace.txt.gz"), "rt") as f:
+        case["trace"] = f.read()
+    return case
+
+
+def build_corpus(recipe, path):
+    kind = recipe["kind"]
+    if kind == "synthetic":
+        corpora.gen_synthetic(path, recipe["bytes"], recipe["seed"], recipe["script"])
+    elif kind == "adversarial":
+        corpora.write_adversarial(path, recipe["seed"])
+    elif kind == "small":
+        corpora.write_small_corpus(path)
+    else:
+        raise ValueError(kind)
+
+
+@pytest.fixture(scope="session")
+def corpus_dir(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("corpora"))
+
+
+_CORPUS_CACHE = {}
+
+
+@pytest.fixture(scope="session")
+def case_corpus(corpus_dir):
+    """Returns a function name -> (case dict, corpus path), corpora built once per session."""
+    def get(name):
+        case = load_case(name)
+        key = json.dumps({k: v for k, v in case["corpus"].items() if k not in ("md5", "size")}, sort_keys=True)
+        if key not in _CORPUS_CACHE:
+            path = os.path.join(corpus_dir, f"corpus_{len(_CORPUS_CACHE)}.txt")
+            build_corpus(case["corpus"], path)
+            assert corpora.md5_file(path) == case["corpus"]["md5"], f"generator drift for {name}"
+            _CORPUS_CACHE[key] = path
+        return case, _CORPUS_CACHE[key]
+    return get
+
+
+@pytest.fixture(scope="session")
+def oracle_bin():
+    subprocess.run(["make", "-s", "-C", ORACLE, "port"], check=True)
+    return os.path.join(ORACLE, "_build", "bpe_oracle")

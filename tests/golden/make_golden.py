@@ -1,0 +1,152 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Runs only in the survey/build container (needs /root/reference): it compiles the reference's
+own BPE sources with zero-initialised malloc (oracle/Makefile target ``ref``)
+and drives them through their C ABI (oracle/ref_driver.c) or their CLI (trainer.cpp), capturing
+
+* ``model.bin``  — the reference .model bytes (bpe.cpp:419-427),
+* ``vocab.txt``  — the reference .vocab bytes (bpe.cpp:416-418),
+* ``trace.txt.gz`` — "M a b freq new_id" per [MERGE] line (bpe.cpp:260) and
+  "B batch completed heap_size top_freq" per batch line (bpe.cpp:369),
+* ``case.json``  — corpus recipe + md5, config, merge count, output md5s.
+
+Corpora are not committed: tests rebuild them from the recipe and check the md5.
+Usage: python tests/golden/make_golden.py [case-name ...]
+"""
+from __future__ import annotations
+
+import gzip
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import corpora  # noqa: E402
+
+REPO = corpora.REPO
+ORACLE = os.path.join(REPO, "oracle")
+
+# name: (corpus recipe, (vocab, unk, coverage, min_pair_freq), via)
+CASES = {
+    "c1_ascii10m_v8192": ({"kind": "synthetic", "bytes": 10_000_000, "seed": 1, "script": "ascii"},
+                          (8192, 0, 0.995, 2000), "api"),
+    "ascii1m_v3000_mpf2": ({"kind": "synthetic", "bytes": 1_000_000, "seed": 11, "script": "ascii"},
+                           (3000, 0, 0.995, 2), "api"),
+    "utf8_2m_v3000_cov9995": ({"kind": "synthetic", "bytes": 2_000_000, "seed": 12, "script": "utf8"},
+                              (3000, 0, 0.9995, 2), "api"),
+    "utf8_2m_v2000_mpf50": ({"kind": "synthetic", "bytes": 2_000_000, "seed": 13, "script": "utf8"},
+                            (2000, 0, 0.995, 50), "api"),
+    "ascii1m_unk7_cov09": ({"kind": "synthetic", "bytes": 1_000_000, "seed": 14, "script": "ascii"},
+                           (1000, 7, 0.9, 3), "api"),
+    "mixed2m_v4000": ({"kind": "synthetic", "bytes": 2_000_000, "seed": 15, "script": "mixed"},
+                      (4000, 0, 0.9995, 2), "api"),
+    "utf8_4m_v8192_mpf5": ({"kind": "synthetic", "bytes": 4_000_000, "seed": 16, "script": "utf8"},
+                           (8192, 0, 0.995, 5), "api"),
+    "ascii1m_unkm1_mpf2": ({"kind": "synthetic", "bytes": 1_000_000, "seed": 17, "script": "ascii"},
+                           (2000, -1, 0.995, 2), "api"),
+    "adv_unk0": ({"kind": "adversarial", "seed": 1}, (600, 0, 0.995, 2), "api"),
+    "adv_unk3_cov09": ({"kind": "adversarial", "seed": 2}, (600, 3, 0.9, 2), "api"),
+    "adv_cov05": ({"kind": "adversarial", "seed": 3}, (600, 0, 0.5, 3), "api"),
+    "adv_unkm1": ({"kind": "adversarial", "seed": 4}, (600, -1, 0.995, 2), "api"),
+    "small_v300": ({"kind": "small"}, (300, 0, 0.995, 2), "api"),
+    "small_v50_zero": ({"kind": "small"}, (50, 0, 0.995, 1000), "api"),
+    "small_v256_zero": ({"kind": "small"}, (256, 0, 0.995, 2), "api"),
+    "small_cov0_mpf0": ({"kind": "small"}, (400, 0, 0.0, 0), "api"),
+    "cli_ascii10m": ({"kind": "synthetic", "bytes": 10_000_000, "seed": 1, "script": "ascii"},
+                     (8192, -1, 0.9995, 2000), "cli"),
+    "cli_utf8_2m_mpf20": ({"kind": "synthetic", "bytes": 2_000_000, "seed": 18, "script": "utf8"},
+                          (3000, -1, 0.9995, 20), "cli"),
+}
+
+MERGE_RE = re.compile(rb"^\[MERGE\]\t Merging \((-?\d+),(-?\d+)\) freq=(\d+) -> new_id=(-?\d+)")
+BATCH_RE = re.compile(rb"^\[INFO\]\t Processing batch of (-?\d+) merges \(completed: (-?\d+)/-?\d+, "
+                      rb"heap size: (\d+), top freq: (\d+)\)")
+
+
+def build_corpus(recipe: dict, path: str) -> None:
+    kind = recipe["kind"]
+    if kind == "synthetic":
+        corpora.gen_synthetic(path, recipe["bytes"], recipe["seed"], recipe["script"])
+    elif kind == "adversarial":
+        corpora.write_adversarial(path, recipe["seed"])
+    elif kind == "small":
+        corpora.write_small_corpus(path)
+    else:
+        raise ValueError(kind)
+
+
+def parse_trace(stdout: bytes) -> str:
+    out = []
+    for line in stdout.splitlines():
+        m = MERGE_RE.match(line)
+        if m:
+            out.append("M %s %s %s %s" % tuple(g.decode() for g in m.groups()))
+            continue
+        m = BATCH_RE.match(line)
+        if m:
+            out.append("B %s %s %s %s" % tuple(g.decode() for g in m.groups()))
+    return "\n".join(out) + ("\n" if out else "")
+
+
+def run_case(name: str, tmp: str) -> None:
+    recipe, (vocab, unk, cov, mpf), via = CASES[name]
+    corpus = os.path.join(tmp, name + ".txt")
+    build_corpus(recipe, corpus)
+    model = os.path.join(tmp, name + ".model")
+    vocabf = os.path.join(tmp, name + ".vocab")
+    if via == "api":
+        cmd = [os.path.join(ORACLE, "_ref", "ref_driver"), corpus, str(vocab), str(unk), repr(cov),
+               str(mpf), model, vocabf]
+    else:
+        # the CLI aborts after saving (unk_id=-1, bpe.cpp:413): line-buffer stdout to keep the trace
+        cmd = ["stdbuf", "-oL", os.path.join(ORACLE, "_ref", "trainer_ref"), f"input={corpus}", "model_type=bpe",
+               f"output_model={model}", f"output_vocab={vocabf}", f"vocab_size={vocab}",
+               f"character_coverage={cov}", f"min_pair_freq={mpf}"]
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    # unk_id < 0 makes the reference write freq[-1] (bpe.cpp:413) and abort in free() after
+    # both files are closed; any other failure is fatal.
+    if via == "api" and proc.returncode != 0 and unk >= 0:
+        raise RuntimeError(f"{name}: reference failed rc={proc.returncode}: {proc.stderr[-2000:]!r}")
+    if not (os.path.exists(model) and os.path.exists(vocabf)):
+        raise RuntimeError(f"{name}: reference produced no files (rc={proc.returncode})")
+    d = os.path.join(HERE, name)
+    os.makedirs(d, exist_ok=True)
+    shutil.copyfile(model, os.path.join(d, "model.bin"))
+    shutil.copyfile(vocabf, os.path.join(d, "vocab.txt"))
+    trace = parse_trace(proc.stdout)
+    with gzip.open(os.path.join(d, "trace.txt.gz"), "wt") as f:
+        f.write(trace)
+    merges = os.path.getsize(model) // 12
+    case = {
+        "name": name,
+        "corpus": dict(recipe, md5=corpora.md5_file(corpus), size=os.path.getsize(corpus)),
+        "config": {"vocab_size": vocab, "unk_id": unk, "character_coverage": cov, "min_pair_freq": mpf},
+        "via": via,
+        "reference_returncode": proc.returncode,
+        "merges": merges,
+        "model_md5": corpora.md5_file(model),
+        "vocab_md5": corpora.md5_file(vocabf),
+        "generator": "tests/golden/make_golden.py (zero-init reference, oracle/Makefile ref)",
+    }
+    with open(os.path.join(d, "case.json"), "w") as f:
+        json.dump(case, f, indent=1, sort_keys=True)
+        f.write("\n")
+    print(f"{name}: merges={merges} rc={proc.returncode}")
+
+
+def main() -> None:
+    subprocess.run(["make", "-C", ORACLE, "ref"], check=True, stdout=subprocess.DEVNULL)
+    names = sys.argv[1:] or list(CASES)
+    with tempfile.TemporaryDirectory() as tmp:
+        for n in names:
+            run_case(n, tmp)
+
+
+if __name__ == "__main__":
+    main()
