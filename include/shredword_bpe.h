@@ -1,0 +1,105 @@
+/* shredword_bpe.h — C ABI of the MI355X BPE trainer (libtrainer.so).
+ *
+ * Drop-in for the reference's BPE C ABI (shredword/csrc/bpe/bpe.h:62-72) as bound by its ctypes
+ * layer (shredword/cbase.py:50-57): same symbol names, argument meaning, return conventions and
+ * BPEConfig layout (bpe.h:43-48; 24 bytes, offsets 0/8/12/16).  The 13 Unigram symbols that
+ * cbase.py:59-71 binds at import are exported as stubs that fail (Unigram is out of scope,
+ * SURVEY.md §2 #7).  Symbols prefixed shred_ are extensions; a reference user never needs them.
+ *
+ * Plain pointers and sizes only.  The Trainer handle is opaque; it is not thread-safe (like the
+ * reference's), and no call holds or needs the Python GIL.
+ */
+#ifndef SHREDWORD_BPE_H
+#define SHREDWORD_BPE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* reference bpe.h:43-48 */
+typedef struct BPEConfig {
+  size_t target_vocab_size;
+  int32_t unk_id;            /* must be >= -2^30 (values below are reserved for word headers) */
+  float character_coverage;  /* outside (0,1) -> 0.995 (bpe.cpp:78) */
+  uint64_t min_pair_freq;    /* 0 -> 2000 (bpe.cpp:79) */
+} BPEConfig;
+
+typedef struct Trainer Trainer;
+
+/* ---- reference BPE ABI (bpe.h:63-71) ---------------------------------------------------- */
+/* replaces bpe.cpp:67-85.  NULL config -> message + exit(EXIT_FAILURE), as the reference. */
+Trainer* create_trainer(const BPEConfig* config);
+/* replaces bpe.cpp:87-96.  NULL -> message + exit(EXIT_FAILURE). */
+void bpe_trainer_destroy(Trainer* trainer);
+/* replaces bpe.cpp:110-185.  0 on success, -1 on NULL args or open failure.  Last call wins.
+ * The distinct-word table is built on the host and uploaded to HBM when a GPU is present. */
+int bpe_load_corpus(Trainer* trainer, const char* input_path);
+/* replaces bpe.cpp:98-108: resets pair info and heap, then bpe_count_bigrams. */
+void bpe_init(Trainer* trainer);
+/* replaces bpe.cpp:187-230: device pair histogram (K1) + reference-ordered heap build. */
+void bpe_count_bigrams(Trainer* trainer);
+/* replaces bpe.cpp:232-323: up to batch_size merges (device K2-K4 + host heap replay).
+ * Returns merges done (0 when the heap is empty), -1 on NULL or when no GPU is usable. */
+int bpe_merge_batch(Trainer* trainer, int batch_size);
+/* replaces bpe.cpp:345-386.  Returns merges performed, -1 on NULL or when no GPU is usable. */
+int bpe_train(Trainer* trainer);
+/* replaces bpe.cpp:388-432: writes .vocab (text) and .model (int32 a, b, new_id per merge). */
+void bpe_save(const Trainer* trainer, const char* model_path, const char* vocab_path);
+
+/* ---- Unigram symbols bound by cbase.py:59-71 (stubs: return failure / NULL) ------------- */
+void* trainerCreate(int vocab_size, float character_coverage, int max_piece_length, int seed_size);
+void trainerDestroy(void* trainer);
+int addTextToTrainer(void* trainer, const char* text);  /* returns false */
+int preprocessTexts(void* trainer);
+int extractInitialSubwords(void* trainer);
+float computeLoss(void* trainer, char** texts, int n);
+double computeTokenLoss(void* trainer, const char* token, char** texts, int n);
+int pruneVocabStep(void* trainer, char** texts, int n, double ratio);
+int updateTokenScores(void* trainer, char** texts, int n);
+int trainUnigram(void* trainer, char** texts, int n, int iterations);
+int getVocab(void* trainer, char*** tokens, double** scores, int* n);
+int saveVocab(void* trainer, const char* path);
+int loadVocab(void* trainer, const char* path);
+
+/* ---- extensions ------------------------------------------------------------------------ */
+/* Options (also read from the environment at create_trainer as SHREDWORD_<KEY>):
+ *   layout = types | stream     device word table: distinct words weighted by count (default)
+ *                               or every occurrence in corpus order with weight 1
+ *   log    = 0 | 1 | 2          quiet / summary (default) / reference-style per-merge lines
+ *   trace  = <path>             "M a b freq new_id" / "B batch done heap top" trace file
+ *   timing = 0 | 1              per-kernel HIP-event timing (shred_get_stats)
+ *   device = <ordinal>          HIP device (default: LOCAL_RANK or 0)
+ * Returns 0, or -1 for an unknown key/value. */
+int shred_set_option(Trainer* trainer, const char* key, const char* value);
+/* Restores the loaded corpus to its unmerged state and forgets merges (benchmark repeats). */
+int shred_reset(Trainer* trainer);
+
+typedef struct ShredStats {
+  double load_seconds, init_seconds, train_seconds;
+  double merge_kernel_ms, count_kernel_ms;
+  double merge_kernel_bytes, count_kernel_bytes;
+  uint64_t merge_launches, count_launches;
+  uint64_t num_words, num_symbols, num_occurrences, num_merges, heap_size, live_tokens;
+  uint64_t device_bytes, num_tiles;
+  int32_t layout, world_size;
+} ShredStats;
+int shred_get_stats(const Trainer* trainer, ShredStats* out);
+
+/* Number of usable HIP devices (0 without a GPU); never initialises more than the runtime. */
+int shred_device_count(void);
+
+/* Multi-GPU (one process per GPU, RCCL over xGMI): rank 0 calls shred_dist_unique_id, the
+ * bytes are broadcast out of band (torch.distributed), then every rank calls shred_dist_init
+ * before create_trainer.  Trainers then shard the word table and all-reduce the per-merge
+ * delta tables.  Returns 0 on success. */
+int shred_dist_unique_id(void* out, size_t cap);
+int shred_dist_init(int rank, int world_size, const void* unique_id, size_t len, int device);
+int shred_dist_finalize(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

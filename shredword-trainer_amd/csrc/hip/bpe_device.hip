@@ -1,0 +1,912 @@
+// MI355X (gfx950) kernels of the BPE merge loop and the Device class that drives them.
+//
+// Integer-only, HBM/LDS-bound work (no MFMA).  Every kernel walks the tiled token stream of
+// device.h with 256-thread workgroups (4 wave64s), 16 consecutive tokens per lane, one 4096-token
+// chunk per iteration; a tile longer than one chunk (a word of > 4095 tokens) is walked chunk by
+// chunk with carries, so no word length is special.
+//
+//   k_pair_count   K1  weighted pair histogram + first touch     (reference bpe.cpp:187-206)
+//   k_merge        K2+K3 match (a,b), emit the 4 neighbour deltas per occurrence, rewrite the
+//                  chunk compacted in place                      (reference bpe.cpp:259-296)
+//   k_collect      K4  touched delta slots -> host records       (FreqChangeMap, bpe.cpp:9-50)
+//   k_token_freq   K6  final weighted token histogram            (reference bpe.cpp:409-415)
+//
+// Deltas and pair counts are staged in per-workgroup LDS hash tables and spilled to HBM tables
+// with 64-bit atomics (sum) and atomicMin (first touch), so the reduction is order-free and the
+// result bit-identical run to run.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../host/common.h"
+#include "../host/device.h"
+
+namespace shred {
+
+#define HIP_OK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) {                                                                 \
+      std::fprintf(stderr, "[ERROR]\t HIP %s failed: %s (%s:%d)\n", #expr, hipGetErrorString(e_), \
+                   __FILE__, __LINE__);                                                     \
+      std::fflush(stderr);                                                                  \
+      std::abort();                                                                         \
+    }                                                                                       \
+  } while (0)
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kPer = 16;
+constexpr int kChunk = kThreads * kPer;  // 4096 tokens = 16 KiB per chunk
+constexpr int kDeltaLds = 1024;          // per-workgroup delta staging slots
+constexpr int kPairLds = 2048;           // per-workgroup pair-count staging slots
+constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
+constexpr unsigned long long kEmpty64 = ~0ull;
+constexpr int32_t kPad = INT32_MIN;      // beyond the tile; also looks like a header
+
+typedef unsigned long long u64;
+
+__device__ __forceinline__ bool is_hdr(int32_t t) { return t < kHeaderLimit; }
+__device__ __forceinline__ uint32_t hdr_rank(int32_t t) { return (uint32_t)(t - kHeaderBase); }
+
+__device__ __forceinline__ u64 mix64(u64 k) {
+  k ^= k >> 33;
+  k *= 0xFF51AFD7ED558CCDull;
+  k ^= k >> 33;
+  k *= 0xC4CEB9FE1A85EC53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// One exclusive block scan of a packed header key (max) and a counter (sum) over 256 lanes.
+struct ScanLds {
+  u64 hdr[4];
+  int cnt[4];
+  long long nona[4];
+};
+
+__device__ __forceinline__ void block_scan_hdr_cnt(u64 hdr, int cnt, ScanLds& s, u64* hdr_excl, int* cnt_excl,
+                                                   u64* hdr_tot, int* cnt_tot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  u64 h = hdr;
+  int c = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    u64 hy = __shfl_up(h, d, 64);
+    int cy = __shfl_up(c, d, 64);
+    if (lane >= d) {
+      h = hy > h ? hy : h;
+      c += cy;
+    }
+  }
+  if (lane == 63) {
+    s.hdr[w] = h;
+    s.cnt[w] = c;
+  }
+  __syncthreads();
+  u64 hp = 0;
+  int cp = 0;
+  for (int i = 0; i < w; ++i) {
+    hp = s.hdr[i] > hp ? s.hdr[i] : hp;
+    cp += s.cnt[i];
+  }
+  u64 ht = 0;
+  int ct = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    ht = s.hdr[i] > ht ? s.hdr[i] : ht;
+    ct += s.cnt[i];
+  }
+  u64 hx = __shfl_up(h, 1, 64);
+  int cx = __shfl_up(c, 1, 64);
+  if (lane == 0) {
+    hx = 0;
+    cx = 0;
+  }
+  *hdr_excl = hx > hp ? hx : hp;
+  *cnt_excl = cx + cp;
+  *hdr_tot = ht;
+  *cnt_tot = ct;
+  __syncthreads();
+}
+
+__device__ __forceinline__ long long block_scan_max_ll(long long x, ScanLds& s, long long* tot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long long v = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    long long y = __shfl_up(v, d, 64);
+    if (lane >= d) v = y > v ? y : v;
+  }
+  if (lane == 63) s.nona[w] = v;
+  __syncthreads();
+  long long pre = -1, t = -1;
+  for (int i = 0; i < 4; ++i) {
+    if (i < w) pre = s.nona[i] > pre ? s.nona[i] : pre;
+    t = s.nona[i] > t ? s.nona[i] : t;
+  }
+  long long ex = __shfl_up(v, 1, 64);
+  if (lane == 0) ex = -1;
+  *tot = t;
+  __syncthreads();
+  return ex > pre ? ex : pre;
+}
+
+// Loads this lane's 16 tokens of chunk [cs, cs+cl) (kPad beyond cl).  16-byte loads where the
+// whole quad is in range: tiles start 16-byte aligned and chunks are 4096 tokens.
+__device__ __forceinline__ void load_chunk(const int32_t* base, uint32_t cs, uint32_t cl, int p0, int32_t (&v)[kPer]) {
+#pragma unroll
+  for (int q = 0; q < kPer / 4; ++q) {
+    const int idx = p0 + 4 * q;
+    if (idx + 4 <= (int)cl) {
+      const int4 x = *reinterpret_cast<const int4*>(base + cs + idx);
+      v[4 * q] = x.x;
+      v[4 * q + 1] = x.y;
+      v[4 * q + 2] = x.z;
+      v[4 * q + 3] = x.w;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[4 * q + r] = (idx + r < (int)cl) ? base[cs + idx + r] : kPad;
+    }
+  }
+}
+
+// Token following this lane's 16 (from the next lane, or from memory at a wave edge).
+__device__ __forceinline__ int32_t next_token(const int32_t* base, uint32_t cs, uint32_t len, int p0, int32_t v0) {
+  int32_t nx = __shfl_down(v0, 1, 64);
+  if ((threadIdx.x & 63) == 63) nx = (cs + p0 + kPer < len) ? base[cs + p0 + kPer] : kPad;
+  return nx;
+}
+
+// ------------------------------------------------------------------------------------------
+// K2+K3: merge scan
+struct MergeParams {
+  int32_t* tok;
+  const uint64_t* tile_off;
+  uint32_t* tile_len;
+  uint32_t ntiles;
+  const uint64_t* weight;
+  int32_t a, b, X;
+  uint32_t slot_cap;
+  u64* dsum;
+  u64* dft;
+  uint32_t* dlist;
+  uint32_t* dcount;
+  u64* stats;  // [0] occurrences merged, [1] tokens rewritten
+};
+
+struct DeltaLds {
+  uint32_t key[kDeltaLds];
+  u64 sum[kDeltaLds];
+  u64 ft[kDeltaLds];
+};
+
+__device__ __forceinline__ void delta_global(const MergeParams& p, uint32_t key, u64 w, u64 ft) {
+  atomicAdd(&p.dsum[key], w);
+  const u64 old = atomicMin(&p.dft[key], ft);
+  if (old == kEmpty64) p.dlist[atomicAdd(p.dcount, 1u)] = key;  // exactly one toucher sees MAX
+}
+
+__device__ __forceinline__ void delta_emit(DeltaLds& h, const MergeParams& p, uint32_t key, u64 w, u64 ft) {
+  uint32_t s = (key * 2654435761u) >> 22;
+  for (int probe = 0; probe < 16; ++probe) {
+    const uint32_t prev = atomicCAS(&h.key[s], kEmpty32, key);
+    if (prev == kEmpty32 || prev == key) {
+      atomicAdd(&h.sum[s], w);
+      atomicMin(&h.ft[s], ft);
+      return;
+    }
+    s = (s + 1) & (kDeltaLds - 1);
+  }
+  delta_global(p, key, w, ft);
+}
+
+__device__ __forceinline__ uint32_t slot_of(int32_t id, uint32_t cap) {
+  return (uint32_t)id < cap ? (uint32_t)id + 1u : 0u;
+}
+
+template <bool kWeighted>
+__global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
+  __shared__ int32_t s_tok[kChunk + 8];  // s_tok[2 + j] = chunk position j; [0],[1] = positions -2,-1
+  __shared__ int32_t s_out[kChunk];
+  __shared__ uint32_t s_mask[kThreads];
+  __shared__ ScanLds s_scan;
+  __shared__ DeltaLds h;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kDeltaLds; i += kThreads) {
+    h.key[i] = kEmpty32;
+    h.sum[i] = 0;
+    h.ft[i] = kEmpty64;
+  }
+  __syncthreads();
+  const int32_t a = p.a, b = p.b, X = p.X;
+  const bool same = (a == b);
+  const int p0 = tid * kPer;
+  u64 n_merged = 0, n_written = 0;
+
+  for (uint32_t tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
+    const uint32_t len = p.tile_len[tile];
+    int32_t* base = p.tok + p.tile_off[tile];
+    long long c_nona = -1;  // last tile index whose token != a (a == b only)
+    u64 c_hdr = 0;          // ((index + 1) << 32) | rank of the last header seen, 0 = none
+    bool c_m1 = false, c_m2 = false;
+    int32_t c_t1 = kPad, c_t2 = kPad;
+    uint32_t c_out = 0;
+    bool dirty = false;
+    for (uint32_t cs = 0; cs < len; cs += kChunk) {
+      const uint32_t cl = min((uint32_t)kChunk, len - cs);
+      const bool more = cs + cl < len;
+      int32_t v[kPer];
+      load_chunk(base, cs, cl, p0, v);
+      const int32_t nx = next_token(base, cs, len, p0, v[0]);
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) any |= (v[j] == a) & ((j + 1 < kPer ? v[j + 1] : nx) == b);
+      const bool any_blk = __syncthreads_or(any);
+      if (!any_blk && !dirty && !more) break;  // rest of the tile is unchanged
+
+      // ---- stage the chunk and its context in LDS
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) s_tok[2 + p0 + j] = v[j];
+      if (tid == 0) {
+        s_tok[0] = c_t2;
+        s_tok[1] = c_t1;
+      }
+      if (tid == kThreads - 1) {
+        s_tok[2 + kChunk] = (cs + kChunk < len) ? base[cs + kChunk] : kPad;
+        s_tok[3 + kChunk] = (cs + kChunk + 1 < len) ? base[cs + kChunk + 1] : kPad;
+      }
+      __syncthreads();
+
+      // ---- occurrences, greedy left to right (runs of a==b pair up from the run start)
+      uint32_t mask = 0;
+      long long nona_tot = -1;
+      if (same) {
+        long long nl = -1;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if (v[j] != a) nl = (long long)(cs + p0 + j);
+        long long last = block_scan_max_ll(nl, s_scan, &nona_tot);
+        last = last > c_nona ? last : c_nona;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const long long gi = (long long)(cs + p0 + j);
+          if (v[j] != a) last = gi;
+          else if (s_tok[3 + p0 + j] == a && ((gi - last - 1) & 1) == 0) mask |= 1u << j;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if (v[j] == a && s_tok[3 + p0 + j] == b) mask |= 1u << j;
+      }
+      s_mask[tid] = mask;
+      __syncthreads();
+      const uint32_t prevm = tid ? s_mask[tid - 1] : ((c_m1 ? 1u << 15 : 0u) | (c_m2 ? 1u << 14 : 0u));
+      const uint32_t m_ext = (mask << 2) | ((prevm >> 14) & 3u);  // bit k <-> position p0 - 2 + k
+      const uint32_t removed = (m_ext >> 1) & 0xFFFFu;           // bit j <-> match at p0 + j - 1
+      const int valid = max(0, min(kPer, (int)cl - p0));
+      const uint32_t vmask = valid >= kPer ? 0xFFFFu : ((1u << valid) - 1u);
+      const int kc = __popc(~removed & vmask);
+      const int nm = __popc(mask);
+      u64 hl = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (j < valid && is_hdr(v[j])) hl = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(v[j]);
+      u64 hdr_ex, hdr_tot;
+      int kc_ex, cnt_tot;
+      block_scan_hdr_cnt(hl, kc | (nm << 16), s_scan, &hdr_ex, &kc_ex, &hdr_tot, &cnt_tot);
+      kc_ex &= 0xFFFF;
+      const int kept = cnt_tot & 0xFFFF;
+      const int matches = cnt_tot >> 16;
+
+      // ---- compacted output (chunk-local)
+      {
+        int o = kc_ex;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if (j < valid && !((removed >> j) & 1u)) s_out[o++] = ((mask >> j) & 1u) ? X : v[j];
+      }
+      // ---- neighbour deltas, 4 per occurrence (bpe.cpp:274-290)
+      if (mask) {
+        u64 hdr = hdr_ex > c_hdr ? hdr_ex : c_hdr;
+        for (int j = 0; j < kPer; ++j) {
+          if (j < valid && is_hdr(v[j])) hdr = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(v[j]);
+          if (!((mask >> j) & 1u)) continue;
+          const uint32_t hidx = (uint32_t)(hdr >> 32) - 1u;
+          const uint32_t rank = (uint32_t)hdr;
+          const uint32_t gi = cs + p0 + j;
+          const u64 w = kWeighted ? p.weight[rank] : 1ull;
+          const u64 ftb = ((u64)rank << 32) | ((u64)(gi - hidx - 1u) << 2);
+          if (gi - 1u > hidx) {  // left neighbour inside the word; X if it was just merged
+            const int32_t left = ((m_ext >> j) & 1u) ? X : s_tok[1 + p0 + j];
+            const uint32_t sl = slot_of(left, p.slot_cap) << 2;
+            delta_emit(h, p, sl | kOldLeft, w, ftb | kOldLeft);
+            delta_emit(h, p, sl | kNewLeft, w, ftb | kNewLeft);
+          }
+          const int32_t right = s_tok[4 + p0 + j];  // original token after b
+          if (!is_hdr(right)) {
+            const uint32_t sr = slot_of(right, p.slot_cap) << 2;
+            delta_emit(h, p, sr | kOldRight, w, ftb | kOldRight);
+            delta_emit(h, p, sr | kNewRight, w, ftb | kNewRight);
+          }
+        }
+      }
+      __syncthreads();  // s_out complete
+      if (dirty || matches > 0 || kept != (int)cl) {
+        for (int j = tid; j < kept; j += kThreads) base[c_out + j] = s_out[j];
+        dirty = true;
+        n_written += (u64)kept;
+      }
+      n_merged += (u64)matches;
+      // ---- carries to the next chunk of this tile
+      c_out += (uint32_t)kept;
+      c_m1 = (s_mask[(cl - 1) / kPer] >> ((cl - 1) % kPer)) & 1u;
+      c_m2 = cl >= 2 ? ((s_mask[(cl - 2) / kPer] >> ((cl - 2) % kPer)) & 1u) : c_m1;
+      c_t2 = cl >= 2 ? s_tok[2 + cl - 2] : s_tok[1];
+      c_t1 = s_tok[2 + cl - 1];
+      c_hdr = hdr_tot > c_hdr ? hdr_tot : c_hdr;
+      if (same) c_nona = nona_tot > c_nona ? nona_tot : c_nona;
+      __syncthreads();  // before the next chunk reuses s_tok / s_out / s_mask
+    }
+    if (dirty && tid == 0) p.tile_len[tile] = c_out;
+  }
+  __syncthreads();
+  for (int i = tid; i < kDeltaLds; i += kThreads)
+    if (h.key[i] != kEmpty32) delta_global(p, h.key[i], h.sum[i], h.ft[i]);
+  if (tid == 0) {
+    if (n_merged) atomicAdd(&p.stats[0], n_merged);
+    if (n_written) atomicAdd(&p.stats[1], n_written);
+  }
+}
+
+// K4: touched slots -> records in host-visible memory; clears the slots for the next merge.
+__global__ __launch_bounds__(kThreads) void k_collect(const uint32_t* dcount, uint32_t* dcount_next, const uint32_t* dlist,
+                                                       u64* dsum, u64* dft, DeltaRecord* out, uint32_t* out_count,
+                                                       u64* stats, u64* out_stats) {
+  const uint32_t n = *dcount;
+  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+    const uint32_t key = dlist[i];
+    DeltaRecord r;
+    r.key = key;
+    r.pad = 0;
+    r.sum = dsum[key];
+    r.ft = dft[key];
+    out[i] = r;
+    dsum[key] = 0;
+    dft[key] = kEmpty64;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *out_count = n;
+    *dcount_next = 0;
+    out_stats[0] = stats[0];
+    out_stats[1] = stats[1];
+  }
+}
+
+// K4 (multi-GPU): after the all-reduce every rank scans the dense prefix instead of its own list.
+__global__ __launch_bounds__(kThreads) void k_collect_dense(uint32_t nkeys, u64* dsum, u64* dft, DeltaRecord* out,
+                                                             uint32_t* out_count) {
+  for (uint32_t key = blockIdx.x * kThreads + threadIdx.x; key < nkeys; key += gridDim.x * kThreads) {
+    const u64 ft = dft[key];
+    if (ft == kEmpty64) continue;
+    DeltaRecord r;
+    r.key = key;
+    r.pad = 0;
+    r.sum = dsum[key];
+    r.ft = ft;
+    out[atomicAdd(out_count, 1u)] = r;
+    dsum[key] = 0;
+    dft[key] = kEmpty64;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K1: pair count
+struct CountParams {
+  const int32_t* tok;
+  const uint64_t* tile_off;
+  const uint32_t* tile_len;
+  uint32_t ntiles;
+  const uint64_t* weight;
+  int32_t unk;
+  u64* tkey;
+  u64* tcnt;
+  u64* tft;
+  u64 tmask;
+  uint32_t* overflow;
+};
+
+struct PairLds {
+  u64 key[kPairLds];
+  u64 cnt[kPairLds];
+  u64 ft[kPairLds];
+};
+
+__device__ __forceinline__ void pair_global(const CountParams& p, u64 key, u64 c, u64 ft) {
+  u64 s = mix64(key) & p.tmask;
+  for (u64 probe = 0; probe <= p.tmask; ++probe) {
+    const u64 prev = atomicCAS(&p.tkey[s], kEmpty64, key);
+    if (prev == kEmpty64 || prev == key) {
+      atomicAdd(&p.tcnt[s], c);
+      atomicMin(&p.tft[s], ft);
+      return;
+    }
+    s = (s + 1) & p.tmask;
+  }
+  atomicOr(p.overflow, 1u);
+}
+
+__device__ __forceinline__ void pair_emit(PairLds& h, const CountParams& p, u64 key, u64 c, u64 ft) {
+  uint32_t s = (uint32_t)(mix64(key) >> 53);  // 11 bits
+  for (int probe = 0; probe < 16; ++probe) {
+    const u64 prev = atomicCAS(&h.key[s], kEmpty64, key);
+    if (prev == kEmpty64 || prev == key) {
+      atomicAdd(&h.cnt[s], c);
+      atomicMin(&h.ft[s], ft);
+      return;
+    }
+    s = (s + 1) & (kPairLds - 1);
+  }
+  pair_global(p, key, c, ft);
+}
+
+template <bool kWeighted>
+__global__ __launch_bounds__(kThreads) void k_pair_count(CountParams p) {
+  __shared__ PairLds h;
+  __shared__ ScanLds s_scan;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kPairLds; i += kThreads) {
+    h.key[i] = kEmpty64;
+    h.cnt[i] = 0;
+    h.ft[i] = kEmpty64;
+  }
+  __syncthreads();
+  const int p0 = tid * kPer;
+  for (uint32_t tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
+    const uint32_t len = p.tile_len[tile];
+    const int32_t* base = p.tok + p.tile_off[tile];
+    u64 c_hdr = 0;
+    for (uint32_t cs = 0; cs < len; cs += kChunk) {
+      const uint32_t cl = min((uint32_t)kChunk, len - cs);
+      int32_t v[kPer];
+      load_chunk(base, cs, cl, p0, v);
+      const int32_t nx = next_token(base, cs, len, p0, v[0]);
+      u64 hl = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (is_hdr(v[j]) && p0 + j < (int)cl) hl = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(v[j]);
+      u64 hdr_ex, hdr_tot;
+      int cx, ct;
+      block_scan_hdr_cnt(hl, 0, s_scan, &hdr_ex, &cx, &hdr_tot, &ct);
+      u64 hdr = hdr_ex > c_hdr ? hdr_ex : c_hdr;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int32_t x = v[j];
+        const int32_t y = j + 1 < kPer ? v[j + 1] : nx;
+        if (is_hdr(x)) {
+          if (p0 + j < (int)cl) hdr = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(x);
+          continue;
+        }
+        if (is_hdr(y) || x == p.unk || y == p.unk) continue;
+        const uint32_t hidx = (uint32_t)(hdr >> 32) - 1u;
+        const uint32_t rank = (uint32_t)hdr;
+        const u64 w = kWeighted ? p.weight[rank] : 1ull;
+        const u64 key = ((u64)(uint32_t)x << 32) | (uint32_t)y;
+        pair_emit(h, p, key, w, ((u64)rank << 32) | (u64)(cs + p0 + j - hidx - 1u));
+      }
+      c_hdr = hdr_tot > c_hdr ? hdr_tot : c_hdr;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < kPairLds; i += kThreads)
+    if (h.key[i] != kEmpty64) pair_global(p, h.key[i], h.cnt[i], h.ft[i]);
+}
+
+__global__ __launch_bounds__(kThreads) void k_pair_collect(const u64* tkey, const u64* tcnt, const u64* tft, u64 cap,
+                                                            PairCount* out, uint32_t out_cap, uint32_t* n) {
+  for (u64 i = (u64)blockIdx.x * kThreads + threadIdx.x; i < cap; i += (u64)gridDim.x * kThreads) {
+    const u64 k = tkey[i];
+    if (k == kEmpty64) continue;
+    PairCount pc;
+    pc.a = (int32_t)(uint32_t)(k >> 32);
+    pc.b = (int32_t)(uint32_t)k;
+    pc.count = tcnt[i];
+    pc.ft = tft[i];
+    const uint32_t i_out = atomicAdd(n + 1, 1u);
+    if (i_out < out_cap) out[i_out] = pc;
+    else atomicOr(n, 2u);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K6: final token histogram over ids [0, T) (the unk count lands on unk_id when it is in range)
+template <bool kWeighted>
+__global__ __launch_bounds__(kThreads) void k_token_freq(const int32_t* tok, const uint64_t* tile_off,
+                                                          const uint32_t* tile_len, uint32_t ntiles,
+                                                          const uint64_t* weight, uint32_t T, u64* freq) {
+  __shared__ ScanLds s_scan;
+  const int p0 = threadIdx.x * kPer;
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint32_t len = tile_len[tile];
+    const int32_t* base = tok + tile_off[tile];
+    u64 c_hdr = 0;
+    for (uint32_t cs = 0; cs < len; cs += kChunk) {
+      const uint32_t cl = min((uint32_t)kChunk, len - cs);
+      int32_t v[kPer];
+      load_chunk(base, cs, cl, p0, v);
+      u64 hl = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (is_hdr(v[j]) && p0 + j < (int)cl) hl = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(v[j]);
+      u64 hdr_ex, hdr_tot;
+      int cx, ct;
+      block_scan_hdr_cnt(hl, 0, s_scan, &hdr_ex, &cx, &hdr_tot, &ct);
+      u64 hdr = hdr_ex > c_hdr ? hdr_ex : c_hdr;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if (is_hdr(v[j])) {
+          if (p0 + j < (int)cl) hdr = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(v[j]);
+          continue;
+        }
+        if ((uint32_t)v[j] >= T) continue;
+        atomicAdd(&freq[v[j]], kWeighted ? weight[(uint32_t)hdr] : 1ull);
+      }
+      c_hdr = hdr_tot > c_hdr ? hdr_tot : c_hdr;
+    }
+  }
+}
+
+__global__ void k_sum_len(const uint32_t* tile_len, uint32_t n, u64* out) {
+  u64 s = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) s += tile_len[i];
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_down(s, d, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+}
+
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+inline u64* U(uint64_t* p) { return reinterpret_cast<u64*>(p); }
+
+template <class T>
+T* dalloc(size_t n, size_t* acc) {
+  void* p = nullptr;
+  if (n == 0) n = 1;
+  HIP_OK(hipMalloc(&p, n * sizeof(T)));
+  *acc += n * sizeof(T);
+  return (T*)p;
+}
+
+}  // namespace
+
+// ==========================================================================================
+bool Device::available(std::string* why) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) {
+    if (why) *why = e != hipSuccess ? std::string("hipGetDeviceCount: ") + hipGetErrorString(e) : "no HIP device";
+    return false;
+  }
+  return true;
+}
+
+Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
+  HIP_OK(hipSetDevice(ordinal_));
+  hipStream_t s;
+  HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  stream_ = s;
+  for (auto& e : ev_) {
+    hipEvent_t ev;
+    HIP_OK(hipEventCreate(&ev));
+    e = ev;
+  }
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, ordinal_));
+  cu_count_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  HIP_OK(hipHostMalloc((void**)&host_count_, 64, hipHostMallocMapped));
+  std::memset(host_count_, 0, 64);
+}
+
+void Device::free_all() {
+  void* ptrs[] = {tok_, tok0_, tile_off_, tile_len_, tile_len0_, weight_, dsum_, dft_, dlist_, dcount_};
+  for (void* p : ptrs)
+    if (p) HIP_OK(hipFree(p));
+  tok_ = tok0_ = nullptr;
+  tile_off_ = nullptr;
+  tile_len_ = tile_len0_ = nullptr;
+  weight_ = nullptr;
+  dsum_ = dft_ = nullptr;
+  dlist_ = dcount_ = nullptr;
+  if (host_recs_) HIP_OK(hipHostFree(host_recs_));
+  host_recs_ = nullptr;
+  host_recs_cap_ = 0;
+  slot_cap_ = 0;
+  ntiles_ = 0;
+  bytes_alloc_ = 0;
+  uploaded_ = false;
+}
+
+Device::~Device() {
+  (void)hipSetDevice(ordinal_);
+  (void)hipStreamSynchronize(S(stream_));
+  free_all();
+  if (host_count_) (void)hipHostFree(host_count_);
+  for (auto e : ev_)
+    if (e) (void)hipEventDestroy((hipEvent_t)e);
+  if (stream_) (void)hipStreamDestroy(S(stream_));
+}
+
+void Device::upload(const WordTable& wt, Layout layout, size_t begin, size_t end) {
+  HIP_OK(hipSetDevice(ordinal_));
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  free_all();
+  layout_ = layout;
+  const bool stream = layout == Layout::kStream;
+  const size_t nent = stream ? wt.occurrence_rank.size() : wt.num_words();
+  if (stream && nent == 0 && wt.total_occurrences > 0) fatal("stream layout requested without occurrence ranks");
+  end = std::min(end, nent);
+  begin = std::min(begin, end);
+  auto rank_of = [&](size_t e) -> uint32_t { return stream ? wt.occurrence_rank[e] : (uint32_t)e; };
+  auto len_of = [&](uint32_t r) -> uint64_t { return wt.offset[r + 1] - wt.offset[r]; };
+
+  // Tile boundaries: whole words, <= kChunk tokens unless one word alone is longer.
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> lens;
+  std::vector<size_t> first_entry;
+  uint64_t pos = 0, fill = 0;
+  for (size_t e = begin; e < end; ++e) {
+    const uint64_t need = len_of(rank_of(e)) + 1;
+    if (need >= (1ull << 31)) fatal("word longer than 2^31 tokens");
+    if (fill > 0 && fill + need > (uint64_t)kChunk) {
+      lens.push_back((uint32_t)fill);
+      pos += (fill + 3) & ~3ull;
+      fill = 0;
+    }
+    if (fill == 0) {
+      off.push_back(pos);
+      first_entry.push_back(e);
+    }
+    fill += need;
+  }
+  if (fill > 0) {
+    lens.push_back((uint32_t)fill);
+    pos += (fill + 3) & ~3ull;
+  }
+  ntiles_ = lens.size();
+  tok_elems_ = pos;
+  first_entry.push_back(end);
+
+  std::vector<int32_t> host(pos + 4, kPad);
+  for (size_t t = 0; t < ntiles_; ++t) {
+    int32_t* dst = host.data() + off[t];
+    for (size_t e = first_entry[t]; e < first_entry[t + 1]; ++e) {
+      const uint32_t r = rank_of(e);
+      *dst++ = (int32_t)((uint32_t)kHeaderBase + r);
+      const uint64_t o = wt.offset[r], l = len_of(r);
+      std::memcpy(dst, wt.symbols.data() + o, l * sizeof(int32_t));
+      dst += l;
+    }
+  }
+  live_tokens0_ = 0;
+  for (uint32_t l : lens) live_tokens0_ += l;
+  nentries_ = end - begin;
+  live_tokens_est_ = live_tokens0_;
+
+  tok_ = dalloc<int32_t>(pos + 4, &bytes_alloc_);
+  tok0_ = dalloc<int32_t>(pos + 4, &bytes_alloc_);
+  tile_off_ = dalloc<uint64_t>(ntiles_, &bytes_alloc_);
+  tile_len_ = dalloc<uint32_t>(ntiles_, &bytes_alloc_);
+  tile_len0_ = dalloc<uint32_t>(ntiles_, &bytes_alloc_);
+  HIP_OK(hipMemcpyAsync(tok0_, host.data(), (pos + 4) * sizeof(int32_t), hipMemcpyHostToDevice, S(stream_)));
+  if (ntiles_) {
+    HIP_OK(hipMemcpyAsync(tile_off_, off.data(), ntiles_ * sizeof(uint64_t), hipMemcpyHostToDevice, S(stream_)));
+    HIP_OK(hipMemcpyAsync(tile_len0_, lens.data(), ntiles_ * sizeof(uint32_t), hipMemcpyHostToDevice, S(stream_)));
+  }
+  if (!stream) {
+    weight_ = dalloc<uint64_t>(wt.num_words(), &bytes_alloc_);
+    if (wt.num_words())
+      HIP_OK(hipMemcpyAsync(weight_, wt.count.data(), wt.num_words() * sizeof(uint64_t), hipMemcpyHostToDevice, S(stream_)));
+  }
+  HIP_OK(hipStreamSynchronize(S(stream_)));  // host staging buffers go out of scope
+  max_id_seen_ = 0;
+  for (int c = 0; c < 256; ++c)
+    if (wt.keep[c]) max_id_seen_ = c;
+  uploaded_ = true;
+  reset_tokens();
+}
+
+void Device::reset_tokens() {
+  HIP_OK(hipSetDevice(ordinal_));
+  if (!uploaded_) return;
+  HIP_OK(hipMemcpyAsync(tok_, tok0_, (tok_elems_ + 4) * sizeof(int32_t), hipMemcpyDeviceToDevice, S(stream_)));
+  if (ntiles_)
+    HIP_OK(hipMemcpyAsync(tile_len_, tile_len0_, ntiles_ * sizeof(uint32_t), hipMemcpyDeviceToDevice, S(stream_)));
+  live_tokens_est_ = live_tokens0_;
+}
+
+uint64_t Device::live_tokens() {
+  HIP_OK(hipSetDevice(ordinal_));
+  if (!ntiles_) return 0;
+  u64* d = dalloc<u64>(1, &bytes_alloc_);
+  HIP_OK(hipMemsetAsync(d, 0, sizeof(u64), S(stream_)));
+  k_sum_len<<<64, 256, 0, S(stream_)>>>(tile_len_, (uint32_t)ntiles_, d);
+  u64 h = 0;
+  HIP_OK(hipMemcpyAsync(&h, d, sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  HIP_OK(hipFree(d));
+  bytes_alloc_ -= sizeof(u64);
+  return h;
+}
+
+void Device::ensure_slots(uint32_t need) {
+  if (need <= slot_cap_ && dsum_) return;
+  uint32_t cap = std::max<uint32_t>(slot_cap_ ? slot_cap_ : 1024, 1024);
+  while (cap < need) cap *= 2;
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  if (dsum_) {
+    HIP_OK(hipFree(dsum_));
+    HIP_OK(hipFree(dft_));
+    HIP_OK(hipFree(dlist_));
+    HIP_OK(hipFree(dcount_));
+    HIP_OK(hipHostFree(host_recs_));
+  }
+  const size_t keys = 4 * ((size_t)cap + 1);
+  dsum_ = dalloc<uint64_t>(keys + 2, &bytes_alloc_);  // + 2 stats words at the end
+  dft_ = dalloc<uint64_t>(keys, &bytes_alloc_);
+  dlist_ = dalloc<uint32_t>(keys, &bytes_alloc_);
+  dcount_ = dalloc<uint32_t>(2, &bytes_alloc_);
+  HIP_OK(hipMemsetAsync(dsum_, 0, (keys + 2) * sizeof(u64), S(stream_)));
+  HIP_OK(hipMemsetAsync(dft_, 0xFF, keys * sizeof(u64), S(stream_)));
+  HIP_OK(hipMemsetAsync(dcount_, 0, 2 * sizeof(uint32_t), S(stream_)));
+  HIP_OK(hipHostMalloc((void**)&host_recs_, keys * sizeof(DeltaRecord), hipHostMallocMapped));
+  host_recs_cap_ = keys;
+  slot_cap_ = cap;
+  parity_ = 0;
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+}
+
+void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
+  HIP_OK(hipSetDevice(ordinal_));
+  out->clear();
+  if (!ntiles_) return;
+  // distinct pairs <= live tokens and <= (ids in play)^2
+  const uint64_t live = live_tokens();
+  const uint64_t ids = (uint64_t)std::max<int32_t>(max_id_seen_, kBaseVocab) + 2;
+  uint64_t bound = std::min<uint64_t>(live, ids * ids);
+  uint64_t cap = 1024;
+  while (cap < 2 * bound && cap < (1ull << 27)) cap *= 2;
+  size_t acc = 0;
+  u64* tkey = dalloc<u64>(cap, &acc);
+  u64* tcnt = dalloc<u64>(cap, &acc);
+  u64* tft = dalloc<u64>(cap, &acc);
+  uint32_t* flags = dalloc<uint32_t>(2, &acc);
+  HIP_OK(hipMemsetAsync(tkey, 0xFF, cap * sizeof(u64), S(stream_)));
+  HIP_OK(hipMemsetAsync(tcnt, 0, cap * sizeof(u64), S(stream_)));
+  HIP_OK(hipMemsetAsync(tft, 0xFF, cap * sizeof(u64), S(stream_)));
+  HIP_OK(hipMemsetAsync(flags, 0, 2 * sizeof(uint32_t), S(stream_)));
+  CountParams cp{tok_, tile_off_, tile_len_, (uint32_t)ntiles_, weight_, unk_id, tkey, tcnt, tft, cap - 1, flags};
+  const int grid = (int)std::min<size_t>(ntiles_, (size_t)cu_count_ * 2);
+  if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[2], S(stream_)));
+  if (layout_ == Layout::kStream) k_pair_count<false><<<grid, kThreads, 0, S(stream_)>>>(cp);
+  else k_pair_count<true><<<grid, kThreads, 0, S(stream_)>>>(cp);
+  HIP_OK(hipGetLastError());
+  if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[3], S(stream_)));
+  const uint32_t out_cap = (uint32_t)std::min<uint64_t>(cap, bound + 1);
+  PairCount* dout = dalloc<PairCount>(out_cap, &acc);
+  k_pair_collect<<<512, kThreads, 0, S(stream_)>>>(tkey, tcnt, tft, cap, dout, out_cap, flags);
+  HIP_OK(hipGetLastError());
+  uint32_t hflags[2];
+  HIP_OK(hipMemcpyAsync(hflags, flags, sizeof(hflags), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  if (hflags[0]) fatal("pair table overflow in k_pair_count / k_pair_collect");
+  out->resize(hflags[1]);
+  if (hflags[1])
+    HIP_OK(hipMemcpy(out->data(), dout, hflags[1] * sizeof(PairCount), hipMemcpyDeviceToHost));
+  if (timing_) {
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[2], (hipEvent_t)ev_[3]));
+    times_.count_ms += ms;
+    times_.count_launches += 1;
+    // tokens + headers read once, plus the per-word weight in the types layout
+    // 4 B per token and per word header (the boundary), 8 B weight per word in the types
+    // layout, 12 B of tile descriptor per tile
+    times_.count_bytes += 4.0 * (double)live + 12.0 * (double)ntiles_ +
+                          (layout_ == Layout::kTypes ? 8.0 * (double)nentries_ : 0.0);
+  }
+  for (void* p : {(void*)tkey, (void*)tcnt, (void*)tft, (void*)flags, (void*)dout}) HIP_OK(hipFree(p));
+}
+
+void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
+  HIP_OK(hipSetDevice(ordinal_));
+  max_id_seen_ = std::max(max_id_seen_, X);
+  ensure_slots((uint32_t)X + 1);
+  if (!ntiles_) return;
+  MergeParams mp{tok_, tile_off_, tile_len_, (uint32_t)ntiles_, weight_, a, b, X, slot_cap_,
+                 U(dsum_), U(dft_), dlist_, dcount_ + parity_, U(dsum_) + 4 * ((size_t)slot_cap_ + 1)};
+  const int grid = (int)std::min<size_t>(ntiles_, (size_t)cu_count_ * 3);
+  if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[0], S(stream_)));
+  if (layout_ == Layout::kStream) k_merge<false><<<grid, kThreads, 0, S(stream_)>>>(mp);
+  else k_merge<true><<<grid, kThreads, 0, S(stream_)>>>(mp);
+  HIP_OK(hipGetLastError());
+  if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[1], S(stream_)));
+}
+
+size_t Device::collect(int32_t X, const DeltaRecord** recs) {
+  HIP_OK(hipSetDevice(ordinal_));
+  (void)X;
+  if (!ntiles_ && !dsum_) {
+    *recs = nullptr;
+    return 0;
+  }
+  u64* stats = U(dsum_) + 4 * ((size_t)slot_cap_ + 1);
+  DeltaRecord* drec = nullptr;
+  uint32_t* dcnt = nullptr;
+  u64* dstats = nullptr;
+  HIP_OK(hipHostGetDevicePointer((void**)&drec, host_recs_, 0));
+  HIP_OK(hipHostGetDevicePointer((void**)&dcnt, host_count_, 0));
+  dstats = (u64*)((char*)dcnt + 16);
+  if (exchange_) {
+    const size_t nkeys = 4 * ((size_t)slot_cap_ + 1);
+    exchange_(exchange_ctx_, dsum_, dft_, nkeys, stream_);
+    HIP_OK(hipMemsetAsync(dcount_, 0, 2 * sizeof(uint32_t), S(stream_)));
+    k_collect_dense<<<256, kThreads, 0, S(stream_)>>>((uint32_t)nkeys, U(dsum_), U(dft_), drec, dcount_);
+    HIP_OK(hipMemcpyAsync(host_count_, dcount_, sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
+    HIP_OK(hipMemsetAsync(dcount_, 0, 2 * sizeof(uint32_t), S(stream_)));
+    HIP_OK(hipMemcpyAsync((u64*)(host_count_ + 4), stats, 2 * sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
+    HIP_OK(hipMemsetAsync(stats, 0, 2 * sizeof(u64), S(stream_)));
+  } else {
+    k_collect<<<64, kThreads, 0, S(stream_)>>>(dcount_ + parity_, dcount_ + (parity_ ^ 1), dlist_, U(dsum_), U(dft_), drec,
+                                               dcnt, stats, dstats);
+    HIP_OK(hipMemsetAsync(stats, 0, 2 * sizeof(u64), S(stream_)));
+  }
+  HIP_OK(hipGetLastError());
+  parity_ ^= 1;
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  const u64* hs = (const u64*)(host_count_ + 4);
+  if (timing_) {
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]));
+    times_.merge_ms += ms;
+    times_.merge_launches += 1;
+    times_.merge_bytes += 4.0 * (double)live_tokens_est_ + 4.0 * (double)hs[1] + 12.0 * (double)ntiles_;
+  }
+  live_tokens_est_ -= hs[0];
+  *recs = host_recs_;
+  return host_count_[0];
+}
+
+void Device::token_freq(size_t T, std::vector<uint64_t>* freq) {
+  HIP_OK(hipSetDevice(ordinal_));
+  freq->assign(T, 0);
+  if (!ntiles_ || !T) return;
+  size_t acc = 0;
+  u64* d = dalloc<u64>(T, &acc);
+  HIP_OK(hipMemsetAsync(d, 0, T * sizeof(u64), S(stream_)));
+  const int grid = (int)std::min<size_t>(ntiles_, (size_t)cu_count_ * 4);
+  if (layout_ == Layout::kStream)
+    k_token_freq<false><<<grid, kThreads, 0, S(stream_)>>>(tok_, tile_off_, tile_len_, (uint32_t)ntiles_, weight_, (uint32_t)T, d);
+  else
+    k_token_freq<true><<<grid, kThreads, 0, S(stream_)>>>(tok_, tile_off_, tile_len_, (uint32_t)ntiles_, weight_, (uint32_t)T, d);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(freq->data(), d, T * sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  HIP_OK(hipFree(d));
+}
+
+void Device::download_tokens(std::vector<int32_t>* out) {
+  HIP_OK(hipSetDevice(ordinal_));
+  out->clear();
+  if (!ntiles_) return;
+  std::vector<int32_t> all(tok_elems_ + 4);
+  std::vector<uint64_t> off(ntiles_);
+  std::vector<uint32_t> lens(ntiles_);
+  HIP_OK(hipMemcpyAsync(all.data(), tok_, all.size() * sizeof(int32_t), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipMemcpyAsync(off.data(), tile_off_, ntiles_ * sizeof(uint64_t), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipMemcpyAsync(lens.data(), tile_len_, ntiles_ * sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  for (size_t t = 0; t < ntiles_; ++t) out->insert(out->end(), all.begin() + off[t], all.begin() + off[t] + lens[t]);
+}
+
+}  // namespace shred

@@ -1,0 +1,328 @@
+// Corpus loading: see corpus.h for the normative rules and reference citations.
+#include "corpus.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cstring>
+#include <thread>
+
+#include "common.h"
+
+namespace shred {
+namespace {
+
+inline bool is_delim(uint8_t c) { return c == '\t' || c == '\r' || c == '\n' || c == ' '; }
+
+struct Range { uint64_t begin, end; };
+
+// fgets(buf, size) on the file from `pos`: reads until size-1 bytes or a '\n' is stored.
+inline uint64_t fgets_end(const uint8_t* d, uint64_t n, uint64_t pos, uint64_t size) {
+  uint64_t lim = std::min<uint64_t>(n, pos + size - 1);
+  const void* nl = std::memchr(d + pos, '\n', lim - pos);
+  return nl ? (uint64_t)((const uint8_t*)nl - d) + 1 : lim;
+}
+
+// The byte ranges the reference's strtok actually sees (bpe.cpp:131-153).  Without NUL bytes
+// every line is read whole, so the visible text is the whole file.
+std::vector<Range> visible_ranges(const uint8_t* d, uint64_t n) {
+  std::vector<Range> out;
+  if (n == 0) return out;
+  if (!std::memchr(d, 0, n)) { out.push_back({0, n}); return out; }
+  uint64_t pos = 0, cap = 4096;  // INITIAL_STR_BUFFER; the buffer never shrinks (bpe.cpp:133-140)
+  while (pos < n) {
+    uint64_t start = pos;
+    pos = fgets_end(d, n, pos, cap);
+    auto strlen_from = [&](uint64_t end) {
+      const void* z = std::memchr(d + start, 0, end - start);
+      return z ? (uint64_t)((const uint8_t*)z - (d + start)) : end - start;
+    };
+    uint64_t len = strlen_from(pos);
+    while (len == cap - 1 && d[start + len - 1] != '\n') {
+      cap *= 2;
+      if (pos >= n) break;                   // fgets returns NULL at EOF
+      pos = fgets_end(d, n, pos, cap - len);  // appends at line + len == start + len == pos
+      len = strlen_from(pos);
+    }
+    if (len) out.push_back({start, start + len});
+  }
+  return out;
+}
+
+// Cuts the visible ranges into pieces of about `target` bytes, only at delimiters.
+std::vector<Range> split_pieces(const uint8_t* d, const std::vector<Range>& rs, uint64_t target) {
+  std::vector<Range> out;
+  for (const Range& r : rs) {
+    uint64_t s = r.begin;
+    while (s < r.end) {
+      uint64_t e = std::min(r.end, s + target);
+      while (e < r.end && !is_delim(d[e])) ++e;
+      out.push_back({s, e});
+      s = e;
+    }
+  }
+  return out;
+}
+
+inline uint64_t word_hash(const uint8_t* p, uint32_t len) {
+  uint64_t h = 0x84222325CBF29CE4ull ^ len;
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t w;
+    std::memcpy(&w, p + i, 8);
+    h = (h ^ w) * 0x100000001B3ull;
+    h ^= h >> 29;
+  }
+  for (; i < len; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
+  h ^= h >> 32;
+  h *= 0xD6E8FEB86659FD93ull;
+  h ^= h >> 32;
+  return h;
+}
+
+struct Entry {
+  uint64_t hash;
+  uint64_t first;  // file offset of the first occurrence (also where the spelling lives)
+  uint64_t count;
+  uint32_t len;
+};
+
+constexpr int kPartBits = 6;
+constexpr int kParts = 1 << kPartBits;
+
+// Open-addressing word counter (one per thread and hash partition).
+struct Counter {
+  std::vector<Entry> ents;
+  std::vector<uint32_t> slots;  // index + 1, 0 = empty
+  uint64_t mask = 0;
+
+  void grow() {
+    uint64_t ns = slots.empty() ? 1024 : 2 * slots.size();
+    std::vector<uint32_t> s(ns, 0);
+    for (uint32_t i = 0; i < ents.size(); ++i) {
+      uint64_t j = ents[i].hash & (ns - 1);
+      while (s[j]) j = (j + 1) & (ns - 1);
+      s[j] = i + 1;
+    }
+    slots.swap(s);
+    mask = ns - 1;
+  }
+  // Adds `cnt` occurrences of the word at d[off, off+len) first seen at `first`.
+  void add(const uint8_t* d, uint64_t hash, uint64_t off, uint32_t len, uint64_t cnt, uint64_t first) {
+    if (2 * (ents.size() + 1) > slots.size()) grow();
+    uint64_t j = hash & mask;
+    for (;;) {
+      uint32_t s = slots[j];
+      if (!s) break;
+      Entry& e = ents[s - 1];
+      if (e.hash == hash && e.len == len && std::memcmp(d + e.first, d + off, len) == 0) {
+        e.count += cnt;
+        if (first < e.first) e.first = first;  // spelling is identical, keep the earliest
+        return;
+      }
+      j = (j + 1) & mask;
+    }
+    ents.push_back({hash, first, cnt, len});
+    slots[j] = (uint32_t)ents.size();
+  }
+  const Entry* find(const uint8_t* d, uint64_t hash, uint64_t off, uint32_t len) const {
+    uint64_t j = hash & mask;
+    for (;;) {
+      uint32_t s = slots[j];
+      if (!s) return nullptr;
+      const Entry& e = ents[s - 1];
+      if (e.hash == hash && e.len == len && std::memcmp(d + e.first, d + off, len) == 0) return &e;
+      j = (j + 1) & mask;
+    }
+  }
+};
+
+template <class F>
+void parallel_for(int threads, size_t n, F&& f) {
+  if (threads <= 1 || n <= 1) {
+    for (size_t i = 0; i < n; ++i) f(i, 0);
+    return;
+  }
+  std::vector<std::thread> pool;
+  std::atomic<size_t> next{0};
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) f(i, t);
+    });
+  for (auto& th : pool) th.join();
+}
+
+template <class F>
+void scan_words(const uint8_t* d, Range r, F&& f) {
+  uint64_t i = r.begin;
+  while (i < r.end) {
+    while (i < r.end && is_delim(d[i])) ++i;
+    uint64_t s = i;
+    while (i < r.end && !is_delim(d[i])) ++i;
+    if (i > s) f(s, (uint32_t)(i - s));
+  }
+}
+
+}  // namespace
+
+void load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordTable* out) {
+  int threads = opt.threads > 0 ? opt.threads : (int)std::thread::hardware_concurrency();
+  threads = std::max(1, std::min(threads, 32));
+  std::vector<Range> vis = visible_ranges(d, n);
+  uint64_t vis_bytes = 0;
+  for (auto& r : vis) vis_bytes += r.end - r.begin;
+  uint64_t target = std::max<uint64_t>(1 << 20, vis_bytes / (uint64_t)(threads * 8) + 1);
+  std::vector<Range> pieces = split_pieces(d, vis, target);
+
+  // Pass 1: thread-local counting, partitioned by hash.
+  std::vector<std::vector<Counter>> local(threads, std::vector<Counter>(kParts));
+  std::vector<uint64_t> piece_words(pieces.size(), 0);
+  parallel_for(threads, pieces.size(), [&](size_t p, int t) {
+    auto& parts = local[t];
+    uint64_t nw = 0;
+    scan_words(d, pieces[p], [&](uint64_t off, uint32_t len) {
+      uint64_t h = word_hash(d + off, len);
+      parts[h >> (64 - kPartBits)].add(d, h, off, len, 1, off);
+      ++nw;
+    });
+    piece_words[p] = nw;
+  });
+
+  // Merge per partition.
+  std::vector<Counter> merged(kParts);
+  parallel_for(threads, kParts, [&](size_t part, int) {
+    Counter& m = merged[part];
+    for (int t = 0; t < threads; ++t)
+      for (const Entry& e : local[t][part].ents) m.add(d, e.hash, e.first, e.len, e.count, e.first);
+  });
+  local.clear();
+  local.shrink_to_fit();
+
+  // Reference word order: (djb2 & 4095, first occurrence).
+  struct Key { uint64_t order; uint32_t part, idx; };
+  std::vector<size_t> part_base(kParts + 1, 0);
+  for (int p = 0; p < kParts; ++p) part_base[p + 1] = part_base[p] + merged[p].ents.size();
+  const size_t W = part_base[kParts];
+  if (W > (size_t)kMaxRank) fatal("corpus has more than 2^30 distinct words");
+  std::vector<Key> keys(W);
+  parallel_for(threads, kParts, [&](size_t p, int) {
+    for (uint32_t i = 0; i < merged[p].ents.size(); ++i) {
+      const Entry& e = merged[p].ents[i];
+      uint64_t h = 5381;
+      for (uint32_t k = 0; k < e.len; ++k) h = h * 33 + d[e.first + k];
+      if (e.first >= (1ull << 52)) fatal("corpus larger than 2^52 bytes");
+      keys[part_base[p] + i] = {((h & 4095) << 52) | e.first, (uint32_t)p, i};
+    }
+  });
+  std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) { return a.order < b.order; });
+
+  WordTable& wt = *out;
+  wt = WordTable();
+  wt.offset.resize(W + 1);
+  wt.count.resize(W);
+  uint64_t S = 0;
+  for (size_t r = 0; r < W; ++r) {
+    const Entry& e = merged[keys[r].part].ents[keys[r].idx];
+    wt.offset[r] = S;
+    wt.count[r] = e.count;
+    S += e.len;
+  }
+  wt.offset[W] = S;
+  wt.bytes.resize(S);
+  parallel_for(threads, (W + 4095) / 4096, [&](size_t blk, int) {
+    size_t r1 = std::min(W, (blk + 1) * 4096);
+    for (size_t r = blk * 4096; r < r1; ++r) {
+      const Entry& e = merged[keys[r].part].ents[keys[r].idx];
+      std::memcpy(wt.bytes.data() + wt.offset[r], d + e.first, e.len);
+    }
+  });
+  uint64_t occ = 0;
+  for (uint64_t c : wt.count) occ += c;
+  wt.total_occurrences = occ;
+
+  // Coverage (bpe.cpp:156-172): unweighted histogram over distinct words.
+  std::vector<std::array<uint64_t, 256>> hist(threads);
+  for (auto& h : hist) h.fill(0);
+  const size_t chunk = 1 << 20;
+  parallel_for(threads, (S + chunk - 1) / chunk, [&](size_t c, int t) {
+    size_t e = std::min<size_t>(S, (c + 1) * chunk);
+    for (size_t i = c * chunk; i < e; ++i) hist[t][wt.bytes[i]]++;
+  });
+  uint64_t cnt[256] = {};
+  for (auto& h : hist)
+    for (int c = 0; c < 256; ++c) cnt[c] += h[c];
+  std::vector<std::pair<int, uint64_t>> cand;
+  for (int bk = 0; bk < 256; ++bk) {
+    int c = (bk - 165) & 255;  // StrMap(256) bucket of the 1-byte key c is (5381*33 + c) & 255
+    if (cnt[c]) cand.push_back({c, cnt[c]});
+  }
+  std::stable_sort(cand.begin(), cand.end(),
+                   [](const std::pair<int, uint64_t>& a, const std::pair<int, uint64_t>& b) { return a.second > b.second; });
+  wt.distinct_bytes = cand.size();
+  wt.kept_bytes = (size_t)((float)cand.size() * opt.coverage);
+  for (size_t i = 0; i < wt.kept_bytes && i < cand.size(); ++i) wt.keep[cand[i].first] = true;
+
+  int32_t map[256];
+  for (int c = 0; c < 256; ++c) map[c] = wt.keep[c] ? c : opt.unk_id;
+  wt.symbols.resize(S);
+  parallel_for(threads, (S + chunk - 1) / chunk, [&](size_t c, int) {
+    size_t e = std::min<size_t>(S, (c + 1) * chunk);
+    for (size_t i = c * chunk; i < e; ++i) wt.symbols[i] = map[wt.bytes[i]];
+  });
+
+  if (opt.want_stream) {
+    // rank of every distinct word, addressable through the merged counters
+    std::vector<std::vector<uint32_t>> rank_of(kParts);
+    for (int p = 0; p < kParts; ++p) rank_of[p].resize(merged[p].ents.size());
+    for (size_t r = 0; r < W; ++r) rank_of[keys[r].part][keys[r].idx] = (uint32_t)r;
+    std::vector<uint64_t> base(pieces.size() + 1, 0);
+    for (size_t p = 0; p < pieces.size(); ++p) base[p + 1] = base[p] + piece_words[p];
+    wt.occurrence_rank.resize(base[pieces.size()]);
+    parallel_for(threads, pieces.size(), [&](size_t p, int) {
+      uint64_t k = base[p];
+      scan_words(d, pieces[p], [&](uint64_t off, uint32_t len) {
+        uint64_t h = word_hash(d + off, len);
+        int part = (int)(h >> (64 - kPartBits));
+        const Entry* e = merged[part].find(d, h, off, len);
+        wt.occurrence_rank[k++] = rank_of[part][(uint32_t)(e - merged[part].ents.data())];
+      });
+    });
+  }
+}
+
+int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::string* err) {
+  int fd = ::open(path, O_RDONLY);
+  if (fd < 0) {
+    if (err) *err = std::string("Couldn't open file: ") + path;
+    return -1;
+  }
+  struct stat st;
+  if (::fstat(fd, &st) != 0) {
+    ::close(fd);
+    if (err) *err = std::string("Couldn't stat file: ") + path;
+    return -1;
+  }
+  size_t n = (size_t)st.st_size;
+  if (n == 0) {
+    ::close(fd);
+    load_corpus_bytes(nullptr, 0, opt, out);
+    return 0;
+  }
+  void* m = ::mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+  ::close(fd);
+  if (m == MAP_FAILED) {
+    if (err) *err = std::string("Couldn't map file: ") + path;
+    return -1;
+  }
+  ::madvise(m, n, MADV_SEQUENTIAL);
+  load_corpus_bytes((const uint8_t*)m, n, opt, out);
+  ::munmap(m, n);
+  return 0;
+}
+
+}  // namespace shred

@@ -1,0 +1,52 @@
+// Corpus loading for the BPE path: raw text -> reference-ordered table of distinct words.
+//
+// Semantics follow the reference bpe_load_corpus (shredword/csrc/bpe/bpe.cpp:110-185) exactly
+// (SURVEY.md Appendix A.1-A.2):
+//  * the file is read with fgets into a buffer that starts at 4096 bytes and doubles, and each
+//    buffer is cut at its first NUL (strlen) before strtok on "\t\r\n " (bpe.cpp:131-153);
+//  * distinct words are ordered by (djb2(word) & 4095, first occurrence) — the iteration order
+//    of the reference's fixed 4096-bucket StrMap (hash.cpp:29-72);
+//  * the byte histogram counts each distinct word's bytes once (histogram.cpp:30-36), candidates
+//    are taken in StrMap(256) order ((c + 165) & 255), stable-sorted by count descending, and the
+//    first (size_t)((float)n * coverage) bytes are kept; other bytes map to unk_id.
+// The implementation is parallel (thread-local hash maps merged by hash partition); the result
+// does not depend on the thread count.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace shred {
+
+struct WordTable {
+  // Distinct words in reference word order ("rank" order).
+  std::vector<uint8_t> bytes;    // concatenated spellings
+  std::vector<uint64_t> offset;  // size W+1: word w occupies bytes/symbols [offset[w], offset[w+1])
+  std::vector<uint64_t> count;   // occurrences of each word
+  std::vector<int32_t> symbols;  // initial symbol ids (byte value or unk_id), same offsets as bytes
+  uint64_t total_occurrences = 0;
+  size_t distinct_bytes = 0;     // `c` of bpe.cpp:165
+  size_t kept_bytes = 0;         // `keep` of bpe.cpp:169
+  bool keep[256] = {};
+  // Stream layout (optional): the type rank of every word occurrence, in corpus order.
+  std::vector<uint32_t> occurrence_rank;
+
+  size_t num_words() const { return count.size(); }
+  size_t num_symbols() const { return symbols.size(); }
+};
+
+struct LoadOptions {
+  int32_t unk_id = 0;
+  float coverage = 0.995f;
+  bool want_stream = false;  // also fill occurrence_rank
+  int threads = 0;           // 0: hardware concurrency (capped at 32)
+};
+
+// Returns 0 on success, -1 if the file cannot be opened/mapped (message in *err).
+int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::string* err);
+
+// Builds a WordTable from in-memory text (same rules); used by tests and tools.
+void load_corpus_bytes(const uint8_t* data, size_t n, const LoadOptions& opt, WordTable* out);
+
+}  // namespace shred

@@ -1,0 +1,122 @@
+// HBM-resident state and kernel launches of the BPE merge loop on one MI355X (gfx950).
+//
+// Layout in HBM (see DESIGN.md "Data layout"):
+//   tok       int32 token stream, cut into tiles of whole words (<= 4096 tokens, or one word
+//             that is longer); every word is preceded by an in-band header INT32_MIN + rank.
+//   tile_off  u64 element offset of each tile (16-byte aligned), tile_len u32 live length.
+//   weight    u64 occurrence count per word rank ("types" layout; the "stream" layout keeps
+//             every occurrence with weight 1 and needs no weight array).
+//   dsum/dft  u64 per (neighbour slot, category): summed weight and min first-touch of the
+//             current merge's neighbour-pair deltas; dlist/dcount: the touched keys.
+// No HIP type appears here so host C++ can include it; bpe_device.hip implements it.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "corpus.h"
+#include "selector.h"
+
+namespace shred {
+
+enum class Layout { kTypes = 0, kStream = 1 };
+
+struct KernelTimes {
+  double merge_ms = 0;   // Σ k_merge durations (HIP events on the trainer stream)
+  double compact_ms = 0; // Σ k_compact_deltas durations
+  double count_ms = 0;   // Σ k_pair_count durations
+  uint64_t merge_launches = 0;
+  uint64_t count_launches = 0;
+  double merge_bytes = 0;  // Σ algorithmic bytes of k_merge launches (4 B per live token read)
+  double count_bytes = 0;  // Σ algorithmic bytes of k_pair_count (tokens + boundaries + weights)
+};
+
+class Device {
+ public:
+  // True when a HIP device is usable; otherwise *why says what is missing.
+  static bool available(std::string* why);
+
+  explicit Device(int device_ordinal);
+  ~Device();
+  Device(const Device&) = delete;
+  Device& operator=(const Device&) = delete;
+
+  // Packs the word table into tiles and uploads it (types: one entry per distinct word;
+  // stream: one entry per occurrence).  Keeps a pristine copy for reset_tokens().
+  void upload(const WordTable& wt, Layout layout, size_t rank_begin = 0, size_t rank_end = SIZE_MAX);
+  // Restores the token stream to its uploaded (unmerged) state.
+  void reset_tokens();
+  bool has_tokens() const { return ntiles_ > 0 || uploaded_; }
+
+  // K1: weighted pair histogram with first touch, pairs holding unk skipped (bpe.cpp:187-206).
+  void count_pairs(int32_t unk_id, std::vector<PairCount>* out);
+
+  // K2+K3 for merge (a,b)->X: rewrites every occurrence in place and reduces neighbour deltas
+  // into the slot tables (left there for exchange()).
+  void merge_scan(int32_t a, int32_t b, int32_t X);
+  // Multi-GPU hook: called between merge_scan and collect(); slot tables are
+  // [prefix_slots * 4] u64 sums followed by the same count of u64 first-touch values.
+  using ExchangeFn = void (*)(void* ctx, uint64_t* dsum, uint64_t* dft, size_t n, void* stream);
+  void set_exchange(ExchangeFn fn, void* ctx) { exchange_ = fn; exchange_ctx_ = ctx; }
+  // K4: compacts the touched slots into records (host-visible) and clears them.
+  size_t collect(int32_t X, const DeltaRecord** recs);
+
+  // K6: final weighted token histogram over ids [0, T); other ids are dropped.
+  void token_freq(size_t T, std::vector<uint64_t>* freq);
+  // Copies the live token stream back (tests): per entry, header then tokens.
+  void download_tokens(std::vector<int32_t>* out);
+
+  void set_timing(bool on) { timing_ = on; }
+  const KernelTimes& times() const { return times_; }
+  void clear_times() { times_ = KernelTimes(); }
+  uint64_t live_tokens();  // Σ tile_len (headers included)
+  size_t num_tiles() const { return ntiles_; }
+  size_t device_bytes() const { return bytes_alloc_; }
+  int ordinal() const { return ordinal_; }
+  void* stream_handle() const { return stream_; }
+
+ private:
+  void ensure_slots(uint32_t need);
+  void free_all();
+
+  int ordinal_ = 0;
+  void* stream_ = nullptr;
+  void* ev_[4] = {};
+  bool timing_ = false;
+  KernelTimes times_;
+  ExchangeFn exchange_ = nullptr;
+  void* exchange_ctx_ = nullptr;
+  int cu_count_ = 256;
+  bool uploaded_ = false;
+  Layout layout_ = Layout::kTypes;
+
+  size_t ntiles_ = 0;
+  size_t tok_elems_ = 0;
+  int32_t* tok_ = nullptr;
+  int32_t* tok0_ = nullptr;
+  uint64_t* tile_off_ = nullptr;
+  uint32_t* tile_len_ = nullptr;
+  uint32_t* tile_len0_ = nullptr;
+  uint64_t* weight_ = nullptr;
+  uint64_t live_tokens0_ = 0;
+  uint64_t nentries_ = 0;
+  uint64_t live_tokens_est_ = 0;
+
+  uint32_t slot_cap_ = 0;  // neighbour slots: id+1 for ids < slot_cap_, slot 0 for unk outside
+  uint64_t* dsum_ = nullptr;
+  uint64_t* dft_ = nullptr;
+  uint32_t* dlist_ = nullptr;
+  uint32_t* dcount_ = nullptr;  // two alternating counters
+  uint32_t parity_ = 0;
+  int32_t max_id_seen_ = 0;
+
+  DeltaRecord* host_recs_ = nullptr;   // pinned, device-visible
+  uint32_t* host_count_ = nullptr;     // pinned, device-visible
+  size_t host_recs_cap_ = 0;
+
+  size_t bytes_alloc_ = 0;
+};
+
+}  // namespace shred

@@ -1,0 +1,157 @@
+// Multi-GPU plumbing over RCCL: see dist.h.
+#include "dist.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <unordered_map>
+
+#include "common.h"
+
+namespace shred {
+
+namespace {
+void nccl_ok(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) {
+    std::fprintf(stderr, "[ERROR]\t RCCL %s failed: %s\n", what, ncclGetErrorString(r));
+    std::fflush(stderr);
+    std::abort();
+  }
+}
+void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "[ERROR]\t HIP %s failed: %s\n", what, hipGetErrorString(e));
+    std::fflush(stderr);
+    std::abort();
+  }
+}
+}  // namespace
+
+DistState& dist_state() {
+  static DistState s;
+  return s;
+}
+
+int dist_unique_id(void* out, size_t cap) {
+  if (cap < sizeof(ncclUniqueId)) return -1;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  std::memcpy(out, &id, sizeof(id));
+  return (int)sizeof(id);
+}
+
+int dist_init(int rank, int world, const void* id, size_t len, int device) {
+  DistState& s = dist_state();
+  if (world <= 1) {
+    s = DistState();
+    s.device = device;
+    return 0;
+  }
+  if (len < sizeof(ncclUniqueId) || rank < 0 || rank >= world) return -1;
+  hip_ok(hipSetDevice(device), "hipSetDevice");
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclComm_t comm;
+  if (ncclCommInitRank(&comm, world, uid, rank) != ncclSuccess) return -1;
+  s.rank = rank;
+  s.world = world;
+  s.device = device;
+  s.comm = comm;
+  return 0;
+}
+
+int dist_finalize() {
+  DistState& s = dist_state();
+  if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
+  s = DistState();
+  return 0;
+}
+
+void dist_allreduce_device(uint64_t* buf, size_t n, bool min_op, void* stream) {
+  if (!dist_active() || n == 0) return;
+  nccl_ok(ncclAllReduce(buf, buf, n, ncclUint64, min_op ? ncclMin : ncclSum, (ncclComm_t)dist_state().comm,
+                        (hipStream_t)stream),
+          "ncclAllReduce");
+}
+
+void dist_allreduce_host(uint64_t* host, size_t n, bool min_op) {
+  if (!dist_active() || n == 0) return;
+  hip_ok(hipSetDevice(dist_state().device), "hipSetDevice");
+  void* d = nullptr;
+  hip_ok(hipMalloc(&d, n * sizeof(uint64_t)), "hipMalloc");
+  hip_ok(hipMemcpy(d, host, n * sizeof(uint64_t), hipMemcpyHostToDevice), "hipMemcpy");
+  dist_allreduce_device((uint64_t*)d, n, min_op, nullptr);
+  hip_ok(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+  hip_ok(hipMemcpy(host, d, n * sizeof(uint64_t), hipMemcpyDeviceToHost), "hipMemcpy");
+  hip_ok(hipFree(d), "hipFree");
+}
+
+void dist_merge_pairs(std::vector<PairCount>* pairs) {
+  if (!dist_active()) return;
+  DistState& s = dist_state();
+  uint64_t n = pairs->size();
+  uint64_t maxn = n;
+  {
+    uint64_t v = maxn;
+    // max via min of the negation
+    uint64_t neg = ~v;
+    dist_allreduce_host(&neg, 1, true);
+    maxn = ~neg;
+  }
+  const size_t rec = sizeof(PairCount);
+  const size_t bytes = (size_t)(maxn + 1) * rec;  // first record carries the count
+  std::vector<uint8_t> send(bytes, 0);
+  PairCount head{};
+  head.count = n;
+  std::memcpy(send.data(), &head, rec);
+  if (n) std::memcpy(send.data() + rec, pairs->data(), n * rec);
+  hip_ok(hipSetDevice(s.device), "hipSetDevice");
+  void *dsend = nullptr, *drecv = nullptr;
+  hip_ok(hipMalloc(&dsend, bytes), "hipMalloc");
+  hip_ok(hipMalloc(&drecv, bytes * s.world), "hipMalloc");
+  hip_ok(hipMemcpy(dsend, send.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy");
+  nccl_ok(ncclAllGather(dsend, drecv, bytes, ncclUint8, (ncclComm_t)s.comm, nullptr), "ncclAllGather");
+  hip_ok(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+  std::vector<uint8_t> recv(bytes * s.world);
+  hip_ok(hipMemcpy(recv.data(), drecv, recv.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+  hip_ok(hipFree(dsend), "hipFree");
+  hip_ok(hipFree(drecv), "hipFree");
+  std::unordered_map<uint64_t, size_t> at;
+  std::vector<PairCount> out;
+  for (int r = 0; r < s.world; ++r) {
+    const uint8_t* blk = recv.data() + (size_t)r * bytes;
+    PairCount h;
+    std::memcpy(&h, blk, rec);
+    for (uint64_t i = 0; i < h.count; ++i) {
+      PairCount p;
+      std::memcpy(&p, blk + (i + 1) * rec, rec);
+      const uint64_t k = pack_pair(p.a, p.b);
+      auto it = at.find(k);
+      if (it == at.end()) {
+        at.emplace(k, out.size());
+        out.push_back(p);
+      } else {
+        out[it->second].count += p.count;
+        out[it->second].ft = std::min(out[it->second].ft, p.ft);
+      }
+    }
+  }
+  pairs->swap(out);
+}
+
+void dist_split(const std::vector<uint64_t>& prefix, int rank, int world, size_t* begin, size_t* end) {
+  const size_t n = prefix.size() - 1;
+  const uint64_t total = prefix.back();
+  auto cut = [&](int r) -> size_t {
+    if (r <= 0) return 0;
+    if (r >= world) return n;
+    const uint64_t target = (uint64_t)((long double)total * r / world);
+    return (size_t)(std::lower_bound(prefix.begin(), prefix.end(), target) - prefix.begin());
+  };
+  *begin = std::min(cut(rank), n);
+  *end = std::min(cut(rank + 1), n);
+}
+
+}  // namespace shred

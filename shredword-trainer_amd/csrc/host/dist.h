@@ -1,0 +1,41 @@
+// Multi-GPU plumbing: one process per MI355X, RCCL over xGMI.
+//
+// The BPE path shards the word table by contiguous word ranges.  Per merge the
+// only exchange is one pair of all-reduces over the live prefix of the neighbour-delta tables
+// (sum of weights, min of first touch) — both order-free, so every rank receives identical
+// records and replays the identical heap.  Setup and the rare host-side reductions (initial
+// pair lists, final token histogram) go through small device staging buffers.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "selector.h"
+
+namespace shred {
+
+struct DistState {
+  int rank = 0;
+  int world = 1;
+  int device = 0;
+  void* comm = nullptr;  // ncclComm_t
+};
+
+DistState& dist_state();
+inline bool dist_active() { return dist_state().world > 1 && dist_state().comm != nullptr; }
+
+int dist_unique_id(void* out, size_t cap);
+int dist_init(int rank, int world, const void* id, size_t len, int device);
+int dist_finalize();
+
+// In-place all-reduce of n u64 device values on `stream` (sum, or min when min_op).
+void dist_allreduce_device(uint64_t* dev_buf, size_t n, bool min_op, void* stream);
+// Same for host values, staged through a device buffer (synchronous).
+void dist_allreduce_host(uint64_t* host, size_t n, bool min_op);
+// Every rank's pair list, merged: counts summed, first touch min (synchronous).
+void dist_merge_pairs(std::vector<PairCount>* pairs);
+// Rank r's share [begin, end) of n weighted items, split at equal cumulative weight.
+void dist_split(const std::vector<uint64_t>& prefix_weight, int rank, int world, size_t* begin, size_t* end);
+
+}  // namespace shred

@@ -1,0 +1,221 @@
+// Exact merge selection: see selector.h for the rules and reference citations.
+#include "selector.h"
+
+#include <algorithm>
+
+#include "common.h"
+
+namespace shred {
+
+namespace {
+inline uint64_t mix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xFF51AFD7ED558CCDull;
+  k ^= k >> 33;
+  k *= 0xC4CEB9FE1A85EC53ull;
+  k ^= k >> 33;
+  return k;
+}
+}  // namespace
+
+void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
+  unk_ = unk_id;
+  min_freq_ = min_pair_freq;
+  infos_.clear();
+  index_.assign(1 << 16, 0);
+  mask_ = index_.size() - 1;
+  heap_.clear();
+}
+
+void Selector::grow_index() {
+  std::vector<uint32_t> idx(index_.size() * 2, 0);
+  uint64_t m = idx.size() - 1;
+  for (uint32_t i = 0; i < infos_.size(); ++i) {
+    uint64_t j = mix64(infos_[i].key) & m;
+    while (idx[j]) j = (j + 1) & m;
+    idx[j] = i + 1;
+  }
+  index_.swap(idx);
+  mask_ = m;
+}
+
+Selector::Info& Selector::get(int32_t a, int32_t b) {
+  const uint64_t key = pack_pair(a, b);
+  uint64_t j = mix64(key) & mask_;
+  for (;;) {
+    uint32_t s = index_[j];
+    if (!s) break;
+    if (infos_[s - 1].key == key) return infos_[s - 1];
+    j = (j + 1) & mask_;
+  }
+  if (2 * (infos_.size() + 1) > index_.size()) {
+    grow_index();
+    j = mix64(key) & mask_;
+    while (index_[j]) j = (j + 1) & mask_;
+  }
+  infos_.push_back({key, 0, 0, (uint32_t)infos_.size()});
+  index_[j] = (uint32_t)infos_.size();
+  return infos_.back();
+}
+
+bool Selector::lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) const {
+  const uint64_t key = pack_pair(a, b);
+  uint64_t j = mix64(key) & mask_;
+  for (;;) {
+    uint32_t s = index_[j];
+    if (!s) break;
+    if (infos_[s - 1].key == key) {
+      *freq = infos_[s - 1].freq;
+      *version = infos_[s - 1].version;
+      return true;
+    }
+    j = (j + 1) & mask_;
+  }
+  *freq = 0;
+  *version = 0;
+  return false;
+}
+
+void Selector::push(int32_t a, int32_t b, uint64_t freq, uint32_t version) {
+  size_t i = heap_.size();
+  heap_.push_back({});
+  const HeapEnt x{a, b, freq, version};
+  while (i > 0) {
+    size_t p = (i - 1) >> 1;
+    if (heap_[p].freq >= freq) break;  // sift up only while parent < child (heap.cpp:76)
+    heap_[i] = heap_[p];
+    i = p;
+  }
+  heap_[i] = x;
+}
+
+Selector::HeapEnt Selector::pop() {
+  HeapEnt top = heap_[0];
+  HeapEnt x = heap_.back();
+  heap_.pop_back();
+  const size_t n = heap_.size();
+  if (n == 0) return top;
+  size_t i = 0;
+  for (;;) {  // left child if strictly greater, then right if strictly greater (heap.cpp:101-106)
+    size_t l = 2 * i + 1, r = l + 1, best = i;
+    uint64_t bf = x.freq;
+    if (l < n && heap_[l].freq > bf) { best = l; bf = heap_[l].freq; }
+    if (r < n && heap_[r].freq > bf) best = r;
+    if (best == i) break;
+    heap_[i] = heap_[best];
+    i = best;
+  }
+  heap_[i] = x;
+  return top;
+}
+
+void Selector::add_counts(std::vector<PairCount> pairs) {
+  // bimap_get is reached in (word rank, position) order, so that is creation order.
+  std::sort(pairs.begin(), pairs.end(), [](const PairCount& x, const PairCount& y) { return x.ft < y.ft; });
+  for (const PairCount& p : pairs) {
+    Info& in = get(p.a, p.b);
+    if (in.freq == 0) in.version = 0;  // bpe.cpp:207-210
+    in.freq += p.count;
+  }
+  // Heap build: bucket 0..4095, chain (creation) order, freq >= min (bpe.cpp:218-225).
+  std::vector<std::pair<uint64_t, uint32_t>> order;
+  order.reserve(infos_.size());
+  for (uint32_t i = 0; i < infos_.size(); ++i) {
+    const Info& in = infos_[i];
+    if (in.freq >= min_freq_) {
+      uint32_t bk = pair_fnv(pair_first(in.key), pair_second(in.key)) & (kPairBuckets - 1);
+      order.push_back({((uint64_t)bk << 32) | in.seq, i});
+    }
+  }
+  std::sort(order.begin(), order.end());
+  for (auto& o : order) {
+    const Info& in = infos_[o.second];
+    push(pair_first(in.key), pair_second(in.key), in.freq, in.version);
+  }
+}
+
+bool Selector::select(int32_t* a, int32_t* b, uint64_t* freq) {
+  while (!heap_.empty()) {
+    HeapEnt top = pop();
+    Info& in = get(top.a, top.b);
+    if (top.version != in.version) continue;  // stale entry
+    uint64_t actual = (top.a == unk_ || top.b == unk_) ? 0 : in.freq;
+    if (actual != in.freq) {
+      in.freq = actual;
+      in.version++;
+      if (actual >= min_freq_) push(top.a, top.b, actual, in.version);
+      continue;
+    }
+    if (actual < min_freq_) continue;
+    *a = top.a;
+    *b = top.b;
+    *freq = actual;
+    return true;
+  }
+  return false;
+}
+
+void Selector::apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n) {
+  // 1. records -> FreqChange entries keyed exactly like the reference's pair_hash.
+  changes_.clear();
+  size_t cap = 64;
+  while (cap < 2 * n + 2) cap <<= 1;
+  change_index_.assign(cap, 0);
+  const uint64_t cm = cap - 1;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t cat = recs[i].key & 3u;
+    const uint32_t slot = recs[i].key >> 2;
+    const int32_t id = slot == 0 ? unk_ : (int32_t)(slot - 1);
+    int32_t first, second;
+    switch (cat) {
+      case kOldLeft: first = id; second = a; break;
+      case kNewLeft: first = id; second = X; break;
+      case kOldRight: first = b; second = id; break;
+      default: first = X; second = id; break;
+    }
+    const uint64_t hk = ((uint64_t)(int64_t)first << 32) | (uint64_t)(int64_t)second;
+    const int64_t d = (cat == kOldLeft || cat == kOldRight) ? -(int64_t)recs[i].sum : (int64_t)recs[i].sum;
+    uint64_t j = mix64(hk) & cm;
+    for (;;) {
+      uint32_t s = change_index_[j];
+      if (!s) {
+        changes_.push_back({hk, d, recs[i].ft});
+        change_index_[j] = (uint32_t)changes_.size();
+        break;
+      }
+      Change& c = changes_[s - 1];
+      if (c.hk == hk) {
+        c.delta += d;
+        if (recs[i].ft < c.ft) c.ft = recs[i].ft;
+        break;
+      }
+      j = (j + 1) & cm;
+    }
+  }
+  // 2. reference application order: bucket (hk % 1024) ascending, latest first touch first.
+  std::sort(changes_.begin(), changes_.end(), [](const Change& x, const Change& y) {
+    const uint64_t bx = x.hk % kDeltaBuckets, by = y.hk % kDeltaBuckets;
+    if (bx != by) return bx < by;
+    return x.ft > y.ft;
+  });
+  for (const Change& c : changes_) {
+    const int32_t f = (int32_t)(uint32_t)(c.hk >> 32), s = (int32_t)(uint32_t)c.hk;
+    if (f == a && s == b) continue;
+    Info& in = get(f, s);
+    if (c.delta < 0) {
+      const uint64_t m = (uint64_t)(-c.delta);
+      in.freq = in.freq >= m ? in.freq - m : 0;
+    } else {
+      in.freq += (uint64_t)c.delta;
+    }
+    if (in.freq >= min_freq_) {
+      in.version++;
+      push(f, s, in.freq, in.version);
+    }
+  }
+  Info& merged = get(a, b);
+  merged.freq = 0;
+  merged.version++;
+}
+
+}  // namespace shred

@@ -1,0 +1,92 @@
+// Exact merge selection for the BPE path: the host half of the merge loop.
+//
+// The device finds every occurrence of the merged pair and reduces its neighbour-pair deltas;
+// this class turns those deltas into the reference's exact pair-info updates and heap pushes,
+// and replays the reference heap to pick the next merge.  Merge order is decided by ties in the
+// reference's binary heap (SURVEY.md §0 finding 2), so bit-exact output needs this replay:
+//
+//  * pair info      Info{freq, version} per pair (reference hash.h:31-45, bimap_get hash.cpp:104-130)
+//  * heap           push sifts up while parent < child; pop sifts down left-first, right only
+//                   if strictly greater (reference heap.cpp:53-114)
+//  * select         bpe_merge_batch's pop loop (bpe.cpp:244-258); the O(S) recompute_freq
+//                   (bpe.cpp:52-65) is replaced by its provable value: 0 for keys holding unk,
+//                   info.freq otherwise (deltas keep non-unk counts exact, SURVEY.md §0 finding 3)
+//  * apply          the FreqChangeMap semantics of bpe.cpp:265-313: deltas keyed by
+//                   ((i64)first << 32) | (i64)second (sign-extension folds every (x, negative) key
+//                   to (-1, negative)), applied bucket (key % 1024) ascending and, inside a bucket,
+//                   in reverse order of first touch, clamped at 0, net-zero entries included.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace shred {
+
+// One device delta record: key = slot * 4 + category (see DeltaCategory); the neighbour id is
+// slot - 1, slot 0 standing for unk_id when unk_id lies outside [0, slot capacity).
+struct DeltaRecord {
+  uint32_t key;
+  uint32_t pad;
+  uint64_t sum;  // Σ word weight over the occurrences (magnitude; sign given by the category)
+  uint64_t ft;   // first touch: (word rank << 32) | (position in word << 2) | category
+};
+static_assert(sizeof(DeltaRecord) == 24, "DeltaRecord layout is shared with the device");
+
+enum DeltaCategory : uint32_t {
+  kOldLeft = 0,   // (p, a)  -= w   (bpe.cpp:276-279)
+  kNewLeft = 1,   // (p, X)  += w
+  kOldRight = 2,  // (b, n)  -= w   (bpe.cpp:283-289)
+  kNewRight = 3,  // (X, n)  += w
+};
+
+struct PairCount {
+  int32_t a, b;
+  uint64_t count;
+  uint64_t ft;  // first touch (word rank << 32) | position: the reference bimap creation order
+};
+
+class Selector {
+ public:
+  void reset(int32_t unk_id, uint64_t min_pair_freq);
+
+  // bpe_count_bigrams (bpe.cpp:187-230): adds counts (new pairs created in first-touch order),
+  // then pushes every pair with freq >= min in (FNV bucket & 4095, creation order).
+  void add_counts(std::vector<PairCount> pairs);
+
+  // bpe_merge_batch's pop loop: true with the pair to merge and its freq; false if the heap
+  // ran empty.
+  bool select(int32_t* a, int32_t* b, uint64_t* freq);
+
+  // Applies one merge's device deltas and finalises the merged key (bpe.cpp:297-318).
+  void apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n);
+
+  size_t heap_size() const { return heap_.size(); }
+  bool heap_empty() const { return heap_.empty(); }
+  uint64_t heap_top_freq() const { return heap_.empty() ? 0 : heap_[0].freq; }
+  size_t num_pairs() const { return infos_.size(); }
+  // freq/version of a pair (0/0 when absent); for tests.
+  bool lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) const;
+  int32_t unk_id() const { return unk_; }
+
+ private:
+  struct Info { uint64_t key; uint64_t freq; uint32_t version; uint32_t seq; };
+  struct HeapEnt { int32_t a, b; uint64_t freq; uint32_t version; };
+  struct Change { uint64_t hk; int64_t delta; uint64_t ft; };
+
+  Info& get(int32_t a, int32_t b);  // get-or-create (bimap_get)
+  void push(int32_t a, int32_t b, uint64_t freq, uint32_t version);
+  HeapEnt pop();
+  void grow_index();
+
+  int32_t unk_ = 0;
+  uint64_t min_freq_ = 2000;
+  std::vector<Info> infos_;
+  std::vector<uint32_t> index_;  // open addressing: info index + 1
+  uint64_t mask_ = 0;
+  std::vector<HeapEnt> heap_;
+  std::vector<Change> changes_;
+  std::vector<uint32_t> change_index_;
+};
+
+}  // namespace shred

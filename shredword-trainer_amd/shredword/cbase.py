@@ -1,0 +1,93 @@
+"""ctypes binding of libtrainer.so (mirrors the reference's shredword/cbase.py).
+
+Library discovery follows the reference (cbase.py:4-26): the first file named ``trainer*`` or
+``libtrainer*`` with a shared-library suffix in this package, ``lib/`` below it, or ``../build``;
+``SHREDWORD_LIB`` overrides.  The library is loaded with RTLD_GLOBAL (cbase.py:29) and the 8 BPE
+plus 13 Unigram symbols are bound at import (cbase.py:50-71), so a library missing any of them
+fails here with AttributeError, as with the reference.  The Trainer handle is opaque.
+"""
+import ctypes
+import os
+import sysconfig
+from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_int, c_int32,
+                    c_size_t, c_uint64, c_void_p)
+
+
+def _get_lib_path():
+    env = os.environ.get("SHREDWORD_LIB")
+    if env:
+        return os.path.abspath(env)
+    pkg_dir = os.path.dirname(os.path.abspath(__file__))
+    names = ("libtrainer", "trainer")
+    exts = [e for e in (".so", ".pyd", ".dll", ".dylib", sysconfig.get_config_var("EXT_SUFFIX")) if e]
+    search = [pkg_dir, os.path.join(pkg_dir, "lib"), os.path.join(pkg_dir, "..", "build")]
+    for d in search:
+        if not os.path.isdir(d):
+            continue
+        for root, _dirs, files in os.walk(d):
+            for f in sorted(files):
+                if f.startswith(names) and any(f.endswith(e) for e in exts):
+                    return os.path.abspath(os.path.join(root, f))
+    available = []
+    for d in search:
+        if os.path.isdir(d):
+            available.extend(os.listdir(d))
+    raise FileNotFoundError(f"Could not find trainer library in {search}. Available files: {available}")
+
+
+_lib_path = _get_lib_path()
+lib = ctypes.CDLL(_lib_path, mode=getattr(ctypes, "RTLD_GLOBAL", 0))
+
+MIN_HEAP_SIZE, MAX_OCCS_PER_MERGE, INITIAL_VOCAB_SIZE, INITIAL_STR_SIZE = 4096, 50000, 256, 4096
+
+
+class BPEConfig(Structure):
+    """reference bpe.h:43-48 / cbase.py:47 (24 bytes, offsets 0/8/12/16)."""
+    _fields_ = [("target_vocab_size", c_size_t), ("unk_id", c_int32),
+                ("character_coverage", c_float), ("min_pair_freq", c_uint64)]
+
+
+class ShredStats(Structure):
+    _fields_ = [("load_seconds", c_double), ("init_seconds", c_double), ("train_seconds", c_double),
+                ("merge_kernel_ms", c_double), ("count_kernel_ms", c_double),
+                ("merge_kernel_bytes", c_double), ("count_kernel_bytes", c_double),
+                ("merge_launches", c_uint64), ("count_launches", c_uint64),
+                ("num_words", c_uint64), ("num_symbols", c_uint64), ("num_occurrences", c_uint64),
+                ("num_merges", c_uint64), ("heap_size", c_uint64), ("live_tokens", c_uint64),
+                ("device_bytes", c_uint64), ("num_tiles", c_uint64),
+                ("layout", c_int32), ("world_size", c_int32)]
+
+
+Trainer = c_void_p
+
+lib.create_trainer.argtypes, lib.create_trainer.restype = [POINTER(BPEConfig)], Trainer
+lib.bpe_trainer_destroy.argtypes, lib.bpe_trainer_destroy.restype = [Trainer], None
+lib.bpe_init.argtypes, lib.bpe_init.restype = [Trainer], None
+lib.bpe_count_bigrams.argtypes, lib.bpe_count_bigrams.restype = [Trainer], None
+lib.bpe_load_corpus.argtypes, lib.bpe_load_corpus.restype = [Trainer, c_char_p], c_int
+lib.bpe_merge_batch.argtypes, lib.bpe_merge_batch.restype = [Trainer, c_int], c_int
+lib.bpe_train.argtypes, lib.bpe_train.restype = [Trainer], c_int
+lib.bpe_save.argtypes, lib.bpe_save.restype = [Trainer, c_char_p, c_char_p], None
+
+lib.trainerCreate.argtypes, lib.trainerCreate.restype = [c_int, c_float, c_int, c_int], c_void_p
+lib.trainerDestroy.argtypes, lib.trainerDestroy.restype = [c_void_p], None
+lib.addTextToTrainer.argtypes, lib.addTextToTrainer.restype = [c_void_p, c_char_p], c_bool
+lib.preprocessTexts.argtypes, lib.preprocessTexts.restype = [c_void_p], c_bool
+lib.extractInitialSubwords.argtypes, lib.extractInitialSubwords.restype = [c_void_p], c_bool
+lib.computeLoss.argtypes, lib.computeLoss.restype = [c_void_p, POINTER(c_char_p), c_int], c_float
+lib.computeTokenLoss.argtypes, lib.computeTokenLoss.restype = [c_void_p, c_char_p, POINTER(c_char_p), c_int], c_double
+lib.pruneVocabStep.argtypes, lib.pruneVocabStep.restype = [c_void_p, POINTER(c_char_p), c_int, c_double], c_bool
+lib.updateTokenScores.argtypes, lib.updateTokenScores.restype = [c_void_p, POINTER(c_char_p), c_int], c_bool
+lib.trainUnigram.argtypes, lib.trainUnigram.restype = [c_void_p, POINTER(c_char_p), c_int, c_int], c_bool
+lib.getVocab.argtypes, lib.getVocab.restype = [c_void_p, POINTER(POINTER(c_char_p)), POINTER(POINTER(c_double)), POINTER(c_int)], c_bool
+lib.saveVocab.argtypes, lib.saveVocab.restype = [c_void_p, c_char_p], c_bool
+lib.loadVocab.argtypes, lib.loadVocab.restype = [c_void_p, c_char_p], c_bool
+
+# extensions (include/shredword_bpe.h)
+lib.shred_set_option.argtypes, lib.shred_set_option.restype = [Trainer, c_char_p, c_char_p], c_int
+lib.shred_reset.argtypes, lib.shred_reset.restype = [Trainer], c_int
+lib.shred_get_stats.argtypes, lib.shred_get_stats.restype = [Trainer, POINTER(ShredStats)], c_int
+lib.shred_device_count.argtypes, lib.shred_device_count.restype = [], c_int
+lib.shred_dist_unique_id.argtypes, lib.shred_dist_unique_id.restype = [c_void_p, c_size_t], c_int
+lib.shred_dist_init.argtypes, lib.shred_dist_init.restype = [c_int, c_int, c_void_p, c_size_t, c_int], c_int
+lib.shred_dist_finalize.argtypes, lib.shred_dist_finalize.restype = [], c_int

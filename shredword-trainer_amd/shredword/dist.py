@@ -1,0 +1,37 @@
+"""Multi-GPU bootstrap: one process per MI355X, RCCL over xGMI (include/shredword_bpe.h).
+
+``init_from_env()`` reads RANK / WORLD_SIZE / LOCAL_RANK (torchrun), has rank 0 create the RCCL
+unique id, broadcasts it with torch.distributed (already initialised by the caller, any backend)
+and initialises the library's communicator.  Trainers created afterwards shard the word table.
+"""
+import ctypes
+import os
+
+from .cbase import lib
+
+
+def init_from_env(device=None):
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) if device is None else int(device)
+    if world <= 1:
+        return 0
+    buf = ctypes.create_string_buffer(512)
+    uid = [None]
+    if rank == 0:
+        n = lib.shred_dist_unique_id(buf, 512)
+        if n <= 0:
+            raise RuntimeError("shred_dist_unique_id failed")
+        uid[0] = bytes(buf.raw[:n])
+    dist.broadcast_object_list(uid, src=0)
+    raw = uid[0]
+    rc = lib.shred_dist_init(rank, world, ctypes.c_char_p(raw), len(raw), local)
+    if rc != 0:
+        raise RuntimeError(f"shred_dist_init failed on rank {rank}")
+    return world
+
+
+def finalize():
+    lib.shred_dist_finalize()

@@ -1,0 +1,68 @@
+"""GPU parity: the HIP path (through the C ABI via the Python drop-in) against the reference
+goldens — every .model byte, .vocab byte, merge line (a, b, freq, new_id) and per-batch heap
+size must match (bit-exact: integer work)."""
+import os
+import subprocess
+
+import pytest
+
+from conftest import PKG, golden_cases
+
+pytestmark = pytest.mark.gpu
+
+
+def _train(case, corpus, tmp_path, layout="types"):
+    from shredword.trainer import BPETrainer
+
+    cfg = case["config"]
+    trace = str(tmp_path / f"trace_{layout}.txt")
+    t = BPETrainer(vocab_size=cfg["vocab_size"], unk_id=cfg["unk_id"],
+                   character_coverage=cfg["character_coverage"], min_pair_freq=cfg["min_pair_freq"])
+    t.set_option("log", 0)
+    t.set_option("layout", layout)
+    t.set_option("trace", trace)
+    t.load_corpus(corpus)
+    merges = t.train()
+    model, vocab = str(tmp_path / "g.model"), str(tmp_path / "g.vocab")
+    t.save(model, vocab)
+    t.destroy()
+    return merges, open(model, "rb").read(), open(vocab, "rb").read(), open(trace).read()
+
+
+API_CASES = [n for n in golden_cases() if not n.startswith("cli_")]
+
+
+@pytest.mark.parametrize("name", API_CASES)
+def test_types_layout_matches_reference(name, case_corpus, tmp_path):
+    case, corpus = case_corpus(name)
+    merges, model, vocab, trace = _train(case, corpus, tmp_path, "types")
+    assert merges == case["merges"]
+    assert trace == case["trace"]
+    assert model == case["model_bytes"]
+    assert vocab == case["vocab_bytes"]
+
+
+@pytest.mark.parametrize("name", ["c1_ascii10m_v8192", "ascii1m_v3000_mpf2", "adv_unk0", "adv_unkm1",
+                                  "ascii1m_unk7_cov09", "small_v300"])
+def test_stream_layout_matches_reference(name, case_corpus, tmp_path):
+    case, corpus = case_corpus(name)
+    merges, model, vocab, trace = _train(case, corpus, tmp_path, "stream")
+    assert merges == case["merges"]
+    assert trace == case["trace"]
+    assert model == case["model_bytes"]
+    assert vocab == case["vocab_bytes"]
+
+
+@pytest.mark.parametrize("name", [n for n in golden_cases() if n.startswith("cli_")])
+def test_cli_matches_reference(name, case_corpus, tmp_path):
+    case, corpus = case_corpus(name)
+    cfg = case["config"]
+    model, vocab = str(tmp_path / "c.model"), str(tmp_path / "c.vocab")
+    proc = subprocess.run([os.path.join(PKG, "bin", "trainer"), f"input={corpus}", "model_type=bpe",
+                           f"output_model={model}", f"output_vocab={vocab}",
+                           f"vocab_size={cfg['vocab_size']}", f"character_coverage={cfg['character_coverage']}",
+                           f"min_pair_freq={cfg['min_pair_freq']}"],
+                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=dict(os.environ, SHREDWORD_LOG="0"))
+    assert proc.returncode == 0, proc.stderr  # the reference CLI segfaults here (rc 139)
+    assert open(model, "rb").read() == case["model_bytes"]
+    assert open(vocab, "rb").read() == case["vocab_bytes"]
