@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Benchmark of the BPE merge path on MI355X (BASELINE.json metric: BPE merges/sec).
+
+A step is one full ``train()`` of the HBM-resident corpus (pair count K1 + heap build + every
+merge to the target vocab or heap exhaustion), preceded by ``reset()`` which restores the
+unmerged token stream on the device.  The default workload is BASELINE.json configs[1] (C2):
+vocab_size=8192 (min_pair_freq 2000, coverage 0.995, unk 0 = the reference Python defaults) on a
+1 GB synthetic UTF-8 corpus from the committed generator (seed 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--layout types|stream]
+
+N > 1 runs under torch.distributed.run, one process per GPU: the word table is sharded by
+contiguous word ranges and each merge all-reduces the neighbour-delta tables over RCCL.  Every
+rank performs the same merges, so ``value`` = merges / max-over-ranks time (fixed corpus:
+strong scaling).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "shredword-trainer_amd")
+sys.path.insert(0, PKG)
+os.environ.setdefault("SHREDWORD_LOG", "0")  # stdout carries exactly one JSON line
+
+CONFIGS = {
+    "c1": dict(bytes=10_000_000, seed=1, script="ascii", vocab=8192, mpf=2000, cov=0.995, unk=0,
+               desc="C1: BPE vocab_size=8192 min_pair_freq=2000 on 10 MB synthetic ASCII corpus"),
+    "c2": dict(bytes=1_000_000_000, seed=2, script="utf8", vocab=8192, mpf=2000, cov=0.995, unk=0,
+               desc="C2: BPE vocab_size=8192 (min_pair_freq=2000) on 1 GB synthetic UTF-8 corpus"),
+    "c3": dict(bytes=10_000_000_000, seed=3, script="utf8", vocab=32000, mpf=2, cov=0.995, unk=0,
+               desc="C3: BPE vocab_size=32000 min_pair_freq=2 on 10 GB synthetic UTF-8 corpus"),
+    "c5": dict(bytes=100_000_000_000, seed=5, script="mixed", vocab=64000, mpf=2000, cov=0.9995, unk=0,
+               desc="C5: BPE vocab_size=64000 coverage=0.9995 on 100 GB mixed-script corpus"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(msg):
+    print(msg, file=sys.stderr, flush=True)
+
+
+def corpus_path(cfg, name):
+    d = os.environ.get("SHREDWORD_BENCH_DIR", os.path.join(os.environ.get("TMPDIR", "/tmp"), "shredword_bench"))
+    os.makedirs(d, exist_ok=True)
+    return os.path.join(d, f"{name}_{cfg['script']}_{cfg['bytes']}_s{cfg['seed']}.txt")
+
+
+def ensure_corpus(cfg, path):
+    if os.path.exists(path) and os.path.getsize(path) == cfg["bytes"]:
+        return 0.0
+    gen = os.path.join(PKG, "bin", "gen_corpus")
+    if not os.path.exists(gen):
+        subprocess.run(["make", "-s", "-C", PKG, os.path.join(PKG, "bin", "gen_corpus")], check=True)
+    t0 = time.time()
+    tmp = path + ".part"
+    threads = str(min(16, os.cpu_count() or 8))
+    subprocess.run([gen, "--bytes", str(cfg["bytes"]), "--seed", str(cfg["seed"]), "--script", cfg["script"],
+                    "--out", tmp, "--threads", threads], check=True)
+    os.replace(tmp, path)
+    return time.time() - t0
+
+
+def cpu_baseline(cfg, path, seconds):
+    """The CPU port (oracle/bpe_oracle.c, reference-faithful merge loop) on one host core,
+    bounded to `seconds` of train time on the same corpus and config."""
+    exe = os.path.join(REPO, "oracle", "_build", "bpe_oracle")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "port"], check=True)
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), "shredword_cpu_baseline")
+
+    def pin():
+        try:
+            os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+        except OSError:
+            pass
+
+    proc = subprocess.run([exe, path, str(cfg["vocab"]), str(cfg["unk"]), repr(cfg["cov"]), str(cfg["mpf"]),
+                           out + ".model", out + ".vocab", "--max-seconds", str(seconds)],
+                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, preexec_fn=pin, check=True)
+    fields = dict(kv.split("=") for kv in proc.stderr.decode().split("TIMING", 1)[1].split())
+    merges, train_s = int(fields["merges"]), float(fields["train"])
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": merges / train_s if train_s > 0 else None, "unit": "merges/s", "cores": 1, "kind": "port",
+        "sample": (f"first {merges} merges (train() capped at {seconds:.0f} s, load {float(fields['load']):.1f} s "
+                   f"excluded) of the same corpus/config, oracle/bpe_oracle.c pinned to 1 core of {cpu} "
+                   f"(nproc={os.cpu_count()})"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--layout", default="types", choices=["types", "stream"])
+    ap.add_argument("--bytes", type=int, default=0, help="override the corpus size (testing)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    cfg = dict(CONFIGS[args.config])
+    if args.bytes:
+        cfg["bytes"] = args.bytes
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    path = corpus_path(cfg, args.config)
+    gen_s = ensure_corpus(cfg, path) if local == 0 else 0.0
+    barrier()
+
+    from shredword import dist as sdist
+    from shredword.trainer import BPETrainer
+    if world > 1:
+        sdist.init_from_env(device=local)
+
+    t = BPETrainer(vocab_size=cfg["vocab"], unk_id=cfg["unk"], character_coverage=cfg["cov"], min_pair_freq=cfg["mpf"])
+    t.set_option("log", 0)
+    t.set_option("device", local)
+    t.set_option("layout", args.layout)
+    t0 = time.time()
+    t.load_corpus(path)
+    load_s = time.time() - t0
+    def train_step():
+        t.reset()
+        n = t._train(t.trainer)  # the BPETrainer.train() ABI call, without its stdout line
+        if n < 0:
+            raise RuntimeError("bpe_train failed")
+        return n
+
+    for _ in range(args.warmup):
+        train_step()
+    t.set_option("timing", 1)
+    t.set_option("clear_stats", 1)
+    # timed region: exactly K steps, bracketed by barrier + device sync
+    barrier()
+    torch.cuda.synchronize()
+    start = time.perf_counter()
+    merges = 0
+    for _ in range(args.steps):
+        merges += train_step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - start
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    st = t.stats()
+    tmpd = os.environ.get("TMPDIR", "/tmp")
+    t._save(t.trainer, os.path.join(tmpd, f"bench_r{rank}.model").encode(),
+            os.path.join(tmpd, f"bench_r{rank}.vocab").encode())
+    t.destroy()
+
+    if rank == 0:
+        mk_ms = st["merge_kernel_ms"] / max(1, st["merge_launches"])
+        mk_bytes = st["merge_kernel_bytes"] / max(1, st["merge_launches"])
+        achieved = (mk_bytes / (mk_ms * 1e-3)) / 1e9 if mk_ms > 0 else None
+        k1_ms = st["count_kernel_ms"] / max(1, st["count_launches"])
+        k1_bytes = st["count_kernel_bytes"] / max(1, st["count_launches"])
+        per_step_merges = merges / max(1, args.steps)
+        result = {
+            "metric": "BPE merges/sec",
+            "value": merges / elapsed,
+            "unit": "merges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (committed deterministic generator, SURVEY.md §8 d2)",
+            "config": {
+                "workload": cfg["desc"],
+                "corpus_bytes": cfg["bytes"], "seed": cfg["seed"], "script": cfg["script"],
+                "vocab_size": cfg["vocab"], "min_pair_freq": cfg["mpf"], "character_coverage": cfg["cov"],
+                "unk_id": cfg["unk"], "layout": args.layout, "parallelism": f"word-range shards x{world}",
+                "merges_per_step": per_step_merges, "distinct_words": st["num_words"],
+                "symbols": st["num_symbols"], "occurrences": st["num_occurrences"], "tiles": st["num_tiles"],
+            },
+            "roofline": {
+                "kernel": "k_merge (fused match + delta + in-place compaction, K2+K3)",
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                "avg_launch_us": 1e3 * mk_ms, "avg_bytes_per_launch": mk_bytes,
+                "launches": st["merge_launches"],
+            },
+            "pair_count": {
+                "kernel": "k_pair_count (K1)", "avg_launch_us": 1e3 * k1_ms, "bytes_per_launch": k1_bytes,
+                "achieved_GBps": (k1_bytes / (k1_ms * 1e-3)) / 1e9 if k1_ms > 0 else None,
+            },
+            "load_s": load_s, "corpus_gen_s": gen_s,
+            "us_per_merge": 1e6 * elapsed / max(1, merges),
+            "merge_kernel_share": (st["merge_kernel_ms"] * 1e-3) / elapsed if elapsed > 0 else None,
+            "host_breakdown_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
+            "init_s_last_step": st["init_seconds"],
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                result["cpu_baseline"] = cpu_baseline(cfg, path, args.cpu_seconds)
+            except Exception as e:  # the GPU number stands on its own
+                result["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        sdist.finalize()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

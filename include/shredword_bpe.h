@@ -79,6 +79,7 @@ int shred_reset(Trainer* trainer);
 
 typedef struct ShredStats {
   double load_seconds, init_seconds, train_seconds;
+  double host_select_seconds, host_launch_seconds, host_wait_seconds, host_apply_seconds;
   double merge_kernel_ms, count_kernel_ms;
   double merge_kernel_bytes, count_kernel_bytes;
   uint64_t merge_launches, count_launches;

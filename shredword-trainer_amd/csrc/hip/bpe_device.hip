@@ -42,7 +42,6 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kPer = 16;
 constexpr int kChunk = kThreads * kPer;  // 4096 tokens = 16 KiB per chunk
-constexpr int kDeltaLds = 1024;          // per-workgroup delta staging slots
 constexpr int kPairLds = 2048;           // per-workgroup pair-count staging slots
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 constexpr unsigned long long kEmpty64 = ~0ull;
@@ -66,7 +65,6 @@ __device__ __forceinline__ u64 mix64(u64 k) {
 struct ScanLds {
   u64 hdr[4];
   int cnt[4];
-  long long nona[4];
 };
 
 __device__ __forceinline__ void block_scan_hdr_cnt(u64 hdr, int cnt, ScanLds& s, u64* hdr_excl, int* cnt_excl,
@@ -114,28 +112,6 @@ __device__ __forceinline__ void block_scan_hdr_cnt(u64 hdr, int cnt, ScanLds& s,
   __syncthreads();
 }
 
-__device__ __forceinline__ long long block_scan_max_ll(long long x, ScanLds& s, long long* tot) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  long long v = x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    long long y = __shfl_up(v, d, 64);
-    if (lane >= d) v = y > v ? y : v;
-  }
-  if (lane == 63) s.nona[w] = v;
-  __syncthreads();
-  long long pre = -1, t = -1;
-  for (int i = 0; i < 4; ++i) {
-    if (i < w) pre = s.nona[i] > pre ? s.nona[i] : pre;
-    t = s.nona[i] > t ? s.nona[i] : t;
-  }
-  long long ex = __shfl_up(v, 1, 64);
-  if (lane == 0) ex = -1;
-  *tot = t;
-  __syncthreads();
-  return ex > pre ? ex : pre;
-}
-
 // Loads this lane's 16 tokens of chunk [cs, cs+cl) (kPad beyond cl).  16-byte loads where the
 // whole quad is in range: tiles start 16-byte aligned and chunks are 4096 tokens.
 __device__ __forceinline__ void load_chunk(const int32_t* base, uint32_t cs, uint32_t cl, int p0, int32_t (&v)[kPer]) {
@@ -163,7 +139,21 @@ __device__ __forceinline__ int32_t next_token(const int32_t* base, uint32_t cs, 
 }
 
 // ------------------------------------------------------------------------------------------
-// K2+K3: merge scan
+// K2+K3(+K4): merge scan, one wavefront per tile.
+//
+// A wave owns a tile (<= 1024 tokens, or one longer word walked in 1024-token chunks): each lane
+// holds 16 consecutive tokens, occurrences / run parity / word headers / output offsets are
+// wave-level scans (no workgroup barrier on the tile path), the 4 neighbour deltas of every
+// occurrence go to a workgroup LDS hash shared by the 4 waves, and a changed chunk is compacted
+// in LDS and written back in place.  The last workgroup to finish (agent-scope release/acquire
+// on a ticket) turns the touched delta slots into host records and raises a host-visible flag,
+// so one launch + one flag wait is the whole device side of a merge.
+constexpr int kWaveTok = 64 * kPer;  // 1024 tokens per wave chunk
+constexpr int kWaves = kThreads / 64;
+constexpr int kDeltaLdsW = 512;
+constexpr uint32_t kFusedCollectMax = 4096;  // beyond this the host launches k_collect
+constexpr uint32_t kNeedCollect = 0x80000000u;
+
 struct MergeParams {
   int32_t* tok;
   const uint64_t* tile_off;
@@ -176,23 +166,31 @@ struct MergeParams {
   u64* dft;
   uint32_t* dlist;
   uint32_t* dcount;
-  u64* stats;  // [0] occurrences merged, [1] tokens rewritten
+  u64* stats;         // [0] occurrences merged, [1] tokens rewritten
+  uint32_t* done;     // completion tickets: [0..7] per blockIdx % 8 group, [8] top
+  int fused;          // 1: last workgroup collects; 0: leave the tables (multi-GPU exchange)
+  DeltaRecord* out;   // host-visible records
+  uint32_t* hcount;   // host-visible: [0] record count (| kNeedCollect), [1] flag = seq
+  u64* hstats;        // host-visible: [0] occurrences, [1] tokens rewritten
+  uint32_t seq;
 };
 
 struct DeltaLds {
-  uint32_t key[kDeltaLds];
-  u64 sum[kDeltaLds];
-  u64 ft[kDeltaLds];
+  uint32_t key[kDeltaLdsW];
+  u64 sum[kDeltaLdsW];
+  u64 ft[kDeltaLdsW];
 };
 
 __device__ __forceinline__ void delta_global(const MergeParams& p, uint32_t key, u64 w, u64 ft) {
   atomicAdd(&p.dsum[key], w);
   const u64 old = atomicMin(&p.dft[key], ft);
-  if (old == kEmpty64) p.dlist[atomicAdd(p.dcount, 1u)] = key;  // exactly one toucher sees MAX
+  if (old == kEmpty64) {  // exactly one toucher sees MAX
+    atomicExch(&p.dlist[atomicAdd(p.dcount, 1u)], key);
+  }
 }
 
 __device__ __forceinline__ void delta_emit(DeltaLds& h, const MergeParams& p, uint32_t key, u64 w, u64 ft) {
-  uint32_t s = (key * 2654435761u) >> 22;
+  uint32_t s = (key * 2654435761u) >> 23;
   for (int probe = 0; probe < 16; ++probe) {
     const uint32_t prev = atomicCAS(&h.key[s], kEmpty32, key);
     if (prev == kEmpty32 || prev == key) {
@@ -200,7 +198,7 @@ __device__ __forceinline__ void delta_emit(DeltaLds& h, const MergeParams& p, ui
       atomicMin(&h.ft[s], ft);
       return;
     }
-    s = (s + 1) & (kDeltaLds - 1);
+    s = (s + 1) & (kDeltaLdsW - 1);
   }
   delta_global(p, key, w, ft);
 }
@@ -209,36 +207,67 @@ __device__ __forceinline__ uint32_t slot_of(int32_t id, uint32_t cap) {
   return (uint32_t)id < cap ? (uint32_t)id + 1u : 0u;
 }
 
+// Orders this wave's LDS accesses across lanes (LDS executes one wave's ops in order; this
+// keeps the compiler from moving them and drains lgkmcnt).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <class T>
+__device__ __forceinline__ T wave_incl_max(T x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T y = __shfl_up(x, d, 64);
+    if (lane >= d) x = y > x ? y : x;
+  }
+  return x;
+}
+
+__device__ __forceinline__ int wave_incl_sum(int x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
 template <bool kWeighted>
 __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
-  __shared__ int32_t s_tok[kChunk + 8];  // s_tok[2 + j] = chunk position j; [0],[1] = positions -2,-1
-  __shared__ int32_t s_out[kChunk];
-  __shared__ uint32_t s_mask[kThreads];
-  __shared__ ScanLds s_scan;
+  __shared__ int32_t s_tok[kWaves][kWaveTok + 8];  // [2 + j] = chunk position j; [0],[1] = -2,-1
   __shared__ DeltaLds h;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < kDeltaLds; i += kThreads) {
+  __shared__ uint32_t s_last;
+  __shared__ u64 s_cnt[2];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int32_t* st = s_tok[wid];
+  for (int i = threadIdx.x; i < kDeltaLdsW; i += kThreads) {
     h.key[i] = kEmpty32;
     h.sum[i] = 0;
     h.ft[i] = kEmpty64;
   }
+  if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
   __syncthreads();
   const int32_t a = p.a, b = p.b, X = p.X;
   const bool same = (a == b);
-  const int p0 = tid * kPer;
-  u64 n_merged = 0, n_written = 0;
+  const int p0 = lane * kPer;
+  u64 n_merged = 0, n_written = 0;  // wave-uniform
 
-  for (uint32_t tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
+  for (uint32_t tile = blockIdx.x * kWaves + wid; tile < p.ntiles; tile += gridDim.x * kWaves) {
     const uint32_t len = p.tile_len[tile];
     int32_t* base = p.tok + p.tile_off[tile];
     long long c_nona = -1;  // last tile index whose token != a (a == b only)
-    u64 c_hdr = 0;          // ((index + 1) << 32) | rank of the last header seen, 0 = none
+    u64 c_hdr = 0;          // ((index + 1) << 32) | rank of the last header, 0 = none
     bool c_m1 = false, c_m2 = false;
     int32_t c_t1 = kPad, c_t2 = kPad;
     uint32_t c_out = 0;
     bool dirty = false;
-    for (uint32_t cs = 0; cs < len; cs += kChunk) {
-      const uint32_t cl = min((uint32_t)kChunk, len - cs);
+    for (uint32_t cs = 0; cs < len; cs += kWaveTok) {
+      const uint32_t cl = min((uint32_t)kWaveTok, len - cs);
       const bool more = cs + cl < len;
       int32_t v[kPer];
       load_chunk(base, cs, cl, p0, v);
@@ -246,23 +275,24 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       bool any = false;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) any |= (v[j] == a) & ((j + 1 < kPer ? v[j + 1] : nx) == b);
-      const bool any_blk = __syncthreads_or(any);
-      if (!any_blk && !dirty && !more) break;  // rest of the tile is unchanged
+      if (!__any(any) && !dirty && !more) break;  // rest of the tile is unchanged
 
-      // ---- stage the chunk and its context in LDS
+      // ---- stage the chunk with 2 tokens of left context and 2 of lookahead
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) s_tok[2 + p0 + j] = v[j];
-      if (tid == 0) {
-        s_tok[0] = c_t2;
-        s_tok[1] = c_t1;
+      for (int j = 0; j < kPer; ++j) st[2 + p0 + j] = v[j];
+      if (lane == 0) {
+        st[0] = c_t2;
+        st[1] = c_t1;
       }
-      if (tid == kThreads - 1) {
-        s_tok[2 + kChunk] = (cs + kChunk < len) ? base[cs + kChunk] : kPad;
-        s_tok[3 + kChunk] = (cs + kChunk + 1 < len) ? base[cs + kChunk + 1] : kPad;
+      if (lane == 63) {
+        st[2 + kWaveTok] = (cs + kWaveTok < len) ? base[cs + kWaveTok] : kPad;
+        st[3 + kWaveTok] = (cs + kWaveTok + 1 < len) ? base[cs + kWaveTok + 1] : kPad;
       }
-      __syncthreads();
+      wave_lds_sync();
+      const int32_t last1 = st[2 + cl - 1];
+      const int32_t last2 = st[2 + cl - 2];  // st[1] when cl == 1
 
-      // ---- occurrences, greedy left to right (runs of a==b pair up from the run start)
+      // ---- occurrences, greedy left to right (runs of a == b pair up from the run start)
       uint32_t mask = 0;
       long long nona_tot = -1;
       if (same) {
@@ -270,64 +300,73 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
           if (v[j] != a) nl = (long long)(cs + p0 + j);
-        long long last = block_scan_max_ll(nl, s_scan, &nona_tot);
+        const long long inc = wave_incl_max(nl);
+        nona_tot = __shfl(inc, 63, 64);
+        long long last = __shfl_up(inc, 1, 64);
+        if (lane == 0) last = -1;
         last = last > c_nona ? last : c_nona;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
           const long long gi = (long long)(cs + p0 + j);
           if (v[j] != a) last = gi;
-          else if (s_tok[3 + p0 + j] == a && ((gi - last - 1) & 1) == 0) mask |= 1u << j;
+          else if ((j + 1 < kPer ? v[j + 1] : nx) == a && ((gi - last - 1) & 1) == 0) mask |= 1u << j;
         }
       } else {
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
-          if (v[j] == a && s_tok[3 + p0 + j] == b) mask |= 1u << j;
+          if (v[j] == a && (j + 1 < kPer ? v[j + 1] : nx) == b) mask |= 1u << j;
       }
-      s_mask[tid] = mask;
-      __syncthreads();
-      const uint32_t prevm = tid ? s_mask[tid - 1] : ((c_m1 ? 1u << 15 : 0u) | (c_m2 ? 1u << 14 : 0u));
+      uint32_t prevm = __shfl_up(mask, 1, 64);
+      if (lane == 0) prevm = (c_m1 ? 1u << 15 : 0u) | (c_m2 ? 1u << 14 : 0u);
       const uint32_t m_ext = (mask << 2) | ((prevm >> 14) & 3u);  // bit k <-> position p0 - 2 + k
       const uint32_t removed = (m_ext >> 1) & 0xFFFFu;           // bit j <-> match at p0 + j - 1
       const int valid = max(0, min(kPer, (int)cl - p0));
       const uint32_t vmask = valid >= kPer ? 0xFFFFu : ((1u << valid) - 1u);
       const int kc = __popc(~removed & vmask);
       const int nm = __popc(mask);
-      u64 hl = 0;
+      uint32_t hmask = 0;  // word headers among this lane's valid positions
 #pragma unroll
       for (int j = 0; j < kPer; ++j)
-        if (j < valid && is_hdr(v[j])) hl = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(v[j]);
-      u64 hdr_ex, hdr_tot;
-      int kc_ex, cnt_tot;
-      block_scan_hdr_cnt(hl, kc | (nm << 16), s_scan, &hdr_ex, &kc_ex, &hdr_tot, &cnt_tot);
-      kc_ex &= 0xFFFF;
-      const int kept = cnt_tot & 0xFFFF;
-      const int matches = cnt_tot >> 16;
-
-      // ---- compacted output (chunk-local)
-      {
-        int o = kc_ex;
-#pragma unroll
-        for (int j = 0; j < kPer; ++j)
-          if (j < valid && !((removed >> j) & 1u)) s_out[o++] = ((mask >> j) & 1u) ? X : v[j];
+        if (is_hdr(v[j])) hmask |= 1u << j;
+      hmask &= vmask;
+      u64 hl = 0;
+      if (hmask) {
+        const int j = 31 - __clz(hmask);
+        hl = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(st[2 + p0 + j]);
       }
+      const u64 hinc = wave_incl_max(hl);
+      u64 hdr_ex = __shfl_up(hinc, 1, 64);
+      if (lane == 0) hdr_ex = 0;
+      const u64 hdr_tot = __shfl(hinc, 63, 64);
+      const int cinc = wave_incl_sum(kc | (nm << 16));
+      const int ctot = __shfl(cinc, 63, 64);
+      const int kc_ex = (cinc - (kc | (nm << 16))) & 0xFFFF;
+      const int kept = ctot & 0xFFFF;
+      const int matches = ctot >> 16;
+
       // ---- neighbour deltas, 4 per occurrence (bpe.cpp:274-290)
       if (mask) {
-        u64 hdr = hdr_ex > c_hdr ? hdr_ex : c_hdr;
-        for (int j = 0; j < kPer; ++j) {
-          if (j < valid && is_hdr(v[j])) hdr = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(v[j]);
-          if (!((mask >> j) & 1u)) continue;
+        const u64 hdr_in = hdr_ex > c_hdr ? hdr_ex : c_hdr;
+        for (uint32_t mrem = mask; mrem; mrem &= mrem - 1) {
+          const int j = __ffs(mrem) - 1;
+          const uint32_t hb = hmask & ((2u << j) - 1u);  // headers at or before j in this lane
+          u64 hdr = hdr_in;
+          if (hb) {
+            const int jh = 31 - __clz(hb);
+            hdr = ((u64)(cs + p0 + jh + 1) << 32) | hdr_rank(st[2 + p0 + jh]);
+          }
           const uint32_t hidx = (uint32_t)(hdr >> 32) - 1u;
           const uint32_t rank = (uint32_t)hdr;
           const uint32_t gi = cs + p0 + j;
           const u64 w = kWeighted ? p.weight[rank] : 1ull;
           const u64 ftb = ((u64)rank << 32) | ((u64)(gi - hidx - 1u) << 2);
           if (gi - 1u > hidx) {  // left neighbour inside the word; X if it was just merged
-            const int32_t left = ((m_ext >> j) & 1u) ? X : s_tok[1 + p0 + j];
+            const int32_t left = ((m_ext >> j) & 1u) ? X : st[1 + p0 + j];
             const uint32_t sl = slot_of(left, p.slot_cap) << 2;
             delta_emit(h, p, sl | kOldLeft, w, ftb | kOldLeft);
             delta_emit(h, p, sl | kNewLeft, w, ftb | kNewLeft);
           }
-          const int32_t right = s_tok[4 + p0 + j];  // original token after b
+          const int32_t right = st[4 + p0 + j];  // original token after b
           if (!is_hdr(right)) {
             const uint32_t sr = slot_of(right, p.slot_cap) << 2;
             delta_emit(h, p, sr | kOldRight, w, ftb | kOldRight);
@@ -335,38 +374,113 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
           }
         }
       }
-      __syncthreads();  // s_out complete
-      if (dirty || matches > 0 || kept != (int)cl) {
-        for (int j = tid; j < kept; j += kThreads) base[c_out + j] = s_out[j];
+      const bool write = dirty || matches > 0 || kept != (int)cl;
+      if (write) {
+        wave_lds_sync();  // every neighbour read is done: compact in place
+        int o = kc_ex;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if (j < valid && !((removed >> j) & 1u)) st[2 + o++] = ((mask >> j) & 1u) ? X : v[j];
+        wave_lds_sync();
+        for (int j = lane; j < kept; j += 64) base[c_out + j] = st[2 + j];
         dirty = true;
         n_written += (u64)kept;
       }
       n_merged += (u64)matches;
       // ---- carries to the next chunk of this tile
       c_out += (uint32_t)kept;
-      c_m1 = (s_mask[(cl - 1) / kPer] >> ((cl - 1) % kPer)) & 1u;
-      c_m2 = cl >= 2 ? ((s_mask[(cl - 2) / kPer] >> ((cl - 2) % kPer)) & 1u) : c_m1;
-      c_t2 = cl >= 2 ? s_tok[2 + cl - 2] : s_tok[1];
-      c_t1 = s_tok[2 + cl - 1];
+      c_m1 = (__shfl(mask, (int)((cl - 1) / kPer), 64) >> ((cl - 1) % kPer)) & 1u;
+      c_m2 = cl >= 2 ? ((__shfl(mask, (int)((cl - 2) / kPer), 64) >> ((cl - 2) % kPer)) & 1u) : c_m1;
+      c_t1 = last1;
+      c_t2 = last2;
       c_hdr = hdr_tot > c_hdr ? hdr_tot : c_hdr;
       if (same) c_nona = nona_tot > c_nona ? nona_tot : c_nona;
-      __syncthreads();  // before the next chunk reuses s_tok / s_out / s_mask
+      wave_lds_sync();  // the copy-out reads st before the next chunk overwrites it
     }
-    if (dirty && tid == 0) p.tile_len[tile] = c_out;
+    if (dirty && lane == 0) p.tile_len[tile] = c_out;
+  }
+  if (lane == 0) {
+    if (n_merged) atomicAdd(&s_cnt[0], n_merged);
+    if (n_written) atomicAdd(&s_cnt[1], n_written);
   }
   __syncthreads();
-  for (int i = tid; i < kDeltaLds; i += kThreads)
+  for (int i = threadIdx.x; i < kDeltaLdsW; i += kThreads)
     if (h.key[i] != kEmpty32) delta_global(p, h.key[i], h.sum[i], h.ft[i]);
-  if (tid == 0) {
-    if (n_merged) atomicAdd(&p.stats[0], n_merged);
-    if (n_written) atomicAdd(&p.stats[1], n_written);
+  if (threadIdx.x == 0) {
+    if (s_cnt[0]) atomicAdd(&p.stats[0], s_cnt[0]);
+    if (s_cnt[1]) atomicAdd(&p.stats[1], s_cnt[1]);
+  }
+  // ---- completion: the slot tables are only ever touched by device-scope atomics (performed
+  // at the memory side), so every wave draining its own vmcnt before the ticket is the whole
+  // hand-off; the collector reads them with atomics too (MI355X_MICROARCH.md, valid forms).
+  // Tickets are sharded by blockIdx % 8 so no counter sees more than gridDim/8 arrivals.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t g = blockIdx.x & 7u;
+    const uint32_t in_group = (gridDim.x - g + 7u) >> 3;
+    bool last = false;
+    if (atomicAdd(&p.done[g], 1u) == in_group - 1u) {
+      atomicExch(&p.done[g], 0u);
+      const uint32_t groups = gridDim.x < 8u ? gridDim.x : 8u;
+      last = atomicAdd(&p.done[8], 1u) == groups - 1u;
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) s_cnt[0] = atomicAdd(p.dcount, 0u);
+  __syncthreads();
+  const uint32_t n = (uint32_t)s_cnt[0];
+  const bool collect = p.fused && n <= kFusedCollectMax;
+  if (collect) {
+    for (uint32_t i0 = 0; i0 < n; i0 += kThreads * 4) {
+      uint32_t key[4];
+      u64 sum[4], ft[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t i = i0 + k * kThreads + threadIdx.x;
+        key[k] = i < n ? atomicOr(&p.dlist[i], 0u) : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t i = i0 + k * kThreads + threadIdx.x;
+        if (i < n) {
+          sum[k] = atomicExch(&p.dsum[key[k]], 0ull);
+          ft[k] = atomicExch(&p.dft[key[k]], kEmpty64);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t i = i0 + k * kThreads + threadIdx.x;
+        if (i < n) {
+          DeltaRecord r;
+          r.key = key[k];
+          r.pad = 0;
+          r.sum = sum[k];
+          r.ft = ft[k];
+          p.out[i] = r;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (p.fused) {
+      if (collect) atomicExch(p.dcount, 0u);
+      p.hstats[0] = atomicExch(&p.stats[0], 0ull);
+      p.hstats[1] = atomicExch(&p.stats[1], 0ull);
+      p.hcount[0] = collect ? n : (n | kNeedCollect);
+    }
+    atomicExch(&p.done[8], 0u);
+    __threadfence_system();
+    __hip_atomic_store(&p.hcount[1], p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
 // K4: touched slots -> records in host-visible memory; clears the slots for the next merge.
-__global__ __launch_bounds__(kThreads) void k_collect(const uint32_t* dcount, uint32_t* dcount_next, const uint32_t* dlist,
-                                                       u64* dsum, u64* dft, DeltaRecord* out, uint32_t* out_count,
-                                                       u64* stats, u64* out_stats) {
+__global__ __launch_bounds__(kThreads) void k_collect(uint32_t* dcount, const uint32_t* dlist, u64* dsum, u64* dft,
+                                                       DeltaRecord* out) {
   const uint32_t n = *dcount;
   for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
     const uint32_t key = dlist[i];
@@ -379,13 +493,9 @@ __global__ __launch_bounds__(kThreads) void k_collect(const uint32_t* dcount, ui
     dsum[key] = 0;
     dft[key] = kEmpty64;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *out_count = n;
-    *dcount_next = 0;
-    out_stats[0] = stats[0];
-    out_stats[1] = stats[1];
-  }
 }
+
+__global__ void k_zero_u32(uint32_t* p) { *p = 0; }
 
 // K4 (multi-GPU): after the all-reduce every rank scans the dense prefix instead of its own list.
 __global__ __launch_bounds__(kThreads) void k_collect_dense(uint32_t nkeys, u64* dsum, u64* dft, DeltaRecord* out,
@@ -605,8 +715,12 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, ordinal_));
   cu_count_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  HIP_OK(hipHostMalloc((void**)&host_count_, 64, hipHostMallocMapped));
+  HIP_OK(hipHostMalloc((void**)&host_count_, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(host_count_, 0, 64);
+  HIP_OK(hipHostGetDevicePointer(&dev_count_, host_count_, 0));
+  int nb = 0;  // resident workgroups of k_merge per CU
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_merge<true>), kThreads, 0));
+  merge_blocks_per_cu_ = nb > 0 ? nb : 4;
 }
 
 void Device::free_all() {
@@ -651,7 +765,8 @@ void Device::upload(const WordTable& wt, Layout layout, size_t begin, size_t end
   auto rank_of = [&](size_t e) -> uint32_t { return stream ? wt.occurrence_rank[e] : (uint32_t)e; };
   auto len_of = [&](uint32_t r) -> uint64_t { return wt.offset[r + 1] - wt.offset[r]; };
 
-  // Tile boundaries: whole words, <= kChunk tokens unless one word alone is longer.
+  // Tile boundaries: whole words, <= kWaveTok tokens (one wave chunk) unless one word alone is
+  // longer (that tile is walked chunk by chunk).
   std::vector<uint64_t> off;
   std::vector<uint32_t> lens;
   std::vector<size_t> first_entry;
@@ -659,7 +774,7 @@ void Device::upload(const WordTable& wt, Layout layout, size_t begin, size_t end
   for (size_t e = begin; e < end; ++e) {
     const uint64_t need = len_of(rank_of(e)) + 1;
     if (need >= (1ull << 31)) fatal("word longer than 2^31 tokens");
-    if (fill > 0 && fill + need > (uint64_t)kChunk) {
+    if (fill > 0 && fill + need > (uint64_t)kWaveTok) {
       lens.push_back((uint32_t)fill);
       pos += (fill + 3) & ~3ull;
       fill = 0;
@@ -756,14 +871,14 @@ void Device::ensure_slots(uint32_t need) {
   dsum_ = dalloc<uint64_t>(keys + 2, &bytes_alloc_);  // + 2 stats words at the end
   dft_ = dalloc<uint64_t>(keys, &bytes_alloc_);
   dlist_ = dalloc<uint32_t>(keys, &bytes_alloc_);
-  dcount_ = dalloc<uint32_t>(2, &bytes_alloc_);
+  dcount_ = dalloc<uint32_t>(16, &bytes_alloc_);  // [0] count, [1..9] tickets
   HIP_OK(hipMemsetAsync(dsum_, 0, (keys + 2) * sizeof(u64), S(stream_)));
   HIP_OK(hipMemsetAsync(dft_, 0xFF, keys * sizeof(u64), S(stream_)));
-  HIP_OK(hipMemsetAsync(dcount_, 0, 2 * sizeof(uint32_t), S(stream_)));
-  HIP_OK(hipHostMalloc((void**)&host_recs_, keys * sizeof(DeltaRecord), hipHostMallocMapped));
+  HIP_OK(hipMemsetAsync(dcount_, 0, 16 * sizeof(uint32_t), S(stream_)));
+  HIP_OK(hipHostMalloc((void**)&host_recs_, keys * sizeof(DeltaRecord), hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_OK(hipHostGetDevicePointer(&dev_recs_, host_recs_, 0));
   host_recs_cap_ = keys;
   slot_cap_ = cap;
-  parity_ = 0;
   HIP_OK(hipStreamSynchronize(S(stream_)));
 }
 
@@ -818,63 +933,96 @@ void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
   for (void* p : {(void*)tkey, (void*)tcnt, (void*)tft, (void*)flags, (void*)dout}) HIP_OK(hipFree(p));
 }
 
+void Device::flush_timing() {
+  if (!timing_pending_) return;
+  timing_pending_ = false;
+  HIP_OK(hipEventSynchronize((hipEvent_t)ev_[1]));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]));
+  times_.merge_ms += ms;
+  times_.merge_launches += 1;
+  times_.merge_bytes += pending_bytes_;
+}
+
 void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
   HIP_OK(hipSetDevice(ordinal_));
   max_id_seen_ = std::max(max_id_seen_, X);
   ensure_slots((uint32_t)X + 1);
+  flush_timing();
   if (!ntiles_) return;
+  ++seq_;
   MergeParams mp{tok_, tile_off_, tile_len_, (uint32_t)ntiles_, weight_, a, b, X, slot_cap_,
-                 U(dsum_), U(dft_), dlist_, dcount_ + parity_, U(dsum_) + 4 * ((size_t)slot_cap_ + 1)};
-  const int grid = (int)std::min<size_t>(ntiles_, (size_t)cu_count_ * 3);
+                 U(dsum_), U(dft_), dlist_, dcount_, U(dsum_) + 4 * ((size_t)slot_cap_ + 1), dcount_ + 1,
+                 exchange_ ? 0 : 1, (DeltaRecord*)dev_recs_, (uint32_t*)dev_count_,
+                 (u64*)((char*)dev_count_ + 16), seq_};
+  const size_t groups = (ntiles_ + kWaves - 1) / kWaves;
+  const int grid = (int)std::min<size_t>(groups, (size_t)cu_count_ * merge_blocks_per_cu_);
   if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[0], S(stream_)));
   if (layout_ == Layout::kStream) k_merge<false><<<grid, kThreads, 0, S(stream_)>>>(mp);
   else k_merge<true><<<grid, kThreads, 0, S(stream_)>>>(mp);
   HIP_OK(hipGetLastError());
-  if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[1], S(stream_)));
+  if (timing_) {
+    HIP_OK(hipEventRecord((hipEvent_t)ev_[1], S(stream_)));
+    timing_pending_ = true;
+    pending_bytes_ = 4.0 * (double)live_tokens_est_ + 12.0 * (double)ntiles_;
+  }
+}
+
+// Spins on the host-visible flag the last workgroup raises (much cheaper than a stream sync).
+void Device::wait_flag() {
+  volatile uint32_t* flag = host_count_ + 1;
+  const double t0 = now_seconds();
+  unsigned spins = 0;
+  while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq_) {
+    __builtin_ia32_pause();
+    if (++spins % 4096 == 0 && now_seconds() - t0 > 120.0) {
+      const hipError_t e = hipStreamQuery(S(stream_));
+      if (e != hipSuccess && e != hipErrorNotReady) HIP_OK(e);
+      if (now_seconds() - t0 > 600.0) fatal("k_merge did not signal completion within 600 s");
+    }
+  }
 }
 
 size_t Device::collect(int32_t X, const DeltaRecord** recs) {
   HIP_OK(hipSetDevice(ordinal_));
   (void)X;
-  if (!ntiles_ && !dsum_) {
-    *recs = nullptr;
-    return 0;
-  }
-  u64* stats = U(dsum_) + 4 * ((size_t)slot_cap_ + 1);
-  DeltaRecord* drec = nullptr;
-  uint32_t* dcnt = nullptr;
-  u64* dstats = nullptr;
-  HIP_OK(hipHostGetDevicePointer((void**)&drec, host_recs_, 0));
-  HIP_OK(hipHostGetDevicePointer((void**)&dcnt, host_count_, 0));
-  dstats = (u64*)((char*)dcnt + 16);
-  if (exchange_) {
-    const size_t nkeys = 4 * ((size_t)slot_cap_ + 1);
-    exchange_(exchange_ctx_, dsum_, dft_, nkeys, stream_);
-    HIP_OK(hipMemsetAsync(dcount_, 0, 2 * sizeof(uint32_t), S(stream_)));
-    k_collect_dense<<<256, kThreads, 0, S(stream_)>>>((uint32_t)nkeys, U(dsum_), U(dft_), drec, dcount_);
-    HIP_OK(hipMemcpyAsync(host_count_, dcount_, sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
-    HIP_OK(hipMemsetAsync(dcount_, 0, 2 * sizeof(uint32_t), S(stream_)));
-    HIP_OK(hipMemcpyAsync((u64*)(host_count_ + 4), stats, 2 * sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
-    HIP_OK(hipMemsetAsync(stats, 0, 2 * sizeof(u64), S(stream_)));
-  } else {
-    k_collect<<<64, kThreads, 0, S(stream_)>>>(dcount_ + parity_, dcount_ + (parity_ ^ 1), dlist_, U(dsum_), U(dft_), drec,
-                                               dcnt, stats, dstats);
-    HIP_OK(hipMemsetAsync(stats, 0, 2 * sizeof(u64), S(stream_)));
-  }
-  HIP_OK(hipGetLastError());
-  parity_ ^= 1;
-  HIP_OK(hipStreamSynchronize(S(stream_)));
+  *recs = host_recs_;
+  if (!ntiles_) return 0;
+  DeltaRecord* drec = (DeltaRecord*)dev_recs_;
+  wait_flag();
   const u64* hs = (const u64*)(host_count_ + 4);
-  if (timing_) {
-    float ms = 0;
-    HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]));
-    times_.merge_ms += ms;
-    times_.merge_launches += 1;
-    times_.merge_bytes += 4.0 * (double)live_tokens_est_ + 4.0 * (double)hs[1] + 12.0 * (double)ntiles_;
+  size_t n;
+  u64* stats = U(dsum_) + 4 * ((size_t)slot_cap_ + 1);
+  if (exchange_) {
+    // multi-GPU: all-reduce the live prefix of the slot tables, then every rank scans it
+    const uint32_t unk_slot = (unk_ >= 0 && (uint32_t)unk_ < slot_cap_) ? (uint32_t)unk_ : 0u;
+    const size_t top = std::max<uint32_t>((uint32_t)X, unk_slot);
+    const size_t nkeys = 4 * (std::min<size_t>(slot_cap_, top + 1) + 1);
+    exchange_(exchange_ctx_, dsum_, dft_, nkeys, stream_);
+    HIP_OK(hipMemsetAsync(dcount_, 0, sizeof(uint32_t), S(stream_)));
+    k_collect_dense<<<256, kThreads, 0, S(stream_)>>>((uint32_t)nkeys, U(dsum_), U(dft_), drec, dcount_);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(host_count_, dcount_, sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
+    HIP_OK(hipMemcpyAsync((u64*)(host_count_ + 4), stats, 2 * sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
+    HIP_OK(hipMemsetAsync(dcount_, 0, sizeof(uint32_t), S(stream_)));
+    HIP_OK(hipMemsetAsync(stats, 0, 2 * sizeof(u64), S(stream_)));
+    HIP_OK(hipStreamSynchronize(S(stream_)));
+    n = host_count_[0];
+  } else {
+    n = host_count_[0];
+    if (n & kNeedCollect) {  // too many touched slots for one workgroup: a wide collect pass
+      n &= ~kNeedCollect;
+      k_collect<<<256, kThreads, 0, S(stream_)>>>(dcount_, dlist_, U(dsum_), U(dft_), drec);
+      HIP_OK(hipGetLastError());
+      k_zero_u32<<<1, 1, 0, S(stream_)>>>(dcount_);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipStreamSynchronize(S(stream_)));
+    }
   }
   live_tokens_est_ -= hs[0];
-  *recs = host_recs_;
-  return host_count_[0];
+  records_total_ += n;
+  records_max_ = std::max<uint64_t>(records_max_, n);
+  return n;
 }
 
 void Device::token_freq(size_t T, std::vector<uint64_t>* freq) {

@@ -69,8 +69,18 @@ class Device {
   void download_tokens(std::vector<int32_t>* out);
 
   void set_timing(bool on) { timing_ = on; }
-  const KernelTimes& times() const { return times_; }
-  void clear_times() { times_ = KernelTimes(); }
+  const KernelTimes& times() {
+    flush_timing();
+    return times_;
+  }
+  void set_unk(int32_t unk) { unk_ = unk; }
+  uint64_t records_total() const { return records_total_; }
+  uint64_t records_max() const { return records_max_; }
+  void clear_times() {
+    flush_timing();
+    times_ = KernelTimes();
+    records_total_ = records_max_ = 0;
+  }
   uint64_t live_tokens();  // Σ tile_len (headers included)
   size_t num_tiles() const { return ntiles_; }
   size_t device_bytes() const { return bytes_alloc_; }
@@ -80,6 +90,8 @@ class Device {
  private:
   void ensure_slots(uint32_t need);
   void free_all();
+  void wait_flag();
+  void flush_timing();
 
   int ordinal_ = 0;
   void* stream_ = nullptr;
@@ -108,10 +120,17 @@ class Device {
   uint64_t* dsum_ = nullptr;
   uint64_t* dft_ = nullptr;
   uint32_t* dlist_ = nullptr;
-  uint32_t* dcount_ = nullptr;  // two alternating counters
-  uint32_t parity_ = 0;
+  uint32_t* dcount_ = nullptr;  // [0] touched-slot count, [1] workgroup completion ticket
+  uint32_t seq_ = 0;            // merge sequence number echoed by the device flag
+  int32_t unk_ = 0;
+  bool timing_pending_ = false;
+  double pending_bytes_ = 0;
+  uint64_t records_total_ = 0, records_max_ = 0;
   int32_t max_id_seen_ = 0;
 
+  void* dev_recs_ = nullptr;            // device address of host_recs_
+  void* dev_count_ = nullptr;           // device address of host_count_
+  int merge_blocks_per_cu_ = 4;
   DeltaRecord* host_recs_ = nullptr;   // pinned, device-visible
   uint32_t* host_count_ = nullptr;     // pinned, device-visible
   size_t host_recs_cap_ = 0;

@@ -43,6 +43,7 @@ struct Trainer {
   int device = -1;
   // stats
   double load_s = 0, init_s = 0, train_s = 0;
+  double select_s = 0, launch_s = 0, wait_s = 0, apply_s = 0;
 };
 
 namespace {
@@ -71,6 +72,10 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
   } else if (key == "timing") {
     t->timing = std::atoi(val.c_str()) != 0;
     if (t->dev) t->dev->set_timing(t->timing);
+  } else if (key == "clear_stats") {
+    t->select_s = t->launch_s = t->wait_s = t->apply_s = 0;
+    t->init_s = t->train_s = 0;
+    if (t->dev) t->dev->clear_times();
   } else if (key == "device") {
     t->device = std::atoi(val.c_str());
   } else {
@@ -100,6 +105,7 @@ bool ensure_device(Trainer* t, const char* caller) {
     if (n > 0) ord = ord % n;
     t->dev.reset(new Device(ord));
     t->dev->set_timing(t->timing);
+    t->dev->set_unk(t->config.unk_id);
     if (dist_active()) t->dev->set_exchange(exchange_allreduce, nullptr);
   }
   if (t->device_stale) {
@@ -133,7 +139,11 @@ void count_into_selector(Trainer* t) {
 bool merge_one(Trainer* t) {
   int32_t a, b;
   uint64_t freq;
-  if (!t->sel.select(&a, &b, &freq)) return false;
+  const double t0 = now_seconds();
+  const bool ok = t->sel.select(&a, &b, &freq);
+  const double t1 = now_seconds();
+  t->select_s += t1 - t0;
+  if (!ok) return false;
   const int32_t X = kBaseVocab + (int32_t)t->num_merges;
   if (t->log >= 2)
     std::printf("[MERGE]\t Merging (%d,%d) freq=%llu -> new_id=%d (merge %zu)\n", a, b, (unsigned long long)freq, X,
@@ -142,9 +152,15 @@ bool merge_one(Trainer* t) {
   t->merge_a.push_back(a);
   t->merge_b.push_back(b);
   t->dev->merge_scan(a, b, X);
+  const double t2 = now_seconds();
   const DeltaRecord* recs = nullptr;
   const size_t n = t->dev->collect(X, &recs);
+  const double t3 = now_seconds();
   t->sel.apply(a, b, X, recs, n);
+  const double t4 = now_seconds();
+  t->launch_s += t2 - t1;
+  t->wait_s += t3 - t2;
+  t->apply_s += t4 - t3;
   t->num_merges++;
   return true;
 }
@@ -343,6 +359,10 @@ int shred_get_stats(const Trainer* t, ShredStats* s) {
   s->load_seconds = t->load_s;
   s->init_seconds = t->init_s;
   s->train_seconds = t->train_s;
+  s->host_select_seconds = t->select_s;
+  s->host_launch_seconds = t->launch_s;
+  s->host_wait_seconds = t->wait_s;
+  s->host_apply_seconds = t->apply_s;
   if (t->dev) {
     const KernelTimes& k = t->dev->times();
     s->merge_kernel_ms = k.merge_ms;

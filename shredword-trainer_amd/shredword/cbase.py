@@ -49,6 +49,8 @@ class BPEConfig(Structure):
 
 class ShredStats(Structure):
     _fields_ = [("load_seconds", c_double), ("init_seconds", c_double), ("train_seconds", c_double),
+                ("host_select_seconds", c_double), ("host_launch_seconds", c_double),
+                ("host_wait_seconds", c_double), ("host_apply_seconds", c_double),
                 ("merge_kernel_ms", c_double), ("count_kernel_ms", c_double),
                 ("merge_kernel_bytes", c_double), ("count_kernel_bytes", c_double),
                 ("merge_launches", c_uint64), ("count_launches", c_uint64),
