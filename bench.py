@@ -211,7 +211,7 @@ def main():
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
                 "avg_launch_us": 1e3 * mk_ms, "avg_bytes_per_launch": mk_bytes,
-                "launches": st["merge_launches"],
+                "launches_sampled": st["merge_launches"], "launches": merges,
             },
             "pair_count": {
                 "kernel": "k_pair_count (K1)", "avg_launch_us": 1e3 * k1_ms, "bytes_per_launch": k1_bytes,
@@ -219,7 +219,7 @@ def main():
             },
             "load_s": load_s, "corpus_gen_s": gen_s,
             "us_per_merge": 1e6 * elapsed / max(1, merges),
-            "merge_kernel_share": (st["merge_kernel_ms"] * 1e-3) / elapsed if elapsed > 0 else None,
+            "merge_kernel_share": (mk_ms * 1e-3 * merges) / elapsed if elapsed > 0 else None,
             "host_breakdown_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
             "init_s_last_step": st["init_seconds"],
         }

@@ -23,6 +23,7 @@
 
 #include "../host/common.h"
 #include "../host/device.h"
+#include "../host/dist.h"
 
 namespace shred {
 
@@ -153,6 +154,7 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kDeltaLdsW = 512;
 constexpr uint32_t kFusedCollectMax = 4096;  // beyond this the host launches k_collect
 constexpr uint32_t kNeedCollect = 0x80000000u;
+constexpr uint32_t kTimingStride = 8;
 
 struct MergeParams {
   int32_t* tok;
@@ -752,82 +754,34 @@ Device::~Device() {
   if (stream_) (void)hipStreamDestroy(S(stream_));
 }
 
-void Device::upload(const WordTable& wt, Layout layout, size_t begin, size_t end) {
+void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint64_t>& weights, int32_t max_id) {
   HIP_OK(hipSetDevice(ordinal_));
   HIP_OK(hipStreamSynchronize(S(stream_)));
   free_all();
   layout_ = layout;
-  const bool stream = layout == Layout::kStream;
-  const size_t nent = stream ? wt.occurrence_rank.size() : wt.num_words();
-  if (stream && nent == 0 && wt.total_occurrences > 0) fatal("stream layout requested without occurrence ranks");
-  end = std::min(end, nent);
-  begin = std::min(begin, end);
-  auto rank_of = [&](size_t e) -> uint32_t { return stream ? wt.occurrence_rank[e] : (uint32_t)e; };
-  auto len_of = [&](uint32_t r) -> uint64_t { return wt.offset[r + 1] - wt.offset[r]; };
-
-  // Tile boundaries: whole words, <= kWaveTok tokens (one wave chunk) unless one word alone is
-  // longer (that tile is walked chunk by chunk).
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> lens;
-  std::vector<size_t> first_entry;
-  uint64_t pos = 0, fill = 0;
-  for (size_t e = begin; e < end; ++e) {
-    const uint64_t need = len_of(rank_of(e)) + 1;
-    if (need >= (1ull << 31)) fatal("word longer than 2^31 tokens");
-    if (fill > 0 && fill + need > (uint64_t)kWaveTok) {
-      lens.push_back((uint32_t)fill);
-      pos += (fill + 3) & ~3ull;
-      fill = 0;
-    }
-    if (fill == 0) {
-      off.push_back(pos);
-      first_entry.push_back(e);
-    }
-    fill += need;
-  }
-  if (fill > 0) {
-    lens.push_back((uint32_t)fill);
-    pos += (fill + 3) & ~3ull;
-  }
-  ntiles_ = lens.size();
-  tok_elems_ = pos;
-  first_entry.push_back(end);
-
-  std::vector<int32_t> host(pos + 4, kPad);
-  for (size_t t = 0; t < ntiles_; ++t) {
-    int32_t* dst = host.data() + off[t];
-    for (size_t e = first_entry[t]; e < first_entry[t + 1]; ++e) {
-      const uint32_t r = rank_of(e);
-      *dst++ = (int32_t)((uint32_t)kHeaderBase + r);
-      const uint64_t o = wt.offset[r], l = len_of(r);
-      std::memcpy(dst, wt.symbols.data() + o, l * sizeof(int32_t));
-      dst += l;
-    }
-  }
-  live_tokens0_ = 0;
-  for (uint32_t l : lens) live_tokens0_ += l;
-  nentries_ = end - begin;
-  live_tokens_est_ = live_tokens0_;
-
-  tok_ = dalloc<int32_t>(pos + 4, &bytes_alloc_);
-  tok0_ = dalloc<int32_t>(pos + 4, &bytes_alloc_);
+  ntiles_ = ts.num_tiles();
+  tok_elems_ = ts.elems;
+  live_tokens0_ = ts.live;
+  live_tokens_est_ = ts.live;
+  nentries_ = ts.entries;
+  tok_ = dalloc<int32_t>(ts.elems + 4, &bytes_alloc_);
+  tok0_ = dalloc<int32_t>(ts.elems + 4, &bytes_alloc_);
   tile_off_ = dalloc<uint64_t>(ntiles_, &bytes_alloc_);
   tile_len_ = dalloc<uint32_t>(ntiles_, &bytes_alloc_);
   tile_len0_ = dalloc<uint32_t>(ntiles_, &bytes_alloc_);
-  HIP_OK(hipMemcpyAsync(tok0_, host.data(), (pos + 4) * sizeof(int32_t), hipMemcpyHostToDevice, S(stream_)));
+  HIP_OK(hipMemcpyAsync(tok0_, ts.tok.data(), (ts.elems + 4) * sizeof(int32_t), hipMemcpyHostToDevice, S(stream_)));
   if (ntiles_) {
-    HIP_OK(hipMemcpyAsync(tile_off_, off.data(), ntiles_ * sizeof(uint64_t), hipMemcpyHostToDevice, S(stream_)));
-    HIP_OK(hipMemcpyAsync(tile_len0_, lens.data(), ntiles_ * sizeof(uint32_t), hipMemcpyHostToDevice, S(stream_)));
+    HIP_OK(hipMemcpyAsync(tile_off_, ts.off.data(), ntiles_ * sizeof(uint64_t), hipMemcpyHostToDevice, S(stream_)));
+    HIP_OK(hipMemcpyAsync(tile_len0_, ts.len.data(), ntiles_ * sizeof(uint32_t), hipMemcpyHostToDevice, S(stream_)));
   }
-  if (!stream) {
-    weight_ = dalloc<uint64_t>(wt.num_words(), &bytes_alloc_);
-    if (wt.num_words())
-      HIP_OK(hipMemcpyAsync(weight_, wt.count.data(), wt.num_words() * sizeof(uint64_t), hipMemcpyHostToDevice, S(stream_)));
+  if (layout == Layout::kTypes) {
+    weight_ = dalloc<uint64_t>(weights.size(), &bytes_alloc_);
+    if (!weights.empty())
+      HIP_OK(hipMemcpyAsync(weight_, weights.data(), weights.size() * sizeof(uint64_t), hipMemcpyHostToDevice,
+                            S(stream_)));
   }
-  HIP_OK(hipStreamSynchronize(S(stream_)));  // host staging buffers go out of scope
-  max_id_seen_ = 0;
-  for (int c = 0; c < 256; ++c)
-    if (wt.keep[c]) max_id_seen_ = c;
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  max_id_seen_ = max_id;
   uploaded_ = true;
   reset_tokens();
 }
@@ -885,7 +839,10 @@ void Device::ensure_slots(uint32_t need) {
 void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
   HIP_OK(hipSetDevice(ordinal_));
   out->clear();
-  if (!ntiles_) return;
+  if (!ntiles_) {
+    dist_merge_pairs(out);
+    return;
+  }
   // distinct pairs <= live tokens and <= (ids in play)^2
   const uint64_t live = live_tokens();
   const uint64_t ids = (uint64_t)std::max<int32_t>(max_id_seen_, kBaseVocab) + 2;
@@ -931,6 +888,7 @@ void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
                           (layout_ == Layout::kTypes ? 8.0 * (double)nentries_ : 0.0);
   }
   for (void* p : {(void*)tkey, (void*)tcnt, (void*)tft, (void*)flags, (void*)dout}) HIP_OK(hipFree(p));
+  dist_merge_pairs(out);
 }
 
 void Device::flush_timing() {
@@ -949,19 +907,24 @@ void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
   max_id_seen_ = std::max(max_id_seen_, X);
   ensure_slots((uint32_t)X + 1);
   flush_timing();
-  if (!ntiles_) return;
+  launched_ = false;
+  if (!ntiles_) return;  // an empty shard still joins collect()'s exchange
   ++seq_;
+  launched_ = true;
   MergeParams mp{tok_, tile_off_, tile_len_, (uint32_t)ntiles_, weight_, a, b, X, slot_cap_,
                  U(dsum_), U(dft_), dlist_, dcount_, U(dsum_) + 4 * ((size_t)slot_cap_ + 1), dcount_ + 1,
                  exchange_ ? 0 : 1, (DeltaRecord*)dev_recs_, (uint32_t*)dev_count_,
                  (u64*)((char*)dev_count_ + 16), seq_};
   const size_t groups = (ntiles_ + kWaves - 1) / kWaves;
   const int grid = (int)std::min<size_t>(groups, (size_t)cu_count_ * merge_blocks_per_cu_);
-  if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[0], S(stream_)));
+  // HIP events bracket every kTimingStride-th launch (an unbiased sample of launch durations
+  // that keeps event overhead out of the timed loop)
+  const bool sample = timing_ && (seq_ % kTimingStride == 0);
+  if (sample) HIP_OK(hipEventRecord((hipEvent_t)ev_[0], S(stream_)));
   if (layout_ == Layout::kStream) k_merge<false><<<grid, kThreads, 0, S(stream_)>>>(mp);
   else k_merge<true><<<grid, kThreads, 0, S(stream_)>>>(mp);
   HIP_OK(hipGetLastError());
-  if (timing_) {
+  if (sample) {
     HIP_OK(hipEventRecord((hipEvent_t)ev_[1], S(stream_)));
     timing_pending_ = true;
     pending_bytes_ = 4.0 * (double)live_tokens_est_ + 12.0 * (double)ntiles_;
@@ -987,9 +950,10 @@ size_t Device::collect(int32_t X, const DeltaRecord** recs) {
   HIP_OK(hipSetDevice(ordinal_));
   (void)X;
   *recs = host_recs_;
-  if (!ntiles_) return 0;
+  if (!ntiles_ && !exchange_) return 0;
   DeltaRecord* drec = (DeltaRecord*)dev_recs_;
-  wait_flag();
+  if (launched_) wait_flag();
+  launched_ = false;
   const u64* hs = (const u64*)(host_count_ + 4);
   size_t n;
   u64* stats = U(dsum_) + 4 * ((size_t)slot_cap_ + 1);
@@ -1028,7 +992,10 @@ size_t Device::collect(int32_t X, const DeltaRecord** recs) {
 void Device::token_freq(size_t T, std::vector<uint64_t>* freq) {
   HIP_OK(hipSetDevice(ordinal_));
   freq->assign(T, 0);
-  if (!ntiles_ || !T) return;
+  if (!ntiles_ || !T) {
+    dist_allreduce_host(freq->data(), T, false);
+    return;
+  }
   size_t acc = 0;
   u64* d = dalloc<u64>(T, &acc);
   HIP_OK(hipMemsetAsync(d, 0, T * sizeof(u64), S(stream_)));
@@ -1041,6 +1008,7 @@ void Device::token_freq(size_t T, std::vector<uint64_t>* freq) {
   HIP_OK(hipMemcpyAsync(freq->data(), d, T * sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
   HIP_OK(hipStreamSynchronize(S(stream_)));
   HIP_OK(hipFree(d));
+  dist_allreduce_host(freq->data(), T, false);
 }
 
 void Device::download_tokens(std::vector<int32_t>* out) {

@@ -17,11 +17,11 @@
 #include <vector>
 
 #include "corpus.h"
+#include "engine.h"
 #include "selector.h"
+#include "tiles.h"
 
 namespace shred {
-
-enum class Layout { kTypes = 0, kStream = 1 };
 
 struct KernelTimes {
   double merge_ms = 0;   // Σ k_merge durations (HIP events on the trainer stream)
@@ -33,7 +33,7 @@ struct KernelTimes {
   double count_bytes = 0;  // Σ algorithmic bytes of k_pair_count (tokens + boundaries + weights)
 };
 
-class Device {
+class Device : public Backend {
  public:
   // True when a HIP device is usable; otherwise *why says what is missing.
   static bool available(std::string* why);
@@ -43,28 +43,29 @@ class Device {
   Device(const Device&) = delete;
   Device& operator=(const Device&) = delete;
 
-  // Packs the word table into tiles and uploads it (types: one entry per distinct word;
-  // stream: one entry per occurrence).  Keeps a pristine copy for reset_tokens().
-  void upload(const WordTable& wt, Layout layout, size_t rank_begin = 0, size_t rank_end = SIZE_MAX);
+  // Uploads a packed tile stream (types: one entry per distinct word, weights = counts; stream:
+  // one entry per occurrence, weight 1) and keeps a pristine copy for reset_tokens().
+  void upload(const TiledStream& ts, Layout layout, const std::vector<uint64_t>& weights, int32_t max_id);
   // Restores the token stream to its uploaded (unmerged) state.
   void reset_tokens();
   bool has_tokens() const { return ntiles_ > 0 || uploaded_; }
 
-  // K1: weighted pair histogram with first touch, pairs holding unk skipped (bpe.cpp:187-206).
-  void count_pairs(int32_t unk_id, std::vector<PairCount>* out);
+  // K1: weighted pair histogram with first touch, pairs holding unk skipped (bpe.cpp:187-206);
+  // under RCCL the per-rank lists are merged (sum, min first touch).
+  void count_pairs(int32_t unk_id, std::vector<PairCount>* out) override;
 
   // K2+K3 for merge (a,b)->X: rewrites every occurrence in place and reduces neighbour deltas
-  // into the slot tables (left there for exchange()).
-  void merge_scan(int32_t a, int32_t b, int32_t X);
+  // into the slot tables.
+  void merge_scan(int32_t a, int32_t b, int32_t X) override;
   // Multi-GPU hook: called between merge_scan and collect(); slot tables are
   // [prefix_slots * 4] u64 sums followed by the same count of u64 first-touch values.
   using ExchangeFn = void (*)(void* ctx, uint64_t* dsum, uint64_t* dft, size_t n, void* stream);
   void set_exchange(ExchangeFn fn, void* ctx) { exchange_ = fn; exchange_ctx_ = ctx; }
-  // K4: compacts the touched slots into records (host-visible) and clears them.
-  size_t collect(int32_t X, const DeltaRecord** recs);
+  // K4: the touched slots as records (host-visible), cleared for the next merge.
+  size_t collect(int32_t X, const DeltaRecord** recs) override;
 
   // K6: final weighted token histogram over ids [0, T); other ids are dropped.
-  void token_freq(size_t T, std::vector<uint64_t>* freq);
+  void token_freq(size_t T, std::vector<uint64_t>* freq) override;
   // Copies the live token stream back (tests): per entry, header then tokens.
   void download_tokens(std::vector<int32_t>* out);
 
@@ -122,6 +123,7 @@ class Device {
   uint32_t* dlist_ = nullptr;
   uint32_t* dcount_ = nullptr;  // [0] touched-slot count, [1] workgroup completion ticket
   uint32_t seq_ = 0;            // merge sequence number echoed by the device flag
+  bool launched_ = false;
   int32_t unk_ = 0;
   bool timing_pending_ = false;
   double pending_bytes_ = 0;

@@ -141,17 +141,4 @@ void dist_merge_pairs(std::vector<PairCount>* pairs) {
   pairs->swap(out);
 }
 
-void dist_split(const std::vector<uint64_t>& prefix, int rank, int world, size_t* begin, size_t* end) {
-  const size_t n = prefix.size() - 1;
-  const uint64_t total = prefix.back();
-  auto cut = [&](int r) -> size_t {
-    if (r <= 0) return 0;
-    if (r >= world) return n;
-    const uint64_t target = (uint64_t)((long double)total * r / world);
-    return (size_t)(std::lower_bound(prefix.begin(), prefix.end(), target) - prefix.begin());
-  };
-  *begin = std::min(cut(rank), n);
-  *end = std::min(cut(rank + 1), n);
-}
-
 }  // namespace shred

@@ -35,7 +35,5 @@ void dist_allreduce_device(uint64_t* dev_buf, size_t n, bool min_op, void* strea
 void dist_allreduce_host(uint64_t* host, size_t n, bool min_op);
 // Every rank's pair list, merged: counts summed, first touch min (synchronous).
 void dist_merge_pairs(std::vector<PairCount>* pairs);
-// Rank r's share [begin, end) of n weighted items, split at equal cumulative weight.
-void dist_split(const std::vector<uint64_t>& prefix_weight, int rank, int world, size_t* begin, size_t* end);
 
 }  // namespace shred

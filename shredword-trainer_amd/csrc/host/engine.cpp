@@ -1,0 +1,141 @@
+// BPE training driver: see engine.h.
+#include "engine.h"
+
+#include <string>
+
+#include "common.h"
+
+namespace shred {
+
+void Engine::configure(size_t target_vocab_size, int32_t unk_id, uint64_t min_pair_freq) {
+  target_vocab_ = target_vocab_size;
+  unk_ = unk_id;
+  min_freq_ = min_pair_freq;
+  sel_.reset(unk_, min_freq_);
+}
+
+void Engine::forget_merges() {
+  merge_a_.clear();
+  merge_b_.clear();
+  sel_.reset(unk_, min_freq_);
+}
+
+void Engine::count_bigrams(Backend& be) {
+  std::vector<PairCount> pairs;
+  be.count_pairs(unk_, &pairs);
+  const size_t unique = pairs.size();
+  sel_.add_counts(std::move(pairs));
+  if (log_ >= 1)
+    std::printf("[INFO]\t Counted %zu unique pairs\n[INFO]\t Added %zu pairs to heap (freq >= %llu)\n", unique,
+                sel_.heap_size(), (unsigned long long)min_freq_);
+}
+
+// One merge (bpe.cpp:244-318): false when the heap holds no valid candidate.
+bool Engine::merge_one(Backend& be) {
+  int32_t a, b;
+  uint64_t freq;
+  const double t0 = now_seconds();
+  const bool ok = sel_.select(&a, &b, &freq);
+  const double t1 = now_seconds();
+  times_.select_s += t1 - t0;
+  if (!ok) return false;
+  const int32_t X = kBaseVocab + (int32_t)merge_a_.size();
+  if (log_ >= 2)
+    std::printf("[MERGE]\t Merging (%d,%d) freq=%llu -> new_id=%d (merge %zu)\n", a, b, (unsigned long long)freq, X,
+                merge_a_.size() + 1);
+  if (trace_) std::fprintf(trace_, "M %d %d %llu %d\n", a, b, (unsigned long long)freq, X);
+  merge_a_.push_back(a);
+  merge_b_.push_back(b);
+  be.merge_scan(a, b, X);
+  const double t2 = now_seconds();
+  const DeltaRecord* recs = nullptr;
+  const size_t n = be.collect(X, &recs);
+  const double t3 = now_seconds();
+  sel_.apply(a, b, X, recs, n);
+  times_.launch_s += t2 - t1;
+  times_.wait_s += t3 - t2;
+  times_.apply_s += now_seconds() - t3;
+  return true;
+}
+
+int Engine::merge_batch(Backend& be, int batch) {
+  if (sel_.heap_empty()) {
+    if (log_ >= 2) std::printf("[INFO]\t Heap is empty, no more merges possible\n");
+    return 0;
+  }
+  int done = 0;
+  while (done < batch && !sel_.heap_empty()) {
+    if (!merge_one(be)) break;
+    ++done;
+  }
+  return done;
+}
+
+int Engine::train(Backend& be) {
+  const double t0 = now_seconds();
+  if (log_ >= 1) std::printf("[INFO]\t Starting BPE training (target vocab size: %zu)\n", target_vocab_);
+  sel_.reset(unk_, min_freq_);  // bpe_init (bpe.cpp:98-108)
+  count_bigrams(be);
+  times_.init_s += now_seconds() - t0;
+  int total = 0;
+  const int target = (int)target_vocab_ - kBaseVocab;  // bpe.cpp:353
+  while (total < target) {
+    if (sel_.heap_empty()) {
+      if (log_ >= 1) std::printf("[INFO]\t Heap exhausted, stopping training\n");
+      break;
+    }
+    const uint64_t tf = sel_.heap_top_freq();
+    int batch = tf > 50000 ? 10 : tf > 20000 ? 5 : tf > 10000 ? 3 : tf > 5000 ? 2 : 1;  // bpe.cpp:363-368
+    if (batch > target - total) batch = target - total;
+    if (trace_) std::fprintf(trace_, "B %d %d %zu %llu\n", batch, total, sel_.heap_size(), (unsigned long long)tf);
+    if (log_ >= 2)
+      std::printf("[INFO]\t Processing batch of %d merges (completed: %d/%d, heap size: %zu, top freq: %llu)\n", batch,
+                  total, target, sel_.heap_size(), (unsigned long long)tf);
+    int merged = 0;
+    while (merged < batch && !sel_.heap_empty()) {
+      if (!merge_one(be)) break;
+      ++merged;
+    }
+    if (merged <= 0) {
+      if (log_ >= 1) std::printf("[WARNING]\t No merges performed, stopping\n");
+      break;
+    }
+    total += merged;
+  }
+  if (trace_) std::fflush(trace_);
+  times_.train_s += now_seconds() - t0;
+  if (log_ >= 1) std::printf("[INFO]\t Training completed. Performed %d merges\n", total);
+  return total;
+}
+
+void Engine::write_outputs(const std::vector<uint64_t>& freq, const char* model_path, const char* vocab_path) const {
+  const size_t M = merge_a_.size(), T = kBaseVocab + M;
+  std::vector<std::string> tok(T);
+  for (size_t i = 1; i < (size_t)kBaseVocab; ++i) tok[i] = std::string(1, (char)i);  // tok[0]: "" as a C string
+  for (size_t m = 0; m < M; ++m) tok[kBaseVocab + m] = tok[merge_a_[m]] + tok[merge_b_[m]];
+  if (FILE* vf = std::fopen(vocab_path, "w")) {
+    for (size_t i = 0; i < T; ++i) {
+      std::fwrite(tok[i].data(), 1, tok[i].size(), vf);
+      std::fprintf(vf, " %llu\n", (unsigned long long)(i < freq.size() ? freq[i] : 0));
+    }
+    std::fclose(vf);
+  } else {
+    std::fprintf(stderr, "[ERROR]\t Couldn't open file: %s\n", vocab_path);
+  }
+  if (FILE* mf = std::fopen(model_path, "wb")) {
+    std::vector<int32_t> rec(3 * M);
+    for (size_t m = 0; m < M; ++m) {
+      rec[3 * m] = merge_a_[m];
+      rec[3 * m + 1] = merge_b_[m];
+      rec[3 * m + 2] = (int32_t)(kBaseVocab + m);
+    }
+    if (M) std::fwrite(rec.data(), sizeof(int32_t), rec.size(), mf);
+    std::fclose(mf);
+  } else {
+    std::fprintf(stderr, "[ERROR]\t Couldn't open file: %s\n", model_path);
+  }
+  if (log_ >= 1)
+    std::printf("[INFO]\tSaved %zu-token vocab to %s and %zu merges to %s\n", T, vocab_path, M, model_path);
+}
+
+}  // namespace shred

@@ -1,13 +1,12 @@
 // C ABI of the MI355X BPE trainer: include/shredword_bpe.h.
 //
-// Control flow mirrors the reference entry points (shredword/csrc/bpe/bpe.cpp) one for one:
-// create_trainer :67-85, bpe_trainer_destroy :87-96, bpe_init :98-108, bpe_load_corpus :110-185,
+// Entry points mirror the reference one for one (shredword/csrc/bpe/bpe.cpp): create_trainer
+// :67-85, bpe_trainer_destroy :87-96, bpe_init :98-108, bpe_load_corpus :110-185,
 // bpe_count_bigrams :187-230, bpe_merge_batch :232-323, bpe_train :345-386, bpe_save :388-432.
-// The merge loop's O(S) scans run on the GPU (Device); heap replay and pair info stay on the host
-// (Selector) because they decide merge order exactly.  There is no CPU fallback: without a usable
-// GPU, train/merge return -1 and save reports an error.
+// The O(S) scans run on the GPU (Device); heap replay and pair info stay on the host (Engine /
+// Selector) because they decide merge order exactly.  There is no CPU fallback: without a usable
+// GPU, train / merge_batch return -1 and save reports an error.
 #include <hip/hip_runtime.h>
-#include <sys/stat.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -21,7 +20,8 @@
 #include "corpus.h"
 #include "device.h"
 #include "dist.h"
-#include "selector.h"
+#include "engine.h"
+#include "tiles.h"
 
 using namespace shred;
 
@@ -31,19 +31,12 @@ struct Trainer {
   bool loaded = false;
   bool device_stale = true;
   std::unique_ptr<Device> dev;
-  Selector sel;
-  std::vector<int32_t> merge_a, merge_b;
-  size_t num_merges = 0;
-  // options
+  Engine engine;
   Layout layout = Layout::kTypes;
-  int log = 1;
-  std::string trace_path;
   FILE* trace = nullptr;
   bool timing = false;
   int device = -1;
-  // stats
-  double load_s = 0, init_s = 0, train_s = 0;
-  double select_s = 0, launch_s = 0, wait_s = 0, apply_s = 0;
+  double load_s = 0;
 };
 
 namespace {
@@ -60,21 +53,17 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
     else return -1;
     t->device_stale = true;
   } else if (key == "log") {
-    t->log = std::atoi(val.c_str());
+    t->engine.set_log(std::atoi(val.c_str()));
   } else if (key == "trace") {
     if (t->trace) std::fclose(t->trace);
-    t->trace = nullptr;
-    t->trace_path = val;
-    if (!val.empty()) {
-      t->trace = std::fopen(val.c_str(), "w");
-      if (!t->trace) return -1;
-    }
+    t->trace = val.empty() ? nullptr : std::fopen(val.c_str(), "w");
+    t->engine.set_trace(t->trace);
+    if (!val.empty() && !t->trace) return -1;
   } else if (key == "timing") {
     t->timing = std::atoi(val.c_str()) != 0;
     if (t->dev) t->dev->set_timing(t->timing);
   } else if (key == "clear_stats") {
-    t->select_s = t->launch_s = t->wait_s = t->apply_s = 0;
-    t->init_s = t->train_s = 0;
+    t->engine.times() = EngineTimes();
     if (t->dev) t->dev->clear_times();
   } else if (key == "device") {
     t->device = std::atoi(val.c_str());
@@ -89,7 +78,7 @@ void exchange_allreduce(void*, uint64_t* dsum, uint64_t* dft, size_t n, void* st
   dist_allreduce_device(dft, n, true, stream);
 }
 
-// Creates the device and uploads this rank's share of the corpus if needed.
+// Creates the device and uploads this rank's share of the word table if needed.
 bool ensure_device(Trainer* t, const char* caller) {
   if (!t->dev) {
     std::string why;
@@ -109,59 +98,21 @@ bool ensure_device(Trainer* t, const char* caller) {
     if (dist_active()) t->dev->set_exchange(exchange_allreduce, nullptr);
   }
   if (t->device_stale) {
-    if (t->layout == Layout::kStream && t->wt.occurrence_rank.size() != t->wt.total_occurrences)
-      fatal("layout=stream needs the corpus loaded with the stream layout selected (set it before load_corpus)");
-    size_t begin = 0, end = SIZE_MAX;
-    if (dist_active()) {
-      const bool stream = t->layout == Layout::kStream;
-      const size_t n = stream ? t->wt.occurrence_rank.size() : t->wt.num_words();
-      std::vector<uint64_t> prefix(n + 1, 0);
-      for (size_t e = 0; e < n; ++e) {
-        const uint32_t r = stream ? t->wt.occurrence_rank[e] : (uint32_t)e;
-        prefix[e + 1] = prefix[e] + (t->wt.offset[r + 1] - t->wt.offset[r]) + 1;
-      }
-      dist_split(prefix, dist_state().rank, dist_state().world, &begin, &end);
+    if (t->layout == Layout::kStream && t->wt.occurrence_rank.size() != t->wt.total_occurrences) {
+      std::fprintf(stderr, "[ERROR]\t %s: layout=stream must be selected before load_corpus\n", caller);
+      return false;
     }
-    t->dev->upload(t->wt, t->layout, begin, end);
+    size_t begin = 0, end = 0;
+    const int rank = dist_active() ? dist_state().rank : 0, world = dist_active() ? dist_state().world : 1;
+    shard_range(t->wt, t->layout, rank, world, &begin, &end);
+    TiledStream ts;
+    pack_tiles(t->wt, t->layout, begin, end, &ts);
+    int32_t max_id = 0;
+    for (int c = 0; c < 256; ++c)
+      if (t->wt.keep[c]) max_id = c;
+    t->dev->upload(ts, t->layout, t->wt.count, max_id);
     t->device_stale = false;
   }
-  return true;
-}
-
-void count_into_selector(Trainer* t) {
-  std::vector<PairCount> pairs;
-  t->dev->count_pairs(t->config.unk_id, &pairs);
-  dist_merge_pairs(&pairs);
-  t->sel.add_counts(std::move(pairs));
-}
-
-// One merge (bpe.cpp:259-318): returns false when the heap has no valid candidate left.
-bool merge_one(Trainer* t) {
-  int32_t a, b;
-  uint64_t freq;
-  const double t0 = now_seconds();
-  const bool ok = t->sel.select(&a, &b, &freq);
-  const double t1 = now_seconds();
-  t->select_s += t1 - t0;
-  if (!ok) return false;
-  const int32_t X = kBaseVocab + (int32_t)t->num_merges;
-  if (t->log >= 2)
-    std::printf("[MERGE]\t Merging (%d,%d) freq=%llu -> new_id=%d (merge %zu)\n", a, b, (unsigned long long)freq, X,
-                t->num_merges + 1);
-  if (t->trace) std::fprintf(t->trace, "M %d %d %llu %d\n", a, b, (unsigned long long)freq, X);
-  t->merge_a.push_back(a);
-  t->merge_b.push_back(b);
-  t->dev->merge_scan(a, b, X);
-  const double t2 = now_seconds();
-  const DeltaRecord* recs = nullptr;
-  const size_t n = t->dev->collect(X, &recs);
-  const double t3 = now_seconds();
-  t->sel.apply(a, b, X, recs, n);
-  const double t4 = now_seconds();
-  t->launch_s += t2 - t1;
-  t->wait_s += t3 - t2;
-  t->apply_s += t4 - t3;
-  t->num_merges++;
   return true;
 }
 
@@ -176,13 +127,13 @@ Trainer* create_trainer(const BPEConfig* config) {
   t->config = *config;
   if (t->config.character_coverage <= 0.0 || t->config.character_coverage >= 1.0) t->config.character_coverage = 0.995f;
   if (t->config.min_pair_freq == 0) t->config.min_pair_freq = kDefaultMinPairFreq;
-  t->sel.reset(t->config.unk_id, t->config.min_pair_freq);
-  t->log = env_int("SHREDWORD_LOG", 1);
+  t->engine.configure(t->config.target_vocab_size, t->config.unk_id, t->config.min_pair_freq);
+  t->engine.set_log(env_int("SHREDWORD_LOG", 1));
   t->timing = env_int("SHREDWORD_TIMING", 0) != 0;
   t->device = env_int("SHREDWORD_DEVICE", -1);
   if (const char* v = std::getenv("SHREDWORD_LAYOUT")) set_option(t, "layout", v);
   if (const char* v = std::getenv("SHREDWORD_TRACE")) set_option(t, "trace", v);
-  if (t->log >= 1) std::printf("[INFO]\t BPE trainer initialized. Heap initialized successfully.\n");
+  if (t->engine.log() >= 1) std::printf("[INFO]\t BPE trainer initialized. Heap initialized successfully.\n");
   return t;
 }
 
@@ -211,30 +162,26 @@ int bpe_load_corpus(Trainer* t, const char* path) {
   t->wt = std::move(wt);  // last load wins (bpe.cpp:176-178)
   t->loaded = true;
   t->device_stale = true;
-  t->sel.reset(t->config.unk_id, t->config.min_pair_freq);
-  if (t->log >= 1)
+  t->engine.reset_selection();
+  if (t->engine.log() >= 1)
     std::printf("[DEBUG]\t Character histogram built with %zu unique characters.\n", t->wt.distinct_bytes);
   // Put the word table in HBM now when a GPU is present, so train() starts HBM-resident.
   std::string why;
-  if (Device::available(&why)) ensure_device(t, "bpe_load_corpus");
+  if (Device::available(&why) && !ensure_device(t, "bpe_load_corpus")) return -1;
   t->load_s = now_seconds() - t0;
   return 0;
 }
 
 void bpe_init(Trainer* t) {
   if (!t) fatal("NULL trainer pointer");
-  t->sel.reset(t->config.unk_id, t->config.min_pair_freq);
+  t->engine.reset_selection();
   bpe_count_bigrams(t);
 }
 
 void bpe_count_bigrams(Trainer* t) {
   if (!t) fatal("NULL trainer pointer");
   if (!ensure_device(t, "bpe_count_bigrams")) return;
-  if (t->log >= 1) std::printf("[INFO]\t Counting bigrams from %zu words...\n", t->wt.num_words());
-  count_into_selector(t);
-  if (t->log >= 1)
-    std::printf("[INFO]\t Added %zu pairs to heap (freq >= %llu)\n", t->sel.heap_size(),
-                (unsigned long long)t->config.min_pair_freq);
+  t->engine.count_bigrams(*t->dev);
 }
 
 int bpe_merge_batch(Trainer* t, int batch_size) {
@@ -243,16 +190,7 @@ int bpe_merge_batch(Trainer* t, int batch_size) {
     return -1;
   }
   if (!ensure_device(t, "bpe_merge_batch")) return -1;
-  if (t->sel.heap_empty()) {
-    if (t->log >= 2) std::printf("[INFO]\t Heap is empty, no more merges possible\n");
-    return 0;
-  }
-  int done = 0;
-  while (done < batch_size && !t->sel.heap_empty()) {
-    if (!merge_one(t)) break;
-    ++done;
-  }
-  return done;
+  return t->engine.merge_batch(*t->dev, batch_size);
 }
 
 int bpe_train(Trainer* t) {
@@ -260,81 +198,20 @@ int bpe_train(Trainer* t) {
     std::fprintf(stderr, "[ERROR]\t Trainer pointer is NULL!\n");
     return -1;
   }
-  const double t0 = now_seconds();
-  if (t->log >= 1)
-    std::printf("[INFO]\t Starting BPE training (target vocab size: %zu)\n", t->config.target_vocab_size);
   if (!ensure_device(t, "bpe_train")) return -1;
-  t->sel.reset(t->config.unk_id, t->config.min_pair_freq);
-  count_into_selector(t);
-  t->init_s = now_seconds() - t0;
-  int total = 0;
-  const int target = (int)t->config.target_vocab_size - kBaseVocab;  // bpe.cpp:353
-  while (total < target) {
-    if (t->sel.heap_empty()) {
-      if (t->log >= 1) std::printf("[INFO]\t Heap exhausted, stopping training\n");
-      break;
-    }
-    const uint64_t tf = t->sel.heap_top_freq();
-    int batch = tf > 50000 ? 10 : tf > 20000 ? 5 : tf > 10000 ? 3 : tf > 5000 ? 2 : 1;  // bpe.cpp:363-368
-    if (batch > target - total) batch = target - total;
-    if (t->trace) std::fprintf(t->trace, "B %d %d %zu %llu\n", batch, total, t->sel.heap_size(), (unsigned long long)tf);
-    if (t->log >= 2)
-      std::printf("[INFO]\t Processing batch of %d merges (completed: %d/%d, heap size: %zu, top freq: %llu)\n", batch,
-                  total, target, t->sel.heap_size(), (unsigned long long)tf);
-    int merged = 0;
-    while (merged < batch && !t->sel.heap_empty()) {
-      if (!merge_one(t)) break;
-      ++merged;
-    }
-    if (merged <= 0) {
-      if (t->log >= 1) std::printf("[WARNING]\t No merges performed, stopping\n");
-      break;
-    }
-    total += merged;
-  }
-  if (t->trace) std::fflush(t->trace);
-  t->train_s = now_seconds() - t0;
-  if (t->log >= 1) std::printf("[INFO]\t Training completed. Performed %d merges\n", total);
-  return total;
+  return t->engine.train(*t->dev);
 }
 
 void bpe_save(const Trainer* tc, const char* model_path, const char* vocab_path) {
   if (!tc) fatal("Trainer pointer is NULL!");
   Trainer* t = const_cast<Trainer*>(tc);
-  const size_t M = t->num_merges, T = kBaseVocab + M;
-  std::vector<std::string> tok(T);
-  for (size_t i = 1; i < (size_t)kBaseVocab; ++i) tok[i] = std::string(1, (char)i);  // tok[0] = "" (C string)
-  for (size_t m = 0; m < M; ++m) tok[kBaseVocab + m] = tok[t->merge_a[m]] + tok[t->merge_b[m]];
-  std::vector<uint64_t> freq(T, 0);
+  std::vector<uint64_t> freq;
   if (t->loaded) {
     if (!ensure_device(t, "bpe_save")) return;
-    t->dev->token_freq(T, &freq);
-    dist_allreduce_host(freq.data(), T, false);
+    t->dev->token_freq(kBaseVocab + t->engine.num_merges(), &freq);
   }
   if (dist_active() && dist_state().rank != 0) return;  // rank 0 writes the files
-  if (FILE* vf = std::fopen(vocab_path, "w")) {
-    for (size_t i = 0; i < T; ++i) {
-      std::fwrite(tok[i].data(), 1, tok[i].size(), vf);
-      std::fprintf(vf, " %llu\n", (unsigned long long)freq[i]);
-    }
-    std::fclose(vf);
-  } else {
-    std::fprintf(stderr, "[ERROR]\t Couldn't open file: %s\n", vocab_path);
-  }
-  if (FILE* mf = std::fopen(model_path, "wb")) {
-    std::vector<int32_t> rec(3 * M);
-    for (size_t m = 0; m < M; ++m) {
-      rec[3 * m] = t->merge_a[m];
-      rec[3 * m + 1] = t->merge_b[m];
-      rec[3 * m + 2] = (int32_t)(kBaseVocab + m);
-    }
-    if (M) std::fwrite(rec.data(), sizeof(int32_t), rec.size(), mf);
-    std::fclose(mf);
-  } else {
-    std::fprintf(stderr, "[ERROR]\t Couldn't open file: %s\n", model_path);
-  }
-  if (t->log >= 1)
-    std::printf("[INFO]\tSaved %zu-token vocab to %s and %zu merges to %s\n", T, vocab_path, M, model_path);
+  t->engine.write_outputs(freq, model_path, vocab_path);
 }
 
 // ---- extensions -----------------------------------------------------------------------------
@@ -346,23 +223,22 @@ int shred_set_option(Trainer* t, const char* key, const char* value) {
 int shred_reset(Trainer* t) {
   if (!t) return -1;
   if (t->dev) t->dev->reset_tokens();
-  t->num_merges = 0;
-  t->merge_a.clear();
-  t->merge_b.clear();
-  t->sel.reset(t->config.unk_id, t->config.min_pair_freq);
+  t->engine.forget_merges();
   return 0;
 }
 
-int shred_get_stats(const Trainer* t, ShredStats* s) {
-  if (!t || !s) return -1;
+int shred_get_stats(const Trainer* tc, ShredStats* s) {
+  if (!tc || !s) return -1;
+  Trainer* t = const_cast<Trainer*>(tc);
   std::memset(s, 0, sizeof(*s));
+  const EngineTimes& et = t->engine.times();
   s->load_seconds = t->load_s;
-  s->init_seconds = t->init_s;
-  s->train_seconds = t->train_s;
-  s->host_select_seconds = t->select_s;
-  s->host_launch_seconds = t->launch_s;
-  s->host_wait_seconds = t->wait_s;
-  s->host_apply_seconds = t->apply_s;
+  s->init_seconds = et.init_s;
+  s->train_seconds = et.train_s;
+  s->host_select_seconds = et.select_s;
+  s->host_launch_seconds = et.launch_s;
+  s->host_wait_seconds = et.wait_s;
+  s->host_apply_seconds = et.apply_s;
   if (t->dev) {
     const KernelTimes& k = t->dev->times();
     s->merge_kernel_ms = k.merge_ms;
@@ -378,8 +254,8 @@ int shred_get_stats(const Trainer* t, ShredStats* s) {
   s->num_words = t->wt.num_words();
   s->num_symbols = t->wt.num_symbols();
   s->num_occurrences = t->wt.total_occurrences;
-  s->num_merges = t->num_merges;
-  s->heap_size = t->sel.heap_size();
+  s->num_merges = t->engine.num_merges();
+  s->heap_size = t->engine.selector().heap_size();
   s->layout = (int32_t)t->layout;
   s->world_size = dist_active() ? dist_state().world : 1;
   return 0;

@@ -1,0 +1,42 @@
+"""ctypes wrapper of the test-only CPU harness (tests/native): product host code + kernel emulation."""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "native", "_build", "libhostharness.so")
+
+EXCHANGE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                               ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t)
+
+
+def load():
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "native")], check=True)
+    lib = ctypes.CDLL(LIB)
+    lib.hh_open.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_uint64,
+                            ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.hh_open.restype = ctypes.c_void_p
+    lib.hh_close.argtypes = [ctypes.c_void_p]
+    lib.hh_set_exchange.argtypes = [ctypes.c_void_p, EXCHANGE_CB, ctypes.c_void_p]
+    lib.hh_train.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.hh_train.restype = ctypes.c_int
+    lib.hh_merge_batch.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.hh_merge_batch.restype = ctypes.c_int
+    lib.hh_init.argtypes = [ctypes.c_void_p]
+    lib.hh_save.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+    for fn in ("hh_num_words", "hh_num_symbols", "hh_num_tiles", "hh_live_tokens", "hh_heap_size",
+               "hh_distinct_bytes", "hh_kept_bytes"):
+        getattr(lib, fn).argtypes = [ctypes.c_void_p]
+        getattr(lib, fn).restype = ctypes.c_uint64
+    lib.hh_word.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
+                            ctypes.POINTER(ctypes.c_uint64)]
+    lib.hh_word.restype = ctypes.c_uint64
+    return lib
+
+
+def open_case(lib, corpus, cfg, layout="types", rank=0, world=1):
+    h = lib.hh_open(corpus.encode(), cfg["vocab_size"], cfg["unk_id"], cfg["character_coverage"],
+                    cfg["min_pair_freq"], 1 if layout == "stream" else 0, rank, world)
+    if not h:
+        raise IOError(corpus)
+    return h

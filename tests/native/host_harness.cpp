@@ -1,0 +1,248 @@
+// Test-only harness: the product's host code (corpus loader, tile packing, Engine, Selector)
+// driven by a CPU emulation of the device kernels, so the host logic and the multi-rank exchange
+// can be checked without a GPU.  NOT part of the product library (built into
+// tests/native/_build/libhostharness.so only).
+//
+// EmuBackend restates, sequentially, the semantics of k_pair_count / k_merge / k_token_freq over
+// the tiled stream of tiles.h: greedy left-to-right occurrences (runs of a==b pair up from the
+// run start), the left neighbour is X when it was just merged, the right neighbour is the original
+// token, deltas keyed (slot, category) with first touch (rank << 32 | pos << 2 | category).
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "corpus.h"
+#include "engine.h"
+#include "selector.h"
+#include "tiles.h"
+
+using namespace shred;
+
+typedef void (*ExchangeCb)(void* ctx, uint64_t* sum, uint64_t* mn, size_t n);
+
+namespace {
+
+inline bool is_hdr(int32_t t) { return t < kHeaderLimit; }
+
+class EmuBackend : public Backend {
+ public:
+  EmuBackend(const WordTable& wt, Layout layout, size_t begin, size_t end, uint32_t slot_cap)
+      : wt_(wt), layout_(layout), cap_(slot_cap) {
+    pack_tiles(wt, layout, begin, end, &ts_);
+    dsum_.assign(4 * ((size_t)cap_ + 1), 0);
+    dft_.assign(4 * ((size_t)cap_ + 1), ~0ull);
+  }
+  void set_exchange(ExchangeCb cb, void* ctx) { cb_ = cb; ctx_ = ctx; }
+
+  uint64_t weight(uint32_t rank) const { return layout_ == Layout::kTypes ? wt_.count[rank] : 1; }
+
+  void count_pairs(int32_t unk, std::vector<PairCount>* out) override {
+    out->clear();
+    const size_t D = 257 * 257;  // ids < 256 plus slot 0 (first count only)
+    std::vector<uint64_t> cnt(D, 0), ft(D, ~0ull);
+    for (size_t t = 0; t < ts_.num_tiles(); ++t) {
+      const int32_t* p = ts_.tok.data() + ts_.off[t];
+      uint32_t hidx = 0, rank = 0;
+      for (uint32_t i = 0; i < ts_.len[t]; ++i) {
+        if (is_hdr(p[i])) { hidx = i; rank = (uint32_t)(p[i] - kHeaderBase); continue; }
+        if (i + 1 >= ts_.len[t] || is_hdr(p[i + 1]) || p[i] == unk || p[i + 1] == unk) continue;
+        if ((uint32_t)p[i] >= 256 || (uint32_t)p[i + 1] >= 256) fatal("emulated count supports ids < 256 only");
+        const size_t k = (size_t)p[i] * 257 + (size_t)p[i + 1];
+        cnt[k] += weight(rank);
+        ft[k] = std::min<uint64_t>(ft[k], ((uint64_t)rank << 32) | (i - hidx - 1));
+      }
+    }
+    if (cb_) cb_(ctx_, cnt.data(), ft.data(), D);
+    for (size_t k = 0; k < D; ++k)
+      if (ft[k] != ~0ull) out->push_back({(int32_t)(k / 257), (int32_t)(k % 257), cnt[k], ft[k]});
+  }
+
+  void emit(uint32_t key, uint64_t w, uint64_t ft) {
+    dsum_[key] += w;
+    if (ft < dft_[key]) dft_[key] = ft;
+  }
+  uint32_t slot(int32_t id) const { return (uint32_t)id < cap_ ? (uint32_t)id + 1 : 0; }
+
+  void merge_scan(int32_t a, int32_t b, int32_t X) override {
+    if ((uint32_t)X >= cap_) fatal("emulated slot capacity exceeded");
+    std::vector<int32_t> out;
+    for (size_t t = 0; t < ts_.num_tiles(); ++t) {
+      int32_t* p = ts_.tok.data() + ts_.off[t];
+      const uint32_t len = ts_.len[t];
+      out.clear();
+      uint32_t hidx = 0, rank = 0;
+      bool prev_x = false;
+      uint32_t i = 0;
+      while (i < len) {
+        const int32_t tk = p[i];
+        if (is_hdr(tk)) {
+          hidx = i;
+          rank = (uint32_t)(tk - kHeaderBase);
+          out.push_back(tk);
+          prev_x = false;
+          ++i;
+          continue;
+        }
+        if (tk == a && i + 1 < len && p[i + 1] == b) {
+          const uint64_t w = weight(rank);
+          const uint64_t ftb = ((uint64_t)rank << 32) | ((uint64_t)(i - hidx - 1) << 2);
+          if (i - 1 > hidx) {
+            const int32_t left = prev_x ? X : p[i - 1];
+            emit(slot(left) * 4 + kOldLeft, w, ftb | kOldLeft);
+            emit(slot(left) * 4 + kNewLeft, w, ftb | kNewLeft);
+          }
+          if (i + 2 < len && !is_hdr(p[i + 2])) {
+            emit(slot(p[i + 2]) * 4 + kOldRight, w, ftb | kOldRight);
+            emit(slot(p[i + 2]) * 4 + kNewRight, w, ftb | kNewRight);
+          }
+          out.push_back(X);
+          prev_x = true;
+          i += 2;
+        } else {
+          out.push_back(tk);
+          prev_x = false;
+          ++i;
+        }
+      }
+      std::memcpy(p, out.data(), out.size() * sizeof(int32_t));
+      ts_.len[t] = (uint32_t)out.size();
+    }
+  }
+
+  size_t collect(int32_t, const DeltaRecord** recs) override {
+    if (cb_) cb_(ctx_, dsum_.data(), dft_.data(), dsum_.size());
+    recs_.clear();
+    for (size_t k = 0; k < dsum_.size(); ++k) {
+      if (dft_[k] == ~0ull) continue;
+      recs_.push_back({(uint32_t)k, 0, dsum_[k], dft_[k]});
+      dsum_[k] = 0;
+      dft_[k] = ~0ull;
+    }
+    *recs = recs_.data();
+    return recs_.size();
+  }
+
+  void token_freq(size_t T, std::vector<uint64_t>* freq) override {
+    freq->assign(T, 0);
+    for (size_t t = 0; t < ts_.num_tiles(); ++t) {
+      const int32_t* p = ts_.tok.data() + ts_.off[t];
+      uint32_t rank = 0;
+      for (uint32_t i = 0; i < ts_.len[t]; ++i) {
+        if (is_hdr(p[i])) { rank = (uint32_t)(p[i] - kHeaderBase); continue; }
+        if ((uint32_t)p[i] < T) (*freq)[p[i]] += weight(rank);
+      }
+    }
+    if (cb_) {
+      std::vector<uint64_t> dummy(T, ~0ull);
+      cb_(ctx_, freq->data(), dummy.data(), T);
+    }
+  }
+
+  const TiledStream& stream() const { return ts_; }
+
+ private:
+  const WordTable& wt_;
+  Layout layout_;
+  uint32_t cap_;
+  TiledStream ts_;
+  std::vector<uint64_t> dsum_, dft_;
+  std::vector<DeltaRecord> recs_;
+  ExchangeCb cb_ = nullptr;
+  void* ctx_ = nullptr;
+};
+
+struct Harness {
+  WordTable wt;
+  std::unique_ptr<EmuBackend> be;
+  Engine engine;
+  FILE* trace = nullptr;
+};
+
+}  // namespace
+
+extern "C" {
+
+void* hh_open(const char* path, uint64_t vocab, int32_t unk, float cov, uint64_t mpf, int layout, int rank, int world) {
+  Harness* h = new Harness();
+  if (cov <= 0.0f || cov >= 1.0f) cov = 0.995f;
+  if (mpf == 0) mpf = kDefaultMinPairFreq;
+  LoadOptions opt;
+  opt.unk_id = unk;
+  opt.coverage = cov;
+  opt.want_stream = layout == 1;
+  opt.threads = 3;  // any thread count must give the same table
+  std::string err;
+  if (load_corpus(path, opt, &h->wt, &err) != 0) {
+    delete h;
+    return nullptr;
+  }
+  const Layout lay = layout == 1 ? Layout::kStream : Layout::kTypes;
+  size_t b = 0, e = 0;
+  shard_range(h->wt, lay, rank, world, &b, &e);
+  uint32_t cap = 1024;
+  while (cap < vocab + 1 || (unk >= 0 && cap < (uint64_t)unk + 1)) cap *= 2;
+  h->be.reset(new EmuBackend(h->wt, lay, b, e, cap));
+  h->engine.configure(vocab, unk, mpf);
+  h->engine.set_log(0);
+  return h;
+}
+
+void hh_close(void* p) {
+  Harness* h = (Harness*)p;
+  if (h->trace) std::fclose(h->trace);
+  delete h;
+}
+
+void hh_set_exchange(void* p, ExchangeCb cb, void* ctx) { ((Harness*)p)->be->set_exchange(cb, ctx); }
+
+int hh_train(void* p, const char* trace_path) {
+  Harness* h = (Harness*)p;
+  if (h->trace) std::fclose(h->trace);
+  h->trace = trace_path ? std::fopen(trace_path, "w") : nullptr;
+  h->engine.set_trace(h->trace);
+  const int n = h->engine.train(*h->be);
+  if (h->trace) std::fflush(h->trace);
+  return n;
+}
+
+int hh_merge_batch(void* p, int batch) { return ((Harness*)p)->engine.merge_batch(*((Harness*)p)->be, batch); }
+void hh_init(void* p) {
+  Harness* h = (Harness*)p;
+  h->engine.reset_selection();
+  h->engine.count_bigrams(*h->be);
+}
+
+void hh_save(void* p, const char* model, const char* vocab, int write) {
+  Harness* h = (Harness*)p;
+  std::vector<uint64_t> freq;
+  h->be->token_freq(kBaseVocab + h->engine.num_merges(), &freq);
+  if (write) h->engine.write_outputs(freq, model, vocab);
+}
+
+uint64_t hh_num_words(void* p) { return ((Harness*)p)->wt.num_words(); }
+uint64_t hh_num_symbols(void* p) { return ((Harness*)p)->wt.num_symbols(); }
+uint64_t hh_num_tiles(void* p) { return ((Harness*)p)->be->stream().num_tiles(); }
+uint64_t hh_live_tokens(void* p) {
+  uint64_t s = 0;
+  for (uint32_t l : ((Harness*)p)->be->stream().len) s += l;
+  return s;
+}
+uint64_t hh_heap_size(void* p) { return ((Harness*)p)->engine.selector().heap_size(); }
+uint64_t hh_distinct_bytes(void* p) { return ((Harness*)p)->wt.distinct_bytes; }
+uint64_t hh_kept_bytes(void* p) { return ((Harness*)p)->wt.kept_bytes; }
+
+// Word i of the reference-ordered table: copies its bytes (up to cap) and returns its length;
+// *count receives its occurrence count.
+uint64_t hh_word(void* p, uint64_t i, uint8_t* buf, uint64_t cap, uint64_t* count) {
+  const WordTable& wt = ((Harness*)p)->wt;
+  const uint64_t o = wt.offset[i], l = wt.offset[i + 1] - o;
+  std::memcpy(buf, wt.bytes.data() + o, std::min(l, cap));
+  *count = wt.count[i];
+  return l;
+}
+
+}  // extern "C"

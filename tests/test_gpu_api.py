@@ -1,0 +1,167 @@
+"""GPU tests of the drop-in API beyond the goldens.
+
+* the reference's own pytest suite (test/test_bpe.py:35-65) on the MI355X trainer;
+* run-to-run determinism (reset + retrain, and a fresh trainer) — device atomics are order-free;
+* bpe_init + bpe_merge_batch through the C ABI;
+* a medium corpus against the CPU oracle (bit-exact) in both layouts;
+* the C2 workload at full size (1 GB) through size-independent invariants: byte conservation
+  (Σ freq(token) x len(token) = Σ word bytes x count) and non-increasing merge frequencies.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import corpora
+from conftest import ORACLE
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(**kw):
+    from shredword.trainer import BPETrainer
+    t = BPETrainer(**kw)
+    t.set_option("log", 0)
+    return t
+
+
+@pytest.fixture(scope="module")
+def small_corpus(tmp_path_factory):
+    p = tmp_path_factory.mktemp("small") / "corpus.txt"
+    corpora.write_small_corpus(str(p))
+    return str(p)
+
+
+def test_reference_train_and_save(small_corpus, tmp_path):
+    """reference test/test_bpe.py:35-54"""
+    model, vocab = tmp_path / "bpe.model", tmp_path / "bpe.vocab"
+    t = _trainer(vocab_size=300, min_pair_freq=2)
+    t.load_corpus(small_corpus)
+    merges = t.train()
+    assert merges > 0
+    t.save(str(model), str(vocab))
+    t.destroy()
+    assert model.exists() and vocab.exists()
+    assert model.stat().st_size == 12 * merges
+    # one line per token; token 10's spelling is itself a newline
+    assert vocab.read_bytes().count(b"\n") == 256 + merges + 1
+
+
+def test_reference_zero_merge_expected(small_corpus):
+    """reference test/test_bpe.py:56-65"""
+    t = _trainer(vocab_size=50, min_pair_freq=1000)
+    t.load_corpus(small_corpus)
+    assert t.train() == 0
+    t.destroy()
+
+
+def _train_bytes(t, tmp_path, tag):
+    n = t.train()
+    m, v = tmp_path / f"{tag}.model", tmp_path / f"{tag}.vocab"
+    t.save(str(m), str(v))
+    return n, m.read_bytes(), v.read_bytes()
+
+
+def test_deterministic_rerun(tmp_path):
+    corpus = str(tmp_path / "c.txt")
+    corpora.gen_synthetic(corpus, 4_000_000, 21, "utf8")
+    t = _trainer(vocab_size=3000, min_pair_freq=2)
+    t.load_corpus(corpus)
+    first = _train_bytes(t, tmp_path, "a")
+    t.reset()
+    second = _train_bytes(t, tmp_path, "b")
+    t.destroy()
+    t2 = _trainer(vocab_size=3000, min_pair_freq=2)
+    t2.load_corpus(corpus)
+    third = _train_bytes(t2, tmp_path, "c")
+    t2.destroy()
+    assert first == second == third
+
+
+def test_init_and_merge_batch_abi(small_corpus, tmp_path):
+    from shredword.cbase import lib
+    ref = _trainer(vocab_size=300, min_pair_freq=2)
+    ref.load_corpus(small_corpus)
+    n_ref, model_ref, vocab_ref = _train_bytes(ref, tmp_path, "ref")
+    ref.destroy()
+    t = _trainer(vocab_size=300, min_pair_freq=2)
+    t.load_corpus(small_corpus)
+    lib.bpe_init(t.trainer)
+    done = 0
+    while done < n_ref:
+        k = lib.bpe_merge_batch(t.trainer, min(5, n_ref - done))
+        assert k > 0
+        done += k
+    m, v = tmp_path / "mb.model", tmp_path / "mb.vocab"
+    t.save(str(m), str(v))
+    t.destroy()
+    assert m.read_bytes() == model_ref and v.read_bytes() == vocab_ref
+
+
+@pytest.mark.parametrize("layout", ["types", "stream"])
+def test_medium_corpus_matches_oracle(layout, tmp_path):
+    corpus = str(tmp_path / "m.txt")
+    corpora.gen_synthetic(corpus, 12_000_000, 31, "mixed")
+    subprocess.run(["make", "-s", "-C", ORACLE, "port"], check=True)
+    om, ov = str(tmp_path / "o.model"), str(tmp_path / "o.vocab")
+    subprocess.run([os.path.join(ORACLE, "_build", "bpe_oracle"), corpus, "6000", "0", "0.9995", "20", om, ov],
+                   check=True, stderr=subprocess.DEVNULL)
+    t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+    t.set_option("layout", layout)
+    t.load_corpus(corpus)
+    n, model, vocab = _train_bytes(t, tmp_path, "g")
+    t.destroy()
+    assert model == open(om, "rb").read()
+    assert vocab == open(ov, "rb").read()
+    assert n > 1000
+
+
+def _parse_vocab(vocab: bytes, ops):
+    """(spelling, freq) per id, walking the file with spellings derived from the merges:
+    a spelling may contain any byte (token 10 is a newline), so lines cannot be split blindly."""
+    spell = [bytes([i]) if i else b"" for i in range(256)]
+    for a, b, _x in ops:
+        spell.append(spell[a] + spell[b])
+    out, pos = [], 0
+    for tok in spell:
+        assert vocab[pos:pos + len(tok)] == tok
+        pos += len(tok)
+        assert vocab[pos:pos + 1] == b" "
+        end = vocab.index(b"\n", pos + 1)
+        out.append((tok, int(vocab[pos + 1:end])))
+        pos = end + 1
+    assert pos == len(vocab)
+    return out
+
+
+def test_full_size_c2_invariants(tmp_path):
+    """C2 at full size (1 GB): invariants that hold for any correct run."""
+    corpus = os.path.join(os.environ.get("TMPDIR", "/tmp"), "shredword_bench", "c2_utf8_1000000000_s2.txt")
+    if not (os.path.exists(corpus) and os.path.getsize(corpus) == 1_000_000_000):
+        os.makedirs(os.path.dirname(corpus), exist_ok=True)
+        corpora.gen_synthetic(corpus, 1_000_000_000, 2, "utf8")
+    t = _trainer(vocab_size=8192, min_pair_freq=2000)
+    trace = str(tmp_path / "trace.txt")
+    t.set_option("trace", trace)
+    t.load_corpus(corpus)
+    n, model, vocab = _train_bytes(t, tmp_path, "c2")
+    st = t.stats()
+    t.destroy()
+    assert n == 7936
+    T = 256 + n
+    ops = np.frombuffer(model, dtype="<i4").reshape(-1, 3)
+    assert (ops[:, 2] == np.arange(256, T)).all()
+    assert (ops[:, :2] < ops[:, 2:3]).all()  # operands exist before their merge
+    toks = _parse_vocab(vocab, ops)
+    assert len(toks) == T
+    # Byte conservation: every byte of every word occurrence ends in exactly one final token.
+    # unk_id = 0 has the empty spelling and counts one byte per unk symbol (byte 0 never occurs).
+    data = np.fromfile(corpus, dtype=np.uint8)
+    delims = int(np.count_nonzero((data == 32) | (data == 10) | (data == 9) | (data == 13)))
+    word_bytes = data.size - delims
+    assert sum(len(tok) * f for tok, f in toks[1:]) + toks[0][1] == word_bytes
+    freqs = [int(ln.split()[3]) for ln in open(trace) if ln.startswith("M ")]
+    assert len(freqs) == n
+    assert all(x >= y for x, y in zip(freqs, freqs[1:])), "merge frequencies must not increase"
+    assert freqs[-1] >= 2000

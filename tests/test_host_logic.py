@@ -1,0 +1,111 @@
+"""CPU tests of the product host logic (no GPU).
+
+The product's corpus loader, tile packing, Engine (reference batch loop / trace) and Selector
+(exact heap replay and FreqChangeMap ordering) run against a CPU emulation of the device
+kernels (tests/native/host_harness.cpp) and must reproduce the reference goldens byte for byte.
+This pins everything on the host side of the C ABI; the GPU tests pin the kernels themselves.
+"""
+import os
+
+import pytest
+
+import hostharness
+from conftest import golden_cases
+
+
+@pytest.fixture(scope="module")
+def hh():
+    return hostharness.load()
+
+
+def _run(hh, case, corpus, tmp_path, layout):
+    h = hostharness.open_case(hh, corpus, case["config"], layout)
+    try:
+        trace = str(tmp_path / f"t_{layout}.txt")
+        merges = hh.hh_train(h, trace.encode())
+        model, vocab = str(tmp_path / "h.model"), str(tmp_path / "h.vocab")
+        hh.hh_save(h, model.encode(), vocab.encode(), 1)
+        return merges, open(model, "rb").read(), open(vocab, "rb").read(), open(trace).read()
+    finally:
+        hh.hh_close(h)
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_host_logic_types_layout(name, hh, case_corpus, tmp_path):
+    case, corpus = case_corpus(name)
+    merges, model, vocab, trace = _run(hh, case, corpus, tmp_path, "types")
+    assert merges == case["merges"]
+    assert trace == case["trace"]
+    assert model == case["model_bytes"]
+    assert vocab == case["vocab_bytes"]
+
+
+@pytest.mark.parametrize("name", ["adv_unk0", "adv_unkm1", "ascii1m_unk7_cov09", "small_v300", "utf8_2m_v2000_mpf50"])
+def test_host_logic_stream_layout(name, hh, case_corpus, tmp_path):
+    case, corpus = case_corpus(name)
+    merges, model, vocab, trace = _run(hh, case, corpus, tmp_path, "stream")
+    assert (merges, trace, model, vocab) == (case["merges"], case["trace"], case["model_bytes"], case["vocab_bytes"])
+
+
+def _py_word_table(data: bytes):
+    """Appendix A.1 restated for NUL-free text: words split on TAB/CR/LF/SPACE, ordered by
+    (djb2(word) & 4095, first occurrence)."""
+    import re
+    first, count = {}, {}
+    for m in re.finditer(rb"[^\t\r\n ]+", data):
+        w = m.group()
+        if w not in first:
+            first[w] = len(first)
+        count[w] = count.get(w, 0) + 1
+
+    def djb2(w):
+        x = 5381
+        for c in w:
+            x = (x * 33 + c) & 0xFFFFFFFFFFFFFFFF
+        return x
+    words = sorted(first, key=lambda w: (djb2(w) & 4095, first[w]))
+    return [(w, count[w]) for w in words]
+
+
+@pytest.mark.parametrize("name", ["small_v300", "ascii1m_v3000_mpf2", "utf8_2m_v2000_mpf50"])
+def test_word_order_matches_python_restatement(name, hh, case_corpus):
+    import ctypes
+    case, corpus = case_corpus(name)
+    h = hostharness.open_case(hh, corpus, case["config"])
+    try:
+        want = _py_word_table(open(corpus, "rb").read())
+        assert hh.hh_num_words(h) == len(want)
+        buf = ctypes.create_string_buffer(4096)
+        cnt = ctypes.c_uint64()
+        for i, (w, c) in enumerate(want):
+            ln = hh.hh_word(h, i, buf, len(buf), ctypes.byref(cnt))
+            assert (buf.raw[:ln], cnt.value) == (w, c), i
+        # coverage: keep = (size_t)(float(n) * float(coverage)) (bpe.cpp:169)
+        import numpy as np
+        n = hh.hh_distinct_bytes(h)
+        assert hh.hh_kept_bytes(h) == int(np.float32(n) * np.float32(case["config"]["character_coverage"]))
+    finally:
+        hh.hh_close(h)
+
+
+def test_merge_batch_matches_train(hh, case_corpus, tmp_path):
+    """bpe_init + repeated bpe_merge_batch reproduces bpe_train's merges (batching is logging-only)."""
+    case, corpus = case_corpus("small_v300")
+    h = hostharness.open_case(hh, corpus, case["config"])
+    try:
+        hh.hh_init(h)
+        total = 0
+        while True:
+            n = hh.hh_merge_batch(h, 7)
+            if n <= 0 or total + n > case["merges"]:
+                total += max(n, 0)
+                break
+            total += n
+            if total >= case["merges"]:
+                break
+        model, vocab = str(tmp_path / "b.model"), str(tmp_path / "b.vocab")
+        hh.hh_save(h, model.encode(), vocab.encode(), 1)
+        got = open(model, "rb").read()
+        assert got[:len(case["model_bytes"])] == case["model_bytes"]
+    finally:
+        hh.hh_close(h)
