@@ -222,6 +222,10 @@ def main():
             "merge_kernel_share": (mk_ms * 1e-3 * merges) / elapsed if elapsed > 0 else None,
             "host_breakdown_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
             "init_s_last_step": st["init_seconds"],
+            "selector_last_step": {k: st[k] for k in ("heap_pops", "heap_stale_pops", "heap_pushes", "delta_records",
+                                                      "apply_cycles_combine", "apply_cycles_order",
+                                                      "apply_cycles_walk")},
+            "tiles_visited_per_merge": st["tiles_visited"] / max(1, merges),
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

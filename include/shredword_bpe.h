@@ -76,6 +76,10 @@ int loadVocab(void* trainer, const char* path);
 int shred_set_option(Trainer* trainer, const char* key, const char* value);
 /* Restores the loaded corpus to its unmerged state and forgets merges (benchmark repeats). */
 int shred_reset(Trainer* trainer);
+/* Diagnostic: runs `iters` device merges of a pair (a, b) that must not occur in the corpus
+ * (so nothing changes), timing launch -> records on the host.  Returns mean microseconds per
+ * merge, or -1 when the pair occurs / no device. */
+double shred_probe_merge(Trainer* trainer, int32_t a, int32_t b, int iters);
 
 typedef struct ShredStats {
   double load_seconds, init_seconds, train_seconds;
@@ -86,6 +90,8 @@ typedef struct ShredStats {
   uint64_t num_words, num_symbols, num_occurrences, num_merges, heap_size, live_tokens;
   uint64_t device_bytes, num_tiles;
   int32_t layout, world_size;
+  uint64_t heap_pops, heap_stale_pops, heap_pushes, delta_records, tiles_visited;
+  uint64_t apply_cycles_combine, apply_cycles_order, apply_cycles_walk;
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -16,6 +16,13 @@
 // result bit-identical run to run.
 #include <hip/hip_runtime.h>
 
+#ifndef SHRED_MAX_GROUPS
+#define SHRED_MAX_GROUPS 256
+#endif
+#ifndef SHRED_DELTA_LDS
+#define SHRED_DELTA_LDS 2048
+#endif
+
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -151,10 +158,12 @@ __device__ __forceinline__ int32_t next_token(const int32_t* base, uint32_t cs, 
 // so one launch + one flag wait is the whole device side of a merge.
 constexpr int kWaveTok = 64 * kPer;  // 1024 tokens per wave chunk
 constexpr int kWaves = kThreads / 64;
-constexpr int kDeltaLdsW = 512;
+constexpr int kDeltaLdsW = SHRED_DELTA_LDS;
 constexpr uint32_t kFusedCollectMax = 4096;  // beyond this the host launches k_collect
 constexpr uint32_t kNeedCollect = 0x80000000u;
 constexpr uint32_t kTimingStride = 8;
+constexpr uint32_t kInlineTiles = 768;     // candidate tiles that fit the kernel arguments
+constexpr int kMaxMergeGroups = SHRED_MAX_GROUPS;  // fat persistent grid: waves walk tiles with prefetch
 
 struct MergeParams {
   int32_t* tok;
@@ -172,9 +181,13 @@ struct MergeParams {
   uint32_t* done;     // completion tickets: [0..7] per blockIdx % 8 group, [8] top
   int fused;          // 1: last workgroup collects; 0: leave the tables (multi-GPU exchange)
   DeltaRecord* out;   // host-visible records
-  uint32_t* hcount;   // host-visible: [0] record count (| kNeedCollect), [1] flag = seq
+  uint32_t* hcount;   // host-visible: [0] record count (| kNeedCollect), [1] flag = seq, [2] matched tiles
   u64* hstats;        // host-visible: [0] occurrences, [1] tokens rewritten
+  uint32_t* mlist;    // host-visible: tiles where the merge matched (-> tiles(X) of the index)
+  uint32_t* mcount;   // device counter for mlist
   uint32_t seq;
+  uint32_t nlist;     // 0: visit every tile; else visit list[0 .. nlist)
+  uint32_t list[kInlineTiles];  // candidate tiles (tile skipping), passed in the kernel arguments
 };
 
 struct DeltaLds {
@@ -192,7 +205,7 @@ __device__ __forceinline__ void delta_global(const MergeParams& p, uint32_t key,
 }
 
 __device__ __forceinline__ void delta_emit(DeltaLds& h, const MergeParams& p, uint32_t key, u64 w, u64 ft) {
-  uint32_t s = (key * 2654435761u) >> 23;
+  uint32_t s = (key * 2654435761u) >> (32 - __builtin_ctz(kDeltaLdsW));
   for (int probe = 0; probe < 16; ++probe) {
     const uint32_t prev = atomicCAS(&h.key[s], kEmpty32, key);
     if (prev == kEmpty32 || prev == key) {
@@ -259,9 +272,31 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
   const int p0 = lane * kPer;
   u64 n_merged = 0, n_written = 0;  // wave-uniform
 
-  for (uint32_t tile = blockIdx.x * kWaves + wid; tile < p.ntiles; tile += gridDim.x * kWaves) {
-    const uint32_t len = p.tile_len[tile];
-    int32_t* base = p.tok + p.tile_off[tile];
+  const uint32_t n_iter = p.nlist ? p.nlist : p.ntiles;
+  const uint32_t stride = gridDim.x * kWaves;
+  uint32_t it = blockIdx.x * kWaves + wid;
+  // first chunk of the wave's next tile, loaded one tile ahead (latency hiding)
+  uint32_t f_tile = 0, f_len = 0;
+  int32_t* f_base = p.tok;
+  int32_t fv[kPer];
+  int32_t f_nx = kPad;
+  auto fetch = [&](uint32_t i) {
+    f_tile = p.nlist ? p.list[i] : i;
+    f_len = p.tile_len[f_tile];
+    f_base = p.tok + p.tile_off[f_tile];
+    load_chunk(f_base, 0, min((uint32_t)kWaveTok, f_len), p0, fv);
+    f_nx = next_token(f_base, 0, f_len, p0, fv[0]);
+  };
+  if (it < n_iter) fetch(it);
+  for (; it < n_iter; it += stride) {
+    const uint32_t tile = f_tile, len = f_len;
+    int32_t* base = f_base;
+    int32_t v0[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) v0[j] = fv[j];
+    const int32_t nx0 = f_nx;
+    if (it + stride < n_iter) fetch(it + stride);
+    uint64_t tile_hits = 0;
     long long c_nona = -1;  // last tile index whose token != a (a == b only)
     u64 c_hdr = 0;          // ((index + 1) << 32) | rank of the last header, 0 = none
     bool c_m1 = false, c_m2 = false;
@@ -272,8 +307,15 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       const uint32_t cl = min((uint32_t)kWaveTok, len - cs);
       const bool more = cs + cl < len;
       int32_t v[kPer];
-      load_chunk(base, cs, cl, p0, v);
-      const int32_t nx = next_token(base, cs, len, p0, v[0]);
+      int32_t nx;
+      if (cs == 0) {
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) v[j] = v0[j];
+        nx = nx0;
+      } else {
+        load_chunk(base, cs, cl, p0, v);
+        nx = next_token(base, cs, len, p0, v[0]);
+      }
       bool any = false;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) any |= (v[j] == a) & ((j + 1 < kPer ? v[j + 1] : nx) == b);
@@ -389,6 +431,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
         n_written += (u64)kept;
       }
       n_merged += (u64)matches;
+      tile_hits += (u64)matches;
       // ---- carries to the next chunk of this tile
       c_out += (uint32_t)kept;
       c_m1 = (__shfl(mask, (int)((cl - 1) / kPer), 64) >> ((cl - 1) % kPer)) & 1u;
@@ -400,6 +443,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       wave_lds_sync();  // the copy-out reads st before the next chunk overwrites it
     }
     if (dirty && lane == 0) p.tile_len[tile] = c_out;
+    if (tile_hits && lane == 0) p.mlist[atomicAdd(p.mcount, 1u)] = tile;
   }
   if (lane == 0) {
     if (n_merged) atomicAdd(&s_cnt[0], n_merged);
@@ -474,6 +518,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       p.hstats[1] = atomicExch(&p.stats[1], 0ull);
       p.hcount[0] = collect ? n : (n | kNeedCollect);
     }
+    p.hcount[2] = atomicExch(p.mcount, 0u);
     atomicExch(&p.done[8], 0u);
     __threadfence_system();
     __hip_atomic_store(&p.hcount[1], p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -720,6 +765,8 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
   HIP_OK(hipHostMalloc((void**)&host_count_, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(host_count_, 0, 64);
   HIP_OK(hipHostGetDevicePointer(&dev_count_, host_count_, 0));
+  merge_params_ = new MergeParams();
+  if (const char* e = std::getenv("SHREDWORD_TILE_SKIP")) skip_ = std::atoi(e) != 0;
   int nb = 0;  // resident workgroups of k_merge per CU
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_merge<true>), kThreads, 0));
   merge_blocks_per_cu_ = nb > 0 ? nb : 4;
@@ -749,6 +796,8 @@ Device::~Device() {
   (void)hipStreamSynchronize(S(stream_));
   free_all();
   if (host_count_) (void)hipHostFree(host_count_);
+  if (host_mlist_) (void)hipHostFree(host_mlist_);
+  delete static_cast<MergeParams*>(merge_params_);
   for (auto e : ev_)
     if (e) (void)hipEventDestroy((hipEvent_t)e);
   if (stream_) (void)hipStreamDestroy(S(stream_));
@@ -781,6 +830,10 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
                             S(stream_)));
   }
   HIP_OK(hipStreamSynchronize(S(stream_)));
+  if (host_mlist_) HIP_OK(hipHostFree(host_mlist_));
+  HIP_OK(hipHostMalloc((void**)&host_mlist_, (ntiles_ + 1) * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_OK(hipHostGetDevicePointer(&dev_mlist_, host_mlist_, 0));
+  index_.build(ts);
   max_id_seen_ = max_id;
   uploaded_ = true;
   reset_tokens();
@@ -793,6 +846,7 @@ void Device::reset_tokens() {
   if (ntiles_)
     HIP_OK(hipMemcpyAsync(tile_len_, tile_len0_, ntiles_ * sizeof(uint32_t), hipMemcpyDeviceToDevice, S(stream_)));
   live_tokens_est_ = live_tokens0_;
+  index_.reset();
 }
 
 uint64_t Device::live_tokens() {
@@ -825,7 +879,7 @@ void Device::ensure_slots(uint32_t need) {
   dsum_ = dalloc<uint64_t>(keys + 2, &bytes_alloc_);  // + 2 stats words at the end
   dft_ = dalloc<uint64_t>(keys, &bytes_alloc_);
   dlist_ = dalloc<uint32_t>(keys, &bytes_alloc_);
-  dcount_ = dalloc<uint32_t>(16, &bytes_alloc_);  // [0] count, [1..9] tickets
+  dcount_ = dalloc<uint32_t>(16, &bytes_alloc_);  // [0] count, [1..9] tickets, [10] matched tiles
   HIP_OK(hipMemsetAsync(dsum_, 0, (keys + 2) * sizeof(u64), S(stream_)));
   HIP_OK(hipMemsetAsync(dft_, 0xFF, keys * sizeof(u64), S(stream_)));
   HIP_OK(hipMemsetAsync(dcount_, 0, 16 * sizeof(uint32_t), S(stream_)));
@@ -911,12 +965,39 @@ void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
   if (!ntiles_) return;  // an empty shard still joins collect()'s exchange
   ++seq_;
   launched_ = true;
-  MergeParams mp{tok_, tile_off_, tile_len_, (uint32_t)ntiles_, weight_, a, b, X, slot_cap_,
-                 U(dsum_), U(dft_), dlist_, dcount_, U(dsum_) + 4 * ((size_t)slot_cap_ + 1), dcount_ + 1,
-                 exchange_ ? 0 : 1, (DeltaRecord*)dev_recs_, (uint32_t*)dev_count_,
-                 (u64*)((char*)dev_count_ + 16), seq_};
-  const size_t groups = (ntiles_ + kWaves - 1) / kWaves;
-  const int grid = (int)std::min<size_t>(groups, (size_t)cu_count_ * merge_blocks_per_cu_);
+  MergeParams& mp = *static_cast<MergeParams*>(merge_params_);
+  mp.tok = tok_;
+  mp.tile_off = tile_off_;
+  mp.tile_len = tile_len_;
+  mp.ntiles = (uint32_t)ntiles_;
+  mp.weight = weight_;
+  mp.a = a;
+  mp.b = b;
+  mp.X = X;
+  mp.slot_cap = slot_cap_;
+  mp.dsum = U(dsum_);
+  mp.dft = U(dft_);
+  mp.dlist = dlist_;
+  mp.dcount = dcount_;
+  mp.stats = U(dsum_) + 4 * ((size_t)slot_cap_ + 1);
+  mp.done = dcount_ + 1;
+  mp.fused = exchange_ ? 0 : 1;
+  mp.out = (DeltaRecord*)dev_recs_;
+  mp.hcount = (uint32_t*)dev_count_;
+  mp.hstats = (u64*)((char*)dev_count_ + 16);
+  mp.mlist = (uint32_t*)dev_mlist_;
+  mp.mcount = dcount_ + 10;
+  mp.seq = seq_;
+  mp.nlist = 0;
+  // tile skipping: visit only tiles(a) ∩ tiles(b) when that list is short
+  if (skip_ && index_.candidates(a, b, &cand_) && cand_.size() <= kInlineTiles) {
+    mp.nlist = (uint32_t)cand_.size();
+    std::memcpy(mp.list, cand_.data(), cand_.size() * sizeof(uint32_t));
+  }
+  const size_t n_iter = mp.nlist ? mp.nlist : ntiles_;
+  visited_tiles_ += n_iter;
+  const size_t groups = (n_iter + kWaves - 1) / kWaves;
+  const int grid = (int)std::min<size_t>(groups, (size_t)kMaxMergeGroups);
   // HIP events bracket every kTimingStride-th launch (an unbiased sample of launch durations
   // that keeps event overhead out of the timed loop)
   const bool sample = timing_ && (seq_ % kTimingStride == 0);
@@ -927,7 +1008,10 @@ void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
   if (sample) {
     HIP_OK(hipEventRecord((hipEvent_t)ev_[1], S(stream_)));
     timing_pending_ = true;
-    pending_bytes_ = 4.0 * (double)live_tokens_est_ + 12.0 * (double)ntiles_;
+    // algorithmic bytes of this launch: the visited tiles' live tokens (estimated from the
+    // mean tile length) + their descriptors
+    const double frac = ntiles_ ? (double)n_iter / (double)ntiles_ : 0.0;
+    pending_bytes_ = frac * 4.0 * (double)live_tokens_est_ + 12.0 * (double)n_iter;
   }
 }
 
@@ -952,7 +1036,10 @@ size_t Device::collect(int32_t X, const DeltaRecord** recs) {
   *recs = host_recs_;
   if (!ntiles_ && !exchange_) return 0;
   DeltaRecord* drec = (DeltaRecord*)dev_recs_;
-  if (launched_) wait_flag();
+  if (launched_) {
+    wait_flag();
+    index_.set_tiles(X, host_mlist_, host_count_[2]);
+  }
   launched_ = false;
   const u64* hs = (const u64*)(host_count_ + 4);
   size_t n;

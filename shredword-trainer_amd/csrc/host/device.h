@@ -76,11 +76,13 @@ class Device : public Backend {
   }
   void set_unk(int32_t unk) { unk_ = unk; }
   uint64_t records_total() const { return records_total_; }
+  uint64_t visited_tiles() const { return visited_tiles_; }
   uint64_t records_max() const { return records_max_; }
   void clear_times() {
     flush_timing();
     times_ = KernelTimes();
     records_total_ = records_max_ = 0;
+    visited_tiles_ = 0;
   }
   uint64_t live_tokens();  // Σ tile_len (headers included)
   size_t num_tiles() const { return ntiles_; }
@@ -130,6 +132,13 @@ class Device : public Backend {
   uint64_t records_total_ = 0, records_max_ = 0;
   int32_t max_id_seen_ = 0;
 
+  void* merge_params_ = nullptr;        // MergeParams kernel arguments (with the inline tile list)
+  TileIndex index_;                     // tile skipping (tiles.h)
+  bool skip_ = true;
+  std::vector<uint32_t> cand_;
+  uint64_t visited_tiles_ = 0;
+  uint32_t* host_mlist_ = nullptr;      // tiles where the last merge matched (pinned)
+  void* dev_mlist_ = nullptr;
   void* dev_recs_ = nullptr;            // device address of host_recs_
   void* dev_count_ = nullptr;           // device address of host_count_
   int merge_blocks_per_cu_ = 4;

@@ -30,15 +30,26 @@ void Engine::count_bigrams(Backend& be) {
                 sel_.heap_size(), (unsigned long long)min_freq_);
 }
 
-// One merge (bpe.cpp:244-318): false when the heap holds no valid candidate.
-bool Engine::merge_one(Backend& be) {
+void Engine::finish_speculation(Backend& be) {
+  if (!spec_active_) return;
+  be.rollback(spec_a_, spec_b_, spec_x_);
+  spec_active_ = false;
+  ++spec_misses_;
+}
+
+// One merge (bpe.cpp:244-318): false when the heap holds no valid candidate.  `remaining` = how
+// many more merges the caller may still ask for (no speculation past the last one).
+bool Engine::merge_one(Backend& be, int remaining) {
   int32_t a, b;
   uint64_t freq;
   const double t0 = now_seconds();
   const bool ok = sel_.select(&a, &b, &freq);
   const double t1 = now_seconds();
   times_.select_s += t1 - t0;
-  if (!ok) return false;
+  if (!ok) {
+    finish_speculation(be);
+    return false;
+  }
   const int32_t X = kBaseVocab + (int32_t)merge_a_.size();
   if (log_ >= 2)
     std::printf("[MERGE]\t Merging (%d,%d) freq=%llu -> new_id=%d (merge %zu)\n", a, b, (unsigned long long)freq, X,
@@ -46,7 +57,24 @@ bool Engine::merge_one(Backend& be) {
   if (trace_) std::fprintf(trace_, "M %d %d %llu %d\n", a, b, (unsigned long long)freq, X);
   merge_a_.push_back(a);
   merge_b_.push_back(b);
-  be.merge_scan(a, b, X);
+  bool launched = false;
+  if (spec_active_) {  // the guess made one merge ago
+    spec_active_ = false;
+    if (spec_a_ == a && spec_b_ == b && spec_x_ == X) {
+      launched = true;
+      ++spec_hits_;
+    } else {
+      be.rollback(spec_a_, spec_b_, spec_x_);
+      ++spec_misses_;
+    }
+  }
+  if (!launched) be.merge_scan(a, b, X);
+  if (speculate_ && remaining > 1 && be.can_speculate() &&
+      sel_.predict_next(a, b, pred_window_, &spec_a_, &spec_b_)) {
+    spec_x_ = X + 1;
+    spec_active_ = true;
+    be.merge_scan(spec_a_, spec_b_, spec_x_);
+  }
   const double t2 = now_seconds();
   const DeltaRecord* recs = nullptr;
   const size_t n = be.collect(X, &recs);
@@ -65,9 +93,10 @@ int Engine::merge_batch(Backend& be, int batch) {
   }
   int done = 0;
   while (done < batch && !sel_.heap_empty()) {
-    if (!merge_one(be)) break;
+    if (!merge_one(be, batch - done)) break;
     ++done;
   }
+  finish_speculation(be);
   return done;
 }
 
@@ -93,7 +122,7 @@ int Engine::train(Backend& be) {
                   total, target, sel_.heap_size(), (unsigned long long)tf);
     int merged = 0;
     while (merged < batch && !sel_.heap_empty()) {
-      if (!merge_one(be)) break;
+      if (!merge_one(be, target - total - merged)) break;
       ++merged;
     }
     if (merged <= 0) {
@@ -102,6 +131,7 @@ int Engine::train(Backend& be) {
     }
     total += merged;
   }
+  finish_speculation(be);
   if (trace_) std::fflush(trace_);
   times_.train_s += now_seconds() - t0;
   if (log_ >= 1) std::printf("[INFO]\t Training completed. Performed %d merges\n", total);

@@ -21,6 +21,11 @@ class Backend {
   // K2+K3: merge (a,b) -> X everywhere; K4: the merge's neighbour-delta records (all ranks).
   virtual void merge_scan(int32_t a, int32_t b, int32_t X) = 0;
   virtual size_t collect(int32_t X, const DeltaRecord** recs) = 0;
+  // Speculation support: a backend that can keep two merges in flight (merge_scan may be called
+  // for X+1 before collect(X)) and can exactly undo the oldest outstanding merge X (which must
+  // be the only one in flight) — rollback expands every X back into (a, b).
+  virtual bool can_speculate() const { return false; }
+  virtual void rollback(int32_t a, int32_t b, int32_t X) {}
   // K6: final weighted token histogram over ids [0, T) (all ranks).
   virtual void token_freq(size_t T, std::vector<uint64_t>* freq) = 0;
 };
@@ -50,9 +55,15 @@ class Engine {
   int32_t merge_second(size_t m) const { return merge_b_[m]; }
   const Selector& selector() const { return sel_; }
   EngineTimes& times() { return times_; }
+  // Speculative pipelining: while the host applies merge m's deltas and replays the heap, the
+  // backend already runs the predicted merge m+1; a wrong guess is rolled back exactly.
+  void set_speculation(bool on) { speculate_ = on; }
+  void finish_speculation(Backend& be);  // rolls back a pending guess (before any other access)
+  uint64_t spec_hits() const { return spec_hits_; }
+  uint64_t spec_misses() const { return spec_misses_; }
 
  private:
-  bool merge_one(Backend& be);
+  bool merge_one(Backend& be, int remaining);
 
   size_t target_vocab_ = 0;
   int32_t unk_ = 0;
@@ -62,6 +73,11 @@ class Engine {
   Selector sel_;
   std::vector<int32_t> merge_a_, merge_b_;
   EngineTimes times_;
+  bool speculate_ = true;
+  size_t pred_window_ = 256;
+  bool spec_active_ = false;
+  int32_t spec_a_ = 0, spec_b_ = 0, spec_x_ = 0;
+  uint64_t spec_hits_ = 0, spec_misses_ = 0;
 };
 
 }  // namespace shred

@@ -21,62 +21,62 @@ inline uint64_t mix64(uint64_t k) {
 void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
   unk_ = unk_id;
   min_freq_ = min_pair_freq;
-  infos_.clear();
-  index_.assign(1 << 16, 0);
-  mask_ = index_.size() - 1;
+  ctr_ = Counters();
+  table_.assign(1 << 20, Info{kEmptyKey, 0, 0, 0});  // 24 MB: no rehash below 512 k pairs
+  mask_ = table_.size() - 1;
+  count_ = 0;
   heap_.clear();
 }
 
-void Selector::grow_index() {
-  std::vector<uint32_t> idx(index_.size() * 2, 0);
-  uint64_t m = idx.size() - 1;
-  for (uint32_t i = 0; i < infos_.size(); ++i) {
-    uint64_t j = mix64(infos_[i].key) & m;
-    while (idx[j]) j = (j + 1) & m;
-    idx[j] = i + 1;
+void Selector::grow() {
+  std::vector<Info> old(table_.size() * 4, Info{kEmptyKey, 0, 0, 0});
+  old.swap(table_);
+  mask_ = table_.size() - 1;
+  for (const Info& in : old) {
+    if (in.key == kEmptyKey) continue;
+    uint64_t j = mix64(in.key) & mask_;
+    while (table_[j].key != kEmptyKey) j = (j + 1) & mask_;
+    table_[j] = in;
   }
-  index_.swap(idx);
-  mask_ = m;
 }
 
 Selector::Info& Selector::get(int32_t a, int32_t b) {
   const uint64_t key = pack_pair(a, b);
   uint64_t j = mix64(key) & mask_;
   for (;;) {
-    uint32_t s = index_[j];
-    if (!s) break;
-    if (infos_[s - 1].key == key) return infos_[s - 1];
+    Info& in = table_[j];
+    if (in.key == key) return in;
+    if (in.key == kEmptyKey) break;
     j = (j + 1) & mask_;
   }
-  if (2 * (infos_.size() + 1) > index_.size()) {
-    grow_index();
+  if (2 * (count_ + 1) > table_.size()) {
+    grow();
     j = mix64(key) & mask_;
-    while (index_[j]) j = (j + 1) & mask_;
+    while (table_[j].key != kEmptyKey) j = (j + 1) & mask_;
   }
-  infos_.push_back({key, 0, 0, (uint32_t)infos_.size()});
-  index_[j] = (uint32_t)infos_.size();
-  return infos_.back();
+  table_[j] = Info{key, 0, 0, (uint32_t)count_++};
+  return table_[j];
+}
+
+const Selector::Info* Selector::find(uint64_t key) const {
+  uint64_t j = mix64(key) & mask_;
+  for (;;) {
+    const Info& in = table_[j];
+    if (in.key == key) return &in;
+    if (in.key == kEmptyKey) return nullptr;
+    j = (j + 1) & mask_;
+  }
 }
 
 bool Selector::lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) const {
-  const uint64_t key = pack_pair(a, b);
-  uint64_t j = mix64(key) & mask_;
-  for (;;) {
-    uint32_t s = index_[j];
-    if (!s) break;
-    if (infos_[s - 1].key == key) {
-      *freq = infos_[s - 1].freq;
-      *version = infos_[s - 1].version;
-      return true;
-    }
-    j = (j + 1) & mask_;
-  }
-  *freq = 0;
-  *version = 0;
-  return false;
+  const Info* in = find(pack_pair(a, b));
+  *freq = in ? in->freq : 0;
+  *version = in ? in->version : 0;
+  return in != nullptr;
 }
 
 void Selector::push(int32_t a, int32_t b, uint64_t freq, uint32_t version) {
+  ++ctr_.pushes;
   size_t i = heap_.size();
   heap_.push_back({});
   const HeapEnt x{a, b, freq, version};
@@ -90,6 +90,7 @@ void Selector::push(int32_t a, int32_t b, uint64_t freq, uint32_t version) {
 }
 
 Selector::HeapEnt Selector::pop() {
+  ++ctr_.pops;
   HeapEnt top = heap_[0];
   HeapEnt x = heap_.back();
   heap_.pop_back();
@@ -118,27 +119,51 @@ void Selector::add_counts(std::vector<PairCount> pairs) {
     in.freq += p.count;
   }
   // Heap build: bucket 0..4095, chain (creation) order, freq >= min (bpe.cpp:218-225).
-  std::vector<std::pair<uint64_t, uint32_t>> order;
-  order.reserve(infos_.size());
-  for (uint32_t i = 0; i < infos_.size(); ++i) {
-    const Info& in = infos_[i];
-    if (in.freq >= min_freq_) {
+  std::vector<std::pair<uint64_t, uint64_t>> order;  // ((bucket << 32) | seq, slot)
+  order.reserve(count_);
+  for (uint64_t i = 0; i < table_.size(); ++i) {
+    const Info& in = table_[i];
+    if (in.key != kEmptyKey && in.freq >= min_freq_) {
       uint32_t bk = pair_fnv(pair_first(in.key), pair_second(in.key)) & (kPairBuckets - 1);
       order.push_back({((uint64_t)bk << 32) | in.seq, i});
     }
   }
   std::sort(order.begin(), order.end());
   for (auto& o : order) {
-    const Info& in = infos_[o.second];
+    const Info& in = table_[o.second];
     push(pair_first(in.key), pair_second(in.key), in.freq, in.version);
   }
+}
+
+bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, int32_t* pb) const {
+  const size_t n = std::min(window, heap_.size());
+  uint64_t best_f = 0;
+  size_t best = SIZE_MAX;
+  for (size_t i = 0; i < n; ++i) {
+    const HeapEnt& e = heap_[i];
+    if (e.freq < best_f || e.freq < min_freq_) continue;
+    if (e.a == a || e.a == b || e.b == a || e.b == b || e.a == unk_ || e.b == unk_) continue;
+    const Info* in = find(pack_pair(e.a, e.b));
+    if (!in || in->version != e.version || in->freq != e.freq) continue;
+    if (e.freq > best_f || best == SIZE_MAX) {
+      best_f = e.freq;
+      best = i;
+    }
+  }
+  if (best == SIZE_MAX) return false;
+  *pa = heap_[best].a;
+  *pb = heap_[best].b;
+  return true;
 }
 
 bool Selector::select(int32_t* a, int32_t* b, uint64_t* freq) {
   while (!heap_.empty()) {
     HeapEnt top = pop();
     Info& in = get(top.a, top.b);
-    if (top.version != in.version) continue;  // stale entry
+    if (top.version != in.version) {  // stale entry
+      ++ctr_.stale;
+      continue;
+    }
     uint64_t actual = (top.a == unk_ || top.b == unk_) ? 0 : in.freq;
     if (actual != in.freq) {
       in.freq = actual;
@@ -156,6 +181,7 @@ bool Selector::select(int32_t* a, int32_t* b, uint64_t* freq) {
 }
 
 void Selector::apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n) {
+  const uint64_t c0 = __builtin_ia32_rdtsc();
   // 1. records -> FreqChange entries keyed exactly like the reference's pair_hash.
   changes_.clear();
   size_t cap = 64;
@@ -192,13 +218,33 @@ void Selector::apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, s
       j = (j + 1) & cm;
     }
   }
+  ctr_.records += n;
+  ctr_.changes += changes_.size();
+  const uint64_t c1 = __builtin_ia32_rdtsc();
+  ctr_.cyc_combine += c1 - c0;
   // 2. reference application order: bucket (hk % 1024) ascending, latest first touch first.
-  std::sort(changes_.begin(), changes_.end(), [](const Change& x, const Change& y) {
-    const uint64_t bx = x.hk % kDeltaBuckets, by = y.hk % kDeltaBuckets;
-    if (bx != by) return bx < by;
-    return x.ft > y.ft;
-  });
-  for (const Change& c : changes_) {
+  //    Counting sort by bucket, then insertion sort inside the (almost always tiny) buckets.
+  bucket_start_.assign(kDeltaBuckets + 1, 0);
+  for (const Change& c : changes_) bucket_start_[(c.hk % kDeltaBuckets) + 1]++;
+  for (int k = 0; k < kDeltaBuckets; ++k) bucket_start_[k + 1] += bucket_start_[k];
+  ordered_.resize(changes_.size());
+  for (const Change& c : changes_) ordered_[bucket_start_[c.hk % kDeltaBuckets]++] = c;
+  for (size_t i = 1; i < ordered_.size(); ++i) {
+    const Change c = ordered_[i];
+    const uint64_t bk = c.hk % kDeltaBuckets;
+    size_t j = i;
+    while (j > 0 && ordered_[j - 1].hk % kDeltaBuckets == bk && ordered_[j - 1].ft < c.ft) {
+      ordered_[j] = ordered_[j - 1];
+      --j;
+    }
+    ordered_[j] = c;
+  }
+  const uint64_t c2 = __builtin_ia32_rdtsc();
+  ctr_.cyc_order += c2 - c1;
+  // the table lines this merge touches, requested before the ordered walk needs them
+  if (2 * (count_ + ordered_.size() + 1) > table_.size()) grow();
+  for (const Change& c : ordered_) __builtin_prefetch(&table_[mix64(pack_pair((int32_t)(c.hk >> 32), (int32_t)c.hk)) & mask_]);
+  for (const Change& c : ordered_) {
     const int32_t f = (int32_t)(uint32_t)(c.hk >> 32), s = (int32_t)(uint32_t)c.hk;
     if (f == a && s == b) continue;
     Info& in = get(f, s);
@@ -216,6 +262,7 @@ void Selector::apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, s
   Info& merged = get(a, b);
   merged.freq = 0;
   merged.version++;
+  ctr_.cyc_walk += __builtin_ia32_rdtsc() - c2;
 }
 
 }  // namespace shred

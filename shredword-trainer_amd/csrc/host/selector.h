@@ -61,32 +61,49 @@ class Selector {
   // Applies one merge's device deltas and finalises the merged key (bpe.cpp:297-318).
   void apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n);
 
+  // Guess of the merge after (a, b), made before (a, b)'s deltas are known: the best valid heap
+  // entry among the first `window` heap slots that shares no token with (a, b).  Used only to
+  // run the next merge speculatively; the exact replay decides.
+  bool predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, int32_t* pb) const;
+
   size_t heap_size() const { return heap_.size(); }
   bool heap_empty() const { return heap_.empty(); }
   uint64_t heap_top_freq() const { return heap_.empty() ? 0 : heap_[0].freq; }
-  size_t num_pairs() const { return infos_.size(); }
+  size_t num_pairs() const { return count_; }
   // freq/version of a pair (0/0 when absent); for tests.
   bool lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) const;
   int32_t unk_id() const { return unk_; }
+  struct Counters {
+    uint64_t pops = 0, stale = 0, pushes = 0, records = 0, changes = 0;
+    uint64_t cyc_combine = 0, cyc_order = 0, cyc_walk = 0;  // TSC cycles inside apply()
+  };
+  const Counters& counters() const { return ctr_; }
 
  private:
+  // One flat open-addressing table: a lookup touches one cache line.  kEmptyKey is the packed
+  // pair (INT32_MIN, INT32_MIN), which no token pair can be (ids are >= -2^30).
   struct Info { uint64_t key; uint64_t freq; uint32_t version; uint32_t seq; };
   struct HeapEnt { int32_t a, b; uint64_t freq; uint32_t version; };
   struct Change { uint64_t hk; int64_t delta; uint64_t ft; };
+  static constexpr uint64_t kEmptyKey = 0x8000000080000000ull;
 
   Info& get(int32_t a, int32_t b);  // get-or-create (bimap_get)
+  const Info* find(uint64_t key) const;
   void push(int32_t a, int32_t b, uint64_t freq, uint32_t version);
   HeapEnt pop();
-  void grow_index();
+  void grow();
 
   int32_t unk_ = 0;
   uint64_t min_freq_ = 2000;
-  std::vector<Info> infos_;
-  std::vector<uint32_t> index_;  // open addressing: info index + 1
+  std::vector<Info> table_;
+  size_t count_ = 0;
   uint64_t mask_ = 0;
   std::vector<HeapEnt> heap_;
   std::vector<Change> changes_;
   std::vector<uint32_t> change_index_;
+  std::vector<uint32_t> bucket_start_;
+  std::vector<Change> ordered_;
+  Counters ctr_;
 };
 
 }  // namespace shred

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <iterator>
 #include <thread>
 
 #include "common.h"
@@ -94,6 +95,118 @@ void pack_tiles(const WordTable& wt, Layout layout, size_t begin, size_t end, Ti
     for (auto& th : pool) th.join();
   }
   for (uint32_t l : ts.len) ts.live += l;
+}
+
+}  // namespace shred
+
+namespace shred {
+
+void TileIndex::make(Set* s, std::vector<uint32_t>&& sorted) const {
+  s->size = sorted.size();
+  s->list.clear();
+  s->bits.clear();
+  if ((uint64_t)sorted.size() * 32 > ntiles_) {  // a bitmap is smaller
+    s->bits.assign((ntiles_ + 63) / 64, 0);
+    for (uint32_t t : sorted) s->bits[t >> 6] |= 1ull << (t & 63);
+  } else {
+    s->list = std::move(sorted);
+  }
+}
+
+void TileIndex::build(const TiledStream& ts) {
+  ntiles_ = (uint32_t)ts.num_tiles();
+  std::vector<std::vector<uint32_t>> tl(256);
+  std::vector<uint32_t> seen(256, UINT32_MAX);
+  for (uint32_t t = 0; t < ntiles_; ++t) {
+    const int32_t* p = ts.tok.data() + ts.off[t];
+    for (uint32_t i = 0; i < ts.len[t]; ++i) {
+      const int32_t id = p[i];
+      if (id < 0) continue;  // headers, negative unk
+      if ((size_t)id >= seen.size()) {
+        seen.resize(id + 1, UINT32_MAX);
+        tl.resize(id + 1);
+      }
+      if (seen[id] != t) {
+        seen[id] = t;
+        tl[id].push_back(t);
+      }
+    }
+  }
+  ids_.assign(tl.size(), Set());
+  for (size_t id = 0; id < tl.size(); ++id) make(&ids_[id], std::move(tl[id]));
+  ids0_ = ids_;
+  // exact tiles of every adjacent pair of base ids
+  std::vector<std::vector<uint32_t>> pl(256 * 256);
+  std::vector<uint32_t> last(256 * 256, UINT32_MAX);
+  for (uint32_t t = 0; t < ntiles_; ++t) {
+    const int32_t* p = ts.tok.data() + ts.off[t];
+    for (uint32_t i = 0; i + 1 < ts.len[t]; ++i) {
+      const uint32_t x = (uint32_t)p[i], y = (uint32_t)p[i + 1];
+      if (x >= 256 || y >= 256) continue;  // headers, unk outside the byte range, merged ids
+      const uint32_t k = x * 256 + y;
+      if (last[k] != t) {
+        last[k] = t;
+        pl[k].push_back(t);
+      }
+    }
+  }
+  base_pairs_.assign(256 * 256, Set());
+  for (size_t k = 0; k < pl.size(); ++k) make(&base_pairs_[k], std::move(pl[k]));
+}
+
+void TileIndex::reset() { ids_ = ids0_; }
+
+void TileIndex::set_tiles(int32_t id, const uint32_t* tiles, size_t n) {
+  if (id < 0) return;
+  if ((size_t)id >= ids_.size()) ids_.resize(id + 1);
+  std::vector<uint32_t> v(tiles, tiles + n);
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  make(&ids_[id], std::move(v));
+}
+
+bool TileIndex::candidates(int32_t a, int32_t b, std::vector<uint32_t>* out) const {
+  out->clear();
+  const size_t limit = ntiles_ / 2;  // beyond this a full scan is as cheap
+  if ((uint32_t)a < 256 && (uint32_t)b < 256 && !base_pairs_.empty()) {
+    const Set& s = base_pairs_[(uint32_t)a * 256 + (uint32_t)b];
+    if (s.size == 0 || s.size > limit) return false;
+    if (!s.list.empty()) {
+      *out = s.list;
+    } else {
+      for (size_t w = 0; w < s.bits.size(); ++w)
+        for (uint64_t m = s.bits[w]; m; m &= m - 1) out->push_back((uint32_t)(w * 64 + __builtin_ctzll(m)));
+    }
+    return true;
+  }
+  const Set* sa = get(a);
+  const Set* sb = get(b);
+  if (!sa || !sb) return false;  // unknown id: be safe, scan everything
+  return intersect(sa, sb, out) && out->size() <= limit;
+}
+
+bool TileIndex::intersect(const Set* sa, const Set* sb, std::vector<uint32_t>* out) const {
+  if (sa->size > sb->size) std::swap(sa, sb);
+  const size_t limit = ntiles_ / 2;
+  if (sa->size > limit || sa->size == 0) return false;
+  if (!sa->list.empty()) {
+    if (!sb->bits.empty()) {
+      for (uint32_t t : sa->list)
+        if ((sb->bits[t >> 6] >> (t & 63)) & 1) out->push_back(t);
+    } else {
+      std::set_intersection(sa->list.begin(), sa->list.end(), sb->list.begin(), sb->list.end(),
+                            std::back_inserter(*out));
+    }
+  } else {  // both dense
+    for (size_t w = 0; w < sa->bits.size(); ++w) {
+      uint64_t m = sa->bits[w] & sb->bits[w];
+      while (m) {
+        out->push_back((uint32_t)(w * 64 + __builtin_ctzll(m)));
+        m &= m - 1;
+      }
+    }
+  }
+  return !out->empty();
 }
 
 }  // namespace shred

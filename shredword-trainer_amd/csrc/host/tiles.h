@@ -36,3 +36,39 @@ void shard_range(const WordTable& wt, Layout layout, int rank, int world, size_t
 void pack_tiles(const WordTable& wt, Layout layout, size_t begin, size_t end, TiledStream* out);
 
 }  // namespace shred
+
+namespace shred {
+
+// Tile skipping: for every token id, a superset of the tiles that hold it.
+// A merge (a, b) only has to visit tiles(a) ∩ tiles(b); the merge reports the tiles where it
+// created X, which become tiles(X).  A merge never creates an adjacency between two tokens
+// that both existed before it, so for pairs of two base ids (< 256) the exact tile list of
+// the initial stream stays a superset for the whole run and replaces the intersection.  Sets
+// with few tiles are sorted lists, frequent ones bitmaps.  Supersets stay correct, so nothing
+// is removed after a merge.
+class TileIndex {
+ public:
+  void build(const TiledStream& ts);
+  void reset();  // back to the state after build()
+  // Candidate tiles of (a, b) in ascending order; false = visiting every tile is cheaper.
+  bool candidates(int32_t a, int32_t b, std::vector<uint32_t>* out) const;
+  void set_tiles(int32_t id, const uint32_t* tiles, size_t n);
+  size_t num_tiles() const { return ntiles_; }
+
+ private:
+  struct Set {
+    std::vector<uint32_t> list;  // sorted, when sparse
+    std::vector<uint64_t> bits;  // when dense
+    size_t size = 0;
+  };
+  void make(Set* s, std::vector<uint32_t>&& sorted) const;
+  const Set* get(int32_t id) const { return (id >= 0 && (size_t)id < ids_.size()) ? &ids_[id] : nullptr; }
+
+  bool intersect(const Set* sa, const Set* sb, std::vector<uint32_t>* out) const;
+
+  uint32_t ntiles_ = 0;
+  std::vector<Set> ids_, ids0_;
+  std::vector<Set> base_pairs_;  // [a * 256 + b] for a, b < 256 (immutable after build)
+};
+
+}  // namespace shred

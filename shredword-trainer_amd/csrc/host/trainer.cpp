@@ -227,6 +227,21 @@ int shred_reset(Trainer* t) {
   return 0;
 }
 
+double shred_probe_merge(Trainer* t, int32_t a, int32_t b, int iters) {
+  if (!t || iters <= 0 || !ensure_device(t, "shred_probe_merge")) return -1.0;
+  const int32_t X = kBaseVocab + (int32_t)t->engine.num_merges();
+  double total = 0;
+  for (int i = 0; i < iters; ++i) {
+    const double t0 = now_seconds();
+    t->dev->merge_scan(a, b, X);
+    const DeltaRecord* recs = nullptr;
+    const size_t n = t->dev->collect(X, &recs);
+    total += now_seconds() - t0;
+    if (n != 0) return -1.0;  // the pair occurs: the probe would have changed the corpus
+  }
+  return 1e6 * total / iters;
+}
+
 int shred_get_stats(const Trainer* tc, ShredStats* s) {
   if (!tc || !s) return -1;
   Trainer* t = const_cast<Trainer*>(tc);
@@ -256,6 +271,15 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
   s->num_occurrences = t->wt.total_occurrences;
   s->num_merges = t->engine.num_merges();
   s->heap_size = t->engine.selector().heap_size();
+  const Selector::Counters& c = t->engine.selector().counters();
+  s->heap_pops = c.pops;
+  s->heap_stale_pops = c.stale;
+  s->heap_pushes = c.pushes;
+  s->delta_records = c.records;
+  s->apply_cycles_combine = c.cyc_combine;
+  s->apply_cycles_order = c.cyc_order;
+  s->apply_cycles_walk = c.cyc_walk;
+  if (t->dev) s->tiles_visited = t->dev->visited_tiles();
   s->layout = (int32_t)t->layout;
   s->world_size = dist_active() ? dist_state().world : 1;
   return 0;

@@ -57,7 +57,11 @@ class ShredStats(Structure):
                 ("num_words", c_uint64), ("num_symbols", c_uint64), ("num_occurrences", c_uint64),
                 ("num_merges", c_uint64), ("heap_size", c_uint64), ("live_tokens", c_uint64),
                 ("device_bytes", c_uint64), ("num_tiles", c_uint64),
-                ("layout", c_int32), ("world_size", c_int32)]
+                ("layout", c_int32), ("world_size", c_int32),
+                ("heap_pops", c_uint64), ("heap_stale_pops", c_uint64), ("heap_pushes", c_uint64),
+                ("delta_records", c_uint64), ("tiles_visited", c_uint64),
+                ("apply_cycles_combine", c_uint64), ("apply_cycles_order", c_uint64),
+                ("apply_cycles_walk", c_uint64)]
 
 
 Trainer = c_void_p
@@ -88,6 +92,7 @@ lib.loadVocab.argtypes, lib.loadVocab.restype = [c_void_p, c_char_p], c_bool
 # extensions (include/shredword_bpe.h)
 lib.shred_set_option.argtypes, lib.shred_set_option.restype = [Trainer, c_char_p, c_char_p], c_int
 lib.shred_reset.argtypes, lib.shred_reset.restype = [Trainer], c_int
+lib.shred_probe_merge.argtypes, lib.shred_probe_merge.restype = [Trainer, c_int32, c_int32, c_int], c_double
 lib.shred_get_stats.argtypes, lib.shred_get_stats.restype = [Trainer, POINTER(ShredStats)], c_int
 lib.shred_device_count.argtypes, lib.shred_device_count.restype = [], c_int
 lib.shred_dist_unique_id.argtypes, lib.shred_dist_unique_id.restype = [c_void_p, c_size_t], c_int

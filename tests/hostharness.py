@@ -25,9 +25,10 @@ def load():
     lib.hh_init.argtypes = [ctypes.c_void_p]
     lib.hh_save.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
     for fn in ("hh_num_words", "hh_num_symbols", "hh_num_tiles", "hh_live_tokens", "hh_heap_size",
-               "hh_distinct_bytes", "hh_kept_bytes"):
+               "hh_distinct_bytes", "hh_kept_bytes", "hh_tiles_visited"):
         getattr(lib, fn).argtypes = [ctypes.c_void_p]
         getattr(lib, fn).restype = ctypes.c_uint64
+    lib.hh_spec.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     lib.hh_word.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                             ctypes.POINTER(ctypes.c_uint64)]
     lib.hh_word.restype = ctypes.c_uint64

@@ -33,10 +33,13 @@ class EmuBackend : public Backend {
   EmuBackend(const WordTable& wt, Layout layout, size_t begin, size_t end, uint32_t slot_cap)
       : wt_(wt), layout_(layout), cap_(slot_cap) {
     pack_tiles(wt, layout, begin, end, &ts_);
+    index_.build(ts_);
     dsum_.assign(4 * ((size_t)cap_ + 1), 0);
     dft_.assign(4 * ((size_t)cap_ + 1), ~0ull);
   }
   void set_exchange(ExchangeCb cb, void* ctx) { cb_ = cb; ctx_ = ctx; }
+  void set_speculation(bool on) { spec_ = on; }
+  bool can_speculate() const override { return spec_ && !cb_; }
 
   uint64_t weight(uint32_t rank) const { return layout_ == Layout::kTypes ? wt_.count[rank] : 1; }
 
@@ -70,9 +73,14 @@ class EmuBackend : public Backend {
   void merge_scan(int32_t a, int32_t b, int32_t X) override {
     if ((uint32_t)X >= cap_) fatal("emulated slot capacity exceeded");
     std::vector<int32_t> out;
-    for (size_t t = 0; t < ts_.num_tiles(); ++t) {
+    std::vector<uint32_t> cand, matched;
+    const bool use_list = index_.candidates(a, b, &cand);
+    const size_t nvisit = use_list ? cand.size() : ts_.num_tiles();
+    for (size_t it = 0; it < nvisit; ++it) {
+      const size_t t = use_list ? cand[it] : it;
       int32_t* p = ts_.tok.data() + ts_.off[t];
       const uint32_t len = ts_.len[t];
+      size_t hits = 0;
       out.clear();
       uint32_t hidx = 0, rank = 0;
       bool prev_x = false;
@@ -101,6 +109,7 @@ class EmuBackend : public Backend {
           }
           out.push_back(X);
           prev_x = true;
+          ++hits;
           i += 2;
         } else {
           out.push_back(tk);
@@ -110,18 +119,64 @@ class EmuBackend : public Backend {
       }
       std::memcpy(p, out.data(), out.size() * sizeof(int32_t));
       ts_.len[t] = (uint32_t)out.size();
+      if (hits) matched.push_back((uint32_t)t);
     }
+    visited_ += nvisit;
+    hist_.push_back((uint32_t)nvisit);
+    Pending pd;
+    pd.a = a;
+    pd.b = b;
+    pd.X = X;
+    pd.matched = std::move(matched);
+    if (!cb_) drain(&pd.recs);  // multi-rank: tables stay for collect()'s exchange
+    queue_.push_back(std::move(pd));
   }
 
-  size_t collect(int32_t, const DeltaRecord** recs) override {
-    if (cb_) cb_(ctx_, dsum_.data(), dft_.data(), dsum_.size());
-    recs_.clear();
+  // touched slots -> records, clearing the tables
+  void drain(std::vector<DeltaRecord>* out) {
+    out->clear();
     for (size_t k = 0; k < dsum_.size(); ++k) {
       if (dft_[k] == ~0ull) continue;
-      recs_.push_back({(uint32_t)k, 0, dsum_[k], dft_[k]});
+      out->push_back({(uint32_t)k, 0, dsum_[k], dft_[k]});
       dsum_[k] = 0;
       dft_[k] = ~0ull;
     }
+  }
+
+  void rollback(int32_t a, int32_t b, int32_t X) override {
+    if (queue_.empty() || queue_.front().X != X) fatal("emulated rollback of a merge that is not outstanding");
+    std::vector<int32_t> out;
+    for (uint32_t t : queue_.front().matched) {  // the exact inverse of the merge: X -> a b
+      int32_t* p = ts_.tok.data() + ts_.off[t];
+      out.clear();
+      for (uint32_t i = 0; i < ts_.len[t]; ++i) {
+        if (p[i] == X) {
+          out.push_back(a);
+          out.push_back(b);
+        } else {
+          out.push_back(p[i]);
+        }
+      }
+      std::memcpy(p, out.data(), out.size() * sizeof(int32_t));
+      ts_.len[t] = (uint32_t)out.size();
+    }
+    queue_.erase(queue_.begin());
+    ++rollbacks_;
+  }
+  uint64_t rollbacks_ = 0;
+  uint64_t visited() const { return visited_; }
+  std::vector<uint32_t> hist_;
+
+  size_t collect(int32_t X, const DeltaRecord** recs) override {
+    if (queue_.empty() || queue_.front().X != X) fatal("emulated collect of a merge that is not outstanding");
+    Pending pd = std::move(queue_.front());
+    queue_.erase(queue_.begin());
+    if (cb_) {
+      cb_(ctx_, dsum_.data(), dft_.data(), dsum_.size());
+      drain(&pd.recs);
+    }
+    index_.set_tiles(X, pd.matched.data(), pd.matched.size());
+    recs_ = std::move(pd.recs);
     *recs = recs_.data();
     return recs_.size();
   }
@@ -149,8 +204,17 @@ class EmuBackend : public Backend {
   Layout layout_;
   uint32_t cap_;
   TiledStream ts_;
+  TileIndex index_;
+  uint64_t visited_ = 0;
   std::vector<uint64_t> dsum_, dft_;
   std::vector<DeltaRecord> recs_;
+  struct Pending {
+    int32_t a = 0, b = 0, X = 0;
+    std::vector<uint32_t> matched;
+    std::vector<DeltaRecord> recs;
+  };
+  std::vector<Pending> queue_;  // merges launched but not collected (at most 2)
+  bool spec_ = true;
   ExchangeCb cb_ = nullptr;
   void* ctx_ = nullptr;
 };
@@ -230,6 +294,30 @@ uint64_t hh_live_tokens(void* p) {
   uint64_t s = 0;
   for (uint32_t l : ((Harness*)p)->be->stream().len) s += l;
   return s;
+}
+uint64_t hh_tiles_visited(void* p) { return ((Harness*)p)->be->visited(); }
+uint64_t hh_visit_hist(void* p, uint32_t* out, uint64_t cap) {
+  const auto& h = ((Harness*)p)->be->hist_;
+  for (size_t i = 0; i < h.size() && i < cap; ++i) out[i] = h[i];
+  return h.size();
+}
+void hh_counters(void* p, uint64_t* out) {
+  const auto& c = ((Harness*)p)->engine.selector().counters();
+  out[0] = c.pops; out[1] = c.stale; out[2] = c.pushes; out[3] = c.records; out[4] = c.changes;
+  out[5] = ((Harness*)p)->engine.selector().num_pairs();
+}
+void hh_spec(void* p, int on, uint64_t* out) {
+  Harness* h = (Harness*)p;
+  if (on >= 0) {
+    h->engine.set_speculation(on != 0);
+    h->be->set_speculation(on != 0);
+  }
+  out[0] = h->engine.spec_hits();
+  out[1] = h->engine.spec_misses();
+}
+void hh_times(void* p, double* out) {
+  const EngineTimes& t = ((Harness*)p)->engine.times();
+  out[0] = t.select_s; out[1] = t.launch_s; out[2] = t.wait_s; out[3] = t.apply_s; out[4] = t.train_s;
 }
 uint64_t hh_heap_size(void* p) { return ((Harness*)p)->engine.selector().heap_size(); }
 uint64_t hh_distinct_bytes(void* p) { return ((Harness*)p)->wt.distinct_bytes; }
