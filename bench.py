@@ -226,6 +226,8 @@ def main():
                                                       "apply_cycles_combine", "apply_cycles_order",
                                                       "apply_cycles_walk")},
             "tiles_visited_per_merge": st["tiles_visited"] / max(1, merges),
+            "speculation": {"hits": st["spec_hits"], "misses": st["spec_misses"],
+                            "hit_rate": st["spec_hits"] / max(1, st["spec_hits"] + st["spec_misses"])},
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

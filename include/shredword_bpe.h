@@ -72,6 +72,10 @@ int loadVocab(void* trainer, const char* path);
  *   trace  = <path>             "M a b freq new_id" / "B batch done heap top" trace file
  *   timing = 0 | 1              per-kernel HIP-event timing (shred_get_stats)
  *   device = <ordinal>          HIP device (default: LOCAL_RANK or 0)
+ *   merge_groups = <n>          k_merge grid cap (tuning; after load_corpus)
+ *   speculate = 0 | 1           run the predicted next merge while the host consumes the
+ *                               current one, rolled back exactly on a wrong guess (default 1;
+ *                               single GPU only, results are identical either way)
  * Returns 0, or -1 for an unknown key/value. */
 int shred_set_option(Trainer* trainer, const char* key, const char* value);
 /* Restores the loaded corpus to its unmerged state and forgets merges (benchmark repeats). */
@@ -80,6 +84,12 @@ int shred_reset(Trainer* trainer);
  * (so nothing changes), timing launch -> records on the host.  Returns mean microseconds per
  * merge, or -1 when the pair occurs / no device. */
 double shred_probe_merge(Trainer* trainer, int32_t a, int32_t b, int iters);
+/* Diagnostic: launches the merge (a, b) -> next id and immediately rolls it back (the undo path
+ * of speculation); the corpus must be unchanged afterwards.  Returns 0, or -1 without a device. */
+int shred_probe_rollback(Trainer* trainer, int32_t a, int32_t b);
+/* Diagnostic: copies the live token stream (per corpus entry: header INT32_MIN + rank, then its
+ * tokens) into out[0 .. cap); returns the full length (call with cap 0 to size), -1 on error. */
+int64_t shred_debug_tokens(Trainer* trainer, int32_t* out, size_t cap);
 
 typedef struct ShredStats {
   double load_seconds, init_seconds, train_seconds;
@@ -92,6 +102,7 @@ typedef struct ShredStats {
   int32_t layout, world_size;
   uint64_t heap_pops, heap_stale_pops, heap_pushes, delta_records, tiles_visited;
   uint64_t apply_cycles_combine, apply_cycles_order, apply_cycles_walk;
+  uint64_t spec_hits, spec_misses;
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -22,6 +22,9 @@
 #ifndef SHRED_DELTA_LDS
 #define SHRED_DELTA_LDS 2048
 #endif
+#ifndef SHRED_SIG_BITS
+#define SHRED_SIG_BITS 8192
+#endif
 
 #include <algorithm>
 #include <cstring>
@@ -54,6 +57,7 @@ constexpr int kPairLds = 2048;           // per-workgroup pair-count staging slo
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 constexpr unsigned long long kEmpty64 = ~0ull;
 constexpr int32_t kPad = INT32_MIN;      // beyond the tile; also looks like a header
+constexpr size_t kStreamPad = kChunk + 64;  // elements allocated past the stream (whole-chunk reads)
 
 typedef unsigned long long u64;
 
@@ -67,6 +71,38 @@ __device__ __forceinline__ u64 mix64(u64 k) {
   k *= 0xC4CEB9FE1A85EC53ull;
   k ^= k >> 33;
   return k;
+}
+
+// Host-visible writes.  Plain stores, published by one system-scope release (L2 write-back)
+// before the flag: measured on MI355X, write-through system stores (sc0 sc1, SHRED_SYS_STORES)
+// are one small PCIe write each and made a merge 2-8x slower, while a flag behind plain stores
+// without the release let the host read stale records.
+#ifdef SHRED_SYS_STORES
+__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#else
+__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) { *p = v; }
+__device__ __forceinline__ void sys_store(unsigned long long* p, unsigned long long v) { *p = v; }
+#endif
+// Raises a host-visible flag after this lane's (and, behind a barrier, its workgroup's) writes.
+__device__ __forceinline__ void sys_flag(uint32_t* flag, uint32_t v) {
+#ifdef SHRED_SYS_STORES
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  __threadfence_system();
+  __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+}
+__device__ __forceinline__ void sys_record(void* rec, uint32_t key, unsigned long long sum, unsigned long long ft) {
+  unsigned long long* r = static_cast<unsigned long long*>(rec);
+  sys_store(r, (unsigned long long)key);
+  sys_store(r + 1, sum);
+  sys_store(r + 2, ft);
 }
 
 // One exclusive block scan of a packed header key (max) and a counter (sum) over 256 lanes.
@@ -120,42 +156,91 @@ __device__ __forceinline__ void block_scan_hdr_cnt(u64 hdr, int cnt, ScanLds& s,
   __syncthreads();
 }
 
-// Loads this lane's 16 tokens of chunk [cs, cs+cl) (kPad beyond cl).  16-byte loads where the
-// whole quad is in range: tiles start 16-byte aligned and chunks are 4096 tokens.
+// ---- wave-level data movement on DPP (gfx9 row / wave shifts and row broadcasts): a few cycles
+// each instead of an LDS round trip per __shfl (ds_bpermute).
+template <int kCtrl, int kRowMask = 0xf, bool kBound = true>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kCtrl, kRowMask, 0xf, kBound);
+}
+template <int kCtrl, int kRowMask = 0xf, bool kBound = true>
+__device__ __forceinline__ u64 dpp64(u64 x) {
+  const uint32_t lo = dpp32<kCtrl, kRowMask, kBound>((uint32_t)x);
+  const uint32_t hi = dpp32<kCtrl, kRowMask, kBound>((uint32_t)(x >> 32));
+  return ((u64)hi << 32) | lo;
+}
+constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i + 1 (lane 63 <- 0)
+constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i - 1 (lane 0 <- 0)
+__device__ __forceinline__ int32_t wave_next(int32_t x) { return (int32_t)dpp32<kDppWaveShl1>((uint32_t)x); }
+__device__ __forceinline__ uint32_t wave_prev(uint32_t x) { return dpp32<kDppWaveShr1>(x); }
+__device__ __forceinline__ u64 wave_prev64(u64 x) { return dpp64<kDppWaveShr1>(x); }
+
+// Inclusive wave scans (sum / max, identity 0): row shifts 1, 2, 4, 8, then row broadcasts 15, 31.
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t x) {
+  x += dpp32<0x111>(x);
+  x += dpp32<0x112>(x);
+  x += dpp32<0x114>(x);
+  x += dpp32<0x118>(x);
+  x += dpp32<0x142, 0xa, false>(x);
+  x += dpp32<0x143, 0xc, false>(x);
+  return x;
+}
+__device__ __forceinline__ u64 max64(u64 a, u64 b) { return a > b ? a : b; }
+__device__ __forceinline__ u64 wave_scan_max64(u64 x) {
+  x = max64(x, dpp64<0x111>(x));
+  x = max64(x, dpp64<0x112>(x));
+  x = max64(x, dpp64<0x114>(x));
+  x = max64(x, dpp64<0x118>(x));
+  x = max64(x, dpp64<0x142, 0xa, false>(x));
+  x = max64(x, dpp64<0x143, 0xc, false>(x));
+  return x;
+}
+__device__ __forceinline__ uint32_t lane_read(uint32_t x, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, lane);
+}
+__device__ __forceinline__ u64 lane_read64(u64 x, int lane) {
+  return ((u64)lane_read((uint32_t)(x >> 32), lane) << 32) | lane_read((uint32_t)x, lane);
+}
+
+// Loads this lane's 16 tokens of chunk [cs, cs+cl) (kPad beyond cl) as four unconditional
+// 16-byte loads: tiles start 16-byte aligned and the stream is padded by kStreamPad elements, so
+// reading a whole chunk from any tile start stays inside the allocation.  Branch-free, all four
+// loads are in flight together (a bounds-checked form compiled to one wait per quad).
 __device__ __forceinline__ void load_chunk(const int32_t* base, uint32_t cs, uint32_t cl, int p0, int32_t (&v)[kPer]) {
+  const int4* q = reinterpret_cast<const int4*>(base + cs + p0);
+  int4 x[kPer / 4];
 #pragma unroll
-  for (int q = 0; q < kPer / 4; ++q) {
-    const int idx = p0 + 4 * q;
-    if (idx + 4 <= (int)cl) {
-      const int4 x = *reinterpret_cast<const int4*>(base + cs + idx);
-      v[4 * q] = x.x;
-      v[4 * q + 1] = x.y;
-      v[4 * q + 2] = x.z;
-      v[4 * q + 3] = x.w;
-    } else {
+  for (int k = 0; k < kPer / 4; ++k) x[k] = q[k];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[4 * q + r] = (idx + r < (int)cl) ? base[cs + idx + r] : kPad;
-    }
+  for (int k = 0; k < kPer / 4; ++k) {
+    v[4 * k] = p0 + 4 * k < (int)cl ? x[k].x : kPad;
+    v[4 * k + 1] = p0 + 4 * k + 1 < (int)cl ? x[k].y : kPad;
+    v[4 * k + 2] = p0 + 4 * k + 2 < (int)cl ? x[k].z : kPad;
+    v[4 * k + 3] = p0 + 4 * k + 3 < (int)cl ? x[k].w : kPad;
   }
 }
 
 // Token following this lane's 16 (from the next lane, or from memory at a wave edge).
 __device__ __forceinline__ int32_t next_token(const int32_t* base, uint32_t cs, uint32_t len, int p0, int32_t v0) {
-  int32_t nx = __shfl_down(v0, 1, 64);
-  if ((threadIdx.x & 63) == 63) nx = (cs + p0 + kPer < len) ? base[cs + p0 + kPer] : kPad;
+  int32_t nx = wave_next(v0);
+  const int32_t m = base[cs + p0 + kPer];  // inside the padded allocation; used by lane 63 only
+  if ((threadIdx.x & 63) == 63) nx = (cs + p0 + kPer < len) ? m : kPad;
   return nx;
 }
 
 // ------------------------------------------------------------------------------------------
-// K2+K3(+K4): merge scan, one wavefront per tile.
+// K2+K3(+K4): merge scan.
 //
-// A wave owns a tile (<= 1024 tokens, or one longer word walked in 1024-token chunks): each lane
-// holds 16 consecutive tokens, occurrences / run parity / word headers / output offsets are
-// wave-level scans (no workgroup barrier on the tile path), the 4 neighbour deltas of every
-// occurrence go to a workgroup LDS hash shared by the 4 waves, and a changed chunk is compacted
-// in LDS and written back in place.  The last workgroup to finish (agent-scope release/acquire
-// on a ticket) turns the touched delta slots into host records and raises a host-visible flag,
-// so one launch + one flag wait is the whole device side of a merge.
+// Filter: every tile carries a pair signature in HBM — an 8192-bit Bloom filter (two hashes) of
+// the adjacent token pairs it holds, a superset of its current pairs.  A workgroup takes windows
+// of kWin candidate tiles (the host's candidate list, or every tile); one wave tests their
+// signatures with one load per lane and publishes the hit mask in LDS.
+// Merge: the 4 waves split the window's hits and walk them kGroup at a time with all first-chunk
+// loads in flight: each lane holds 16 consecutive tokens; occurrences, run parity,
+// word headers and output offsets are wave-level scans; the 4 neighbour deltas of every
+// occurrence go to a workgroup LDS hash; a changed chunk is compacted in LDS, written back in
+// place, and (for single-chunk tiles) the tile's signature is rebuilt from the compacted chunk.
+// Completion: the last workgroup (per-XCD sharded tickets) turns the touched delta slots into host
+// records and raises a host-visible flag, so one launch + one flag wait is a merge's device side.
 constexpr int kWaveTok = 64 * kPer;  // 1024 tokens per wave chunk
 constexpr int kWaves = kThreads / 64;
 constexpr int kDeltaLdsW = SHRED_DELTA_LDS;
@@ -163,7 +248,84 @@ constexpr uint32_t kFusedCollectMax = 4096;  // beyond this the host launches k_
 constexpr uint32_t kNeedCollect = 0x80000000u;
 constexpr uint32_t kTimingStride = 8;
 constexpr uint32_t kInlineTiles = 768;     // candidate tiles that fit the kernel arguments
-constexpr int kMaxMergeGroups = SHRED_MAX_GROUPS;  // fat persistent grid: waves walk tiles with prefetch
+constexpr int kGroup = 4;                  // tiles walked together per wave (loads in flight)
+constexpr int kMaxMergeGroups = SHRED_MAX_GROUPS;
+constexpr int kSigBits = SHRED_SIG_BITS;   // per-tile pair signature
+constexpr int kSigWords = kSigBits / 32;
+constexpr uint32_t kWin = 32;              // candidate tiles per workgroup window (filter pass)
+constexpr uint32_t kMtLds = 256;           // matched tiles a workgroup keeps in LDS (more: global list)
+constexpr int kRegHdr = 8;                 // region header: nrec, nmt, spill, pad, merged (2), written (2)
+[[maybe_unused]] constexpr int kStamps = 18;               // SHRED_STAMPS: entry, init, windows, flush, ticket, collect, flag
+#ifdef SHRED_STAMPS
+#define STAMP(k) \
+  if (threadIdx.x == 0) p.stamps[blockIdx.x * kStamps + (k)] = __builtin_amdgcn_s_memrealtime()
+#define STAMP_ONCE(k) \
+  if (threadIdx.x == 0 && p.stamps[blockIdx.x * kStamps + (k)] == 0) \
+    p.stamps[blockIdx.x * kStamps + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define STAMP(k)
+#define STAMP_ONCE(k)
+#endif
+static_assert(kSigWords % 256 == 0 || kSigWords == 64 || kSigWords == 128, "signature written as 16 B per lane");
+
+// The two signature bits of pair (x, y).
+__device__ __forceinline__ void sig_bits(int32_t x, int32_t y, uint32_t* h1, uint32_t* h2) {
+  uint32_t k = (uint32_t)x * 0x9E3779B1u ^ ((uint32_t)y + 0x7F4A7C15u) * 0x85EBCA77u;
+  k ^= k >> 15;
+  k *= 0x2C1B3C6Du;
+  k ^= k >> 12;
+  k *= 0x297A2D39u;
+  k ^= k >> 15;
+  *h1 = k & (kSigBits - 1);
+  *h2 = (k >> 16) & (kSigBits - 1);
+}
+
+__device__ __forceinline__ void sig_add(uint32_t* s, int32_t x, int32_t y) {
+  uint32_t h1, h2;
+  sig_bits(x, y, &h1, &h2);
+  atomicOr(&s[h1 >> 5], 1u << (h1 & 31));
+  atomicOr(&s[h2 >> 5], 1u << (h2 & 31));
+}
+
+// Writes a wave's LDS signature to the tile's HBM signature (16 B per lane per pass).
+__device__ __forceinline__ void sig_store(uint32_t* dst, const uint32_t* s, int lane) {
+  for (int w = lane * 4; w < kSigWords; w += 256) {
+    uint4 v;
+    v.x = s[w];
+    v.y = s[w + 1];
+    v.z = s[w + 2];
+    v.w = s[w + 3];
+    *reinterpret_cast<uint4*>(dst + w) = v;
+  }
+}
+
+__device__ __forceinline__ void sig_clear(uint32_t* s, int lane) {
+  for (int w = lane; w < kSigWords; w += 64) s[w] = 0;
+}
+
+// Orders this wave's LDS accesses across lanes (LDS executes one wave's ops in order; this
+// keeps the compiler from moving them and drains lgkmcnt).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Rebuilds a single-chunk tile's signature from its tokens v (this lane's 16, kPad beyond) and
+// the token after them (nx); longer tiles keep an all-ones signature.
+__device__ __forceinline__ void sig_rebuild(uint32_t* s_sig, uint32_t* dst, const int32_t (&v)[kPer], int32_t nx,
+                                            int lane) {
+  sig_clear(s_sig, lane);
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int32_t x = v[j], y = j + 1 < kPer ? v[j + 1] : nx;
+    if (!is_hdr(x) && !is_hdr(y)) sig_add(s_sig, x, y);
+  }
+  wave_lds_sync();
+  sig_store(dst, s_sig, lane);
+}
 
 struct MergeParams {
   int32_t* tok;
@@ -176,24 +338,33 @@ struct MergeParams {
   u64* dsum;
   u64* dft;
   uint32_t* dlist;
-  uint32_t* dcount;
+  uint32_t* dcount;   // [0] touched slots, [1..9] tickets, [10] matched tiles
   u64* stats;         // [0] occurrences merged, [1] tokens rewritten
   uint32_t* done;     // completion tickets: [0..7] per blockIdx % 8 group, [8] top
   int fused;          // 1: last workgroup collects; 0: leave the tables (multi-GPU exchange)
   DeltaRecord* out;   // host-visible records
-  uint32_t* hcount;   // host-visible: [0] record count (| kNeedCollect), [1] flag = seq, [2] matched tiles
+  uint32_t* hcount;   // host-visible: [0] record count (| kNeedCollect), [1] flag = seq, [2] matched tiles,
+                      // [3] first record k_collect writes (kNeedCollect)
   u64* hstats;        // host-visible: [0] occurrences, [1] tokens rewritten
-  uint32_t* mlist;    // host-visible: tiles where the merge matched (-> tiles(X) of the index)
+  uint32_t* mlist;    // device: tiles where the merge matched (atomic writes, any XCD)
   uint32_t* mcount;   // device counter for mlist
+  uint32_t* hmlist;   // host-visible copy of mlist (-> tiles(X) of the index), by the last workgroup
+  uint32_t* sig;      // kSigWords per tile
+  uint32_t* rhdr;     // fused: per-workgroup region headers (kRegHdr u32 each)
+  u64* rrec;          // fused: per-workgroup records, kDeltaLdsW x 3 u64 each
+  uint32_t* rtile;    // fused: per-workgroup matched tiles, kMtLds each
+  int filter;         // 1: test tile signatures before loading tiles
+  u64* stamps;        // SHRED_STAMPS diagnostic: kStamps s_memrealtime values per workgroup
   uint32_t seq;
-  uint32_t nlist;     // 0: visit every tile; else visit list[0 .. nlist)
-  uint32_t list[kInlineTiles];  // candidate tiles (tile skipping), passed in the kernel arguments
+  uint32_t nlist;     // 0: every tile is a candidate; else list[0 .. nlist)
+  uint32_t list[kInlineTiles];  // candidate tiles (host tile index), passed in the kernel arguments
 };
 
 struct DeltaLds {
   uint32_t key[kDeltaLdsW];
   u64 sum[kDeltaLdsW];
   u64 ft[kDeltaLdsW];
+  uint32_t spill;  // some delta went to the global tables
 };
 
 __device__ __forceinline__ void delta_global(const MergeParams& p, uint32_t key, u64 w, u64 ft) {
@@ -215,6 +386,7 @@ __device__ __forceinline__ void delta_emit(DeltaLds& h, const MergeParams& p, ui
     }
     s = (s + 1) & (kDeltaLdsW - 1);
   }
+  h.spill = 1;
   delta_global(p, key, w, ft);
 }
 
@@ -222,80 +394,139 @@ __device__ __forceinline__ uint32_t slot_of(int32_t id, uint32_t cap) {
   return (uint32_t)id < cap ? (uint32_t)id + 1u : 0u;
 }
 
-// Orders this wave's LDS accesses across lanes (LDS executes one wave's ops in order; this
-// keeps the compiler from moving them and drains lgkmcnt).
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-template <class T>
-__device__ __forceinline__ T wave_incl_max(T x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const T y = __shfl_up(x, d, 64);
-    if (lane >= d) x = y > x ? y : x;
-  }
-  return x;
-}
-
-__device__ __forceinline__ int wave_incl_sum(int x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  return x;
-}
+__device__ __forceinline__ int wave_incl_sum(int x) { return (int)wave_scan_add((uint32_t)x); }
 
 template <bool kWeighted>
 __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
   __shared__ int32_t s_tok[kWaves][kWaveTok + 8];  // [2 + j] = chunk position j; [0],[1] = -2,-1
+  __shared__ uint32_t s_sig[kWaves][kSigWords];
   __shared__ DeltaLds h;
   __shared__ uint32_t s_last;
   __shared__ u64 s_cnt[2];
+  __shared__ u64 s_hits;
+  __shared__ uint32_t s_wt[kWin];  // the window's candidate tiles
+  __shared__ uint32_t s_mt[kMtLds];
+  __shared__ uint32_t s_nmt, s_nrec;
+  __shared__ uint32_t s_pre[kMaxMergeGroups + 1], s_pmt[kMaxMergeGroups + 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int32_t* st = s_tok[wid];
+  STAMP(0);
+#ifdef SHRED_STAMPS
+  if (threadIdx.x == 0) p.stamps[blockIdx.x * kStamps + 16] = __builtin_amdgcn_s_memtime();
+#endif
   for (int i = threadIdx.x; i < kDeltaLdsW; i += kThreads) {
     h.key[i] = kEmpty32;
     h.sum[i] = 0;
     h.ft[i] = kEmpty64;
   }
   if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    s_nmt = 0;
+    s_nrec = 0;
+    h.spill = 0;
+  }
   __syncthreads();
+  STAMP(1);
   const int32_t a = p.a, b = p.b, X = p.X;
   const bool same = (a == b);
   const int p0 = lane * kPer;
   u64 n_merged = 0, n_written = 0;  // wave-uniform
 
-  const uint32_t n_iter = p.nlist ? p.nlist : p.ntiles;
-  const uint32_t stride = gridDim.x * kWaves;
-  uint32_t it = blockIdx.x * kWaves + wid;
-  // first chunk of the wave's next tile, loaded one tile ahead (latency hiding)
-  uint32_t f_tile = 0, f_len = 0;
-  int32_t* f_base = p.tok;
-  int32_t fv[kPer];
-  int32_t f_nx = kPad;
-  auto fetch = [&](uint32_t i) {
-    f_tile = p.nlist ? p.list[i] : i;
-    f_len = p.tile_len[f_tile];
-    f_base = p.tok + p.tile_off[f_tile];
-    load_chunk(f_base, 0, min((uint32_t)kWaveTok, f_len), p0, fv);
-    f_nx = next_token(f_base, 0, f_len, p0, fv[0]);
-  };
-  if (it < n_iter) fetch(it);
-  for (; it < n_iter; it += stride) {
-    const uint32_t tile = f_tile, len = f_len;
-    int32_t* base = f_base;
+  // ---- windows of kWin candidates: filter, then the waves split the hits
+  const uint32_t n_cand = p.nlist ? p.nlist : p.ntiles;
+  const uint32_t nwin = (n_cand + kWin - 1) / kWin;
+  uint32_t h1, h2;
+  sig_bits(a, b, &h1, &h2);
+  for (uint32_t win = blockIdx.x; win < nwin; win += gridDim.x) {
+    if (wid == 0) {
+      const uint32_t i = win * kWin + (uint32_t)lane;
+      const bool in = (uint32_t)lane < kWin && i < n_cand;
+      uint32_t t = in ? i : 0u;
+      if (p.nlist) {  // uniform indices: scalar loads of the kernel-argument list
+        t = 0;
+#pragma unroll
+        for (int k = 0; k < (int)kWin; ++k) {
+          const uint32_t ik = win * kWin + (uint32_t)k;
+          const uint32_t v = ik < n_cand ? p.list[ik] : 0u;
+          if (lane == k) t = v;
+        }
+      }
+      if ((uint32_t)lane < kWin) s_wt[lane] = t;
+      bool hit = in;
+      if (p.filter) {
+        const uint32_t* sg = p.sig + (size_t)t * kSigWords;
+        const uint32_t w1 = sg[h1 >> 5], w2 = sg[h2 >> 5];
+        hit = in && ((w1 >> (h1 & 31)) & 1u) && ((w2 >> (h2 & 31)) & 1u);
+      }
+      const u64 m = __ballot(hit);
+      if (lane == 0) s_hits = m;
+    }
+    __syncthreads();
+    STAMP_ONCE(8);
+    const u64 hits = s_hits;
+    // this wave's share: the hits whose rank among the window's hits is wid (mod kWaves)
+    const bool mine_b = ((hits >> lane) & 1ull) &&
+                        ((uint32_t)__popcll(hits & ((1ull << lane) - 1ull)) & (kWaves - 1)) == (uint32_t)wid;
+    u64 mine = __ballot(mine_b);
+    while (mine) {
+    uint32_t gt[kGroup], gl[kGroup];
+    uint64_t go[kGroup];
+    int32_t gv[kGroup][kPer];
+    int32_t gn[kGroup];
+    uint32_t gmask = 0;
+    {  // lane k < qn takes the wave's next hit k
+      uint32_t qn = 0, pos = 0;
+      for (int k = 0; k < kGroup && mine; ++k) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(mine);
+        mine &= mine - 1;
+        if ((uint32_t)lane == (uint32_t)k) pos = j;
+        ++qn;
+      }
+      const uint32_t t = (uint32_t)lane < qn ? s_wt[pos] : 0u;
+      const uint64_t o = p.tile_off[t];
+      const uint32_t l0 = p.tile_len[t];
+      const uint32_t l = (uint32_t)lane < qn ? l0 : 0u;
+#pragma unroll
+      for (int k = 0; k < kGroup; ++k) {
+        gt[k] = (uint32_t)__builtin_amdgcn_readlane((int)t, k);
+        gl[k] = (uint32_t)__builtin_amdgcn_readlane((int)l, k);
+        go[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(o >> 32), k) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)o, k);
+      }
+    }
+    STAMP_ONCE(9);
+    // all loads first (a cross-lane shuffle waits for every outstanding load)
+    int32_t gm[kGroup];
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k) {
+      const int32_t* gb = p.tok + go[k];
+      load_chunk(gb, 0, min((uint32_t)kWaveTok, gl[k]), p0, gv[k]);
+      gm[k] = gb[p0 + kPer];  // inside the padded allocation; lane 63's lookahead
+    }
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k) {
+      gn[k] = wave_next(gv[k][0]);
+      if (lane == 63) gn[k] = (uint32_t)(p0 + kPer) < gl[k] ? gm[k] : kPad;
+    }
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k) {
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) any |= (gv[k][j] == a) & ((j + 1 < kPer ? gv[k][j + 1] : gn[k]) == b);
+      if (__any(any) || gl[k] > (uint32_t)kWaveTok) gmask |= 1u << k;
+    }
+    STAMP_ONCE(10);
+#pragma unroll 1
+    for (int k = 0; k < kGroup; ++k) {
+    if (!((gmask >> k) & 1u)) continue;
+#define SHRED_SEL(arr) (k == 0 ? arr[0] : k == 1 ? arr[1] : k == 2 ? arr[2] : arr[3])
+    const uint32_t tile = SHRED_SEL(gt), len = SHRED_SEL(gl);
+    int32_t* base = p.tok + SHRED_SEL(go);
     int32_t v0[kPer];
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) v0[j] = fv[j];
-    const int32_t nx0 = f_nx;
-    if (it + stride < n_iter) fetch(it + stride);
+    for (int j = 0; j < kPer; ++j) v0[j] = k == 0 ? gv[0][j] : k == 1 ? gv[1][j] : k == 2 ? gv[2][j] : gv[3][j];
+    const int32_t nx0 = SHRED_SEL(gn);
+#undef SHRED_SEL
     uint64_t tile_hits = 0;
     long long c_nona = -1;  // last tile index whose token != a (a == b only)
     u64 c_hdr = 0;          // ((index + 1) << 32) | rank of the last header, 0 = none
@@ -333,6 +564,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
         st[3 + kWaveTok] = (cs + kWaveTok + 1 < len) ? base[cs + kWaveTok + 1] : kPad;
       }
       wave_lds_sync();
+      STAMP_ONCE(12);
       const int32_t last1 = st[2 + cl - 1];
       const int32_t last2 = st[2 + cl - 2];  // st[1] when cl == 1
 
@@ -340,14 +572,13 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       uint32_t mask = 0;
       long long nona_tot = -1;
       if (same) {
-        long long nl = -1;
+        u64 nl = 0;  // last index whose token != a, + 1 (0 = none)
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
-          if (v[j] != a) nl = (long long)(cs + p0 + j);
-        const long long inc = wave_incl_max(nl);
-        nona_tot = __shfl(inc, 63, 64);
-        long long last = __shfl_up(inc, 1, 64);
-        if (lane == 0) last = -1;
+          if (v[j] != a) nl = (u64)(cs + p0 + j) + 1;
+        const u64 inc = wave_scan_max64(nl);
+        nona_tot = (long long)lane_read64(inc, 63) - 1;
+        long long last = (long long)wave_prev64(inc) - 1;
         last = last > c_nona ? last : c_nona;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
@@ -360,7 +591,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
         for (int j = 0; j < kPer; ++j)
           if (v[j] == a && (j + 1 < kPer ? v[j + 1] : nx) == b) mask |= 1u << j;
       }
-      uint32_t prevm = __shfl_up(mask, 1, 64);
+      uint32_t prevm = wave_prev(mask);
       if (lane == 0) prevm = (c_m1 ? 1u << 15 : 0u) | (c_m2 ? 1u << 14 : 0u);
       const uint32_t m_ext = (mask << 2) | ((prevm >> 14) & 3u);  // bit k <-> position p0 - 2 + k
       const uint32_t removed = (m_ext >> 1) & 0xFFFFu;           // bit j <-> match at p0 + j - 1
@@ -378,12 +609,11 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
         const int j = 31 - __clz(hmask);
         hl = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(st[2 + p0 + j]);
       }
-      const u64 hinc = wave_incl_max(hl);
-      u64 hdr_ex = __shfl_up(hinc, 1, 64);
-      if (lane == 0) hdr_ex = 0;
-      const u64 hdr_tot = __shfl(hinc, 63, 64);
+      const u64 hinc = wave_scan_max64(hl);
+      const u64 hdr_ex = wave_prev64(hinc);
+      const u64 hdr_tot = lane_read64(hinc, 63);
       const int cinc = wave_incl_sum(kc | (nm << 16));
-      const int ctot = __shfl(cinc, 63, 64);
+      const int ctot = (int)lane_read((uint32_t)cinc, 63);
       const int kc_ex = (cinc - (kc | (nm << 16))) & 0xFFFF;
       const int kept = ctot & 0xFFFF;
       const int matches = ctot >> 16;
@@ -418,6 +648,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
           }
         }
       }
+      STAMP_ONCE(13);
       const bool write = dirty || matches > 0 || kept != (int)cl;
       if (write) {
         wave_lds_sync();  // every neighbour read is done: compact in place
@@ -429,13 +660,22 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
         for (int j = lane; j < kept; j += 64) base[c_out + j] = st[2 + j];
         dirty = true;
         n_written += (u64)kept;
+        STAMP_ONCE(14);
+        if (len <= (uint32_t)kWaveTok) {  // single-chunk tile: its signature from the compacted chunk
+          int32_t w[kPer];
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) w[j] = p0 + j < kept ? st[2 + p0 + j] : kPad;
+          const int32_t wn = p0 + kPer < kept ? st[2 + p0 + kPer] : kPad;
+          sig_rebuild(s_sig[wid], p.sig + (size_t)tile * kSigWords, w, wn, lane);
+          STAMP_ONCE(15);
+        }
       }
       n_merged += (u64)matches;
       tile_hits += (u64)matches;
       // ---- carries to the next chunk of this tile
       c_out += (uint32_t)kept;
-      c_m1 = (__shfl(mask, (int)((cl - 1) / kPer), 64) >> ((cl - 1) % kPer)) & 1u;
-      c_m2 = cl >= 2 ? ((__shfl(mask, (int)((cl - 2) / kPer), 64) >> ((cl - 2) % kPer)) & 1u) : c_m1;
+      c_m1 = (lane_read(mask, (int)((cl - 1) / kPer)) >> ((cl - 1) % kPer)) & 1u;
+      c_m2 = cl >= 2 ? ((lane_read(mask, (int)((cl - 2) / kPer)) >> ((cl - 2) % kPer)) & 1u) : c_m1;
       c_t1 = last1;
       c_t2 = last2;
       c_hdr = hdr_tot > c_hdr ? hdr_tot : c_hdr;
@@ -443,87 +683,218 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       wave_lds_sync();  // the copy-out reads st before the next chunk overwrites it
     }
     if (dirty && lane == 0) p.tile_len[tile] = c_out;
-    if (tile_hits && lane == 0) p.mlist[atomicAdd(p.mcount, 1u)] = tile;
+    if (tile_hits && lane == 0) {
+      const uint32_t k = p.fused ? atomicAdd(&s_nmt, 1u) : kMtLds;
+      if (k < kMtLds) s_mt[k] = tile;
+      else atomicExch(&p.mlist[atomicAdd(p.mcount, 1u)], tile);
+    }
+    }  // tiles of the group
+    STAMP_ONCE(11);
+    }  // this wave's hits
+    __syncthreads();  // s_hits is rewritten by the next window
   }
+  STAMP(2);
   if (lane == 0) {
     if (n_merged) atomicAdd(&s_cnt[0], n_merged);
     if (n_written) atomicAdd(&s_cnt[1], n_written);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kDeltaLdsW; i += kThreads)
-    if (h.key[i] != kEmpty32) delta_global(p, h.key[i], h.sum[i], h.ft[i]);
-  if (threadIdx.x == 0) {
-    if (s_cnt[0]) atomicAdd(&p.stats[0], s_cnt[0]);
-    if (s_cnt[1]) atomicAdd(&p.stats[1], s_cnt[1]);
+  if (p.fused) {
+    // ---- this workgroup's region: LDS-reduced records, matched tiles and counts, written
+    // through (sc1) so the collecting workgroup on any XCD reads them with sc1 loads after the
+    // ticket (MI355X_MICROARCH.md, valid forms: sc1 stores, vmcnt drain, atomic ticket)
+    u64* rr = p.rrec + (size_t)blockIdx.x * kDeltaLdsW * 3;
+    for (int i = threadIdx.x; i < kDeltaLdsW; i += kThreads) {
+      if (h.key[i] == kEmpty32) continue;
+      const uint32_t k = atomicAdd(&s_nrec, 1u);
+      __hip_atomic_store(rr + 3 * k, (u64)h.key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rr + 3 * k + 1, h.sum[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rr + 3 * k + 2, h.ft[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t nmt = min(s_nmt, kMtLds);
+    for (uint32_t i = threadIdx.x; i < nmt; i += kThreads)
+      __hip_atomic_store(p.rtile + (size_t)blockIdx.x * kMtLds + i, s_mt[i], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t* hd = p.rhdr + (size_t)blockIdx.x * kRegHdr;
+      __hip_atomic_store(hd, s_nrec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(hd + 1, nmt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(hd + 2, h.spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<u64*>(hd + 4), s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<u64*>(hd + 6), s_cnt[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else {
+    // multi-GPU: everything into the global slot tables (all-reduced before the collect)
+    for (int i = threadIdx.x; i < kDeltaLdsW; i += kThreads)
+      if (h.key[i] != kEmpty32) delta_global(p, h.key[i], h.sum[i], h.ft[i]);
+    if (threadIdx.x == 0) {
+      if (s_cnt[0]) atomicAdd(&p.stats[0], s_cnt[0]);
+      if (s_cnt[1]) atomicAdd(&p.stats[1], s_cnt[1]);
+    }
   }
-  // ---- completion: the slot tables are only ever touched by device-scope atomics (performed
-  // at the memory side), so every wave draining its own vmcnt before the ticket is the whole
-  // hand-off; the collector reads them with atomics too (MI355X_MICROARCH.md, valid forms).
-  // Tickets are sharded by blockIdx % 8 so no counter sees more than gridDim/8 arrivals.
+  // ---- completion ticket: every wave drains its stores/atomics first.  One counter for small
+  // grids; sharded by blockIdx % 8 above that, so no counter sees more than gridDim/8 arrivals.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  STAMP(3);
   if (threadIdx.x == 0) {
-    const uint32_t g = blockIdx.x & 7u;
-    const uint32_t in_group = (gridDim.x - g + 7u) >> 3;
     bool last = false;
-    if (atomicAdd(&p.done[g], 1u) == in_group - 1u) {
-      atomicExch(&p.done[g], 0u);
-      const uint32_t groups = gridDim.x < 8u ? gridDim.x : 8u;
-      last = atomicAdd(&p.done[8], 1u) == groups - 1u;
+    if (gridDim.x <= 32u) {
+      last = atomicAdd(&p.done[8], 1u) == gridDim.x - 1u;
+    } else {
+      const uint32_t g = blockIdx.x & 7u;
+      const uint32_t in_group = (gridDim.x - g + 7u) >> 3;
+      if (atomicAdd(&p.done[g], 1u) == in_group - 1u) {
+        atomicExch(&p.done[g], 0u);
+        last = atomicAdd(&p.done[8], 1u) == 7u;
+      }
     }
     s_last = last;
   }
   __syncthreads();
+  STAMP(4);
+#ifdef SHRED_STAMPS
+  if (threadIdx.x == 0) p.stamps[blockIdx.x * kStamps + 17] = __builtin_amdgcn_s_memtime();
+#endif
   if (!s_last) return;
-  if (threadIdx.x == 0) s_cnt[0] = atomicAdd(p.dcount, 0u);
-  __syncthreads();
-  const uint32_t n = (uint32_t)s_cnt[0];
-  const bool collect = p.fused && n <= kFusedCollectMax;
-  if (collect) {
+  const uint32_t G = gridDim.x;
+  uint32_t n = 0, nm = 0, base = 0;
+  bool need_collect = false;
+  if (p.fused) {
+    // ---- gather the regions: headers, prefix offsets, then records and tiles to the host
+    u64 merged = 0, written = 0;
+    uint32_t spill = 0;
+    if (threadIdx.x == 0) {
+      s_cnt[0] = 0;
+      s_cnt[1] = 0;
+      s_nrec = 0;
+    }
+    __syncthreads();
+    // one header per thread (G <= kThreads), then exclusive prefix sums by wave scans
+    uint32_t my_nrec = 0, my_nmt = 0;
+    const uint32_t g = threadIdx.x;
+    if (g < G) {
+      const uint32_t* hd = p.rhdr + (size_t)g * kRegHdr;
+      my_nrec = __hip_atomic_load(hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      my_nmt = __hip_atomic_load(hd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      spill = __hip_atomic_load(hd + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      merged = __hip_atomic_load(reinterpret_cast<const u64*>(hd + 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      written = __hip_atomic_load(reinterpret_cast<const u64*>(hd + 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (merged) atomicAdd(&s_cnt[0], merged);
+    if (written) atomicAdd(&s_cnt[1], written);
+    if (spill) atomicOr(&s_nrec, 1u);
+    const uint32_t ir = wave_scan_add(my_nrec), im = wave_scan_add(my_nmt);
+    __shared__ uint32_t s_wtot[2][kWaves];
+    if (lane == 63) {
+      s_wtot[0][wid] = ir;
+      s_wtot[1][wid] = im;
+    }
+    __syncthreads();
+    uint32_t br = 0, bm = 0;
+    for (int w = 0; w < wid; ++w) {
+      br += s_wtot[0][w];
+      bm += s_wtot[1][w];
+    }
+    if (g < G) {
+      s_pre[g] = br + ir - my_nrec;
+      s_pmt[g] = bm + im - my_nmt;
+    }
+    if (g == G - 1) {
+      s_pre[G] = br + ir;
+      s_pmt[G] = bm + im;
+    }
+    __syncthreads();
+    n = s_pre[G];
+    nm = s_pmt[G];
+    auto owner = [&](const uint32_t* pre, uint32_t i) {  // the workgroup whose range holds i
+      uint32_t lo = 0, hi = G;                            // pre[lo] <= i < pre[hi]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= i) lo = mid;
+        else hi = mid;
+      }
+      return lo;
+    };
     for (uint32_t i0 = 0; i0 < n; i0 += kThreads * 4) {
-      uint32_t key[4];
-      u64 sum[4], ft[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t i = i0 + k * kThreads + threadIdx.x;
-        key[k] = i < n ? atomicOr(&p.dlist[i], 0u) : 0u;
-      }
+      u64 r[4][3];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint32_t i = i0 + k * kThreads + threadIdx.x;
         if (i < n) {
-          sum[k] = atomicExch(&p.dsum[key[k]], 0ull);
-          ft[k] = atomicExch(&p.dft[key[k]], kEmpty64);
+          const uint32_t g = owner(s_pre, i);
+          const u64* src = p.rrec + ((size_t)g * kDeltaLdsW + (i - s_pre[g])) * 3;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) r[k][c] = __hip_atomic_load(src + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint32_t i = i0 + k * kThreads + threadIdx.x;
-        if (i < n) {
-          DeltaRecord r;
-          r.key = key[k];
-          r.pad = 0;
-          r.sum = sum[k];
-          r.ft = ft[k];
-          p.out[i] = r;
-        }
+        if (i < n) sys_record(p.out + i, (uint32_t)r[k][0], r[k][1], r[k][2]);
       }
     }
+    for (uint32_t i = threadIdx.x; i < nm; i += kThreads) {
+      const uint32_t g = owner(s_pmt, i);
+      sys_store(p.hmlist + i,
+                __hip_atomic_load(p.rtile + (size_t)g * kMtLds + (i - s_pmt[g]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    // workgroups with more matched tiles than their LDS list: the rest is in the global list
+    if (threadIdx.x == 0) s_hits = atomicExch(p.mcount, 0u);
+    __syncthreads();
+    const uint32_t ng = (uint32_t)s_hits;
+    for (uint32_t i = threadIdx.x; i < ng; i += kThreads) sys_store(p.hmlist + nm + i, atomicOr(&p.mlist[i], 0u));
+    nm += ng;
+    if (s_nrec) {  // spilled deltas in the global tables: append them (or leave them to k_collect)
+      __syncthreads();
+      if (threadIdx.x == 0) s_hits = atomicAdd(p.dcount, 0u);
+      __syncthreads();
+      const uint32_t ngl = (uint32_t)s_hits;
+      base = n;
+      if (ngl <= kFusedCollectMax) {
+        for (uint32_t i = threadIdx.x; i < ngl; i += kThreads) {
+          const uint32_t key = atomicOr(&p.dlist[i], 0u);
+          const u64 sum = atomicExch(&p.dsum[key], 0ull);
+          const u64 ft = atomicExch(&p.dft[key], kEmpty64);
+          sys_record(p.out + n + i, key, sum, ft);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) atomicExch(p.dcount, 0u);
+      } else {
+        need_collect = true;
+      }
+      n += ngl;
+    }
+  } else {
+    if (threadIdx.x == 0) {
+      s_cnt[0] = atomicAdd(p.dcount, 0u);
+      s_cnt[1] = atomicExch(p.mcount, 0u);
+    }
+    __syncthreads();
+    n = (uint32_t)s_cnt[0];
+    nm = (uint32_t)s_cnt[1];
+    for (uint32_t i = threadIdx.x; i < nm; i += kThreads) sys_store(p.hmlist + i, atomicOr(&p.mlist[i], 0u));
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  STAMP(5);
   if (threadIdx.x == 0) {
     if (p.fused) {
-      if (collect) atomicExch(p.dcount, 0u);
-      p.hstats[0] = atomicExch(&p.stats[0], 0ull);
-      p.hstats[1] = atomicExch(&p.stats[1], 0ull);
-      p.hcount[0] = collect ? n : (n | kNeedCollect);
+      sys_store(&p.hstats[0], s_cnt[0]);
+      sys_store(&p.hstats[1], s_cnt[1]);
+      sys_store(&p.hcount[0], need_collect ? (n | kNeedCollect) : n);
+      sys_store(&p.hcount[3], base);
     }
-    p.hcount[2] = atomicExch(p.mcount, 0u);
+    sys_store(&p.hcount[2], nm);
     atomicExch(&p.done[8], 0u);
-    __threadfence_system();
-    __hip_atomic_store(&p.hcount[1], p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    STAMP(6);
+    sys_flag(&p.hcount[1], p.seq);
+    STAMP(7);
   }
 }
+
 
 // K4: touched slots -> records in host-visible memory; clears the slots for the next merge.
 __global__ __launch_bounds__(kThreads) void k_collect(uint32_t* dcount, const uint32_t* dlist, u64* dsum, u64* dft,
@@ -558,6 +929,126 @@ __global__ __launch_bounds__(kThreads) void k_collect_dense(uint32_t nkeys, u64*
     out[atomicAdd(out_count, 1u)] = r;
     dsum[key] = 0;
     dft[key] = kEmpty64;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Rollback of a speculative merge (a,b)->X: every X in the tiles the merge reported is expanded
+// back into "a b", in place, wave per tile.  Chunks are walked from the tile's end so each
+// chunk's (right-shifted) output only lands on input that has already been read; the result is
+// exactly the pre-merge tile because X is a fresh id.  A restored single-chunk tile gets its
+// signature rebuilt.  Workgroup 0 also clears the slot tables when the merge left them
+// uncollected (more touched slots than the fused collect handles).
+struct UnmergeParams {
+  int32_t* tok;
+  const uint64_t* tile_off;
+  uint32_t* tile_len;
+  const uint32_t* mlist;   // host-visible matched tiles written by the merge's last workgroup
+  const uint32_t* mcount;  // host-visible count written by the merge's last workgroup
+  int32_t a, b, X;
+  uint32_t* dcount;
+  const uint32_t* dlist;
+  u64* dsum;
+  u64* dft;
+  uint32_t* sig;
+};
+
+__global__ __launch_bounds__(kThreads) void k_unmerge(UnmergeParams p) {
+  __shared__ uint32_t s_sig[kWaves][kSigWords];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int p0 = lane * kPer;
+  const uint32_t n = *p.mcount;
+  for (uint32_t i = blockIdx.x * kWaves + wid; i < n; i += gridDim.x * kWaves) {
+    const uint32_t tile = p.mlist[i];
+    const uint32_t len = p.tile_len[tile];
+    int32_t* base = p.tok + p.tile_off[tile];
+    int total = 0;
+    for (uint32_t cs = 0; cs < len; cs += kWaveTok) {
+      int32_t v[kPer];
+      load_chunk(base, cs, min((uint32_t)kWaveTok, len - cs), p0, v);
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) c += v[j] == p.X;
+      total += c;
+    }
+    total = (int)lane_read((uint32_t)wave_incl_sum(total), 63);
+    if (total == 0) continue;
+    int after = 0;  // X count in the chunks right of the current one
+    const uint32_t last_cs = ((len - 1) / kWaveTok) * kWaveTok;
+    for (long long cs = last_cs; cs >= 0; cs -= kWaveTok) {
+      const uint32_t cl = min((uint32_t)kWaveTok, len - (uint32_t)cs);
+      int32_t v[kPer];
+      load_chunk(base, (uint32_t)cs, cl, p0, v);
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) c += v[j] == p.X;
+      const int inc = wave_incl_sum(c);
+      const int ctot = (int)lane_read((uint32_t)inc, 63);
+      uint32_t o = (uint32_t)cs + (uint32_t)p0 + (uint32_t)(total - after - ctot) + (uint32_t)(inc - c);
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if (p0 + j >= (int)cl) continue;
+        if (v[j] == p.X) {
+          base[o] = p.a;
+          base[o + 1] = p.b;
+          o += 2;
+        } else {
+          base[o] = v[j];
+          o += 1;
+        }
+      }
+      after += ctot;
+    }
+    const uint32_t nlen = len + (uint32_t)total;
+    if (lane == 0) p.tile_len[tile] = nlen;
+    if (nlen <= (uint32_t)kWaveTok) {
+      // re-read the restored tile (this wave's own stores: ordered by a workgroup-scope fence)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      int32_t v[kPer];
+      load_chunk(base, 0, nlen, p0, v);
+      const int32_t m = base[p0 + kPer];
+      int32_t nx = wave_next(v[0]);
+      if (lane == 63) nx = (uint32_t)(p0 + kPer) < nlen ? m : kPad;
+      sig_rebuild(s_sig[wid], p.sig + (size_t)tile * kSigWords, v, nx, lane);
+    }
+  }
+  if (blockIdx.x == 0) {  // tables left by an uncollected merge
+    __shared__ uint32_t s_n;
+    if (threadIdx.x == 0) s_n = *p.dcount;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < s_n; i += kThreads) {
+      const uint32_t key = p.dlist[i];
+      p.dsum[key] = 0;
+      p.dft[key] = kEmpty64;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n) *p.dcount = 0;
+  }
+}
+
+// Builds every tile's pair signature from scratch (upload / reset): wave per tile; a tile longer
+// than one wave chunk gets an all-ones signature (always a candidate).
+__global__ __launch_bounds__(kThreads) void k_sig_build(const int32_t* tok, const uint64_t* tile_off,
+                                                         const uint32_t* tile_len, uint32_t ntiles, uint32_t* sig) {
+  __shared__ uint32_t s_sig[kWaves][kSigWords];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int p0 = lane * kPer;
+  for (uint32_t t = blockIdx.x * kWaves + wid; t < ntiles; t += gridDim.x * kWaves) {
+    const uint32_t len = tile_len[t];
+    uint32_t* dst = sig + (size_t)t * kSigWords;
+    if (len > (uint32_t)kWaveTok) {
+      for (int w = lane; w < kSigWords; w += 64) dst[w] = ~0u;
+      continue;
+    }
+    const int32_t* base = tok + tile_off[t];
+    int32_t v[kPer];
+    load_chunk(base, 0, len, p0, v);
+    const int32_t m = base[p0 + kPer];
+    int32_t nx = wave_next(v[0]);
+    if (lane == 63) nx = (uint32_t)(p0 + kPer) < len ? m : kPad;
+    sig_rebuild(s_sig[wid], dst, v, nx, lane);
   }
 }
 
@@ -754,38 +1245,82 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
   hipStream_t s;
   HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   stream_ = s;
+  HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  aux_stream_ = s;
   for (auto& e : ev_) {
     hipEvent_t ev;
     HIP_OK(hipEventCreate(&ev));
     e = ev;
   }
+  for (int i = 0; i < kEvPairs; ++i) {
+    for (auto& e : mev_[i]) {
+      hipEvent_t ev;
+      HIP_OK(hipEventCreate(&ev));
+      e = ev;
+    }
+    ev_free_.push_back(i);
+  }
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, ordinal_));
   cu_count_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  HIP_OK(hipHostMalloc((void**)&host_count_, 64, hipHostMallocMapped | hipHostMallocCoherent));
-  std::memset(host_count_, 0, 64);
-  HIP_OK(hipHostGetDevicePointer(&dev_count_, host_count_, 0));
+  const unsigned pin = hipHostMallocMapped | hipHostMallocCoherent;
+  for (MergeSlot& sl : slot_) {
+    HIP_OK(hipHostMalloc((void**)&sl.host_count, 64, pin));
+    std::memset(sl.host_count, 0, 64);
+    HIP_OK(hipHostGetDevicePointer(&sl.dev_count, sl.host_count, 0));
+  }
+  if (const char* e = std::getenv("SHREDWORD_MERGE_GROUPS")) set_merge_groups(std::atoi(e));
   merge_params_ = new MergeParams();
+  unmerge_params_ = new UnmergeParams();
+  // diagnostic per-launch log: "C seq X candidates grid 0 merged records" / "R seq X candidates grid 0"
+  if (const char* e = std::getenv("SHREDWORD_MERGE_LOG")) merge_log_ = std::fopen(e, "w");
+#ifdef SHRED_STAMPS
+  HIP_OK(hipMalloc(&stamps_, (size_t)kMaxMergeGroups * 4 * kStamps * sizeof(u64)));
+  HIP_OK(hipMemset(stamps_, 0, (size_t)kMaxMergeGroups * 4 * kStamps * sizeof(u64)));
+#endif
   if (const char* e = std::getenv("SHREDWORD_TILE_SKIP")) skip_ = std::atoi(e) != 0;
   int nb = 0;  // resident workgroups of k_merge per CU
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_merge<true>), kThreads, 0));
   merge_blocks_per_cu_ = nb > 0 ? nb : 4;
 }
 
+// Grid cap of k_merge (tuning).
+void Device::set_merge_groups(int groups) { max_groups_ = std::max(1, std::min(kMaxMergeGroups, groups)); }
+
+void Device::free_slot(MergeSlot& s, bool keep_host) {
+  for (void* p : {(void*)s.dsum, (void*)s.dft, (void*)s.dlist, (void*)s.dcount})
+    if (p) HIP_OK(hipFree(p));
+  s.dsum = s.dft = nullptr;
+  s.dlist = s.dcount = nullptr;
+  if (s.host_recs) HIP_OK(hipHostFree(s.host_recs));
+  s.host_recs = nullptr;
+  s.cap = 0;
+  s.launched = false;
+  if (!keep_host) {
+    if (s.host_mlist) HIP_OK(hipHostFree(s.host_mlist));
+    s.host_mlist = nullptr;
+    if (s.host_count) HIP_OK(hipHostFree(s.host_count));
+    s.host_count = nullptr;
+    if (s.dmlist) HIP_OK(hipFree(s.dmlist));
+    s.dmlist = nullptr;
+    for (void* q : {(void*)s.rhdr, (void*)s.rrec, (void*)s.rtile})
+      if (q) HIP_OK(hipFree(q));
+    s.rhdr = nullptr;
+    s.rrec = nullptr;
+    s.rtile = nullptr;
+  }
+}
+
 void Device::free_all() {
-  void* ptrs[] = {tok_, tok0_, tile_off_, tile_len_, tile_len0_, weight_, dsum_, dft_, dlist_, dcount_};
+  void* ptrs[] = {tok_, tok0_, tile_off_, tile_len_, tile_len0_, weight_, sig_};
   for (void* p : ptrs)
     if (p) HIP_OK(hipFree(p));
+  sig_ = nullptr;
   tok_ = tok0_ = nullptr;
   tile_off_ = nullptr;
   tile_len_ = tile_len0_ = nullptr;
   weight_ = nullptr;
-  dsum_ = dft_ = nullptr;
-  dlist_ = dcount_ = nullptr;
-  if (host_recs_) HIP_OK(hipHostFree(host_recs_));
-  host_recs_ = nullptr;
-  host_recs_cap_ = 0;
-  slot_cap_ = 0;
+  for (MergeSlot& s : slot_) free_slot(s, true);
   ntiles_ = 0;
   bytes_alloc_ = 0;
   uploaded_ = false;
@@ -794,18 +1329,25 @@ void Device::free_all() {
 Device::~Device() {
   (void)hipSetDevice(ordinal_);
   (void)hipStreamSynchronize(S(stream_));
+  (void)hipStreamSynchronize(S(aux_stream_));
   free_all();
-  if (host_count_) (void)hipHostFree(host_count_);
-  if (host_mlist_) (void)hipHostFree(host_mlist_);
+  for (MergeSlot& s : slot_) free_slot(s, false);
   delete static_cast<MergeParams*>(merge_params_);
+  delete static_cast<UnmergeParams*>(unmerge_params_);
   for (auto e : ev_)
     if (e) (void)hipEventDestroy((hipEvent_t)e);
+  for (auto& pr : mev_)
+    for (auto e : pr)
+      if (e) (void)hipEventDestroy((hipEvent_t)e);
   if (stream_) (void)hipStreamDestroy(S(stream_));
+  if (merge_log_) std::fclose(merge_log_);
+  if (aux_stream_) (void)hipStreamDestroy(S(aux_stream_));
 }
 
 void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint64_t>& weights, int32_t max_id) {
   HIP_OK(hipSetDevice(ordinal_));
   HIP_OK(hipStreamSynchronize(S(stream_)));
+  flush_timing(true);
   free_all();
   layout_ = layout;
   ntiles_ = ts.num_tiles();
@@ -813,8 +1355,8 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
   live_tokens0_ = ts.live;
   live_tokens_est_ = ts.live;
   nentries_ = ts.entries;
-  tok_ = dalloc<int32_t>(ts.elems + 4, &bytes_alloc_);
-  tok0_ = dalloc<int32_t>(ts.elems + 4, &bytes_alloc_);
+  tok_ = dalloc<int32_t>(ts.elems + 4 + kStreamPad, &bytes_alloc_);
+  tok0_ = dalloc<int32_t>(ts.elems + 4 + kStreamPad, &bytes_alloc_);
   tile_off_ = dalloc<uint64_t>(ntiles_, &bytes_alloc_);
   tile_len_ = dalloc<uint32_t>(ntiles_, &bytes_alloc_);
   tile_len0_ = dalloc<uint32_t>(ntiles_, &bytes_alloc_);
@@ -830,9 +1372,22 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
                             S(stream_)));
   }
   HIP_OK(hipStreamSynchronize(S(stream_)));
-  if (host_mlist_) HIP_OK(hipHostFree(host_mlist_));
-  HIP_OK(hipHostMalloc((void**)&host_mlist_, (ntiles_ + 1) * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
-  HIP_OK(hipHostGetDevicePointer(&dev_mlist_, host_mlist_, 0));
+  for (MergeSlot& s : slot_) {
+    if (s.host_mlist) HIP_OK(hipHostFree(s.host_mlist));
+    HIP_OK(hipHostMalloc((void**)&s.host_mlist, (ntiles_ + 1) * sizeof(uint32_t),
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_OK(hipHostGetDevicePointer(&s.dev_mlist, s.host_mlist, 0));
+    if (s.dmlist) HIP_OK(hipFree(s.dmlist));
+    s.dmlist = dalloc<uint32_t>(ntiles_ + 1, &bytes_alloc_);
+    // per-workgroup regions of the fused completion (k_merge)
+    if (!s.rhdr) {
+      s.rhdr = dalloc<uint32_t>((size_t)kMaxMergeGroups * kRegHdr, &bytes_alloc_);
+      s.rrec = dalloc<uint64_t>((size_t)kMaxMergeGroups * kDeltaLdsW * 3, &bytes_alloc_);
+      s.rtile = dalloc<uint32_t>((size_t)kMaxMergeGroups * kMtLds, &bytes_alloc_);
+    }
+  }
+  // per-tile pair signatures (built by reset_tokens)
+  sig_ = dalloc<uint32_t>(std::max<size_t>(ntiles_, 1) * kSigWords, &bytes_alloc_);
   index_.build(ts);
   max_id_seen_ = max_id;
   uploaded_ = true;
@@ -842,9 +1397,15 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
 void Device::reset_tokens() {
   HIP_OK(hipSetDevice(ordinal_));
   if (!uploaded_) return;
+  for (const MergeSlot& s : slot_)
+    if (s.launched) fatal("reset_tokens with a merge in flight");
   HIP_OK(hipMemcpyAsync(tok_, tok0_, (tok_elems_ + 4) * sizeof(int32_t), hipMemcpyDeviceToDevice, S(stream_)));
-  if (ntiles_)
+  if (ntiles_) {
     HIP_OK(hipMemcpyAsync(tile_len_, tile_len0_, ntiles_ * sizeof(uint32_t), hipMemcpyDeviceToDevice, S(stream_)));
+    const int grid = (int)std::min<size_t>((ntiles_ + kWaves - 1) / kWaves, (size_t)cu_count_ * 8);
+    k_sig_build<<<grid, kThreads, 0, S(stream_)>>>(tok_, tile_off_, tile_len_, (uint32_t)ntiles_, sig_);
+    HIP_OK(hipGetLastError());
+  }
   live_tokens_est_ = live_tokens0_;
   index_.reset();
 }
@@ -863,30 +1424,31 @@ uint64_t Device::live_tokens() {
   return h;
 }
 
-void Device::ensure_slots(uint32_t need) {
-  if (need <= slot_cap_ && dsum_) return;
-  uint32_t cap = std::max<uint32_t>(slot_cap_ ? slot_cap_ : 1024, 1024);
+// Sizes one merge slot's tables for ids < need.  Only called for the slot about to be
+// launched, which is never the one still in flight, so the other slot's results survive.
+void Device::ensure_slots(MergeSlot& s, uint32_t need) {
+  if (need <= s.cap && s.dsum) return;
+  uint32_t cap = std::max<uint32_t>(s.cap ? s.cap : 4096, 4096);
   while (cap < need) cap *= 2;
   HIP_OK(hipStreamSynchronize(S(stream_)));
-  if (dsum_) {
-    HIP_OK(hipFree(dsum_));
-    HIP_OK(hipFree(dft_));
-    HIP_OK(hipFree(dlist_));
-    HIP_OK(hipFree(dcount_));
-    HIP_OK(hipHostFree(host_recs_));
-  }
+  HIP_OK(hipStreamSynchronize(S(aux_stream_)));
+  const size_t old_bytes = s.dsum ? 4 * ((size_t)s.cap + 1) * 20 + 16 + 64 : 0;  // as allocated below
+  free_slot(s, true);
+  bytes_alloc_ -= old_bytes;
   const size_t keys = 4 * ((size_t)cap + 1);
-  dsum_ = dalloc<uint64_t>(keys + 2, &bytes_alloc_);  // + 2 stats words at the end
-  dft_ = dalloc<uint64_t>(keys, &bytes_alloc_);
-  dlist_ = dalloc<uint32_t>(keys, &bytes_alloc_);
-  dcount_ = dalloc<uint32_t>(16, &bytes_alloc_);  // [0] count, [1..9] tickets, [10] matched tiles
-  HIP_OK(hipMemsetAsync(dsum_, 0, (keys + 2) * sizeof(u64), S(stream_)));
-  HIP_OK(hipMemsetAsync(dft_, 0xFF, keys * sizeof(u64), S(stream_)));
-  HIP_OK(hipMemsetAsync(dcount_, 0, 16 * sizeof(uint32_t), S(stream_)));
-  HIP_OK(hipHostMalloc((void**)&host_recs_, keys * sizeof(DeltaRecord), hipHostMallocMapped | hipHostMallocCoherent));
-  HIP_OK(hipHostGetDevicePointer(&dev_recs_, host_recs_, 0));
-  host_recs_cap_ = keys;
-  slot_cap_ = cap;
+  s.dsum = dalloc<uint64_t>(keys + 2, &bytes_alloc_);  // + 2 stats words at the end
+  s.dft = dalloc<uint64_t>(keys, &bytes_alloc_);
+  s.dlist = dalloc<uint32_t>(keys, &bytes_alloc_);
+  s.dcount = dalloc<uint32_t>(16, &bytes_alloc_);
+  HIP_OK(hipMemsetAsync(s.dsum, 0, (keys + 2) * sizeof(u64), S(stream_)));
+  HIP_OK(hipMemsetAsync(s.dft, 0xFF, keys * sizeof(u64), S(stream_)));
+  HIP_OK(hipMemsetAsync(s.dcount, 0, 16 * sizeof(uint32_t), S(stream_)));
+  // records: the fused completion ships every workgroup's LDS-reduced records (duplicates across
+  // workgroups included), at most kMaxMergeGroups x kDeltaLdsW, plus spilled global slots
+  const size_t rec_cap = keys + (size_t)kMaxMergeGroups * kDeltaLdsW;
+  HIP_OK(hipHostMalloc((void**)&s.host_recs, rec_cap * sizeof(DeltaRecord), hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_OK(hipHostGetDevicePointer(&s.dev_recs, s.host_recs, 0));
+  s.cap = cap;
   HIP_OK(hipStreamSynchronize(S(stream_)));
 }
 
@@ -935,7 +1497,6 @@ void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
     HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[2], (hipEvent_t)ev_[3]));
     times_.count_ms += ms;
     times_.count_launches += 1;
-    // tokens + headers read once, plus the per-word weight in the types layout
     // 4 B per token and per word header (the boundary), 8 B weight per word in the types
     // layout, 12 B of tile descriptor per tile
     times_.count_bytes += 4.0 * (double)live + 12.0 * (double)ntiles_ +
@@ -945,26 +1506,42 @@ void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
   dist_merge_pairs(out);
 }
 
-void Device::flush_timing() {
-  if (!timing_pending_) return;
-  timing_pending_ = false;
-  HIP_OK(hipEventSynchronize((hipEvent_t)ev_[1]));
-  float ms = 0;
-  HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]));
-  times_.merge_ms += ms;
-  times_.merge_launches += 1;
-  times_.merge_bytes += pending_bytes_;
+// Folds completed sampled k_merge launches into times_ (block: wait for all of them).
+void Device::flush_timing(bool block) {
+  size_t keep = 0;
+  for (size_t i = 0; i < ev_pending_.size(); ++i) {
+    const PendingEv pe = ev_pending_[i];
+    hipEvent_t e1 = (hipEvent_t)mev_[pe.pair][1];
+    if (block) {
+      HIP_OK(hipEventSynchronize(e1));
+    } else {
+      const hipError_t q = hipEventQuery(e1);
+      if (q == hipErrorNotReady) {
+        ev_pending_[keep++] = pe;
+        continue;
+      }
+      HIP_OK(q);
+    }
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)mev_[pe.pair][0], e1));
+    times_.merge_ms += ms;
+    times_.merge_launches += 1;
+    times_.merge_bytes += pe.bytes;
+    ev_free_.push_back(pe.pair);
+  }
+  ev_pending_.resize(keep);
 }
 
 void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
   HIP_OK(hipSetDevice(ordinal_));
+  MergeSlot& sl = slot_[X & 1];
+  if (sl.launched) fatal("merge_scan: the slot of this merge parity is still in flight");
   max_id_seen_ = std::max(max_id_seen_, X);
-  ensure_slots((uint32_t)X + 1);
-  flush_timing();
-  launched_ = false;
+  ensure_slots(sl, (uint32_t)X + 1);
+  sl.X = X;
   if (!ntiles_) return;  // an empty shard still joins collect()'s exchange
-  ++seq_;
-  launched_ = true;
+  sl.seq = ++seq_;
+  sl.launched = true;
   MergeParams& mp = *static_cast<MergeParams*>(merge_params_);
   mp.tok = tok_;
   mp.tile_off = tile_off_;
@@ -974,53 +1551,68 @@ void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
   mp.a = a;
   mp.b = b;
   mp.X = X;
-  mp.slot_cap = slot_cap_;
-  mp.dsum = U(dsum_);
-  mp.dft = U(dft_);
-  mp.dlist = dlist_;
-  mp.dcount = dcount_;
-  mp.stats = U(dsum_) + 4 * ((size_t)slot_cap_ + 1);
-  mp.done = dcount_ + 1;
+  mp.slot_cap = sl.cap;
+  mp.dsum = U(sl.dsum);
+  mp.dft = U(sl.dft);
+  mp.dlist = sl.dlist;
+  mp.dcount = sl.dcount;
+  mp.stats = U(sl.dsum) + 4 * ((size_t)sl.cap + 1);
+  mp.done = sl.dcount + 1;
   mp.fused = exchange_ ? 0 : 1;
-  mp.out = (DeltaRecord*)dev_recs_;
-  mp.hcount = (uint32_t*)dev_count_;
-  mp.hstats = (u64*)((char*)dev_count_ + 16);
-  mp.mlist = (uint32_t*)dev_mlist_;
-  mp.mcount = dcount_ + 10;
-  mp.seq = seq_;
+  mp.out = (DeltaRecord*)sl.dev_recs;
+  mp.hcount = (uint32_t*)sl.dev_count;
+  mp.hstats = (u64*)((char*)sl.dev_count + 16);
+  mp.mlist = sl.dmlist;
+  mp.hmlist = (uint32_t*)sl.dev_mlist;
+  mp.mcount = sl.dcount + 10;
+  mp.seq = sl.seq;
   mp.nlist = 0;
-  // tile skipping: visit only tiles(a) ∩ tiles(b) when that list is short
+  // tile skipping: visit only the tiles that can hold (a,b) when that list is short
   if (skip_ && index_.candidates(a, b, &cand_) && cand_.size() <= kInlineTiles) {
     mp.nlist = (uint32_t)cand_.size();
     std::memcpy(mp.list, cand_.data(), cand_.size() * sizeof(uint32_t));
   }
   const size_t n_iter = mp.nlist ? mp.nlist : ntiles_;
   visited_tiles_ += n_iter;
-  const size_t groups = (n_iter + kWaves - 1) / kWaves;
-  const int grid = (int)std::min<size_t>(groups, (size_t)kMaxMergeGroups);
+  const size_t groups = (n_iter + kWin - 1) / kWin;  // one filter window per workgroup and pass
+  const int grid = (int)std::min<size_t>(groups, (size_t)max_groups_);
+  mp.sig = sig_;
+  mp.stamps = stamps_;
+  mp.rhdr = sl.rhdr;
+  mp.rrec = U(sl.rrec);
+  mp.rtile = sl.rtile;
+  mp.filter = n_iter > 2 * kWin ? 1 : 0;  // short lists: load the tiles straight away
+  sl.grid = (uint32_t)grid;
+  sl.n_iter = (uint32_t)n_iter;
   // HIP events bracket every kTimingStride-th launch (an unbiased sample of launch durations
-  // that keeps event overhead out of the timed loop)
-  const bool sample = timing_ && (seq_ % kTimingStride == 0);
-  if (sample) HIP_OK(hipEventRecord((hipEvent_t)ev_[0], S(stream_)));
+  // that keeps event overhead out of the timed loop); they are read back without blocking
+  int pair = -1;
+  if (timing_ && sl.seq % kTimingStride == 0) {
+    flush_timing(false);
+    if (!ev_free_.empty()) {
+      pair = ev_free_.back();
+      ev_free_.pop_back();
+      HIP_OK(hipEventRecord((hipEvent_t)mev_[pair][0], S(stream_)));
+    }
+  }
   if (layout_ == Layout::kStream) k_merge<false><<<grid, kThreads, 0, S(stream_)>>>(mp);
   else k_merge<true><<<grid, kThreads, 0, S(stream_)>>>(mp);
   HIP_OK(hipGetLastError());
-  if (sample) {
-    HIP_OK(hipEventRecord((hipEvent_t)ev_[1], S(stream_)));
-    timing_pending_ = true;
+  if (pair >= 0) {
+    HIP_OK(hipEventRecord((hipEvent_t)mev_[pair][1], S(stream_)));
     // algorithmic bytes of this launch: the visited tiles' live tokens (estimated from the
     // mean tile length) + their descriptors
     const double frac = ntiles_ ? (double)n_iter / (double)ntiles_ : 0.0;
-    pending_bytes_ = frac * 4.0 * (double)live_tokens_est_ + 12.0 * (double)n_iter;
+    ev_pending_.push_back({pair, frac * 4.0 * (double)live_tokens_est_ + 12.0 * (double)n_iter});
   }
 }
 
 // Spins on the host-visible flag the last workgroup raises (much cheaper than a stream sync).
-void Device::wait_flag() {
-  volatile uint32_t* flag = host_count_ + 1;
+void Device::wait_flag(const MergeSlot& s) {
+  volatile uint32_t* flag = s.host_count + 1;
   const double t0 = now_seconds();
   unsigned spins = 0;
-  while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq_) {
+  while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != s.seq) {
     __builtin_ia32_pause();
     if (++spins % 4096 == 0 && now_seconds() - t0 > 120.0) {
       const hipError_t e = hipStreamQuery(S(stream_));
@@ -1032,48 +1624,111 @@ void Device::wait_flag() {
 
 size_t Device::collect(int32_t X, const DeltaRecord** recs) {
   HIP_OK(hipSetDevice(ordinal_));
-  (void)X;
-  *recs = host_recs_;
+  MergeSlot& sl = slot_[X & 1];
+  if (sl.X != X) fatal("collect: merge X is not the one in its slot");
+  *recs = sl.host_recs;
   if (!ntiles_ && !exchange_) return 0;
-  DeltaRecord* drec = (DeltaRecord*)dev_recs_;
-  if (launched_) {
-    wait_flag();
-    index_.set_tiles(X, host_mlist_, host_count_[2]);
+  DeltaRecord* drec = (DeltaRecord*)sl.dev_recs;
+  if (sl.launched) {
+    wait_flag(sl);
+    index_.set_tiles(X, sl.host_mlist, sl.host_count[2]);
   }
-  launched_ = false;
-  const u64* hs = (const u64*)(host_count_ + 4);
+  sl.launched = false;
+  const u64* hs = (const u64*)(sl.host_count + 4);
   size_t n;
-  u64* stats = U(dsum_) + 4 * ((size_t)slot_cap_ + 1);
+  u64* stats = U(sl.dsum) + 4 * ((size_t)sl.cap + 1);
   if (exchange_) {
     // multi-GPU: all-reduce the live prefix of the slot tables, then every rank scans it
-    const uint32_t unk_slot = (unk_ >= 0 && (uint32_t)unk_ < slot_cap_) ? (uint32_t)unk_ : 0u;
+    const uint32_t unk_slot = (unk_ >= 0 && (uint32_t)unk_ < sl.cap) ? (uint32_t)unk_ : 0u;
     const size_t top = std::max<uint32_t>((uint32_t)X, unk_slot);
-    const size_t nkeys = 4 * (std::min<size_t>(slot_cap_, top + 1) + 1);
-    exchange_(exchange_ctx_, dsum_, dft_, nkeys, stream_);
-    HIP_OK(hipMemsetAsync(dcount_, 0, sizeof(uint32_t), S(stream_)));
-    k_collect_dense<<<256, kThreads, 0, S(stream_)>>>((uint32_t)nkeys, U(dsum_), U(dft_), drec, dcount_);
+    const size_t nkeys = 4 * (std::min<size_t>(sl.cap, top + 1) + 1);
+    exchange_(exchange_ctx_, sl.dsum, sl.dft, nkeys, stream_);
+    HIP_OK(hipMemsetAsync(sl.dcount, 0, sizeof(uint32_t), S(stream_)));
+    k_collect_dense<<<256, kThreads, 0, S(stream_)>>>((uint32_t)nkeys, U(sl.dsum), U(sl.dft), drec, sl.dcount);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(host_count_, dcount_, sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
-    HIP_OK(hipMemcpyAsync((u64*)(host_count_ + 4), stats, 2 * sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
-    HIP_OK(hipMemsetAsync(dcount_, 0, sizeof(uint32_t), S(stream_)));
+    HIP_OK(hipMemcpyAsync(sl.host_count, sl.dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
+    HIP_OK(hipMemcpyAsync((u64*)(sl.host_count + 4), stats, 2 * sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
+    HIP_OK(hipMemsetAsync(sl.dcount, 0, sizeof(uint32_t), S(stream_)));
     HIP_OK(hipMemsetAsync(stats, 0, 2 * sizeof(u64), S(stream_)));
     HIP_OK(hipStreamSynchronize(S(stream_)));
-    n = host_count_[0];
+    n = sl.host_count[0];
   } else {
-    n = host_count_[0];
-    if (n & kNeedCollect) {  // too many touched slots for one workgroup: a wide collect pass
+    n = sl.host_count[0];
+    if (n & kNeedCollect) {
+      // too many touched slots for one workgroup: a wide collect pass, on the side stream so
+      // it does not wait behind a speculative merge already queued on the main one (the flag
+      // says this merge's table updates are complete)
       n &= ~kNeedCollect;
-      k_collect<<<256, kThreads, 0, S(stream_)>>>(dcount_, dlist_, U(dsum_), U(dft_), drec);
+      k_collect<<<256, kThreads, 0, S(aux_stream_)>>>(sl.dcount, sl.dlist, U(sl.dsum), U(sl.dft),
+                                                        drec + sl.host_count[3]);
       HIP_OK(hipGetLastError());
-      k_zero_u32<<<1, 1, 0, S(stream_)>>>(dcount_);
+      k_zero_u32<<<1, 1, 0, S(aux_stream_)>>>(sl.dcount);
       HIP_OK(hipGetLastError());
-      HIP_OK(hipStreamSynchronize(S(stream_)));
+      HIP_OK(hipStreamSynchronize(S(aux_stream_)));
     }
   }
+  if (timing_) flush_timing(false);
   live_tokens_est_ -= hs[0];
   records_total_ += n;
   records_max_ = std::max<uint64_t>(records_max_, n);
+  if (merge_log_) {
+    std::fprintf(merge_log_, "C %u %d %u %u %d %llu %zu", sl.seq, X, sl.n_iter, sl.grid, 0,
+                 (unsigned long long)hs[0], n);
+#ifdef SHRED_STAMPS
+    // per phase: when the last workgroup got there, in us after the first workgroup started
+    std::vector<u64> st((size_t)sl.grid * kStamps);
+    HIP_OK(hipStreamSynchronize(S(stream_)));
+    HIP_OK(hipMemcpy(st.data(), stamps_, st.size() * sizeof(u64), hipMemcpyDeviceToHost));
+    u64 t0 = ~0ull;
+    for (uint32_t g = 0; g < sl.grid; ++g) t0 = std::min(t0, st[(size_t)g * kStamps]);
+    for (int k = 1; k < 8; ++k) {
+      u64 mx = 0;
+      for (uint32_t g = 0; g < sl.grid; ++g) {
+        const u64 v = st[(size_t)g * kStamps + k];
+        if (v != 0 && v != ~0ull) mx = std::max(mx, v);
+      }
+      std::fprintf(merge_log_, " %.2f", mx >= t0 ? (double)(mx - t0) / 100.0 : -1.0);
+    }
+    // shader clock of workgroup 0 between its start and its ticket (MHz)
+    std::fprintf(merge_log_, " %.0f", st[4] > st[0] ? (double)(st[17] - st[16]) / (double)(st[4] - st[0]) * 100.0 : -1.0);
+    // workgroup 0's first pass through the window phases, relative to its own start
+    for (int k = 8; k < 16; ++k) {
+      const u64 v = st[k], s0 = st[0];
+      std::fprintf(merge_log_, " %.2f", v >= s0 && v != 0 ? (double)(v - s0) / 100.0 : -1.0);
+    }
+    HIP_OK(hipMemset(stamps_, 0, st.size() * sizeof(u64)));
+#endif
+    std::fprintf(merge_log_, "\n");
+  }
   return n;
+}
+
+void Device::rollback(int32_t a, int32_t b, int32_t X) {
+  HIP_OK(hipSetDevice(ordinal_));
+  MergeSlot& sl = slot_[X & 1];
+  if (sl.X != X) fatal("rollback: merge X is not the one in its slot");
+  ++rollbacks_;
+  if (!sl.launched) return;
+  sl.launched = false;
+  if (merge_log_) std::fprintf(merge_log_, "R %u %d %u %u %d\n", sl.seq, X, sl.n_iter, sl.grid, 0);
+  // queued behind the merge on the same stream: the host never waits for a wrong guess
+  UnmergeParams& up = *static_cast<UnmergeParams*>(unmerge_params_);
+  up.tok = tok_;
+  up.tile_off = tile_off_;
+  up.tile_len = tile_len_;
+  up.mlist = (const uint32_t*)sl.dev_mlist;  // host-mapped list the merge's last workgroup wrote
+  up.mcount = (const uint32_t*)sl.dev_count + 2;
+  up.a = a;
+  up.b = b;
+  up.X = X;
+  up.dcount = sl.dcount;
+  up.dlist = sl.dlist;
+  up.dsum = U(sl.dsum);
+  up.dft = U(sl.dft);
+  up.sig = sig_;
+  const int grid = kMaxMergeGroups;
+  k_unmerge<<<grid, kThreads, 0, S(stream_)>>>(up);
+  HIP_OK(hipGetLastError());
 }
 
 void Device::token_freq(size_t T, std::vector<uint64_t>* freq) {

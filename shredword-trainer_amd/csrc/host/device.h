@@ -7,11 +7,13 @@
 //   weight    u64 occurrence count per word rank ("types" layout; the "stream" layout keeps
 //             every occurrence with weight 1 and needs no weight array).
 //   dsum/dft  u64 per (neighbour slot, category): summed weight and min first-touch of the
-//             current merge's neighbour-pair deltas; dlist/dcount: the touched keys.
+//             current merge's neighbour-pair deltas; dlist/dcount: the touched keys.  Two sets
+//             (merge parity), so a speculative merge X+1 can run while merge X is consumed.
 // No HIP type appears here so host C++ can include it; bpe_device.hip implements it.
 #pragma once
 
 #include <cstddef>
+#include <cstdio>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -55,7 +57,8 @@ class Device : public Backend {
   void count_pairs(int32_t unk_id, std::vector<PairCount>* out) override;
 
   // K2+K3 for merge (a,b)->X: rewrites every occurrence in place and reduces neighbour deltas
-  // into the slot tables.
+  // into the slot tables.  Two merges may be in flight (X and X+1, speculation): each parity of
+  // X owns its own tables, host-visible records, flag and matched-tile list.
   void merge_scan(int32_t a, int32_t b, int32_t X) override;
   // Multi-GPU hook: called between merge_scan and collect(); slot tables are
   // [prefix_slots * 4] u64 sums followed by the same count of u64 first-touch values.
@@ -63,6 +66,13 @@ class Device : public Backend {
   void set_exchange(ExchangeFn fn, void* ctx) { exchange_ = fn; exchange_ctx_ = ctx; }
   // K4: the touched slots as records (host-visible), cleared for the next merge.
   size_t collect(int32_t X, const DeltaRecord** recs) override;
+  // Speculation (single GPU only): undo the outstanding merge X with k_unmerge, host-free.
+  bool can_speculate() const override { return speculate_ && !exchange_; }
+  void rollback(int32_t a, int32_t b, int32_t X) override;
+  void set_speculation(bool on) { speculate_ = on; }
+  // Tuning: k_merge grid cap.
+  void set_merge_groups(int groups);
+  uint64_t rollbacks() const { return rollbacks_; }
 
   // K6: final weighted token histogram over ids [0, T); other ids are dropped.
   void token_freq(size_t T, std::vector<uint64_t>* freq) override;
@@ -71,7 +81,7 @@ class Device : public Backend {
 
   void set_timing(bool on) { timing_ = on; }
   const KernelTimes& times() {
-    flush_timing();
+    flush_timing(true);
     return times_;
   }
   void set_unk(int32_t unk) { unk_ = unk; }
@@ -79,7 +89,7 @@ class Device : public Backend {
   uint64_t visited_tiles() const { return visited_tiles_; }
   uint64_t records_max() const { return records_max_; }
   void clear_times() {
-    flush_timing();
+    flush_timing(true);
     times_ = KernelTimes();
     records_total_ = records_max_ = 0;
     visited_tiles_ = 0;
@@ -91,14 +101,48 @@ class Device : public Backend {
   void* stream_handle() const { return stream_; }
 
  private:
-  void ensure_slots(uint32_t need);
+  // Resources of one in-flight merge (X & 1 selects the slot).
+  struct MergeSlot {
+    uint32_t cap = 0;  // neighbour slots: id+1 for ids < cap, slot 0 for unk outside
+    uint64_t* dsum = nullptr;  // 4 * (cap + 1) keys + 2 stats words
+    uint64_t* dft = nullptr;
+    uint32_t* dlist = nullptr;
+    uint32_t* dcount = nullptr;  // [0] touched-slot count, [1..9] completion tickets, [10] matched tiles
+    DeltaRecord* host_recs = nullptr;  // pinned, device-visible
+    void* dev_recs = nullptr;
+    uint32_t* host_count = nullptr;    // pinned: [0] records (| need-collect), [1] flag, [2] matched tiles,
+    void* dev_count = nullptr;         //         bytes 16..31: occurrences merged, tokens rewritten
+    uint32_t* dmlist = nullptr;        // device: tiles where the merge matched (overflow / multi-GPU)
+    uint32_t* rhdr = nullptr;          // device: per-workgroup regions of the fused completion
+    uint64_t* rrec = nullptr;
+    uint32_t* rtile = nullptr;
+    uint32_t* host_mlist = nullptr;    // pinned copy, written by the merge's last workgroup
+    void* dev_mlist = nullptr;
+    uint32_t grid = 0;
+    uint32_t n_iter = 0;  // candidate tiles of the launch
+    bool launched = false;
+    uint32_t seq = 0;
+    int32_t X = -1;
+  };
+  void ensure_slots(MergeSlot& s, uint32_t need);
+  void free_slot(MergeSlot& s, bool keep_host);
   void free_all();
-  void wait_flag();
-  void flush_timing();
+  void wait_flag(const MergeSlot& s);
+  void flush_timing(bool block);
 
   int ordinal_ = 0;
   void* stream_ = nullptr;
-  void* ev_[4] = {};
+  void* aux_stream_ = nullptr;  // wide collect of a slot while the other slot's merge runs
+  void* ev_[4] = {};            // [2],[3]: pair count
+  // sampled k_merge launch timing: a ring of event pairs read back without blocking
+  static constexpr int kEvPairs = 16;
+  void* mev_[kEvPairs][2] = {};
+  struct PendingEv {
+    int pair;
+    double bytes;
+  };
+  std::vector<PendingEv> ev_pending_;
+  std::vector<int> ev_free_;
   bool timing_ = false;
   KernelTimes times_;
   ExchangeFn exchange_ = nullptr;
@@ -116,35 +160,28 @@ class Device : public Backend {
   uint32_t* tile_len0_ = nullptr;
   uint64_t* weight_ = nullptr;
   uint64_t live_tokens0_ = 0;
+  uint32_t* sig_ = nullptr;    // per-tile pair signature (Bloom filter), see k_merge
+  unsigned long long* stamps_ = nullptr;  // SHRED_STAMPS diagnostic build only
   uint64_t nentries_ = 0;
   uint64_t live_tokens_est_ = 0;
 
-  uint32_t slot_cap_ = 0;  // neighbour slots: id+1 for ids < slot_cap_, slot 0 for unk outside
-  uint64_t* dsum_ = nullptr;
-  uint64_t* dft_ = nullptr;
-  uint32_t* dlist_ = nullptr;
-  uint32_t* dcount_ = nullptr;  // [0] touched-slot count, [1] workgroup completion ticket
-  uint32_t seq_ = 0;            // merge sequence number echoed by the device flag
-  bool launched_ = false;
+  MergeSlot slot_[2];
+  uint32_t seq_ = 0;            // launch sequence number echoed by the device flag
   int32_t unk_ = 0;
-  bool timing_pending_ = false;
-  double pending_bytes_ = 0;
   uint64_t records_total_ = 0, records_max_ = 0;
   int32_t max_id_seen_ = 0;
+  bool speculate_ = true;
+  uint64_t rollbacks_ = 0;
 
   void* merge_params_ = nullptr;        // MergeParams kernel arguments (with the inline tile list)
+  void* unmerge_params_ = nullptr;      // UnmergeParams kernel arguments
+  int max_groups_ = 256;                // k_merge grid cap (env SHREDWORD_MERGE_GROUPS)
+  FILE* merge_log_ = nullptr;           // SHREDWORD_MERGE_LOG diagnostic
   TileIndex index_;                     // tile skipping (tiles.h)
   bool skip_ = true;
   std::vector<uint32_t> cand_;
   uint64_t visited_tiles_ = 0;
-  uint32_t* host_mlist_ = nullptr;      // tiles where the last merge matched (pinned)
-  void* dev_mlist_ = nullptr;
-  void* dev_recs_ = nullptr;            // device address of host_recs_
-  void* dev_count_ = nullptr;           // device address of host_count_
   int merge_blocks_per_cu_ = 4;
-  DeltaRecord* host_recs_ = nullptr;   // pinned, device-visible
-  uint32_t* host_count_ = nullptr;     // pinned, device-visible
-  size_t host_recs_cap_ = 0;
 
   size_t bytes_alloc_ = 0;
 };

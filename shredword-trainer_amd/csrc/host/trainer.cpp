@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -65,6 +66,11 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
   } else if (key == "clear_stats") {
     t->engine.times() = EngineTimes();
     if (t->dev) t->dev->clear_times();
+  } else if (key == "merge_groups") {
+    if (!t->dev) return -1;  // tuning of an existing device (after load_corpus)
+    t->dev->set_merge_groups(std::atoi(val.c_str()));
+  } else if (key == "speculate") {
+    t->engine.set_speculation(std::atoi(val.c_str()) != 0);
   } else if (key == "device") {
     t->device = std::atoi(val.c_str());
   } else {
@@ -133,6 +139,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   t->device = env_int("SHREDWORD_DEVICE", -1);
   if (const char* v = std::getenv("SHREDWORD_LAYOUT")) set_option(t, "layout", v);
   if (const char* v = std::getenv("SHREDWORD_TRACE")) set_option(t, "trace", v);
+  t->engine.set_speculation(env_int("SHREDWORD_SPECULATE", 1) != 0);
   if (t->engine.log() >= 1) std::printf("[INFO]\t BPE trainer initialized. Heap initialized successfully.\n");
   return t;
 }
@@ -242,6 +249,22 @@ double shred_probe_merge(Trainer* t, int32_t a, int32_t b, int iters) {
   return 1e6 * total / iters;
 }
 
+int shred_probe_rollback(Trainer* t, int32_t a, int32_t b) {
+  if (!t || !ensure_device(t, "shred_probe_rollback")) return -1;
+  const int32_t X = kBaseVocab + (int32_t)t->engine.num_merges();
+  t->dev->merge_scan(a, b, X);
+  t->dev->rollback(a, b, X);
+  return 0;
+}
+
+int64_t shred_debug_tokens(Trainer* t, int32_t* out, size_t cap) {
+  if (!t || !ensure_device(t, "shred_debug_tokens")) return -1;
+  std::vector<int32_t> v;
+  t->dev->download_tokens(&v);
+  if (out) std::memcpy(out, v.data(), std::min(cap, v.size()) * sizeof(int32_t));
+  return (int64_t)v.size();
+}
+
 int shred_get_stats(const Trainer* tc, ShredStats* s) {
   if (!tc || !s) return -1;
   Trainer* t = const_cast<Trainer*>(tc);
@@ -280,6 +303,8 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
   s->apply_cycles_order = c.cyc_order;
   s->apply_cycles_walk = c.cyc_walk;
   if (t->dev) s->tiles_visited = t->dev->visited_tiles();
+  s->spec_hits = t->engine.spec_hits();
+  s->spec_misses = t->engine.spec_misses();
   s->layout = (int32_t)t->layout;
   s->world_size = dist_active() ? dist_state().world : 1;
   return 0;

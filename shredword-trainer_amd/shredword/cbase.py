@@ -9,7 +9,7 @@ fails here with AttributeError, as with the reference.  The Trainer handle is op
 import ctypes
 import os
 import sysconfig
-from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_int, c_int32,
+from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_int, c_int32, c_int64,
                     c_size_t, c_uint64, c_void_p)
 
 
@@ -61,7 +61,8 @@ class ShredStats(Structure):
                 ("heap_pops", c_uint64), ("heap_stale_pops", c_uint64), ("heap_pushes", c_uint64),
                 ("delta_records", c_uint64), ("tiles_visited", c_uint64),
                 ("apply_cycles_combine", c_uint64), ("apply_cycles_order", c_uint64),
-                ("apply_cycles_walk", c_uint64)]
+                ("apply_cycles_walk", c_uint64),
+                ("spec_hits", c_uint64), ("spec_misses", c_uint64)]
 
 
 Trainer = c_void_p
@@ -93,6 +94,8 @@ lib.loadVocab.argtypes, lib.loadVocab.restype = [c_void_p, c_char_p], c_bool
 lib.shred_set_option.argtypes, lib.shred_set_option.restype = [Trainer, c_char_p, c_char_p], c_int
 lib.shred_reset.argtypes, lib.shred_reset.restype = [Trainer], c_int
 lib.shred_probe_merge.argtypes, lib.shred_probe_merge.restype = [Trainer, c_int32, c_int32, c_int], c_double
+lib.shred_probe_rollback.argtypes, lib.shred_probe_rollback.restype = [Trainer, c_int32, c_int32], c_int
+lib.shred_debug_tokens.argtypes, lib.shred_debug_tokens.restype = [Trainer, POINTER(c_int32), c_size_t], c_int64
 lib.shred_get_stats.argtypes, lib.shred_get_stats.restype = [Trainer, POINTER(ShredStats)], c_int
 lib.shred_device_count.argtypes, lib.shred_device_count.restype = [], c_int
 lib.shred_dist_unique_id.argtypes, lib.shred_dist_unique_id.restype = [c_void_p, c_size_t], c_int

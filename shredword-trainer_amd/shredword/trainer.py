@@ -4,7 +4,7 @@ Same constructor defaults, method names, argument meaning and errors as the refe
 ``load_corpus`` raises IOError for a missing file or a failed load, ``train`` returns the merge
 count (RuntimeError if negative) and prints ``Training completed: N merges performed.``,
 ``save`` creates parent directories, ``destroy`` is idempotent and runs from ``__exit__`` and
-``__del__``.  Extensions: ``set_option``, ``reset``, ``stats``.
+``__del__``.  Extensions: ``set_option``, ``reset``, ``stats``, ``tokens``.
 """
 import ctypes
 import os
@@ -54,6 +54,17 @@ class BPETrainer:
     def reset(self) -> None:
         """Restore the loaded corpus to its unmerged state (benchmark repeats)."""
         lib.shred_reset(self.trainer)
+
+    def tokens(self):
+        """The live device token stream (diagnostic): per entry a header INT32_MIN + rank, then
+        its tokens, as a numpy int32 array."""
+        import numpy as np
+        n = lib.shred_debug_tokens(self.trainer, None, 0)
+        if n < 0:
+            raise RuntimeError("no device token stream")
+        out = np.empty(n, dtype=np.int32)
+        lib.shred_debug_tokens(self.trainer, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n)
+        return out
 
     def stats(self) -> dict:
         s = ShredStats()

@@ -28,6 +28,10 @@ def load():
                "hh_distinct_bytes", "hh_kept_bytes", "hh_tiles_visited"):
         getattr(lib, fn).argtypes = [ctypes.c_void_p]
         getattr(lib, fn).restype = ctypes.c_uint64
+    lib.hh_visit_hist.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64]
+    lib.hh_visit_hist.restype = ctypes.c_uint64
+    lib.hh_match_hist.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64]
+    lib.hh_match_hist.restype = ctypes.c_uint64
     lib.hh_spec.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     lib.hh_word.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                             ctypes.POINTER(ctypes.c_uint64)]

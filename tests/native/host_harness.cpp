@@ -65,6 +65,10 @@ class EmuBackend : public Backend {
   }
 
   void emit(uint32_t key, uint64_t w, uint64_t ft) {
+    if (raw_) {  // direct mode: unreduced records, duplicates combined by the host
+      raw_->push_back({key, 0, w, ft});
+      return;
+    }
     dsum_[key] += w;
     if (ft < dft_[key]) dft_[key] = ft;
   }
@@ -76,6 +80,9 @@ class EmuBackend : public Backend {
     std::vector<uint32_t> cand, matched;
     const bool use_list = index_.candidates(a, b, &cand);
     const size_t nvisit = use_list ? cand.size() : ts_.num_tiles();
+    // like the device's direct mode: candidate-list merges ship per-occurrence records
+    std::vector<DeltaRecord> raw;
+    raw_ = (use_list && !cb_ && direct_) ? &raw : nullptr;
     for (size_t it = 0; it < nvisit; ++it) {
       const size_t t = use_list ? cand[it] : it;
       int32_t* p = ts_.tok.data() + ts_.off[t];
@@ -123,12 +130,15 @@ class EmuBackend : public Backend {
     }
     visited_ += nvisit;
     hist_.push_back((uint32_t)nvisit);
+    mhist_.push_back((uint32_t)matched.size());
     Pending pd;
     pd.a = a;
     pd.b = b;
     pd.X = X;
     pd.matched = std::move(matched);
-    if (!cb_) drain(&pd.recs);  // multi-rank: tables stay for collect()'s exchange
+    if (raw_) pd.recs = std::move(raw);
+    else if (!cb_) drain(&pd.recs);  // multi-rank: tables stay for collect()'s exchange
+    raw_ = nullptr;
     queue_.push_back(std::move(pd));
   }
 
@@ -207,6 +217,11 @@ class EmuBackend : public Backend {
   TileIndex index_;
   uint64_t visited_ = 0;
   std::vector<uint64_t> dsum_, dft_;
+  std::vector<DeltaRecord>* raw_ = nullptr;
+ public:
+  std::vector<uint32_t> mhist_;  // matched tiles per launch
+ private:
+  bool direct_ = std::getenv("HH_DIRECT") ? std::atoi(std::getenv("HH_DIRECT")) != 0 : true;
   std::vector<DeltaRecord> recs_;
   struct Pending {
     int32_t a = 0, b = 0, X = 0;
@@ -296,6 +311,11 @@ uint64_t hh_live_tokens(void* p) {
   return s;
 }
 uint64_t hh_tiles_visited(void* p) { return ((Harness*)p)->be->visited(); }
+uint64_t hh_match_hist(void* p, uint32_t* out, uint64_t cap) {
+  const auto& h = ((Harness*)p)->be->mhist_;
+  for (size_t i = 0; i < h.size() && i < cap; ++i) out[i] = h[i];
+  return h.size();
+}
 uint64_t hh_visit_hist(void* p, uint32_t* out, uint64_t cap) {
   const auto& h = ((Harness*)p)->be->hist_;
   for (size_t i = 0; i < h.size() && i < cap; ++i) out[i] = h[i];

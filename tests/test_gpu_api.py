@@ -4,6 +4,7 @@
 * run-to-run determinism (reset + retrain, and a fresh trainer) — device atomics are order-free;
 * bpe_init + bpe_merge_batch through the C ABI;
 * a medium corpus against the CPU oracle (bit-exact) in both layouts;
+* speculation: k_unmerge restores the stream exactly; speculation on/off in lock step;
 * the C2 workload at full size (1 GB) through size-independent invariants: byte conservation
   (Σ freq(token) x len(token) = Σ word bytes x count) and non-increasing merge frequencies.
 """
@@ -115,6 +116,59 @@ def test_medium_corpus_matches_oracle(layout, tmp_path):
     assert model == open(om, "rb").read()
     assert vocab == open(ov, "rb").read()
     assert n > 1000
+
+
+@pytest.fixture(scope="module")
+def medium_corpus(tmp_path_factory):
+    path = str(tmp_path_factory.mktemp("med") / "m.txt")
+    corpora.gen_synthetic(path, 12_000_000, 31, "mixed")
+    return path
+
+
+def test_rollback_restores_stream(medium_corpus):
+    """The undo path of speculation (k_unmerge) leaves the corpus bit-identical, including
+    a == b runs and pairs spanning many tiles."""
+    from shredword.cbase import lib
+    t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+    t.set_option("layout", "stream")
+    t.load_corpus(medium_corpus)
+    lib.bpe_init(t.trainer)
+    assert lib.bpe_merge_batch(t.trainer, 40) == 40
+    before = t.tokens()
+    for pair in [(101, 32), (32, 116), (116, 104), (101, 101), (108, 108), (256, 257), (32, 32)]:
+        assert lib.shred_probe_rollback(t.trainer, *pair) == 0
+        after = t.tokens()
+        assert after.shape == before.shape and (after == before).all(), pair
+    t.destroy()
+
+
+@pytest.mark.parametrize("layout", ["stream", "types"])
+def test_speculation_lockstep(layout, medium_corpus):
+    """Speculative pipelining on vs off, in bpe_merge_batch chunks: identical merges and an
+    identical device token stream after every chunk (rollbacks included)."""
+    from shredword.cbase import lib
+    ts = []
+    for spec in (0, 1):
+        t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+        t.set_option("layout", layout)
+        t.set_option("speculate", spec)
+        t.load_corpus(medium_corpus)
+        lib.bpe_init(t.trainer)
+        ts.append(t)
+    done = 0
+    for chunk in [64, 1, 7, 200, 33] * 40:
+        na = lib.bpe_merge_batch(ts[0].trainer, chunk)
+        nb = lib.bpe_merge_batch(ts[1].trainer, chunk)
+        assert na == nb
+        xa, xb = ts[0].tokens(), ts[1].tokens()
+        assert xa.shape == xb.shape and (xa == xb).all(), f"streams differ after {done + na} merges"
+        done += na
+        if na < chunk:
+            break
+    st = ts[1].stats()
+    assert st["spec_hits"] > 0 and st["spec_misses"] > 0
+    for t in ts:
+        t.destroy()
 
 
 def _parse_vocab(vocab: bytes, ops):
