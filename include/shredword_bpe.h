@@ -73,9 +73,11 @@ int loadVocab(void* trainer, const char* path);
  *   timing = 0 | 1              per-kernel HIP-event timing (shred_get_stats)
  *   device = <ordinal>          HIP device (default: LOCAL_RANK or 0)
  *   merge_groups = <n>          k_merge grid cap (tuning; after load_corpus)
- *   speculate = 0 | 1           run the predicted next merge while the host consumes the
- *                               current one, rolled back exactly on a wrong guess (default 1;
- *                               single GPU only, results are identical either way)
+ *   speculate = 0 | 1           merge chains: run the selected merge together with merges
+ *                               guessed from the heap in one device pass, confirm them one by
+ *                               one, roll a wrong tail back exactly (default 1; single GPU only;
+ *                               results are identical either way)
+ *   chain = <n>                 longest merge chain (default 6, at most 8; 1 = no guesses)
  * Returns 0, or -1 for an unknown key/value. */
 int shred_set_option(Trainer* trainer, const char* key, const char* value);
 /* Restores the loaded corpus to its unmerged state and forgets merges (benchmark repeats). */

@@ -249,10 +249,16 @@ constexpr uint32_t kNeedCollect = 0x80000000u;
 constexpr uint32_t kTimingStride = 8;
 constexpr uint32_t kInlineTiles = 768;     // candidate tiles that fit the kernel arguments
 constexpr int kGroup = 4;                  // tiles walked together per wave (loads in flight)
+// LDS staging index skew: lane l touches positions 16 l + j together, which unskewed all fall in
+// two of the 32 banks; i + i / 16 gives a stride of 17 words, conflict-free.
+__device__ __forceinline__ int SK(int i) { return i + (i >> 4); }
+constexpr int kStPad = kWaveTok + 8 + (kWaveTok + 8) / 16 + 1;
 constexpr int kMaxMergeGroups = SHRED_MAX_GROUPS;
 constexpr int kSigBits = SHRED_SIG_BITS;   // per-tile pair signature
 constexpr int kSigWords = kSigBits / 32;
 constexpr uint32_t kWin = 32;              // candidate tiles per workgroup window (filter pass)
+constexpr int kMaxChain = 8;               // merges one k_merge launch applies in order
+constexpr int kChainShift = 27;            // matched-tile entries: tile | (chain index << 27)
 constexpr uint32_t kMtLds = 256;           // matched tiles a workgroup keeps in LDS (more: global list)
 constexpr int kRegHdr = 8;                 // region header: nrec, nmt, spill, pad, merged (2), written (2)
 [[maybe_unused]] constexpr int kStamps = 18;               // SHRED_STAMPS: entry, init, windows, flush, ticket, collect, flag
@@ -266,6 +272,7 @@ constexpr int kRegHdr = 8;                 // region header: nrec, nmt, spill, p
 #define STAMP(k)
 #define STAMP_ONCE(k)
 #endif
+static_assert(kMaxChain == Device::kChainMax, "chain length shared with the host");
 static_assert(kSigWords % 256 == 0 || kSigWords == 64 || kSigWords == 128, "signature written as 16 B per lane");
 
 // The two signature bits of pair (x, y).
@@ -333,7 +340,10 @@ struct MergeParams {
   uint32_t* tile_len;
   uint32_t ntiles;
   const uint64_t* weight;
-  int32_t a, b, X;
+  int32_t X0;               // merge i of the chain: (ca[i], cb[i]) -> X0 + i
+  int32_t nchain;
+  int32_t ca[kMaxChain], cb[kMaxChain];
+  uint32_t keys_per_merge;  // delta key of merge i: i * keys_per_merge + (slot << 2 | category)
   uint32_t slot_cap;
   u64* dsum;
   u64* dft;
@@ -398,7 +408,7 @@ __device__ __forceinline__ int wave_incl_sum(int x) { return (int)wave_scan_add(
 
 template <bool kWeighted>
 __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
-  __shared__ int32_t s_tok[kWaves][kWaveTok + 8];  // [2 + j] = chunk position j; [0],[1] = -2,-1
+  __shared__ int32_t s_tok[kWaves][kStPad];  // [SK(2 + j)] = chunk position j; [SK(0)],[SK(1)] = -2,-1
   __shared__ uint32_t s_sig[kWaves][kSigWords];
   __shared__ DeltaLds h;
   __shared__ uint32_t s_last;
@@ -427,16 +437,13 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
   }
   __syncthreads();
   STAMP(1);
-  const int32_t a = p.a, b = p.b, X = p.X;
-  const bool same = (a == b);
   const int p0 = lane * kPer;
+  const int nchain = p.nchain;
   u64 n_merged = 0, n_written = 0;  // wave-uniform
 
   // ---- windows of kWin candidates: filter, then the waves split the hits
   const uint32_t n_cand = p.nlist ? p.nlist : p.ntiles;
   const uint32_t nwin = (n_cand + kWin - 1) / kWin;
-  uint32_t h1, h2;
-  sig_bits(a, b, &h1, &h2);
   for (uint32_t win = blockIdx.x; win < nwin; win += gridDim.x) {
     if (wid == 0) {
       const uint32_t i = win * kWin + (uint32_t)lane;
@@ -453,10 +460,16 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       }
       if ((uint32_t)lane < kWin) s_wt[lane] = t;
       bool hit = in;
-      if (p.filter) {
+      if (p.filter) {  // may the tile hold any pair of the chain?
         const uint32_t* sg = p.sig + (size_t)t * kSigWords;
-        const uint32_t w1 = sg[h1 >> 5], w2 = sg[h2 >> 5];
-        hit = in && ((w1 >> (h1 & 31)) & 1u) && ((w2 >> (h2 & 31)) & 1u);
+        bool any = false;
+        for (int cj = 0; cj < nchain; ++cj) {
+          uint32_t h1, h2;
+          sig_bits(p.ca[cj], p.cb[cj], &h1, &h2);
+          const uint32_t w1 = sg[h1 >> 5], w2 = sg[h2 >> 5];
+          any |= ((w1 >> (h1 & 31)) & 1u) && ((w2 >> (h2 & 31)) & 1u);
+        }
+        hit = in && any;
       }
       const u64 m = __ballot(hit);
       if (lane == 0) s_hits = m;
@@ -508,13 +521,19 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       gn[k] = wave_next(gv[k][0]);
       if (lane == 63) gn[k] = (uint32_t)(p0 + kPer) < gl[k] ? gm[k] : kPad;
     }
+    for (int cj = 0; cj < nchain; ++cj) {  // a chain merge's pair cannot appear through an earlier one
+      const int32_t a = p.ca[cj], b = p.cb[cj];
 #pragma unroll
-    for (int k = 0; k < kGroup; ++k) {
-      bool any = false;
+      for (int k = 0; k < kGroup; ++k) {
+        bool any = false;
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) any |= (gv[k][j] == a) & ((j + 1 < kPer ? gv[k][j + 1] : gn[k]) == b);
-      if (__any(any) || gl[k] > (uint32_t)kWaveTok) gmask |= 1u << k;
+        for (int j = 0; j < kPer; ++j) any |= (gv[k][j] == a) & ((j + 1 < kPer ? gv[k][j + 1] : gn[k]) == b);
+        if (__any(any)) gmask |= 1u << k;
+      }
     }
+#pragma unroll
+    for (int k = 0; k < kGroup; ++k)
+      if (gl[k] > (uint32_t)kWaveTok) gmask |= 1u << k;
     STAMP_ONCE(10);
 #pragma unroll 1
     for (int k = 0; k < kGroup; ++k) {
@@ -525,8 +544,28 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
     int32_t v0[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) v0[j] = k == 0 ? gv[0][j] : k == 1 ? gv[1][j] : k == 2 ? gv[2][j] : gv[3][j];
-    const int32_t nx0 = SHRED_SEL(gn);
+    int32_t nx0 = SHRED_SEL(gn);
 #undef SHRED_SEL
+    // The chain's merges in order.  A single-chunk tile stays in registers (cur) between merges
+    // and is written back once; a longer tile is rewritten in HBM chunk by chunk per merge.
+    const bool single = len <= (uint32_t)kWaveTok;
+    int32_t cur[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) cur[j] = v0[j];
+    int32_t cur_nx = nx0;
+    uint32_t cur_len = len;
+    bool tdirty = false;
+#pragma unroll 1
+    for (int cj = 0; cj < nchain; ++cj) {
+    const int32_t a = p.ca[cj], b = p.cb[cj], X = p.X0 + cj;
+    const bool same = (a == b);
+    const uint32_t kofs = (uint32_t)cj * p.keys_per_merge;
+    if (!single && tdirty) {  // re-read a long tile rewritten by an earlier merge of the chain
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      load_chunk(base, 0, min((uint32_t)kWaveTok, cur_len), p0, v0);
+      nx0 = next_token(base, 0, cur_len, p0, v0[0]);
+    }
+    const uint32_t tlen = cur_len;
     uint64_t tile_hits = 0;
     long long c_nona = -1;  // last tile index whose token != a (a == b only)
     u64 c_hdr = 0;          // ((index + 1) << 32) | rank of the last header, 0 = none
@@ -534,18 +573,18 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
     int32_t c_t1 = kPad, c_t2 = kPad;
     uint32_t c_out = 0;
     bool dirty = false;
-    for (uint32_t cs = 0; cs < len; cs += kWaveTok) {
-      const uint32_t cl = min((uint32_t)kWaveTok, len - cs);
-      const bool more = cs + cl < len;
+    for (uint32_t cs = 0; cs < tlen; cs += kWaveTok) {
+      const uint32_t cl = min((uint32_t)kWaveTok, tlen - cs);
+      const bool more = cs + cl < tlen;
       int32_t v[kPer];
       int32_t nx;
       if (cs == 0) {
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) v[j] = v0[j];
-        nx = nx0;
+        for (int j = 0; j < kPer; ++j) v[j] = single ? cur[j] : v0[j];
+        nx = single ? cur_nx : nx0;
       } else {
         load_chunk(base, cs, cl, p0, v);
-        nx = next_token(base, cs, len, p0, v[0]);
+        nx = next_token(base, cs, tlen, p0, v[0]);
       }
       bool any = false;
 #pragma unroll
@@ -554,19 +593,19 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
 
       // ---- stage the chunk with 2 tokens of left context and 2 of lookahead
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) st[2 + p0 + j] = v[j];
+      for (int j = 0; j < kPer; ++j) st[SK(2 + p0 + j)] = v[j];
       if (lane == 0) {
-        st[0] = c_t2;
-        st[1] = c_t1;
+        st[SK(0)] = c_t2;
+        st[SK(1)] = c_t1;
       }
       if (lane == 63) {
-        st[2 + kWaveTok] = (cs + kWaveTok < len) ? base[cs + kWaveTok] : kPad;
-        st[3 + kWaveTok] = (cs + kWaveTok + 1 < len) ? base[cs + kWaveTok + 1] : kPad;
+        st[SK(2 + kWaveTok)] = (cs + kWaveTok < tlen) ? base[cs + kWaveTok] : kPad;
+        st[SK(3 + kWaveTok)] = (cs + kWaveTok + 1 < tlen) ? base[cs + kWaveTok + 1] : kPad;
       }
       wave_lds_sync();
       STAMP_ONCE(12);
-      const int32_t last1 = st[2 + cl - 1];
-      const int32_t last2 = st[2 + cl - 2];  // st[1] when cl == 1
+      const int32_t last1 = st[SK(2 + cl - 1)];
+      const int32_t last2 = st[SK(2 + cl - 2)];  // st[SK(1)] when cl == 1
 
       // ---- occurrences, greedy left to right (runs of a == b pair up from the run start)
       uint32_t mask = 0;
@@ -607,7 +646,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       u64 hl = 0;
       if (hmask) {
         const int j = 31 - __clz(hmask);
-        hl = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(st[2 + p0 + j]);
+        hl = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(st[SK(2 + p0 + j)]);
       }
       const u64 hinc = wave_scan_max64(hl);
       const u64 hdr_ex = wave_prev64(hinc);
@@ -627,7 +666,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
           u64 hdr = hdr_in;
           if (hb) {
             const int jh = 31 - __clz(hb);
-            hdr = ((u64)(cs + p0 + jh + 1) << 32) | hdr_rank(st[2 + p0 + jh]);
+            hdr = ((u64)(cs + p0 + jh + 1) << 32) | hdr_rank(st[SK(2 + p0 + jh)]);
           }
           const uint32_t hidx = (uint32_t)(hdr >> 32) - 1u;
           const uint32_t rank = (uint32_t)hdr;
@@ -635,16 +674,16 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
           const u64 w = kWeighted ? p.weight[rank] : 1ull;
           const u64 ftb = ((u64)rank << 32) | ((u64)(gi - hidx - 1u) << 2);
           if (gi - 1u > hidx) {  // left neighbour inside the word; X if it was just merged
-            const int32_t left = ((m_ext >> j) & 1u) ? X : st[1 + p0 + j];
+            const int32_t left = ((m_ext >> j) & 1u) ? X : st[SK(1 + p0 + j)];
             const uint32_t sl = slot_of(left, p.slot_cap) << 2;
-            delta_emit(h, p, sl | kOldLeft, w, ftb | kOldLeft);
-            delta_emit(h, p, sl | kNewLeft, w, ftb | kNewLeft);
+            delta_emit(h, p, kofs + (sl | kOldLeft), w, ftb | kOldLeft);
+            delta_emit(h, p, kofs + (sl | kNewLeft), w, ftb | kNewLeft);
           }
-          const int32_t right = st[4 + p0 + j];  // original token after b
+          const int32_t right = st[SK(4 + p0 + j)];  // original token after b
           if (!is_hdr(right)) {
             const uint32_t sr = slot_of(right, p.slot_cap) << 2;
-            delta_emit(h, p, sr | kOldRight, w, ftb | kOldRight);
-            delta_emit(h, p, sr | kNewRight, w, ftb | kNewRight);
+            delta_emit(h, p, kofs + (sr | kOldRight), w, ftb | kOldRight);
+            delta_emit(h, p, kofs + (sr | kNewRight), w, ftb | kNewRight);
           }
         }
       }
@@ -655,20 +694,21 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
         int o = kc_ex;
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
-          if (j < valid && !((removed >> j) & 1u)) st[2 + o++] = ((mask >> j) & 1u) ? X : v[j];
+          if (j < valid && !((removed >> j) & 1u)) st[SK(2 + o++)] = ((mask >> j) & 1u) ? X : v[j];
         wave_lds_sync();
-        for (int j = lane; j < kept; j += 64) base[c_out + j] = st[2 + j];
+        if (single) {  // the tile lives on in registers: cur <- compacted chunk
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) cur[j] = p0 + j < kept ? st[SK(2 + p0 + j)] : kPad;
+          cur_nx = p0 + kPer < kept ? st[SK(2 + p0 + kPer)] : kPad;
+          cur_len = (uint32_t)kept;
+          tdirty = true;
+        } else {
+          for (int j = lane; j < kept; j += 64) base[c_out + j] = st[SK(2 + j)];
+        }
         dirty = true;
         n_written += (u64)kept;
         STAMP_ONCE(14);
-        if (len <= (uint32_t)kWaveTok) {  // single-chunk tile: its signature from the compacted chunk
-          int32_t w[kPer];
-#pragma unroll
-          for (int j = 0; j < kPer; ++j) w[j] = p0 + j < kept ? st[2 + p0 + j] : kPad;
-          const int32_t wn = p0 + kPer < kept ? st[2 + p0 + kPer] : kPad;
-          sig_rebuild(s_sig[wid], p.sig + (size_t)tile * kSigWords, w, wn, lane);
-          STAMP_ONCE(15);
-        }
+
       }
       n_merged += (u64)matches;
       tile_hits += (u64)matches;
@@ -682,11 +722,34 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       if (same) c_nona = nona_tot > c_nona ? nona_tot : c_nona;
       wave_lds_sync();  // the copy-out reads st before the next chunk overwrites it
     }
-    if (dirty && lane == 0) p.tile_len[tile] = c_out;
+    if (!single && dirty) {
+      if (lane == 0) p.tile_len[tile] = c_out;
+      cur_len = c_out;
+      tdirty = true;
+    }
     if (tile_hits && lane == 0) {
+      const uint32_t ent = tile | ((uint32_t)cj << kChainShift);
       const uint32_t k = p.fused ? atomicAdd(&s_nmt, 1u) : kMtLds;
-      if (k < kMtLds) s_mt[k] = tile;
-      else atomicExch(&p.mlist[atomicAdd(p.mcount, 1u)], tile);
+      if (k < kMtLds) s_mt[k] = ent;
+      else atomicExch(&p.mlist[atomicAdd(p.mcount, 1u)], ent);
+    }
+    }  // merges of the chain
+    if (single && tdirty) {  // write the tile back once, within its allocation, and re-sign it
+      const uint32_t cap = (len + 3u) & ~3u;
+#pragma unroll
+      for (int q = 0; q < kPer / 4; ++q) {
+        if ((uint32_t)(p0 + 4 * q) < cap) {
+          int4 o;
+          o.x = cur[4 * q];
+          o.y = cur[4 * q + 1];
+          o.z = cur[4 * q + 2];
+          o.w = cur[4 * q + 3];
+          *reinterpret_cast<int4*>(base + p0 + 4 * q) = o;
+        }
+      }
+      if (lane == 0) p.tile_len[tile] = cur_len;
+      sig_rebuild(s_sig[wid], p.sig + (size_t)tile * kSigWords, cur, cur_nx, lane);
+      STAMP_ONCE(15);
     }
     }  // tiles of the group
     STAMP_ONCE(11);
@@ -933,19 +996,23 @@ __global__ __launch_bounds__(kThreads) void k_collect_dense(uint32_t nkeys, u64*
 }
 
 // ------------------------------------------------------------------------------------------
-// Rollback of a speculative merge (a,b)->X: every X in the tiles the merge reported is expanded
-// back into "a b", in place, wave per tile.  Chunks are walked from the tile's end so each
-// chunk's (right-shifted) output only lands on input that has already been read; the result is
-// exactly the pre-merge tile because X is a fresh id.  A restored single-chunk tile gets its
-// signature rebuilt.  Workgroup 0 also clears the slot tables when the merge left them
-// uncollected (more touched slots than the fused collect handles).
+// Rollback of the unconfirmed tail of a merge chain: in every listed tile, each undone merge
+// (a,b)->X is expanded back into "a b", newest first, so the tile is exactly as before those
+// merges (their X are fresh ids, and their pairs never involve another chain id).  A tile whose
+// restored length fits one wave chunk is expanded in registers through LDS, written back once and
+// re-signed; a longer one is expanded in place in HBM, chunks walked from the end so a chunk's
+// right-shifted output only lands on input already read.  Workgroup 0 also clears the slot
+// tables when the chain spilled into them.
 struct UnmergeParams {
   int32_t* tok;
   const uint64_t* tile_off;
   uint32_t* tile_len;
-  const uint32_t* mlist;   // host-visible matched tiles written by the merge's last workgroup
-  const uint32_t* mcount;  // host-visible count written by the merge's last workgroup
-  int32_t a, b, X;
+  const uint32_t* tiles;  // host-mapped list of the tiles to restore
+  uint32_t ntl;
+  const uint32_t* ntl_dev;  // if set: the count, written to host memory by the merge itself
+  int32_t nundo;          // undo merges ux0 + u, u < nundo
+  int32_t ux0;
+  int32_t ua[kMaxChain], ub[kMaxChain];
   uint32_t* dcount;
   const uint32_t* dlist;
   u64* dsum;
@@ -955,66 +1022,122 @@ struct UnmergeParams {
 
 __global__ __launch_bounds__(kThreads) void k_unmerge(UnmergeParams p) {
   __shared__ uint32_t s_sig[kWaves][kSigWords];
+  __shared__ int32_t s_buf[kWaves][kStPad];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int p0 = lane * kPer;
-  const uint32_t n = *p.mcount;
-  for (uint32_t i = blockIdx.x * kWaves + wid; i < n; i += gridDim.x * kWaves) {
-    const uint32_t tile = p.mlist[i];
+  int32_t* buf = s_buf[wid];
+  const uint32_t xlo = (uint32_t)p.ux0, nun = (uint32_t)p.nundo;
+  const uint32_t ntl = p.ntl_dev ? *p.ntl_dev : p.ntl;
+  for (uint32_t i = blockIdx.x * kWaves + wid; i < ntl; i += gridDim.x * kWaves) {
+    const uint32_t tile = p.tiles[i];
     const uint32_t len = p.tile_len[tile];
     int32_t* base = p.tok + p.tile_off[tile];
-    int total = 0;
+    int cnt = 0;  // every undone X in the tile: the restored length
     for (uint32_t cs = 0; cs < len; cs += kWaveTok) {
       int32_t v[kPer];
       load_chunk(base, cs, min((uint32_t)kWaveTok, len - cs), p0, v);
-      int c = 0;
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) c += v[j] == p.X;
-      total += c;
+      for (int j = 0; j < kPer; ++j) cnt += (uint32_t)v[j] - xlo < nun;
     }
-    total = (int)lane_read((uint32_t)wave_incl_sum(total), 63);
-    if (total == 0) continue;
-    int after = 0;  // X count in the chunks right of the current one
-    const uint32_t last_cs = ((len - 1) / kWaveTok) * kWaveTok;
-    for (long long cs = last_cs; cs >= 0; cs -= kWaveTok) {
-      const uint32_t cl = min((uint32_t)kWaveTok, len - (uint32_t)cs);
+    cnt = (int)lane_read((uint32_t)wave_incl_sum(cnt), 63);
+    if (cnt == 0) continue;
+    const uint32_t final_len = len + (uint32_t)cnt;
+    if (final_len <= (uint32_t)kWaveTok) {
       int32_t v[kPer];
-      load_chunk(base, (uint32_t)cs, cl, p0, v);
-      int c = 0;
+      load_chunk(base, 0, len, p0, v);
+      uint32_t cl = len;
+      for (int u = p.nundo - 1; u >= 0; --u) {
+        const int32_t X = p.ux0 + u, a = p.ua[u], b = p.ub[u];
+        int c = 0;
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) c += v[j] == p.X;
-      const int inc = wave_incl_sum(c);
-      const int ctot = (int)lane_read((uint32_t)inc, 63);
-      uint32_t o = (uint32_t)cs + (uint32_t)p0 + (uint32_t)(total - after - ctot) + (uint32_t)(inc - c);
+        for (int j = 0; j < kPer; ++j) c += v[j] == X;
+        const int inc = wave_incl_sum(c);
+        const int ctot = (int)lane_read((uint32_t)inc, 63);
+        if (ctot == 0) continue;
+        uint32_t o = (uint32_t)p0 + (uint32_t)(inc - c);
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) {
-        if (p0 + j >= (int)cl) continue;
-        if (v[j] == p.X) {
-          base[o] = p.a;
-          base[o + 1] = p.b;
-          o += 2;
-        } else {
-          base[o] = v[j];
-          o += 1;
+        for (int j = 0; j < kPer; ++j) {
+          if ((uint32_t)(p0 + j) >= cl) continue;
+          if (v[j] == X) {
+            buf[SK(o)] = a;
+            buf[SK(o + 1)] = b;
+            o += 2;
+          } else {
+            buf[SK(o)] = v[j];
+            o += 1;
+          }
+        }
+        wave_lds_sync();
+        cl += (uint32_t)ctot;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) v[j] = (uint32_t)(p0 + j) < cl ? buf[SK(p0 + j)] : kPad;
+        wave_lds_sync();
+      }
+      const uint32_t cap = (cl + 3u) & ~3u;  // within the tile's allocation (>= its original length)
+#pragma unroll
+      for (int q = 0; q < kPer / 4; ++q) {
+        if ((uint32_t)(p0 + 4 * q) < cap) {
+          int4 w;
+          w.x = v[4 * q];
+          w.y = v[4 * q + 1];
+          w.z = v[4 * q + 2];
+          w.w = v[4 * q + 3];
+          *reinterpret_cast<int4*>(base + p0 + 4 * q) = w;
         }
       }
-      after += ctot;
-    }
-    const uint32_t nlen = len + (uint32_t)total;
-    if (lane == 0) p.tile_len[tile] = nlen;
-    if (nlen <= (uint32_t)kWaveTok) {
-      // re-read the restored tile (this wave's own stores: ordered by a workgroup-scope fence)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      int32_t v[kPer];
-      load_chunk(base, 0, nlen, p0, v);
-      const int32_t m = base[p0 + kPer];
+      if (lane == 0) p.tile_len[tile] = cl;
       int32_t nx = wave_next(v[0]);
-      if (lane == 63) nx = (uint32_t)(p0 + kPer) < nlen ? m : kPad;
+      if (lane == 63) nx = kPad;
       sig_rebuild(s_sig[wid], p.sig + (size_t)tile * kSigWords, v, nx, lane);
+      continue;
+    }
+    // a tile longer than one chunk (its signature stays all-ones)
+    uint32_t tl = len;
+    for (int u = p.nundo - 1; u >= 0; --u) {
+      const int32_t X = p.ux0 + u, a = p.ua[u], b = p.ub[u];
+      if (u != p.nundo - 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // our own rewrite
+      int total = 0;
+      for (uint32_t cs = 0; cs < tl; cs += kWaveTok) {
+        int32_t v[kPer];
+        load_chunk(base, cs, min((uint32_t)kWaveTok, tl - cs), p0, v);
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) c += v[j] == X;
+        total += c;
+      }
+      total = (int)lane_read((uint32_t)wave_incl_sum(total), 63);
+      if (total == 0) continue;
+      int after = 0;  // X count in the chunks right of the current one
+      const uint32_t last_cs = ((tl - 1) / kWaveTok) * kWaveTok;
+      for (long long cs = last_cs; cs >= 0; cs -= kWaveTok) {
+        const uint32_t cl = min((uint32_t)kWaveTok, tl - (uint32_t)cs);
+        int32_t v[kPer];
+        load_chunk(base, (uint32_t)cs, cl, p0, v);
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) c += v[j] == X;
+        const int inc = wave_incl_sum(c);
+        const int ctot = (int)lane_read((uint32_t)inc, 63);
+        uint32_t o = (uint32_t)cs + (uint32_t)p0 + (uint32_t)(total - after - ctot) + (uint32_t)(inc - c);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          if (p0 + j >= (int)cl) continue;
+          if (v[j] == X) {
+            base[o] = a;
+            base[o + 1] = b;
+            o += 2;
+          } else {
+            base[o] = v[j];
+            o += 1;
+          }
+        }
+        after += ctot;
+      }
+      tl += (uint32_t)total;
+      if (lane == 0) p.tile_len[tile] = tl;
     }
   }
-  if (blockIdx.x == 0) {  // tables left by an uncollected merge
+  if (blockIdx.x == 0) {  // tables left by a spilled chain
     __shared__ uint32_t s_n;
     if (threadIdx.x == 0) s_n = *p.dcount;
     __syncthreads();
@@ -1332,6 +1455,7 @@ Device::~Device() {
   (void)hipStreamSynchronize(S(aux_stream_));
   free_all();
   for (MergeSlot& s : slot_) free_slot(s, false);
+  if (host_ulist_) (void)hipHostFree(host_ulist_);
   delete static_cast<MergeParams*>(merge_params_);
   delete static_cast<UnmergeParams*>(unmerge_params_);
   for (auto e : ev_)
@@ -1374,11 +1498,12 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
   HIP_OK(hipStreamSynchronize(S(stream_)));
   for (MergeSlot& s : slot_) {
     if (s.host_mlist) HIP_OK(hipHostFree(s.host_mlist));
-    HIP_OK(hipHostMalloc((void**)&s.host_mlist, (ntiles_ + 1) * sizeof(uint32_t),
+    // one entry per (tile, chain merge) that matched
+    HIP_OK(hipHostMalloc((void**)&s.host_mlist, ((size_t)ntiles_ * kChainMax + 1) * sizeof(uint32_t),
                          hipHostMallocMapped | hipHostMallocCoherent));
     HIP_OK(hipHostGetDevicePointer(&s.dev_mlist, s.host_mlist, 0));
     if (s.dmlist) HIP_OK(hipFree(s.dmlist));
-    s.dmlist = dalloc<uint32_t>(ntiles_ + 1, &bytes_alloc_);
+    s.dmlist = dalloc<uint32_t>((size_t)ntiles_ * kChainMax + 1, &bytes_alloc_);
     // per-workgroup regions of the fused completion (k_merge)
     if (!s.rhdr) {
       s.rhdr = dalloc<uint32_t>((size_t)kMaxMergeGroups * kRegHdr, &bytes_alloc_);
@@ -1386,6 +1511,12 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
       s.rtile = dalloc<uint32_t>((size_t)kMaxMergeGroups * kMtLds, &bytes_alloc_);
     }
   }
+  if (host_ulist_) HIP_OK(hipHostFree(host_ulist_));
+  HIP_OK(hipHostMalloc((void**)&host_ulist_, (ntiles_ + 1) * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_OK(hipHostGetDevicePointer(&dev_ulist_, host_ulist_, 0));
+  run_count_ = 0;
+  run_head_ = 0;
+  unmerge_pending_ = false;
   // per-tile pair signatures (built by reset_tokens)
   sig_ = dalloc<uint32_t>(std::max<size_t>(ntiles_, 1) * kSigWords, &bytes_alloc_);
   index_.build(ts);
@@ -1432,10 +1563,11 @@ void Device::ensure_slots(MergeSlot& s, uint32_t need) {
   while (cap < need) cap *= 2;
   HIP_OK(hipStreamSynchronize(S(stream_)));
   HIP_OK(hipStreamSynchronize(S(aux_stream_)));
-  const size_t old_bytes = s.dsum ? 4 * ((size_t)s.cap + 1) * 20 + 16 + 64 : 0;  // as allocated below
+  const size_t old_bytes = s.dsum ? (size_t)kChainMax * 4 * ((size_t)s.cap + 1) * 20 + 16 + 64 : 0;
   free_slot(s, true);
   bytes_alloc_ -= old_bytes;
-  const size_t keys = 4 * ((size_t)cap + 1);
+  keys_per_merge_ = (uint32_t)(4 * ((size_t)cap + 1));
+  const size_t keys = (size_t)kChainMax * keys_per_merge_;  // one key range per chain merge
   s.dsum = dalloc<uint64_t>(keys + 2, &bytes_alloc_);  // + 2 stats words at the end
   s.dft = dalloc<uint64_t>(keys, &bytes_alloc_);
   s.dlist = dalloc<uint32_t>(keys, &bytes_alloc_);
@@ -1532,13 +1664,23 @@ void Device::flush_timing(bool block) {
   ev_pending_.resize(keep);
 }
 
-void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
+void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   HIP_OK(hipSetDevice(ordinal_));
-  MergeSlot& sl = slot_[X & 1];
-  if (sl.launched) fatal("merge_scan: the slot of this merge parity is still in flight");
-  max_id_seen_ = std::max(max_id_seen_, X);
-  ensure_slots(sl, (uint32_t)X + 1);
-  sl.X = X;
+  if (n < 1 || n > kChainMax || (exchange_ && n != 1)) fatal("merge_chain: bad chain length");
+  if (run_count_ >= 2) fatal("merge_chain: two launches are already in flight");
+  ChainRun& run = run_at(run_count_);
+  run.slot = (run_head_ + run_count_) & 1;
+  MergeSlot& sl = slot_[run.slot];
+  if (sl.launched) fatal("merge_chain: the slot is still in flight");
+  const int32_t Xn = X0 + n - 1;
+  max_id_seen_ = std::max(max_id_seen_, Xn);
+  ensure_slots(sl, (uint32_t)Xn + 1);
+  run.X0 = X0;
+  run.n = n;
+  run.collected = 0;
+  run.waited = false;
+  for (int i = 0; i < 2 * n; ++i) run.ab[i] = ab[i];
+  ++run_count_;
   if (!ntiles_) return;  // an empty shard still joins collect()'s exchange
   sl.seq = ++seq_;
   sl.launched = true;
@@ -1548,15 +1690,19 @@ void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
   mp.tile_len = tile_len_;
   mp.ntiles = (uint32_t)ntiles_;
   mp.weight = weight_;
-  mp.a = a;
-  mp.b = b;
-  mp.X = X;
+  mp.X0 = X0;
+  mp.nchain = n;
+  for (int i = 0; i < n; ++i) {
+    mp.ca[i] = ab[2 * i];
+    mp.cb[i] = ab[2 * i + 1];
+  }
+  mp.keys_per_merge = keys_per_merge_;
   mp.slot_cap = sl.cap;
   mp.dsum = U(sl.dsum);
   mp.dft = U(sl.dft);
   mp.dlist = sl.dlist;
   mp.dcount = sl.dcount;
-  mp.stats = U(sl.dsum) + 4 * ((size_t)sl.cap + 1);
+  mp.stats = U(sl.dsum) + (size_t)kChainMax * keys_per_merge_;
   mp.done = sl.dcount + 1;
   mp.fused = exchange_ ? 0 : 1;
   mp.out = (DeltaRecord*)sl.dev_recs;
@@ -1567,8 +1713,27 @@ void Device::merge_scan(int32_t a, int32_t b, int32_t X) {
   mp.mcount = sl.dcount + 10;
   mp.seq = sl.seq;
   mp.nlist = 0;
-  // tile skipping: visit only the tiles that can hold (a,b) when that list is short
-  if (skip_ && index_.candidates(a, b, &cand_) && cand_.size() <= kInlineTiles) {
+  // tile skipping: the union of the chain's candidate tiles when it is short
+  bool use_list = skip_;
+  cand_.clear();
+  if (n == 1) {
+    use_list = use_list && index_.candidates(ab[0], ab[1], &cand_) && cand_.size() <= kInlineTiles;
+  }
+  for (int i = 0; i < n && n > 1 && use_list; ++i) {
+    if (!index_.candidates(ab[2 * i], ab[2 * i + 1], &cand1_)) {
+      use_list = false;
+      break;
+    }
+    if (i == 0) {
+      cand_.swap(cand1_);
+    } else {
+      cand2_.clear();
+      std::set_union(cand_.begin(), cand_.end(), cand1_.begin(), cand1_.end(), std::back_inserter(cand2_));
+      cand_.swap(cand2_);
+    }
+    if (cand_.size() > kInlineTiles) use_list = false;
+  }
+  if (use_list && !cand_.empty()) {
     mp.nlist = (uint32_t)cand_.size();
     std::memcpy(mp.list, cand_.data(), cand_.size() * sizeof(uint32_t));
   }
@@ -1622,25 +1787,31 @@ void Device::wait_flag(const MergeSlot& s) {
   }
 }
 
-size_t Device::collect(int32_t X, const DeltaRecord** recs) {
-  HIP_OK(hipSetDevice(ordinal_));
-  MergeSlot& sl = slot_[X & 1];
-  if (sl.X != X) fatal("collect: merge X is not the one in its slot");
-  *recs = sl.host_recs;
-  if (!ntiles_ && !exchange_) return 0;
+// Waits for a run's launch and splits its records and matched tiles per merge.
+void Device::finish_launch(ChainRun& run_) {
+  MergeSlot& sl = slot_[run_.slot];
+  run_.waited = true;
+  for (int i = 0; i < run_.n; ++i) {
+    run_.rp[i] = nullptr;
+    run_.tp[i] = nullptr;
+    run_.rn[i] = run_.tn[i] = 0;
+  }
+  if (!ntiles_ && !exchange_) return;
   DeltaRecord* drec = (DeltaRecord*)sl.dev_recs;
   if (sl.launched) {
     wait_flag(sl);
-    index_.set_tiles(X, sl.host_mlist, sl.host_count[2]);
+    unmerge_pending_ = false;  // stream order: an earlier k_unmerge has finished
   }
+  const bool launched = sl.launched;
   sl.launched = false;
   const u64* hs = (const u64*)(sl.host_count + 4);
   size_t n;
-  u64* stats = U(sl.dsum) + 4 * ((size_t)sl.cap + 1);
+  u64* stats = U(sl.dsum) + (size_t)kChainMax * keys_per_merge_;
+  const uint32_t nm = launched ? sl.host_count[2] : 0;
   if (exchange_) {
     // multi-GPU: all-reduce the live prefix of the slot tables, then every rank scans it
     const uint32_t unk_slot = (unk_ >= 0 && (uint32_t)unk_ < sl.cap) ? (uint32_t)unk_ : 0u;
-    const size_t top = std::max<uint32_t>((uint32_t)X, unk_slot);
+    const size_t top = std::max<uint32_t>((uint32_t)run_.X0, unk_slot);
     const size_t nkeys = 4 * (std::min<size_t>(sl.cap, top + 1) + 1);
     exchange_(exchange_ctx_, sl.dsum, sl.dft, nkeys, stream_);
     HIP_OK(hipMemsetAsync(sl.dcount, 0, sizeof(uint32_t), S(stream_)));
@@ -1654,10 +1825,7 @@ size_t Device::collect(int32_t X, const DeltaRecord** recs) {
     n = sl.host_count[0];
   } else {
     n = sl.host_count[0];
-    if (n & kNeedCollect) {
-      // too many touched slots for one workgroup: a wide collect pass, on the side stream so
-      // it does not wait behind a speculative merge already queued on the main one (the flag
-      // says this merge's table updates are complete)
+    if (n & kNeedCollect) {  // too many spilled slots for one workgroup: a wide collect pass
       n &= ~kNeedCollect;
       k_collect<<<256, kThreads, 0, S(aux_stream_)>>>(sl.dcount, sl.dlist, U(sl.dsum), U(sl.dft),
                                                         drec + sl.host_count[3]);
@@ -1667,12 +1835,44 @@ size_t Device::collect(int32_t X, const DeltaRecord** recs) {
       HIP_OK(hipStreamSynchronize(S(aux_stream_)));
     }
   }
+  if (run_.n == 1) {  // one merge: its keys and tiles carry no chain index
+    run_.rp[0] = sl.host_recs;
+    run_.rn[0] = n;
+    run_.tp[0] = sl.host_mlist;
+    run_.tn[0] = nm;
+  } else {
+    // records carry chain index * keys_per_merge + key; tiles carry the index in their top bits
+    for (int i = 0; i < run_.n; ++i) {
+      run_.recs[i].clear();
+      run_.tiles[i].clear();
+    }
+    const DeltaRecord* r = sl.host_recs;
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t j = r[i].key / keys_per_merge_;
+      if (j >= (uint32_t)run_.n) fatal("k_merge record of a merge outside the chain");
+      DeltaRecord d = r[i];
+      d.key -= j * keys_per_merge_;
+      run_.recs[j].push_back(d);
+    }
+    for (uint32_t i = 0; i < nm; ++i) {
+      const uint32_t e = sl.host_mlist[i];
+      const uint32_t j = e >> kChainShift;
+      if (j >= (uint32_t)run_.n) fatal("k_merge matched tile of a merge outside the chain");
+      run_.tiles[j].push_back(e & ((1u << kChainShift) - 1u));
+    }
+    for (int i = 0; i < run_.n; ++i) {
+      run_.rp[i] = run_.recs[i].data();
+      run_.rn[i] = run_.recs[i].size();
+      run_.tp[i] = run_.tiles[i].data();
+      run_.tn[i] = run_.tiles[i].size();
+    }
+  }
   if (timing_) flush_timing(false);
-  live_tokens_est_ -= hs[0];
+  if (launched) live_tokens_est_ -= hs[0];
   records_total_ += n;
   records_max_ = std::max<uint64_t>(records_max_, n);
   if (merge_log_) {
-    std::fprintf(merge_log_, "C %u %d %u %u %d %llu %zu", sl.seq, X, sl.n_iter, sl.grid, 0,
+    std::fprintf(merge_log_, "C %u %d %u %u %d %llu %zu", sl.seq, run_.X0, sl.n_iter, sl.grid, run_.n,
                  (unsigned long long)hs[0], n);
 #ifdef SHRED_STAMPS
     // per phase: when the last workgroup got there, in us after the first workgroup started
@@ -1700,33 +1900,104 @@ size_t Device::collect(int32_t X, const DeltaRecord** recs) {
 #endif
     std::fprintf(merge_log_, "\n");
   }
+}
+
+size_t Device::collect(int32_t X, const DeltaRecord** recs) {
+  HIP_OK(hipSetDevice(ordinal_));
+  if (run_count_ == 0) fatal("collect: no launch in flight");
+  ChainRun& run = run_at(0);
+  const int j = X - run.X0;
+  if (j != run.collected || j >= run.n) fatal("collect: merge X is not the next merge of the oldest launch");
+  if (!run.waited) finish_launch(run);
+  index_.set_tiles(X, run.tp[j], run.tn[j]);
+  ++run.collected;
+  *recs = run.rp[j];
+  const size_t n = run.rn[j];
+  if (run.collected == run.n) {  // the oldest launch is consumed (its record vectors stay valid)
+    run_head_ = (run_head_ + 1) & 1;
+    --run_count_;
+  }
   return n;
 }
 
-void Device::rollback(int32_t a, int32_t b, int32_t X) {
+void Device::rollback(int32_t X) {
   HIP_OK(hipSetDevice(ordinal_));
-  MergeSlot& sl = slot_[X & 1];
-  if (sl.X != X) fatal("rollback: merge X is not the one in its slot");
   ++rollbacks_;
-  if (!sl.launched) return;
-  sl.launched = false;
-  if (merge_log_) std::fprintf(merge_log_, "R %u %d %u %u %d\n", sl.seq, X, sl.n_iter, sl.grid, 0);
-  // queued behind the merge on the same stream: the host never waits for a wrong guess
+  // every uncollected merge >= X, newest launch first
+  for (int k = run_count_ - 1; k >= 0; --k) {
+    ChainRun& run = run_at(k);
+    const int j0 = std::max(X - run.X0, run.collected);
+    if (j0 >= run.n) continue;
+    if (!run.waited && run.n == 1) {
+      // a single merge not waited for: k_unmerge reads its matched tiles and their count from
+      // the host memory the merge writes, queued behind it, so the host does not wait at all
+      unmerge_launch(run, nullptr, 0);
+      slot_[run.slot].launched = false;
+      run.waited = true;
+    } else {
+      if (!run.waited) finish_launch(run);
+      unmerge_run(run, j0);
+    }
+    run.n = j0;
+  }
+  while (run_count_ > 0 && run_at(run_count_ - 1).collected == run_at(run_count_ - 1).n) --run_count_;
+}
+
+// k_unmerge for merges j0 .. n-1 of a run (queued on the stream: the host never waits for it).
+void Device::unmerge_run(ChainRun& run_, int j0) {
+  const int nundo = run_.n - j0;
+  if (!ntiles_ || nundo <= 0) return;
+  // the tiles where any undone merge matched, once each (one merge lists each tile once)
+  ulist_.clear();
+  for (int j = j0; j < j0 + nundo; ++j) ulist_.insert(ulist_.end(), run_.tp[j], run_.tp[j] + run_.tn[j]);
+  if (nundo > 1) {
+    std::sort(ulist_.begin(), ulist_.end());
+    ulist_.erase(std::unique(ulist_.begin(), ulist_.end()), ulist_.end());
+  }
+  MergeSlot& sl = slot_[run_.slot];
+  if (merge_log_) std::fprintf(merge_log_, "R %u %d %zu %d\n", sl.seq, run_.X0 + j0, ulist_.size(), nundo);
+  if (ulist_.empty()) return;
+  // the previous k_unmerge may still read the list: it is ordered before this one on the
+  // stream, but the host overwrites the pinned list now, so wait for it first
+  if (unmerge_pending_) HIP_OK(hipStreamSynchronize(S(stream_)));
+  std::memcpy(host_ulist_, ulist_.data(), ulist_.size() * sizeof(uint32_t));
+  unmerge_pending_ = true;
+  unmerge_launch(run_, host_ulist_, ulist_.size(), j0);
+}
+
+// Queues k_unmerge for merges j0 .. n-1 of a run over `tiles` (host-visible, n_tiles of them),
+// or, with tiles == nullptr, over the single merge's own matched-tile list in host memory.
+void Device::unmerge_launch(ChainRun& run_, const uint32_t* tiles, size_t n_tiles, int j0) {
+  const int nundo = run_.n - j0;
+  MergeSlot& sl = slot_[run_.slot];
   UnmergeParams& up = *static_cast<UnmergeParams*>(unmerge_params_);
   up.tok = tok_;
   up.tile_off = tile_off_;
   up.tile_len = tile_len_;
-  up.mlist = (const uint32_t*)sl.dev_mlist;  // host-mapped list the merge's last workgroup wrote
-  up.mcount = (const uint32_t*)sl.dev_count + 2;
-  up.a = a;
-  up.b = b;
-  up.X = X;
+  if (tiles) {
+    void* d = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&d, const_cast<uint32_t*>(tiles), 0));
+    up.tiles = (const uint32_t*)d;
+    up.ntl = (uint32_t)n_tiles;
+    up.ntl_dev = nullptr;
+  } else {
+    up.tiles = (const uint32_t*)sl.dev_mlist;
+    up.ntl = 0;
+    up.ntl_dev = (const uint32_t*)sl.dev_count + 2;
+  }
+  up.nundo = nundo;
+  up.ux0 = run_.X0 + j0;
+  for (int j = 0; j < nundo; ++j) {
+    up.ua[j] = run_.ab[2 * (j0 + j)];
+    up.ub[j] = run_.ab[2 * (j0 + j) + 1];
+  }
   up.dcount = sl.dcount;
   up.dlist = sl.dlist;
   up.dsum = U(sl.dsum);
   up.dft = U(sl.dft);
   up.sig = sig_;
-  const int grid = kMaxMergeGroups;
+  const int grid = tiles ? (int)std::min<size_t>((n_tiles + kWaves - 1) / kWaves, (size_t)kMaxMergeGroups)
+                         : kMaxMergeGroups;
   k_unmerge<<<grid, kThreads, 0, S(stream_)>>>(up);
   HIP_OK(hipGetLastError());
 }

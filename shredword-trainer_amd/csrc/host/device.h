@@ -56,23 +56,24 @@ class Device : public Backend {
   // under RCCL the per-rank lists are merged (sum, min first touch).
   void count_pairs(int32_t unk_id, std::vector<PairCount>* out) override;
 
-  // K2+K3 for merge (a,b)->X: rewrites every occurrence in place and reduces neighbour deltas
-  // into the slot tables.  Two merges may be in flight (X and X+1, speculation): each parity of
-  // X owns its own tables, host-visible records, flag and matched-tile list.
-  void merge_scan(int32_t a, int32_t b, int32_t X) override;
-  // Multi-GPU hook: called between merge_scan and collect(); slot tables are
+  // K2+K3 for a chain of merges (ab[2i], ab[2i+1]) -> X0 + i: one k_merge launch applies them in
+  // order per tile and reduces each merge's neighbour deltas separately.
+  void merge_chain(const int32_t* ab, int n, int32_t X0) override;
+  // Multi-GPU hook: called between merge_chain and collect(); slot tables are
   // [prefix_slots * 4] u64 sums followed by the same count of u64 first-touch values.
   using ExchangeFn = void (*)(void* ctx, uint64_t* dsum, uint64_t* dft, size_t n, void* stream);
   void set_exchange(ExchangeFn fn, void* ctx) { exchange_ = fn; exchange_ctx_ = ctx; }
-  // K4: the touched slots as records (host-visible), cleared for the next merge.
+  // K4: merge X's records (host memory); the first collect of a chain waits for the launch.
   size_t collect(int32_t X, const DeltaRecord** recs) override;
-  // Speculation (single GPU only): undo the outstanding merge X with k_unmerge, host-free.
-  bool can_speculate() const override { return speculate_ && !exchange_; }
-  void rollback(int32_t a, int32_t b, int32_t X) override;
+  static constexpr int kChainMax = 8;
+  int max_chain() const override { return speculate_ && !exchange_ ? kChainMax : 1; }
+  bool can_overlap() const override { return speculate_ && !exchange_; }
+  // Undoes the chain's uncollected merges >= X with k_unmerge (newest first), host-free.
+  void rollback(int32_t X) override;
   void set_speculation(bool on) { speculate_ = on; }
+  uint64_t rollbacks() const { return rollbacks_; }
   // Tuning: k_merge grid cap.
   void set_merge_groups(int groups);
-  uint64_t rollbacks() const { return rollbacks_; }
 
   // K6: final weighted token histogram over ids [0, T); other ids are dropped.
   void token_freq(size_t T, std::vector<uint64_t>* freq) override;
@@ -101,33 +102,53 @@ class Device : public Backend {
   void* stream_handle() const { return stream_; }
 
  private:
-  // Resources of one in-flight merge (X & 1 selects the slot).
+  // Device tables and host-visible buffers of a merge launch.
   struct MergeSlot {
     uint32_t cap = 0;  // neighbour slots: id+1 for ids < cap, slot 0 for unk outside
-    uint64_t* dsum = nullptr;  // 4 * (cap + 1) keys + 2 stats words
+    uint64_t* dsum = nullptr;  // kChainMax x 4 (cap + 1) keys + 2 stats words
     uint64_t* dft = nullptr;
     uint32_t* dlist = nullptr;
     uint32_t* dcount = nullptr;  // [0] touched-slot count, [1..9] completion tickets, [10] matched tiles
     DeltaRecord* host_recs = nullptr;  // pinned, device-visible
     void* dev_recs = nullptr;
     uint32_t* host_count = nullptr;    // pinned: [0] records (| need-collect), [1] flag, [2] matched tiles,
-    void* dev_count = nullptr;         //         bytes 16..31: occurrences merged, tokens rewritten
-    uint32_t* dmlist = nullptr;        // device: tiles where the merge matched (overflow / multi-GPU)
+    void* dev_count = nullptr;         //         [3] k_collect offset, bytes 16..31: occurrences, tokens
+    uint32_t* dmlist = nullptr;        // device: matched tiles beyond a workgroup's LDS list / multi-GPU
     uint32_t* rhdr = nullptr;          // device: per-workgroup regions of the fused completion
     uint64_t* rrec = nullptr;
     uint32_t* rtile = nullptr;
-    uint32_t* host_mlist = nullptr;    // pinned copy, written by the merge's last workgroup
+    uint32_t* host_mlist = nullptr;    // pinned: matched tiles (tile | chain index << 27)
     void* dev_mlist = nullptr;
     uint32_t grid = 0;
     uint32_t n_iter = 0;  // candidate tiles of the launch
     bool launched = false;
     uint32_t seq = 0;
-    int32_t X = -1;
+  };
+  // A launch: merges X0 .. X0+n-1, collected in order.  Up to two runs are in flight (the
+  // second launched before the first is collected); run r uses slot_[r's slot].
+  struct ChainRun {
+    int slot = 0;
+    int32_t X0 = 0;
+    int n = 0;
+    int collected = 0;
+    bool waited = false;
+    int32_t ab[2 * kChainMax] = {};
+    // merge j's records and matched tiles: straight in the slot's pinned buffers for a single
+    // merge, else split into the vectors below
+    const DeltaRecord* rp[kChainMax] = {};
+    size_t rn[kChainMax] = {};
+    const uint32_t* tp[kChainMax] = {};
+    size_t tn[kChainMax] = {};
+    std::vector<DeltaRecord> recs[kChainMax];
+    std::vector<uint32_t> tiles[kChainMax];
   };
   void ensure_slots(MergeSlot& s, uint32_t need);
   void free_slot(MergeSlot& s, bool keep_host);
   void free_all();
   void wait_flag(const MergeSlot& s);
+  void finish_launch(ChainRun& run);
+  void unmerge_run(ChainRun& run, int j0);
+  void unmerge_launch(ChainRun& run, const uint32_t* tiles, size_t n_tiles, int j0 = 0);
   void flush_timing(bool block);
 
   int ordinal_ = 0;
@@ -166,6 +187,14 @@ class Device : public Backend {
   uint64_t live_tokens_est_ = 0;
 
   MergeSlot slot_[2];
+  ChainRun runs_[2];
+  int run_head_ = 0, run_count_ = 0;  // runs_[run_head_] is the oldest in flight
+  ChainRun& run_at(int k) { return runs_[(run_head_ + k) & 1]; }
+  uint32_t keys_per_merge_ = 0;
+  uint32_t* host_ulist_ = nullptr;  // pinned: tiles to unmerge
+  void* dev_ulist_ = nullptr;
+  std::vector<uint32_t> ulist_;
+  bool unmerge_pending_ = false;  // a k_unmerge reading host_ulist_ may still run
   uint32_t seq_ = 0;            // launch sequence number echoed by the device flag
   int32_t unk_ = 0;
   uint64_t records_total_ = 0, records_max_ = 0;
@@ -179,7 +208,7 @@ class Device : public Backend {
   FILE* merge_log_ = nullptr;           // SHREDWORD_MERGE_LOG diagnostic
   TileIndex index_;                     // tile skipping (tiles.h)
   bool skip_ = true;
-  std::vector<uint32_t> cand_;
+  std::vector<uint32_t> cand_, cand1_, cand2_;
   uint64_t visited_tiles_ = 0;
   int merge_blocks_per_cu_ = 4;
 

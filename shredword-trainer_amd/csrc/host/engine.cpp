@@ -1,6 +1,7 @@
 // BPE training driver: see engine.h.
 #include "engine.h"
 
+#include <algorithm>
 #include <string>
 
 #include "common.h"
@@ -31,14 +32,14 @@ void Engine::count_bigrams(Backend& be) {
 }
 
 void Engine::finish_speculation(Backend& be) {
-  if (!spec_active_) return;
-  be.rollback(spec_a_, spec_b_, spec_x_);
-  spec_active_ = false;
+  if (pending_.empty()) return;
+  be.rollback(pending_.front().X);
+  pending_.clear();
   ++spec_misses_;
 }
 
 // One merge (bpe.cpp:244-318): false when the heap holds no valid candidate.  `remaining` = how
-// many more merges the caller may still ask for (no speculation past the last one).
+// many more merges the caller may still ask for (no guess runs past them).
 bool Engine::merge_one(Backend& be, int remaining) {
   int32_t a, b;
   uint64_t freq;
@@ -57,23 +58,40 @@ bool Engine::merge_one(Backend& be, int remaining) {
   if (trace_) std::fprintf(trace_, "M %d %d %llu %d\n", a, b, (unsigned long long)freq, X);
   merge_a_.push_back(a);
   merge_b_.push_back(b);
+  if (probe_k_) {
+    std::vector<int32_t> c(2 * probe_k_);
+    c.resize(2 * sel_.predict_chain(a, b, probe_window_, probe_k_, c.data()));
+    chain_log_.push_back(std::move(c));
+  }
   bool launched = false;
-  if (spec_active_) {  // the guess made one merge ago
-    spec_active_ = false;
-    if (spec_a_ == a && spec_b_ == b && spec_x_ == X) {
+  if (!pending_.empty()) {  // the oldest unconfirmed guess
+    const Guess& g = pending_.front();
+    if (g.X == X && g.a == a && g.b == b) {
       launched = true;
+      pending_.erase(pending_.begin());
       ++spec_hits_;
     } else {
-      be.rollback(spec_a_, spec_b_, spec_x_);
-      ++spec_misses_;
+      finish_speculation(be);
     }
   }
-  if (!launched) be.merge_scan(a, b, X);
-  if (speculate_ && remaining > 1 && be.can_speculate() &&
-      sel_.predict_next(a, b, pred_window_, &spec_a_, &spec_b_)) {
-    spec_x_ = X + 1;
-    spec_active_ = true;
-    be.merge_scan(spec_a_, spec_b_, spec_x_);
+  const int chain = speculate_ ? std::max(1, std::min(std::min(chain_max_, be.max_chain()), remaining)) : 1;
+  if (!launched) {
+    chain_ab_.assign(2 * (size_t)chain, 0);
+    chain_ab_[0] = a;
+    chain_ab_[1] = b;
+    const int n = 1 + (chain > 1 ? (int)sel_.predict_chain(a, b, chain_window_, (size_t)chain - 1, chain_ab_.data() + 2) : 0);
+    for (int i = 1; i < n; ++i) pending_.push_back({chain_ab_[2 * i], chain_ab_[2 * i + 1], X + i});
+    ++launches_;
+    be.merge_chain(chain_ab_.data(), n, X);
+  }
+  // overlap: the next merge's guess runs while this one is consumed
+  if (speculate_ && chain == 1 && pending_.empty() && remaining > 1 && be.can_overlap()) {
+    Guess g{0, 0, X + 1};
+    if (sel_.predict_next(a, b, pred_window_, &g.a, &g.b)) {
+      pending_.push_back(g);
+      ++launches_;
+      be.merge_scan(g.a, g.b, g.X);
+    }
   }
   const double t2 = now_seconds();
   const DeltaRecord* recs = nullptr;

@@ -18,14 +18,22 @@ class Backend {
   virtual ~Backend() = default;
   // K1: pair histogram with first touch over every rank's share, pairs holding unk skipped.
   virtual void count_pairs(int32_t unk_id, std::vector<PairCount>* out) = 0;
-  // K2+K3: merge (a,b) -> X everywhere; K4: the merge's neighbour-delta records (all ranks).
-  virtual void merge_scan(int32_t a, int32_t b, int32_t X) = 0;
+  // K2+K3: applies the merges (ab[2i], ab[2i+1]) -> X0 + i for i < n, in order, as one device
+  // pass; K4: collect(X) then returns each merge's neighbour-delta records (all ranks), in order.
+  virtual void merge_chain(const int32_t* ab, int n, int32_t X0) = 0;
+  void merge_scan(int32_t a, int32_t b, int32_t X) {
+    const int32_t ab[2] = {a, b};
+    merge_chain(ab, 1, X);
+  }
   virtual size_t collect(int32_t X, const DeltaRecord** recs) = 0;
-  // Speculation support: a backend that can keep two merges in flight (merge_scan may be called
-  // for X+1 before collect(X)) and can exactly undo the oldest outstanding merge X (which must
-  // be the only one in flight) — rollback expands every X back into (a, b).
-  virtual bool can_speculate() const { return false; }
-  virtual void rollback(int32_t a, int32_t b, int32_t X) {}
+  // Longest chain the backend runs (1: one merge per pass, e.g. under a multi-GPU exchange).
+  virtual int max_chain() const { return 1; }
+  // True when a second launch may be issued before the first is collected (its merges run
+  // after the first launch's on the device).
+  virtual bool can_overlap() const { return false; }
+  // Undoes every launched merge with id >= X that was not collected, newest first (each
+  // expands its X back into (a, b)), so the corpus is exactly as before those merges.
+  virtual void rollback(int32_t X) {}
   // K6: final weighted token histogram over ids [0, T) (all ranks).
   virtual void token_freq(size_t T, std::vector<uint64_t>* freq) = 0;
 };
@@ -55,12 +63,24 @@ class Engine {
   int32_t merge_second(size_t m) const { return merge_b_[m]; }
   const Selector& selector() const { return sel_; }
   EngineTimes& times() { return times_; }
-  // Speculative pipelining: while the host applies merge m's deltas and replays the heap, the
-  // backend already runs the predicted merge m+1; a wrong guess is rolled back exactly.
+  // Speculation, in one of two modes (results are identical either way):
+  //  * overlap (default): while the host consumes merge m, the backend already runs a second
+  //    launch with the merge guessed to come next (Selector::predict_next);
+  //  * chain (set_chain(n > 1)): the selected merge and up to n-1 guessed successors
+  //    (Selector::predict_chain) run in one launch.
+  // Guesses are confirmed one by one by the exact selection; a wrong tail is rolled back.
+  void set_chain(int max_len, size_t window) {
+    chain_max_ = max_len < 1 ? 1 : max_len;
+    chain_window_ = window;
+  }
   void set_speculation(bool on) { speculate_ = on; }
-  void finish_speculation(Backend& be);  // rolls back a pending guess (before any other access)
+  void finish_speculation(Backend& be);  // rolls back unconfirmed guesses (before any other access)
   uint64_t spec_hits() const { return spec_hits_; }
   uint64_t spec_misses() const { return spec_misses_; }
+  uint64_t launches() const { return launches_; }
+  // Diagnostic: record a predicted chain of k merges after every selection.
+  void set_chain_probe(size_t k, size_t window) { probe_k_ = k; probe_window_ = window; }
+  const std::vector<std::vector<int32_t>>& chain_log() const { return chain_log_; }
 
  private:
   bool merge_one(Backend& be, int remaining);
@@ -74,10 +94,17 @@ class Engine {
   std::vector<int32_t> merge_a_, merge_b_;
   EngineTimes times_;
   bool speculate_ = true;
+  int chain_max_ = 1;
+  size_t chain_window_ = 2048;
   size_t pred_window_ = 256;
-  bool spec_active_ = false;
-  int32_t spec_a_ = 0, spec_b_ = 0, spec_x_ = 0;
-  uint64_t spec_hits_ = 0, spec_misses_ = 0;
+  struct Guess {
+    int32_t a, b, X;
+  };
+  std::vector<Guess> pending_;  // launched guesses awaiting confirmation, oldest first
+  std::vector<int32_t> chain_ab_;
+  uint64_t spec_hits_ = 0, spec_misses_ = 0, launches_ = 0;
+  size_t probe_k_ = 0, probe_window_ = 256;
+  std::vector<std::vector<int32_t>> chain_log_;
 };
 
 }  // namespace shred

@@ -156,6 +156,34 @@ bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, in
   return true;
 }
 
+size_t Selector::predict_chain(int32_t a, int32_t b, size_t window, size_t k, int32_t* out) const {
+  const size_t n = std::min(window, heap_.size());
+  std::vector<std::pair<uint64_t, size_t>> cand;  // (freq, heap slot) of the valid entries
+  for (size_t i = 0; i < n; ++i) {
+    const HeapEnt& e = heap_[i];
+    if (e.freq < min_freq_ || e.a == unk_ || e.b == unk_) continue;
+    const Info* in = find(pack_pair(e.a, e.b));
+    if (!in || in->version != e.version || in->freq != e.freq) continue;
+    cand.push_back({e.freq, i});
+  }
+  std::stable_sort(cand.begin(), cand.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+  std::vector<int32_t> used = {a, b};
+  size_t m = 0;
+  for (const auto& c : cand) {
+    if (m == k) break;
+    const HeapEnt& e = heap_[c.second];
+    bool clash = false;
+    for (int32_t u : used) clash |= e.a == u || e.b == u;
+    if (clash) continue;
+    out[2 * m] = e.a;
+    out[2 * m + 1] = e.b;
+    used.push_back(e.a);
+    used.push_back(e.b);
+    ++m;
+  }
+  return m;
+}
+
 bool Selector::select(int32_t* a, int32_t* b, uint64_t* freq) {
   while (!heap_.empty()) {
     HeapEnt top = pop();

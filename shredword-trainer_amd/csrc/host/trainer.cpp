@@ -69,6 +69,8 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
   } else if (key == "merge_groups") {
     if (!t->dev) return -1;  // tuning of an existing device (after load_corpus)
     t->dev->set_merge_groups(std::atoi(val.c_str()));
+  } else if (key == "chain") {
+    t->engine.set_chain(std::atoi(val.c_str()), 2048);
   } else if (key == "speculate") {
     t->engine.set_speculation(std::atoi(val.c_str()) != 0);
   } else if (key == "device") {
@@ -140,6 +142,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   if (const char* v = std::getenv("SHREDWORD_LAYOUT")) set_option(t, "layout", v);
   if (const char* v = std::getenv("SHREDWORD_TRACE")) set_option(t, "trace", v);
   t->engine.set_speculation(env_int("SHREDWORD_SPECULATE", 1) != 0);
+  if (const char* v = std::getenv("SHREDWORD_CHAIN")) set_option(t, "chain", v);
   if (t->engine.log() >= 1) std::printf("[INFO]\t BPE trainer initialized. Heap initialized successfully.\n");
   return t;
 }
@@ -253,7 +256,7 @@ int shred_probe_rollback(Trainer* t, int32_t a, int32_t b) {
   if (!t || !ensure_device(t, "shred_probe_rollback")) return -1;
   const int32_t X = kBaseVocab + (int32_t)t->engine.num_merges();
   t->dev->merge_scan(a, b, X);
-  t->dev->rollback(a, b, X);
+  t->dev->rollback(X);
   return 0;
 }
 

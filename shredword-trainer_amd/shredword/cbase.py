@@ -94,8 +94,9 @@ lib.loadVocab.argtypes, lib.loadVocab.restype = [c_void_p, c_char_p], c_bool
 lib.shred_set_option.argtypes, lib.shred_set_option.restype = [Trainer, c_char_p, c_char_p], c_int
 lib.shred_reset.argtypes, lib.shred_reset.restype = [Trainer], c_int
 lib.shred_probe_merge.argtypes, lib.shred_probe_merge.restype = [Trainer, c_int32, c_int32, c_int], c_double
-lib.shred_probe_rollback.argtypes, lib.shred_probe_rollback.restype = [Trainer, c_int32, c_int32], c_int
-lib.shred_debug_tokens.argtypes, lib.shred_debug_tokens.restype = [Trainer, POINTER(c_int32), c_size_t], c_int64
+if hasattr(lib, "shred_probe_rollback"):  # diagnostics (absent from older builds)
+    lib.shred_probe_rollback.argtypes, lib.shred_probe_rollback.restype = [Trainer, c_int32, c_int32], c_int
+    lib.shred_debug_tokens.argtypes, lib.shred_debug_tokens.restype = [Trainer, POINTER(c_int32), c_size_t], c_int64
 lib.shred_get_stats.argtypes, lib.shred_get_stats.restype = [Trainer, POINTER(ShredStats)], c_int
 lib.shred_device_count.argtypes, lib.shred_device_count.restype = [], c_int
 lib.shred_dist_unique_id.argtypes, lib.shred_dist_unique_id.restype = [c_void_p, c_size_t], c_int

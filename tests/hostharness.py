@@ -32,6 +32,8 @@ def load():
     lib.hh_visit_hist.restype = ctypes.c_uint64
     lib.hh_match_hist.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64]
     lib.hh_match_hist.restype = ctypes.c_uint64
+    lib.hh_chain_probe.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    lib.hh_chain_hist.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     lib.hh_spec.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     lib.hh_word.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                             ctypes.POINTER(ctypes.c_uint64)]

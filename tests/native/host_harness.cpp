@@ -39,7 +39,8 @@ class EmuBackend : public Backend {
   }
   void set_exchange(ExchangeCb cb, void* ctx) { cb_ = cb; ctx_ = ctx; }
   void set_speculation(bool on) { spec_ = on; }
-  bool can_speculate() const override { return spec_ && !cb_; }
+  int max_chain() const override { return spec_ && !cb_ ? 64 : 1; }
+  bool can_overlap() const override { return spec_ && !cb_; }
 
   uint64_t weight(uint32_t rank) const { return layout_ == Layout::kTypes ? wt_.count[rank] : 1; }
 
@@ -74,7 +75,11 @@ class EmuBackend : public Backend {
   }
   uint32_t slot(int32_t id) const { return (uint32_t)id < cap_ ? (uint32_t)id + 1 : 0; }
 
-  void merge_scan(int32_t a, int32_t b, int32_t X) override {
+  void merge_chain(const int32_t* ab, int n, int32_t X0) override {
+    for (int i = 0; i < n; ++i) merge_one(ab[2 * i], ab[2 * i + 1], X0 + i);
+  }
+
+  void merge_one(int32_t a, int32_t b, int32_t X) {
     if ((uint32_t)X >= cap_) fatal("emulated slot capacity exceeded");
     std::vector<int32_t> out;
     std::vector<uint32_t> cand, matched;
@@ -153,25 +158,28 @@ class EmuBackend : public Backend {
     }
   }
 
-  void rollback(int32_t a, int32_t b, int32_t X) override {
-    if (queue_.empty() || queue_.front().X != X) fatal("emulated rollback of a merge that is not outstanding");
-    std::vector<int32_t> out;
-    for (uint32_t t : queue_.front().matched) {  // the exact inverse of the merge: X -> a b
-      int32_t* p = ts_.tok.data() + ts_.off[t];
-      out.clear();
-      for (uint32_t i = 0; i < ts_.len[t]; ++i) {
-        if (p[i] == X) {
-          out.push_back(a);
-          out.push_back(b);
-        } else {
-          out.push_back(p[i]);
+  void rollback(int32_t X) override {
+    while (!queue_.empty() && queue_.back().X >= X) {  // newest first
+      const Pending& pd = queue_.back();
+      std::vector<int32_t> out;
+      for (uint32_t t : pd.matched) {  // the exact inverse of the merge: X -> a b
+        int32_t* p = ts_.tok.data() + ts_.off[t];
+        out.clear();
+        for (uint32_t i = 0; i < ts_.len[t]; ++i) {
+          if (p[i] == pd.X) {
+            out.push_back(pd.a);
+            out.push_back(pd.b);
+          } else {
+            out.push_back(p[i]);
+          }
         }
+        std::memcpy(p, out.data(), out.size() * sizeof(int32_t));
+        ts_.len[t] = (uint32_t)out.size();
       }
-      std::memcpy(p, out.data(), out.size() * sizeof(int32_t));
-      ts_.len[t] = (uint32_t)out.size();
+      queue_.pop_back();
+      ++rollbacks_;
     }
-    queue_.erase(queue_.begin());
-    ++rollbacks_;
+    if (!queue_.empty() && queue_.front().X >= X) fatal("emulated rollback out of order");
   }
   uint64_t rollbacks_ = 0;
   uint64_t visited() const { return visited_; }
@@ -228,7 +236,7 @@ class EmuBackend : public Backend {
     std::vector<uint32_t> matched;
     std::vector<DeltaRecord> recs;
   };
-  std::vector<Pending> queue_;  // merges launched but not collected (at most 2)
+  std::vector<Pending> queue_;  // merges launched but not collected, oldest first
   bool spec_ = true;
   ExchangeCb cb_ = nullptr;
   void* ctx_ = nullptr;
@@ -325,6 +333,23 @@ void hh_counters(void* p, uint64_t* out) {
   const auto& c = ((Harness*)p)->engine.selector().counters();
   out[0] = c.pops; out[1] = c.stale; out[2] = c.pushes; out[3] = c.records; out[4] = c.changes;
   out[5] = ((Harness*)p)->engine.selector().num_pairs();
+}
+// Chain prediction acceptance: hist[j] = selections whose predicted chain matched exactly the
+// next j merges (j = 0..k).
+void hh_chain_probe(void* p, int k, int window) { ((Harness*)p)->engine.set_chain_probe((size_t)k, (size_t)window); }
+void hh_chain_hist(void* p, uint64_t* hist, int k) {
+  Harness* h = (Harness*)p;
+  const auto& log = h->engine.chain_log();
+  const size_t M = h->engine.num_merges();
+  for (int j = 0; j <= k; ++j) hist[j] = 0;
+  for (size_t i = 0; i < log.size() && i < M; ++i) {
+    int m = 0;
+    for (size_t j = 0; 2 * j < log[i].size() && i + 1 + j < M; ++j) {
+      if (log[i][2 * j] != h->engine.merge_first(i + 1 + j) || log[i][2 * j + 1] != h->engine.merge_second(i + 1 + j)) break;
+      ++m;
+    }
+    hist[m]++;
+  }
 }
 void hh_spec(void* p, int on, uint64_t* out) {
   Harness* h = (Harness*)p;
