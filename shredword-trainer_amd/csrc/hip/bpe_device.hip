@@ -27,6 +27,7 @@
 #endif
 
 #include <algorithm>
+#include <type_traits>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -1294,6 +1295,136 @@ __global__ __launch_bounds__(kThreads) void k_pair_collect(const u64* tkey, cons
 }
 
 // ------------------------------------------------------------------------------------------
+// K1 when every id is a byte (the initial count: ids < 256, unk skipped): a dense 256 x 256
+// table.  One wave per tile (16 tokens per lane, DPP header scan), 512-thread workgroups for
+// memory-level parallelism, a 4096-slot LDS pair hash per workgroup (first touch updated only
+// when smaller), spills and the final flush go straight to the dense HBM table (no probing).
+constexpr int kDenseThreads = 512;
+constexpr int kDenseWaves = kDenseThreads / 64;
+constexpr int kDenseLds = 4096;
+constexpr uint32_t kDensePairs = 256u * 256u;
+
+struct DenseCountParams {
+  const int32_t* tok;
+  const uint64_t* tile_off;
+  const uint32_t* tile_len;
+  uint32_t ntiles;
+  const uint64_t* weight;
+  int32_t unk;
+  u64* cnt;  // kDensePairs, zeroed
+  u64* ft;   // kDensePairs, all ones
+};
+
+// Counts are u64 for weighted (types) tiles and u32 for unweighted (stream) ones: a workgroup
+// never sees 2^32 occurrences, and 32-bit LDS atomics are the cheaper ones.
+template <class C>
+struct DenseLds {
+  uint32_t key[kDenseLds];
+  C cnt[kDenseLds];
+  u64 ft[kDenseLds];
+};
+
+template <class C>
+__device__ __forceinline__ void dense_emit(DenseLds<C>& h, const DenseCountParams& p, uint32_t key, C w, u64 ft) {
+  uint32_t s = (key * 2654435761u) >> (32 - 12);
+  for (int probe = 0; probe < 8; ++probe) {
+    uint32_t k = h.key[s];
+    if (k == kEmpty32) {
+      k = atomicCAS(&h.key[s], kEmpty32, key);
+      if (k == kEmpty32) k = key;
+    }
+    if (k == key) {
+      atomicAdd(&h.cnt[s], w);
+      if (ft < h.ft[s]) atomicMin(&h.ft[s], ft);
+      return;
+    }
+    s = (s + 1) & (kDenseLds - 1);
+  }
+  atomicAdd(&p.cnt[key], (u64)w);
+  atomicMin(&p.ft[key], ft);
+}
+
+template <bool kWeighted>
+__global__ __launch_bounds__(kDenseThreads) void k_pair_dense(DenseCountParams p) {
+  typedef typename std::conditional<kWeighted, u64, uint32_t>::type C;
+  __shared__ DenseLds<C> h;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int p0 = lane * kPer;
+  for (int i = threadIdx.x; i < kDenseLds; i += kDenseThreads) {
+    h.key[i] = kEmpty32;
+    h.cnt[i] = 0;
+    h.ft[i] = kEmpty64;
+  }
+  __syncthreads();
+  for (uint32_t t = blockIdx.x * kDenseWaves + wid; t < p.ntiles; t += gridDim.x * kDenseWaves) {
+    const uint32_t len = p.tile_len[t];
+    const int32_t* base = p.tok + p.tile_off[t];
+    u64 c_hdr = 0;  // ((index + 1) << 32) | rank of the last header so far
+    for (uint32_t cs = 0; cs < len; cs += kWaveTok) {
+      const uint32_t cl = min((uint32_t)kWaveTok, len - cs);
+      int32_t v[kPer];
+      load_chunk(base, cs, cl, p0, v);
+      const int32_t nx = next_token(base, cs, len, p0, v[0]);
+      uint32_t hmask = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (is_hdr(v[j]) && p0 + j < (int)cl) hmask |= 1u << j;
+      u64 hl = 0;
+      if (hmask) {
+        const int j = 31 - __clz(hmask);
+        hl = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(v[j]);
+      }
+      const u64 hinc = wave_scan_max64(hl);
+      u64 hdr = wave_prev64(hinc);
+      hdr = hdr > c_hdr ? hdr : c_hdr;
+      uint32_t w_rank = ~0u;
+      C w = 1;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int32_t x = v[j];
+        const int32_t y = j + 1 < kPer ? v[j + 1] : nx;
+        if (is_hdr(x)) {
+          hdr = ((u64)(cs + p0 + j + 1) << 32) | hdr_rank(x);
+          continue;
+        }
+        if (is_hdr(y) || x == p.unk || y == p.unk) continue;
+        const uint32_t hidx = (uint32_t)(hdr >> 32) - 1u;
+        const uint32_t rank = (uint32_t)hdr;
+        if (kWeighted && rank != w_rank) {
+          w = (C)p.weight[rank];
+          w_rank = rank;
+        }
+        const uint32_t key = ((uint32_t)x << 8) | (uint32_t)y;
+        dense_emit(h, p, key, w, ((u64)rank << 32) | (u64)(cs + p0 + j - hidx - 1u));
+      }
+      const u64 htot = lane_read64(hinc, 63);
+      c_hdr = htot > c_hdr ? htot : c_hdr;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kDenseLds; i += kDenseThreads) {
+    const uint32_t k = h.key[i];
+    if (k == kEmpty32) continue;
+    atomicAdd(&p.cnt[k], (u64)h.cnt[i]);
+    atomicMin(&p.ft[k], h.ft[i]);
+  }
+}
+
+// Dense table -> PairCount list (pairs with a count).
+__global__ __launch_bounds__(kThreads) void k_pair_dense_collect(const u64* cnt, const u64* ft, PairCount* out,
+                                                                  uint32_t* n) {
+  for (uint32_t k = blockIdx.x * kThreads + threadIdx.x; k < kDensePairs; k += gridDim.x * kThreads) {
+    if (ft[k] == kEmpty64) continue;
+    PairCount pc;
+    pc.a = (int32_t)(k >> 8);
+    pc.b = (int32_t)(k & 255u);
+    pc.count = cnt[k];
+    pc.ft = ft[k];
+    out[atomicAdd(n, 1u)] = pc;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // K6: final token histogram over ids [0, T) (the unk count lands on unk_id when it is in range)
 template <bool kWeighted>
 __global__ __launch_bounds__(kThreads) void k_token_freq(const int32_t* tok, const uint64_t* tile_off,
@@ -1521,6 +1652,7 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
   sig_ = dalloc<uint32_t>(std::max<size_t>(ntiles_, 1) * kSigWords, &bytes_alloc_);
   index_.build(ts);
   max_id_seen_ = max_id;
+  max_id0_ = max_id;
   uploaded_ = true;
   reset_tokens();
 }
@@ -1538,6 +1670,7 @@ void Device::reset_tokens() {
     HIP_OK(hipGetLastError());
   }
   live_tokens_est_ = live_tokens0_;
+  max_id_seen_ = max_id0_;
   index_.reset();
 }
 
@@ -1591,8 +1724,13 @@ void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
     dist_merge_pairs(out);
     return;
   }
-  // distinct pairs <= live tokens and <= (ids in play)^2
   const uint64_t live = live_tokens();
+  if (max_id_seen_ < kBaseVocab) {  // every id in the stream is a byte or unk (skipped)
+    count_pairs_dense(unk_id, live, out);
+    dist_merge_pairs(out);
+    return;
+  }
+  // distinct pairs <= live tokens and <= (ids in play)^2
   const uint64_t ids = (uint64_t)std::max<int32_t>(max_id_seen_, kBaseVocab) + 2;
   uint64_t bound = std::min<uint64_t>(live, ids * ids);
   uint64_t cap = 1024;
@@ -1636,6 +1774,49 @@ void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
   }
   for (void* p : {(void*)tkey, (void*)tcnt, (void*)tft, (void*)flags, (void*)dout}) HIP_OK(hipFree(p));
   dist_merge_pairs(out);
+}
+
+// K1 with every id a byte: dense tables, no hashing in HBM.
+void Device::count_pairs_dense(int32_t unk_id, uint64_t live, std::vector<PairCount>* out) {
+  size_t acc = 0;
+  u64* cnt = dalloc<u64>(kDensePairs, &acc);
+  u64* ft = dalloc<u64>(kDensePairs, &acc);
+  uint32_t* n = dalloc<uint32_t>(1, &acc);
+  PairCount* dout = dalloc<PairCount>(kDensePairs, &acc);
+  HIP_OK(hipMemsetAsync(cnt, 0, kDensePairs * sizeof(u64), S(stream_)));
+  HIP_OK(hipMemsetAsync(ft, 0xFF, kDensePairs * sizeof(u64), S(stream_)));
+  HIP_OK(hipMemsetAsync(n, 0, sizeof(uint32_t), S(stream_)));
+  DenseCountParams dp{tok_, tile_off_, tile_len_, (uint32_t)ntiles_, weight_, unk_id, cnt, ft};
+  int per_cu = 0;
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_pair_dense<true>),
+                                                      kDenseThreads, 0));
+  // >= 32 K tokens per workgroup: each one flushes its LDS table with HBM atomics at the end
+  const size_t by_tokens = (size_t)(live / 32768) + 1;
+  const int grid = (int)std::min<size_t>(std::min<size_t>((ntiles_ + kDenseWaves - 1) / kDenseWaves, by_tokens),
+                                         (size_t)cu_count_ * (size_t)std::max(1, per_cu));
+  if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[2], S(stream_)));
+  if (layout_ == Layout::kStream) k_pair_dense<false><<<grid, kDenseThreads, 0, S(stream_)>>>(dp);
+  else k_pair_dense<true><<<grid, kDenseThreads, 0, S(stream_)>>>(dp);
+  HIP_OK(hipGetLastError());
+  if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[3], S(stream_)));
+  k_pair_dense_collect<<<64, kThreads, 0, S(stream_)>>>(cnt, ft, dout, n);
+  HIP_OK(hipGetLastError());
+  uint32_t hn = 0;
+  HIP_OK(hipMemcpyAsync(&hn, n, sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  out->resize(hn);
+  if (hn) HIP_OK(hipMemcpy(out->data(), dout, hn * sizeof(PairCount), hipMemcpyDeviceToHost));
+  if (timing_) {
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[2], (hipEvent_t)ev_[3]));
+    times_.count_ms += ms;
+    times_.count_launches += 1;
+    // 4 B per token and per word header (the boundary), 8 B weight per word in the types
+    // layout, 12 B of tile descriptor per tile
+    times_.count_bytes += 4.0 * (double)live + 12.0 * (double)ntiles_ +
+                          (layout_ == Layout::kTypes ? 8.0 * (double)nentries_ : 0.0);
+  }
+  for (void* q : {(void*)cnt, (void*)ft, (void*)n, (void*)dout}) HIP_OK(hipFree(q));
 }
 
 // Folds completed sampled k_merge launches into times_ (block: wait for all of them).

@@ -147,6 +147,7 @@ class Device : public Backend {
   void free_all();
   void wait_flag(const MergeSlot& s);
   void finish_launch(ChainRun& run);
+  void count_pairs_dense(int32_t unk_id, uint64_t live, std::vector<PairCount>* out);
   void unmerge_run(ChainRun& run, int j0);
   void unmerge_launch(ChainRun& run, const uint32_t* tiles, size_t n_tiles, int j0 = 0);
   void flush_timing(bool block);
@@ -199,6 +200,7 @@ class Device : public Backend {
   int32_t unk_ = 0;
   uint64_t records_total_ = 0, records_max_ = 0;
   int32_t max_id_seen_ = 0;
+  int32_t max_id0_ = 0;  // max id at upload (reset_tokens restores it)
   bool speculate_ = true;
   uint64_t rollbacks_ = 0;
 
