@@ -100,6 +100,28 @@ def cpu_baseline(cfg, path, seconds):
     }
 
 
+PMC_NOTE = ("HBM bytes per k_merge launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, "
+            "FETCH doubled for gfx950 16-B reads), committed as profiles/r01_<config>_<layout>_pmc_traffic.json "
+            "by shredword-trainer_amd/tools/pmc_summary.py")
+
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def pmc_traffic(cfg_name, layout):
+    """Measured HBM bytes per k_merge launch for this workload, from the committed PMC summary."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", f"*_{cfg_name}_{layout}_pmc_traffic.json")), reverse=True):
+        try:
+            k = json.load(open(path))["kernels"]
+            ent = k.get("k_merge<true>" if layout == "types" else "k_merge<false>")
+            if ent:
+                return ent["hbm_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
+            continue
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -207,9 +229,12 @@ def main():
                 "symbols": st["num_symbols"], "occurrences": st["num_occurrences"], "tiles": st["num_tiles"],
             },
             "roofline": {
-                "kernel": "k_merge (fused match + delta + in-place compaction, K2+K3)",
+                "kernel": "k_merge (signature filter + fused match/delta/compaction, K2+K3)",
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": pmc_traffic(args.config, args.layout),
+                "traffic_source": PMC_NOTE,
+                "algorithmic_bytes": "4 B x live tokens per merge (SURVEY.md §8 d4, K2)",
                 "avg_launch_us": 1e3 * mk_ms, "avg_bytes_per_launch": mk_bytes,
                 "launches_sampled": st["merge_launches"], "launches": merges,
             },

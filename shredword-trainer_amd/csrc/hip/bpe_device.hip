@@ -1946,10 +1946,9 @@ void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   HIP_OK(hipGetLastError());
   if (pair >= 0) {
     HIP_OK(hipEventRecord((hipEvent_t)mev_[pair][1], S(stream_)));
-    // algorithmic bytes of this launch: the visited tiles' live tokens (estimated from the
-    // mean tile length) + their descriptors
-    const double frac = ntiles_ ? (double)n_iter / (double)ntiles_ : 0.0;
-    ev_pending_.push_back({pair, frac * 4.0 * (double)live_tokens_est_ + 12.0 * (double)n_iter});
+    // algorithmic bytes of a merge: 4 B per live token, i.e. the scan
+    // the reference makes per merge; the signature filter and tile index read far less
+    ev_pending_.push_back({pair, 4.0 * (double)live_tokens_est_ * (double)n});
   }
 }
 
