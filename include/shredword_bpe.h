@@ -73,11 +73,17 @@ int loadVocab(void* trainer, const char* path);
  *   timing = 0 | 1              per-kernel HIP-event timing (shred_get_stats)
  *   device = <ordinal>          HIP device (default: LOCAL_RANK or 0)
  *   merge_groups = <n>          k_merge grid cap (tuning; after load_corpus)
- *   speculate = 0 | 1           merge chains: run the selected merge together with merges
- *                               guessed from the heap in one device pass, confirm them one by
- *                               one, roll a wrong tail back exactly (default 1; single GPU only;
- *                               results are identical either way)
- *   chain = <n>                 longest merge chain (default 6, at most 8; 1 = no guesses)
+ *   speculate = 0 | 1           speculation (default 1; results are identical either way): the
+ *                               merge guessed to come next (from the heap) runs on the device
+ *                               while the host consumes the current one; a wrong guess is rolled
+ *                               back exactly on the device
+ *   chain = <n>                 instead of one guess beside each merge, run the selected merge and
+ *                               up to n-1 guessed successors in one launch (default 1 = off, at
+ *                               most 8)
+ *   exchange = local | off      test: run the multi-GPU records exchange over a single-rank RCCL
+ *                               communicator (before load_corpus)
+ *   exchange_bucket = <n>       multi-GPU: records per rank in the fixed all-gather bucket
+ *                               (default 1024; larger record sets take a second round)
  * Returns 0, or -1 for an unknown key/value. */
 int shred_set_option(Trainer* trainer, const char* key, const char* value);
 /* Restores the loaded corpus to its unmerged state and forgets merges (benchmark repeats). */
@@ -105,6 +111,7 @@ typedef struct ShredStats {
   uint64_t heap_pops, heap_stale_pops, heap_pushes, delta_records, tiles_visited;
   uint64_t apply_cycles_combine, apply_cycles_order, apply_cycles_walk;
   uint64_t spec_hits, spec_misses;
+  uint64_t exchange_overflows; /* multi-GPU: merges whose records needed a second all-gather */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

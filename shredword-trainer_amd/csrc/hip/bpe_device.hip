@@ -352,8 +352,9 @@ struct MergeParams {
   uint32_t* dcount;   // [0] touched slots, [1..9] tickets, [10] matched tiles
   u64* stats;         // [0] occurrences merged, [1] tokens rewritten
   uint32_t* done;     // completion tickets: [0..7] per blockIdx % 8 group, [8] top
-  int fused;          // 1: last workgroup collects; 0: leave the tables (multi-GPU exchange)
-  DeltaRecord* out;   // host-visible records
+  DeltaRecord* out;   // records: host-visible, or (multi-GPU) this rank's device bucket
+  uint32_t* xhdr;     // multi-GPU: the bucket header ([0] record count | kNeedCollect, [1] k_collect
+                      // offset); the flag is then raised by k_xout after the exchange
   uint32_t* hcount;   // host-visible: [0] record count (| kNeedCollect), [1] flag = seq, [2] matched tiles,
                       // [3] first record k_collect writes (kNeedCollect)
   u64* hstats;        // host-visible: [0] occurrences, [1] tokens rewritten
@@ -730,7 +731,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
     }
     if (tile_hits && lane == 0) {
       const uint32_t ent = tile | ((uint32_t)cj << kChainShift);
-      const uint32_t k = p.fused ? atomicAdd(&s_nmt, 1u) : kMtLds;
+      const uint32_t k = atomicAdd(&s_nmt, 1u);
       if (k < kMtLds) s_mt[k] = ent;
       else atomicExch(&p.mlist[atomicAdd(p.mcount, 1u)], ent);
     }
@@ -763,7 +764,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
     if (n_written) atomicAdd(&s_cnt[1], n_written);
   }
   __syncthreads();
-  if (p.fused) {
+  {
     // ---- this workgroup's region: LDS-reduced records, matched tiles and counts, written
     // through (sc1) so the collecting workgroup on any XCD reads them with sc1 loads after the
     // ticket (MI355X_MICROARCH.md, valid forms: sc1 stores, vmcnt drain, atomic ticket)
@@ -788,14 +789,6 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       __hip_atomic_store(hd + 2, h.spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(reinterpret_cast<u64*>(hd + 4), s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(reinterpret_cast<u64*>(hd + 6), s_cnt[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  } else {
-    // multi-GPU: everything into the global slot tables (all-reduced before the collect)
-    for (int i = threadIdx.x; i < kDeltaLdsW; i += kThreads)
-      if (h.key[i] != kEmpty32) delta_global(p, h.key[i], h.sum[i], h.ft[i]);
-    if (threadIdx.x == 0) {
-      if (s_cnt[0]) atomicAdd(&p.stats[0], s_cnt[0]);
-      if (s_cnt[1]) atomicAdd(&p.stats[1], s_cnt[1]);
     }
   }
   // ---- completion ticket: every wave drains its stores/atomics first.  One counter for small
@@ -826,7 +819,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
   const uint32_t G = gridDim.x;
   uint32_t n = 0, nm = 0, base = 0;
   bool need_collect = false;
-  if (p.fused) {
+  {
     // ---- gather the regions: headers, prefix offsets, then records and tiles to the host
     u64 merged = 0, written = 0;
     uint32_t spill = 0;
@@ -931,32 +924,75 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       }
       n += ngl;
     }
-  } else {
-    if (threadIdx.x == 0) {
-      s_cnt[0] = atomicAdd(p.dcount, 0u);
-      s_cnt[1] = atomicExch(p.mcount, 0u);
-    }
-    __syncthreads();
-    n = (uint32_t)s_cnt[0];
-    nm = (uint32_t)s_cnt[1];
-    for (uint32_t i = threadIdx.x; i < nm; i += kThreads) sys_store(p.hmlist + i, atomicOr(&p.mlist[i], 0u));
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   STAMP(5);
   if (threadIdx.x == 0) {
-    if (p.fused) {
-      sys_store(&p.hstats[0], s_cnt[0]);
-      sys_store(&p.hstats[1], s_cnt[1]);
-      sys_store(&p.hcount[0], need_collect ? (n | kNeedCollect) : n);
-      sys_store(&p.hcount[3], base);
-    }
+    sys_store(&p.hstats[0], s_cnt[0]);
+    sys_store(&p.hstats[1], s_cnt[1]);
+    sys_store(&p.hcount[0], need_collect ? (n | kNeedCollect) : n);
+    sys_store(&p.hcount[3], base);
     sys_store(&p.hcount[2], nm);
     atomicExch(&p.done[8], 0u);
     STAMP(6);
-    sys_flag(&p.hcount[1], p.seq);
+    if (p.xhdr) {  // multi-GPU: the bucket header; k_xout raises the flag after the exchange
+      p.xhdr[0] = need_collect ? (n | kNeedCollect) : n;
+      p.xhdr[1] = base;
+      __threadfence_system();
+    } else {
+      sys_flag(&p.hcount[1], p.seq);
+    }
     STAMP(7);
   }
+}
+
+// Multi-GPU (K4 after the all-gather): the gathered buckets -> one host-visible record list.
+// Rank r contributes the records that are valid in its bucket: min(count, bucket) — or, when
+// its spilled deltas still wait for k_collect, min(k_collect offset, bucket); the rest goes
+// through the host's overflow round.  One workgroup, so the flag follows every host store.
+struct XoutParams {
+  const uint8_t* recv;  // world buckets of `bucket` bytes: u32 header[8], then records
+  uint32_t bucket;
+  uint32_t cap;         // records per bucket
+  uint32_t world;
+  DeltaRecord* out;     // host-visible, world x cap records
+  uint32_t* hx;         // host-visible: per rank [count | kNeedCollect, k_collect offset]
+  uint32_t* flag;       // host-visible completion flag
+  uint32_t seq;
+};
+
+__device__ __forceinline__ uint32_t bucket_valid(uint32_t h0, uint32_t h1, uint32_t cap) {
+  const uint32_t n = (h0 & kNeedCollect) ? h1 : h0;
+  return min(n, cap);
+}
+
+__global__ __launch_bounds__(1024) void k_xout(XoutParams p) {
+  __shared__ uint32_t s_pre[65];
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < p.world; ++r) {
+      const uint32_t* h = reinterpret_cast<const uint32_t*>(p.recv + (size_t)r * p.bucket);
+      s_pre[r] = acc;
+      acc += bucket_valid(h[0], h[1], p.cap);
+    }
+    s_pre[p.world] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < p.world) {
+    const uint32_t* h = reinterpret_cast<const uint32_t*>(p.recv + (size_t)threadIdx.x * p.bucket);
+    sys_store(p.hx + 2 * threadIdx.x, h[0]);
+    sys_store(p.hx + 2 * threadIdx.x + 1, h[1]);
+  }
+  for (uint32_t r = 0; r < p.world; ++r) {
+    const u64* src = reinterpret_cast<const u64*>(p.recv + (size_t)r * p.bucket + 32);
+    const uint32_t nv = s_pre[r + 1] - s_pre[r];
+    for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x)
+      sys_record(p.out + s_pre[r] + i, (uint32_t)src[3 * i], src[3 * i + 1], src[3 * i + 2]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) sys_flag(p.flag, p.seq);
 }
 
 
@@ -978,23 +1014,6 @@ __global__ __launch_bounds__(kThreads) void k_collect(uint32_t* dcount, const ui
 }
 
 __global__ void k_zero_u32(uint32_t* p) { *p = 0; }
-
-// K4 (multi-GPU): after the all-reduce every rank scans the dense prefix instead of its own list.
-__global__ __launch_bounds__(kThreads) void k_collect_dense(uint32_t nkeys, u64* dsum, u64* dft, DeltaRecord* out,
-                                                             uint32_t* out_count) {
-  for (uint32_t key = blockIdx.x * kThreads + threadIdx.x; key < nkeys; key += gridDim.x * kThreads) {
-    const u64 ft = dft[key];
-    if (ft == kEmpty64) continue;
-    DeltaRecord r;
-    r.key = key;
-    r.pad = 0;
-    r.sum = dsum[key];
-    r.ft = ft;
-    out[atomicAdd(out_count, 1u)] = r;
-    dsum[key] = 0;
-    dft[key] = kEmpty64;
-  }
-}
 
 // ------------------------------------------------------------------------------------------
 // Rollback of the unconfirmed tail of a merge chain: in every listed tile, each undone merge
@@ -1541,6 +1560,13 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
 // Grid cap of k_merge (tuning).
 void Device::set_merge_groups(int groups) { max_groups_ = std::max(1, std::min(kMaxMergeGroups, groups)); }
 
+void Device::set_exchange(const Exchange& x) {
+  if (slot_[0].dsum || slot_[1].dsum) fatal("set_exchange: merge buffers already exist");
+  if (x.world < 1 || x.world > 64 || !x.allgather || x.bucket_records < 1) fatal("set_exchange: bad exchange");
+  xchg_ = x;
+  exchange_ = true;
+}
+
 void Device::free_slot(MergeSlot& s, bool keep_host) {
   for (void* p : {(void*)s.dsum, (void*)s.dft, (void*)s.dlist, (void*)s.dcount})
     if (p) HIP_OK(hipFree(p));
@@ -1548,6 +1574,13 @@ void Device::free_slot(MergeSlot& s, bool keep_host) {
   s.dlist = s.dcount = nullptr;
   if (s.host_recs) HIP_OK(hipHostFree(s.host_recs));
   s.host_recs = nullptr;
+  for (void* q : {(void*)s.xsend, (void*)s.xrecv})
+    if (q) HIP_OK(hipFree(q));
+  s.xsend = s.xrecv = nullptr;
+  for (void* q : {(void*)s.host_xrecs, (void*)s.host_xhdr})
+    if (q) HIP_OK(hipHostFree(q));
+  s.host_xrecs = nullptr;
+  s.host_xhdr = nullptr;
   s.cap = 0;
   s.launched = false;
   if (!keep_host) {
@@ -1575,6 +1608,9 @@ void Device::free_all() {
   tile_len_ = tile_len0_ = nullptr;
   weight_ = nullptr;
   for (MergeSlot& s : slot_) free_slot(s, true);
+  if (xrecv2_) HIP_OK(hipFree(xrecv2_));
+  xrecv2_ = nullptr;
+  xrecv2_bytes_ = 0;
   ntiles_ = 0;
   bytes_alloc_ = 0;
   uploaded_ = false;
@@ -1696,7 +1732,11 @@ void Device::ensure_slots(MergeSlot& s, uint32_t need) {
   while (cap < need) cap *= 2;
   HIP_OK(hipStreamSynchronize(S(stream_)));
   HIP_OK(hipStreamSynchronize(S(aux_stream_)));
-  const size_t old_bytes = s.dsum ? (size_t)kChainMax * 4 * ((size_t)s.cap + 1) * 20 + 16 + 64 : 0;
+  size_t old_bytes = s.dsum ? (size_t)kChainMax * 4 * ((size_t)s.cap + 1) * 20 + 16 + 64 : 0;
+  if (s.xsend) {
+    const size_t old_rec_cap = (size_t)kChainMax * 4 * ((size_t)s.cap + 1) + (size_t)kMaxMergeGroups * kDeltaLdsW;
+    old_bytes += 32 + (xchg_.bucket_records + old_rec_cap) * sizeof(DeltaRecord) + xchg_.world * exchange_bucket_bytes();
+  }
   free_slot(s, true);
   bytes_alloc_ -= old_bytes;
   keys_per_merge_ = (uint32_t)(4 * ((size_t)cap + 1));
@@ -1713,6 +1753,16 @@ void Device::ensure_slots(MergeSlot& s, uint32_t need) {
   const size_t rec_cap = keys + (size_t)kMaxMergeGroups * kDeltaLdsW;
   HIP_OK(hipHostMalloc((void**)&s.host_recs, rec_cap * sizeof(DeltaRecord), hipHostMallocMapped | hipHostMallocCoherent));
   HIP_OK(hipHostGetDevicePointer(&s.dev_recs, s.host_recs, 0));
+  if (exchange_) {
+    // the bucket header, then room for every record plus one overflow window past the bucket
+    const size_t W = (size_t)xchg_.world, cap_x = xchg_.bucket_records;
+    s.xsend = dalloc<uint8_t>(32 + (cap_x + rec_cap) * sizeof(DeltaRecord), &bytes_alloc_);
+    s.xrecv = dalloc<uint8_t>(W * exchange_bucket_bytes(), &bytes_alloc_);
+    HIP_OK(hipHostMalloc((void**)&s.host_xrecs, W * cap_x * sizeof(DeltaRecord), hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_OK(hipHostGetDevicePointer(&s.dev_xrecs, s.host_xrecs, 0));
+    HIP_OK(hipHostMalloc((void**)&s.host_xhdr, 2 * W * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_OK(hipHostGetDevicePointer(&s.dev_xhdr, s.host_xhdr, 0));
+  }
   s.cap = cap;
   HIP_OK(hipStreamSynchronize(S(stream_)));
 }
@@ -1847,7 +1897,7 @@ void Device::flush_timing(bool block) {
 
 void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   HIP_OK(hipSetDevice(ordinal_));
-  if (n < 1 || n > kChainMax || (exchange_ && n != 1)) fatal("merge_chain: bad chain length");
+  if (n < 1 || n > kChainMax) fatal("merge_chain: bad chain length");
   if (run_count_ >= 2) fatal("merge_chain: two launches are already in flight");
   ChainRun& run = run_at(run_count_);
   run.slot = (run_head_ + run_count_) & 1;
@@ -1862,9 +1912,15 @@ void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   run.waited = false;
   for (int i = 0; i < 2 * n; ++i) run.ab[i] = ab[i];
   ++run_count_;
-  if (!ntiles_) return;  // an empty shard still joins collect()'s exchange
+  if (!ntiles_ && !exchange_) return;
   sl.seq = ++seq_;
   sl.launched = true;
+  if (!ntiles_) {  // an empty shard still joins the exchange, with an empty bucket
+    std::memset(sl.host_count, 0, 32);
+    HIP_OK(hipMemsetAsync(sl.xsend, 0, 32, S(stream_)));
+    exchange_launch(sl);
+    return;
+  }
   MergeParams& mp = *static_cast<MergeParams*>(merge_params_);
   mp.tok = tok_;
   mp.tile_off = tile_off_;
@@ -1885,8 +1941,8 @@ void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   mp.dcount = sl.dcount;
   mp.stats = U(sl.dsum) + (size_t)kChainMax * keys_per_merge_;
   mp.done = sl.dcount + 1;
-  mp.fused = exchange_ ? 0 : 1;
-  mp.out = (DeltaRecord*)sl.dev_recs;
+  mp.out = exchange_ ? (DeltaRecord*)(sl.xsend + 32) : (DeltaRecord*)sl.dev_recs;
+  mp.xhdr = exchange_ ? (uint32_t*)sl.xsend : nullptr;
   mp.hcount = (uint32_t*)sl.dev_count;
   mp.hstats = (u64*)((char*)sl.dev_count + 16);
   mp.mlist = sl.dmlist;
@@ -1950,6 +2006,75 @@ void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
     // the reference makes per merge; the signature filter and tile index read far less
     ev_pending_.push_back({pair, 4.0 * (double)live_tokens_est_ * (double)n});
   }
+  if (exchange_) exchange_launch(sl);
+}
+
+// Queued behind the slot's k_merge: the bucket all-gather over RCCL, then k_xout copies the
+// valid records of every rank to the host and raises the slot's flag.  Every rank queues the
+// same sequence of exchanges (the host decisions are identical on all ranks).
+void Device::exchange_launch(MergeSlot& sl) {
+  const size_t bucket = exchange_bucket_bytes();
+  xchg_.allgather(xchg_.comm, sl.xsend, sl.xrecv, bucket, stream_);
+  XoutParams xp;
+  xp.recv = sl.xrecv;
+  xp.bucket = (uint32_t)bucket;
+  xp.cap = xchg_.bucket_records;
+  xp.world = (uint32_t)xchg_.world;
+  xp.out = (DeltaRecord*)sl.dev_xrecs;
+  xp.hx = (uint32_t*)sl.dev_xhdr;
+  xp.flag = (uint32_t*)sl.dev_count + 1;
+  xp.seq = sl.seq;
+  k_xout<<<1, 1024, 0, S(stream_)>>>(xp);
+  HIP_OK(hipGetLastError());
+}
+
+// After the slot's flag: every rank's records, concatenated.  A rank whose records did not fit
+// its bucket (or whose spilled deltas still need k_collect) sends the remainder in one more
+// all-gather, sized by the largest remainder; every rank sees the same headers, so all of them
+// take part in that round.
+size_t Device::exchange_finish(MergeSlot& sl, const DeltaRecord** recs) {
+  const int W = xchg_.world;
+  const uint32_t cap = xchg_.bucket_records;
+  size_t nvalid = 0, extra_max = 0;
+  uint32_t valid[64], total[64];
+  for (int r = 0; r < W; ++r) {
+    const uint32_t h0 = sl.host_xhdr[2 * r], h1 = sl.host_xhdr[2 * r + 1];
+    total[r] = h0 & ~kNeedCollect;
+    valid[r] = std::min((h0 & kNeedCollect) ? h1 : h0 & ~kNeedCollect, cap);
+    nvalid += valid[r];
+    extra_max = std::max<size_t>(extra_max, total[r] - valid[r]);
+  }
+  *recs = sl.host_xrecs;
+  if (extra_max == 0) return nvalid;
+  ++x_overflows_;
+  const uint32_t me = (uint32_t)xchg_.rank;
+  DeltaRecord* mine = (DeltaRecord*)(sl.xsend + 32);
+  if (ntiles_ && (sl.host_count[0] & kNeedCollect)) {  // this rank's spilled deltas, behind its records
+    k_collect<<<256, kThreads, 0, S(stream_)>>>(sl.dcount, sl.dlist, U(sl.dsum), U(sl.dft), mine + sl.host_count[3]);
+    HIP_OK(hipGetLastError());
+    k_zero_u32<<<1, 1, 0, S(stream_)>>>(sl.dcount);
+    HIP_OK(hipGetLastError());
+  }
+  const size_t bytes = extra_max * sizeof(DeltaRecord);
+  if (xrecv2_bytes_ < bytes * W) {
+    HIP_OK(hipStreamSynchronize(S(stream_)));
+    if (xrecv2_) HIP_OK(hipFree(xrecv2_));
+    xrecv2_bytes_ = bytes * W;
+    HIP_OK(hipMalloc((void**)&xrecv2_, xrecv2_bytes_));
+  }
+  // the send window starts at this rank's first record not yet sent; the slot's send buffer has
+  // room for a full window past any valid prefix (see ensure_slots)
+  xchg_.allgather(xchg_.comm, mine + valid[me], xrecv2_, bytes, stream_);
+  xstage_.resize(bytes * W);
+  HIP_OK(hipMemcpyAsync(xstage_.data(), xrecv2_, bytes * W, hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  sl.xall.assign(sl.host_xrecs, sl.host_xrecs + nvalid);
+  for (int r = 0; r < W; ++r) {
+    const DeltaRecord* src = (const DeltaRecord*)(xstage_.data() + (size_t)r * bytes);
+    sl.xall.insert(sl.xall.end(), src, src + (total[r] - valid[r]));
+  }
+  *recs = sl.xall.data();
+  return sl.xall.size();
 }
 
 // Spins on the host-visible flag the last workgroup raises (much cheaper than a stream sync).
@@ -1986,23 +2111,10 @@ void Device::finish_launch(ChainRun& run_) {
   sl.launched = false;
   const u64* hs = (const u64*)(sl.host_count + 4);
   size_t n;
-  u64* stats = U(sl.dsum) + (size_t)kChainMax * keys_per_merge_;
   const uint32_t nm = launched ? sl.host_count[2] : 0;
+  const DeltaRecord* all = sl.host_recs;
   if (exchange_) {
-    // multi-GPU: all-reduce the live prefix of the slot tables, then every rank scans it
-    const uint32_t unk_slot = (unk_ >= 0 && (uint32_t)unk_ < sl.cap) ? (uint32_t)unk_ : 0u;
-    const size_t top = std::max<uint32_t>((uint32_t)run_.X0, unk_slot);
-    const size_t nkeys = 4 * (std::min<size_t>(sl.cap, top + 1) + 1);
-    exchange_(exchange_ctx_, sl.dsum, sl.dft, nkeys, stream_);
-    HIP_OK(hipMemsetAsync(sl.dcount, 0, sizeof(uint32_t), S(stream_)));
-    k_collect_dense<<<256, kThreads, 0, S(stream_)>>>((uint32_t)nkeys, U(sl.dsum), U(sl.dft), drec, sl.dcount);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(sl.host_count, sl.dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
-    HIP_OK(hipMemcpyAsync((u64*)(sl.host_count + 4), stats, 2 * sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
-    HIP_OK(hipMemsetAsync(sl.dcount, 0, sizeof(uint32_t), S(stream_)));
-    HIP_OK(hipMemsetAsync(stats, 0, 2 * sizeof(u64), S(stream_)));
-    HIP_OK(hipStreamSynchronize(S(stream_)));
-    n = sl.host_count[0];
+    n = exchange_finish(sl, &all);
   } else {
     n = sl.host_count[0];
     if (n & kNeedCollect) {  // too many spilled slots for one workgroup: a wide collect pass
@@ -2016,7 +2128,7 @@ void Device::finish_launch(ChainRun& run_) {
     }
   }
   if (run_.n == 1) {  // one merge: its keys and tiles carry no chain index
-    run_.rp[0] = sl.host_recs;
+    run_.rp[0] = all;
     run_.rn[0] = n;
     run_.tp[0] = sl.host_mlist;
     run_.tn[0] = nm;
@@ -2026,7 +2138,7 @@ void Device::finish_launch(ChainRun& run_) {
       run_.recs[i].clear();
       run_.tiles[i].clear();
     }
-    const DeltaRecord* r = sl.host_recs;
+    const DeltaRecord* r = all;
     for (size_t i = 0; i < n; ++i) {
       const uint32_t j = r[i].key / keys_per_merge_;
       if (j >= (uint32_t)run_.n) fatal("k_merge record of a merge outside the chain");
@@ -2111,7 +2223,7 @@ void Device::rollback(int32_t X) {
     if (!run.waited && run.n == 1) {
       // a single merge not waited for: k_unmerge reads its matched tiles and their count from
       // the host memory the merge writes, queued behind it, so the host does not wait at all
-      unmerge_launch(run, nullptr, 0);
+      if (ntiles_) unmerge_launch(run, nullptr, 0);
       slot_[run.slot].launched = false;
       run.waited = true;
     } else {

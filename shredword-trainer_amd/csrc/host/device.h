@@ -59,15 +59,24 @@ class Device : public Backend {
   // K2+K3 for a chain of merges (ab[2i], ab[2i+1]) -> X0 + i: one k_merge launch applies them in
   // order per tile and reduces each merge's neighbour deltas separately.
   void merge_chain(const int32_t* ab, int n, int32_t X0) override;
-  // Multi-GPU hook: called between merge_chain and collect(); slot tables are
-  // [prefix_slots * 4] u64 sums followed by the same count of u64 first-touch values.
-  using ExchangeFn = void (*)(void* ctx, uint64_t* dsum, uint64_t* dft, size_t n, void* stream);
-  void set_exchange(ExchangeFn fn, void* ctx) { exchange_ = fn; exchange_ctx_ = ctx; }
+  // Multi-GPU: every launch's compacted records are all-gathered (fixed buckets of
+  // `bucket_records` records per rank, RCCL over xGMI, queued behind k_merge on the stream);
+  // collect() then returns the concatenation of all ranks' records, which the host combines
+  // (sum of weights, min first touch) exactly like one rank's duplicate records.
+  struct Exchange {
+    int rank = 0, world = 1;
+    void* comm = nullptr;
+    // in-place-free all-gather of `bytes` per rank from send into recv (world x bytes)
+    void (*allgather)(void* comm, const void* send, void* recv, size_t bytes, void* stream) = nullptr;
+    uint32_t bucket_records = 1024;
+  };
+  void set_exchange(const Exchange& x);
   // K4: merge X's records (host memory); the first collect of a chain waits for the launch.
   size_t collect(int32_t X, const DeltaRecord** recs) override;
   static constexpr int kChainMax = 8;
-  int max_chain() const override { return speculate_ && !exchange_ ? kChainMax : 1; }
-  bool can_overlap() const override { return speculate_ && !exchange_; }
+  int max_chain() const override { return speculate_ ? kChainMax : 1; }
+  bool can_overlap() const override { return speculate_; }
+  uint64_t exchange_overflows() const { return x_overflows_; }
   // Undoes the chain's uncollected merges >= X with k_unmerge (newest first), host-free.
   void rollback(int32_t X) override;
   void set_speculation(bool on) { speculate_ = on; }
@@ -119,6 +128,15 @@ class Device : public Backend {
     uint32_t* rtile = nullptr;
     uint32_t* host_mlist = nullptr;    // pinned: matched tiles (tile | chain index << 27)
     void* dev_mlist = nullptr;
+    // multi-GPU: this rank's bucket (32-byte header, then records; records past the bucket
+    // stay behind it for the overflow round), the gathered buckets, and their pinned copy
+    uint8_t* xsend = nullptr;
+    uint8_t* xrecv = nullptr;
+    DeltaRecord* host_xrecs = nullptr;  // pinned: world x bucket records, concatenated
+    void* dev_xrecs = nullptr;
+    uint32_t* host_xhdr = nullptr;      // pinned: per rank [records | need-collect, k_collect offset]
+    void* dev_xhdr = nullptr;
+    std::vector<DeltaRecord> xall;      // all ranks' records when a bucket overflowed
     uint32_t grid = 0;
     uint32_t n_iter = 0;  // candidate tiles of the launch
     bool launched = false;
@@ -147,6 +165,9 @@ class Device : public Backend {
   void free_all();
   void wait_flag(const MergeSlot& s);
   void finish_launch(ChainRun& run);
+  size_t exchange_bucket_bytes() const { return 32 + (size_t)xchg_.bucket_records * 24; }
+  void exchange_launch(MergeSlot& sl);
+  size_t exchange_finish(MergeSlot& sl, const DeltaRecord** recs);
   void count_pairs_dense(int32_t unk_id, uint64_t live, std::vector<PairCount>* out);
   void unmerge_run(ChainRun& run, int j0);
   void unmerge_launch(ChainRun& run, const uint32_t* tiles, size_t n_tiles, int j0 = 0);
@@ -167,8 +188,12 @@ class Device : public Backend {
   std::vector<int> ev_free_;
   bool timing_ = false;
   KernelTimes times_;
-  ExchangeFn exchange_ = nullptr;
-  void* exchange_ctx_ = nullptr;
+  Exchange xchg_;
+  bool exchange_ = false;  // xchg_ is set up: every launch is followed by the records exchange
+  uint8_t* xrecv2_ = nullptr;  // overflow round: world x the largest remainder (grown on demand)
+  size_t xrecv2_bytes_ = 0;
+  std::vector<uint8_t> xstage_;
+  uint64_t x_overflows_ = 0;
   int cu_count_ = 256;
   bool uploaded_ = false;
   Layout layout_ = Layout::kTypes;

@@ -69,6 +69,22 @@ int dist_finalize() {
   return 0;
 }
 
+void dist_allgather_device(void* comm, const void* send, void* recv, size_t bytes, void* stream) {
+  nccl_ok(ncclAllGather(send, recv, bytes, ncclUint8, (ncclComm_t)comm, (hipStream_t)stream), "ncclAllGather");
+}
+
+void* dist_local_comm(int device) {
+  static std::unordered_map<int, ncclComm_t> comms;
+  auto it = comms.find(device);
+  if (it != comms.end()) return it->second;
+  hip_ok(hipSetDevice(device), "hipSetDevice");
+  ncclComm_t comm;
+  int dev = device;
+  nccl_ok(ncclCommInitAll(&comm, 1, &dev), "ncclCommInitAll");
+  comms.emplace(device, comm);
+  return comm;
+}
+
 void dist_allreduce_device(uint64_t* buf, size_t n, bool min_op, void* stream) {
   if (!dist_active() || n == 0) return;
   nccl_ok(ncclAllReduce(buf, buf, n, ncclUint64, min_op ? ncclMin : ncclSum, (ncclComm_t)dist_state().comm,

@@ -1,9 +1,10 @@
 // Multi-GPU plumbing: one process per MI355X, RCCL over xGMI.
 //
 // The BPE path shards the word table by contiguous word ranges.  Per merge the
-// only exchange is one pair of all-reduces over the live prefix of the neighbour-delta tables
-// (sum of weights, min of first touch) — both order-free, so every rank receives identical
-// records and replays the identical heap.  Setup and the rare host-side reductions (initial
+// only exchange is one all-gather of every rank's compacted neighbour-delta records (a fixed
+// bucket per rank; a second round only when a bucket overflows), so every rank receives the
+// identical record multiset, combines it (sum of weights, min of first touch: order-free) and
+// replays the identical heap.  Setup and the rare host-side reductions (initial
 // pair lists, final token histogram) go through small device staging buffers.
 #pragma once
 
@@ -29,6 +30,11 @@ int dist_unique_id(void* out, size_t cap);
 int dist_init(int rank, int world, const void* id, size_t len, int device);
 int dist_finalize();
 
+// All-gather of `bytes` per rank (device buffers; recv holds world x bytes) on `stream`, over
+// `comm` (an ncclComm_t: the job's, or the single-rank one below).
+void dist_allgather_device(void* comm, const void* send, void* recv, size_t bytes, void* stream);
+// A single-rank communicator on `device` (tests: runs the multi-GPU exchange path on one GPU).
+void* dist_local_comm(int device);
 // In-place all-reduce of n u64 device values on `stream` (sum, or min when min_op).
 void dist_allreduce_device(uint64_t* dev_buf, size_t n, bool min_op, void* stream);
 // Same for host values, staged through a device buffer (synchronous).

@@ -37,6 +37,8 @@ struct Trainer {
   FILE* trace = nullptr;
   bool timing = false;
   int device = -1;
+  bool local_exchange = false;   // test: the multi-GPU exchange over a single-rank communicator
+  uint32_t exchange_bucket = 0;  // records per rank and exchange bucket (0: default)
   double load_s = 0;
 };
 
@@ -73,6 +75,17 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
     t->engine.set_chain(std::atoi(val.c_str()), 2048);
   } else if (key == "speculate") {
     t->engine.set_speculation(std::atoi(val.c_str()) != 0);
+  } else if (key == "exchange" || key == "exchange_bucket") {
+    if (t->dev) return -1;  // fixed when the device is created (load_corpus)
+    if (key == "exchange") {
+      if (val == "local") t->local_exchange = true;
+      else if (val == "off" || val == "0") t->local_exchange = false;
+      else return -1;
+    } else {
+      const int b = std::atoi(val.c_str());
+      if (b < 1) return -1;
+      t->exchange_bucket = (uint32_t)b;
+    }
   } else if (key == "device") {
     t->device = std::atoi(val.c_str());
   } else {
@@ -81,10 +94,6 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
   return 0;
 }
 
-void exchange_allreduce(void*, uint64_t* dsum, uint64_t* dft, size_t n, void* stream) {
-  dist_allreduce_device(dsum, n, false, stream);
-  dist_allreduce_device(dft, n, true, stream);
-}
 
 // Creates the device and uploads this rank's share of the word table if needed.
 bool ensure_device(Trainer* t, const char* caller) {
@@ -103,7 +112,20 @@ bool ensure_device(Trainer* t, const char* caller) {
     t->dev.reset(new Device(ord));
     t->dev->set_timing(t->timing);
     t->dev->set_unk(t->config.unk_id);
-    if (dist_active()) t->dev->set_exchange(exchange_allreduce, nullptr);
+    if (dist_active() || t->local_exchange) {
+      Device::Exchange x;
+      if (dist_active()) {
+        x.rank = dist_state().rank;
+        x.world = dist_state().world;
+        x.comm = dist_state().comm;
+      } else {
+        x.comm = dist_local_comm(ord);
+      }
+      x.allgather = dist_allgather_device;
+      const int b = t->exchange_bucket ? (int)t->exchange_bucket : env_int("SHREDWORD_EXCHANGE_BUCKET", 0);
+      if (b > 0) x.bucket_records = (uint32_t)b;
+      t->dev->set_exchange(x);
+    }
   }
   if (t->device_stale) {
     if (t->layout == Layout::kStream && t->wt.occurrence_rank.size() != t->wt.total_occurrences) {
@@ -306,6 +328,7 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
   s->apply_cycles_order = c.cyc_order;
   s->apply_cycles_walk = c.cyc_walk;
   if (t->dev) s->tiles_visited = t->dev->visited_tiles();
+  if (t->dev) s->exchange_overflows = t->dev->exchange_overflows();
   s->spec_hits = t->engine.spec_hits();
   s->spec_misses = t->engine.spec_misses();
   s->layout = (int32_t)t->layout;

@@ -62,7 +62,8 @@ class ShredStats(Structure):
                 ("delta_records", c_uint64), ("tiles_visited", c_uint64),
                 ("apply_cycles_combine", c_uint64), ("apply_cycles_order", c_uint64),
                 ("apply_cycles_walk", c_uint64),
-                ("spec_hits", c_uint64), ("spec_misses", c_uint64)]
+                ("spec_hits", c_uint64), ("spec_misses", c_uint64),
+                ("exchange_overflows", c_uint64)]
 
 
 Trainer = c_void_p

@@ -8,6 +8,9 @@ LIB = os.path.join(HERE, "native", "_build", "libhostharness.so")
 
 EXCHANGE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t)
+# records all-gather: (ctx, send, nbytes, out_bytes*) -> concatenated bytes (callback-owned)
+GATHER_CB = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                             ctypes.POINTER(ctypes.c_size_t))
 
 
 def load():
@@ -17,7 +20,7 @@ def load():
                             ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.hh_open.restype = ctypes.c_void_p
     lib.hh_close.argtypes = [ctypes.c_void_p]
-    lib.hh_set_exchange.argtypes = [ctypes.c_void_p, EXCHANGE_CB, ctypes.c_void_p]
+    lib.hh_set_exchange.argtypes = [ctypes.c_void_p, EXCHANGE_CB, GATHER_CB, ctypes.c_void_p]
     lib.hh_train.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     lib.hh_train.restype = ctypes.c_int
     lib.hh_merge_batch.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -32,6 +35,7 @@ def load():
     lib.hh_visit_hist.restype = ctypes.c_uint64
     lib.hh_match_hist.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64]
     lib.hh_match_hist.restype = ctypes.c_uint64
+    lib.hh_set_chain.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.hh_chain_probe.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     lib.hh_chain_hist.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     lib.hh_spec.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]

@@ -22,7 +22,11 @@
 
 using namespace shred;
 
+// Dense reduction (initial pair counts, final token histogram): sum into `sum`, min into `mn`.
 typedef void (*ExchangeCb)(void* ctx, uint64_t* sum, uint64_t* mn, size_t n);
+// Per-merge records exchange, as the device's RCCL all-gather: every rank's bytes concatenated
+// in rank order; the returned buffer belongs to the callback and stays valid until its next call.
+typedef const void* (*GatherCb)(void* ctx, const void* send, size_t nbytes, size_t* out_bytes);
 
 namespace {
 
@@ -37,10 +41,14 @@ class EmuBackend : public Backend {
     dsum_.assign(4 * ((size_t)cap_ + 1), 0);
     dft_.assign(4 * ((size_t)cap_ + 1), ~0ull);
   }
-  void set_exchange(ExchangeCb cb, void* ctx) { cb_ = cb; ctx_ = ctx; }
+  void set_exchange(ExchangeCb cb, GatherCb gather, void* ctx) {
+    cb_ = cb;
+    gather_ = gather;
+    ctx_ = ctx;
+  }
   void set_speculation(bool on) { spec_ = on; }
-  int max_chain() const override { return spec_ && !cb_ ? 64 : 1; }
-  bool can_overlap() const override { return spec_ && !cb_; }
+  int max_chain() const override { return spec_ ? 64 : 1; }
+  bool can_overlap() const override { return spec_; }
 
   uint64_t weight(uint32_t rank) const { return layout_ == Layout::kTypes ? wt_.count[rank] : 1; }
 
@@ -87,7 +95,7 @@ class EmuBackend : public Backend {
     const size_t nvisit = use_list ? cand.size() : ts_.num_tiles();
     // like the device's direct mode: candidate-list merges ship per-occurrence records
     std::vector<DeltaRecord> raw;
-    raw_ = (use_list && !cb_ && direct_) ? &raw : nullptr;
+    raw_ = (use_list && direct_) ? &raw : nullptr;
     for (size_t it = 0; it < nvisit; ++it) {
       const size_t t = use_list ? cand[it] : it;
       int32_t* p = ts_.tok.data() + ts_.off[t];
@@ -142,7 +150,7 @@ class EmuBackend : public Backend {
     pd.X = X;
     pd.matched = std::move(matched);
     if (raw_) pd.recs = std::move(raw);
-    else if (!cb_) drain(&pd.recs);  // multi-rank: tables stay for collect()'s exchange
+    else drain(&pd.recs);
     raw_ = nullptr;
     queue_.push_back(std::move(pd));
   }
@@ -189,9 +197,12 @@ class EmuBackend : public Backend {
     if (queue_.empty() || queue_.front().X != X) fatal("emulated collect of a merge that is not outstanding");
     Pending pd = std::move(queue_.front());
     queue_.erase(queue_.begin());
-    if (cb_) {
-      cb_(ctx_, dsum_.data(), dft_.data(), dsum_.size());
-      drain(&pd.recs);
+    if (gather_) {  // multi-rank: every rank's records, concatenated (the host combines them)
+      size_t nb = 0;
+      const void* all = gather_(ctx_, pd.recs.data(), pd.recs.size() * sizeof(DeltaRecord), &nb);
+      if (nb % sizeof(DeltaRecord)) fatal("emulated exchange returned a partial record");
+      pd.recs.resize(nb / sizeof(DeltaRecord));
+      if (nb) std::memcpy(pd.recs.data(), all, nb);
     }
     index_.set_tiles(X, pd.matched.data(), pd.matched.size());
     recs_ = std::move(pd.recs);
@@ -239,6 +250,7 @@ class EmuBackend : public Backend {
   std::vector<Pending> queue_;  // merges launched but not collected, oldest first
   bool spec_ = true;
   ExchangeCb cb_ = nullptr;
+  GatherCb gather_ = nullptr;
   void* ctx_ = nullptr;
 };
 
@@ -284,7 +296,9 @@ void hh_close(void* p) {
   delete h;
 }
 
-void hh_set_exchange(void* p, ExchangeCb cb, void* ctx) { ((Harness*)p)->be->set_exchange(cb, ctx); }
+void hh_set_exchange(void* p, ExchangeCb cb, GatherCb gather, void* ctx) {
+  ((Harness*)p)->be->set_exchange(cb, gather, ctx);
+}
 
 int hh_train(void* p, const char* trace_path) {
   Harness* h = (Harness*)p;
@@ -336,6 +350,7 @@ void hh_counters(void* p, uint64_t* out) {
 }
 // Chain prediction acceptance: hist[j] = selections whose predicted chain matched exactly the
 // next j merges (j = 0..k).
+void hh_set_chain(void* p, int n) { ((Harness*)p)->engine.set_chain(n, 2048); }
 void hh_chain_probe(void* p, int k, int window) { ((Harness*)p)->engine.set_chain_probe((size_t)k, (size_t)window); }
 void hh_chain_hist(void* p, uint64_t* hist, int k) {
   Harness* h = (Harness*)p;

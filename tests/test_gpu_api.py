@@ -125,6 +125,36 @@ def medium_corpus(tmp_path_factory):
     return path
 
 
+@pytest.fixture(scope="module")
+def medium_oracle(medium_corpus, tmp_path_factory):
+    d = tmp_path_factory.mktemp("medo")
+    subprocess.run(["make", "-s", "-C", ORACLE, "port"], check=True)
+    om, ov = str(d / "o.model"), str(d / "o.vocab")
+    subprocess.run([os.path.join(ORACLE, "_build", "bpe_oracle"), medium_corpus, "6000", "0", "0.9995", "20", om, ov],
+                   check=True, stderr=subprocess.DEVNULL)
+    return open(om, "rb").read(), open(ov, "rb").read()
+
+
+@pytest.mark.parametrize("layout,bucket", [("types", 0), ("types", 8), ("stream", 64)])
+def test_exchange_path_matches_oracle(layout, bucket, medium_corpus, medium_oracle, tmp_path):
+    """The multi-GPU path on one GPU: every merge's records go through the RCCL all-gather (a
+    single-rank communicator) and k_xout, small buckets force the overflow round."""
+    t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+    t.set_option("layout", layout)
+    t.set_option("exchange", "local")
+    if bucket:
+        t.set_option("exchange_bucket", bucket)
+    t.load_corpus(medium_corpus)
+    n, model, vocab = _train_bytes(t, tmp_path, "x")
+    st = t.stats()
+    t.destroy()
+    assert (model, vocab) == medium_oracle
+    assert n > 1000
+    assert st["spec_hits"] > 0
+    if bucket:
+        assert st["exchange_overflows"] > 0
+
+
 def test_rollback_restores_stream(medium_corpus):
     """The undo path of speculation (k_unmerge) leaves the corpus bit-identical, including
     a == b runs and pairs spanning many tiles."""

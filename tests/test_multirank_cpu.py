@@ -1,6 +1,6 @@
-"""World-size > 1 path on CPU (gloo): sharding by word ranges + per-merge all-reduce of the delta
-tables must give the reference's bytes, identical on every rank (output bytes
-invariant over world size)."""
+"""World-size > 1 path on CPU (gloo): sharding by word ranges + the per-merge all-gather of every
+rank's delta records must give the reference's bytes, identical on every rank (SURVEY.md §8 e1:
+output bytes invariant over world size), with speculation (overlap or chains) on as on one GPU."""
 import os
 import socket
 import subprocess
@@ -17,10 +17,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("name,layout,world", [("small_v300", "types", 2), ("adv_unk0", "types", 2),
-                                               ("adv_unkm1", "stream", 2), ("ascii1m_unk7_cov09", "types", 3),
-                                               ("utf8_2m_v2000_mpf50", "types", 2)])
-def test_sharded_exchange_matches_reference(name, layout, world, case_corpus, tmp_path):
+@pytest.mark.parametrize("name,layout,world,spec,chain", [
+    ("small_v300", "types", 2, 1, 1), ("adv_unk0", "types", 2, 1, 1), ("adv_unkm1", "stream", 2, 1, 1),
+    ("ascii1m_unk7_cov09", "types", 3, 1, 1), ("utf8_2m_v2000_mpf50", "types", 2, 1, 1),
+    ("utf8_2m_v2000_mpf50", "types", 2, 0, 1), ("ascii1m_unk7_cov09", "stream", 2, 1, 4)])
+def test_sharded_exchange_matches_reference(name, layout, world, spec, chain, case_corpus, tmp_path):
     case, corpus = case_corpus(name)
     cfg = case["config"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
@@ -30,7 +31,7 @@ def test_sharded_exchange_matches_reference(name, layout, world, case_corpus, tm
         e = dict(env, RANK=str(r))
         procs.append(subprocess.Popen([sys.executable, os.path.join(TESTS, "multirank_worker.py"), corpus,
                                        str(cfg["vocab_size"]), str(cfg["unk_id"]), repr(cfg["character_coverage"]),
-                                       str(cfg["min_pair_freq"]), layout, str(tmp_path)],
+                                       str(cfg["min_pair_freq"]), layout, str(tmp_path), str(spec), str(chain)],
                                       env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     outs = [p.communicate(timeout=600)[0].decode(errors="replace") for p in procs]
     for p, o in zip(procs, outs):
@@ -38,7 +39,33 @@ def test_sharded_exchange_matches_reference(name, layout, world, case_corpus, tm
     infos = [open(tmp_path / f"info_r{r}.txt").read().split() for r in range(world)]
     assert all(int(i[0]) == case["merges"] for i in infos)
     assert all(int(i[1]) > 0 for i in infos), "every rank must own a non-empty shard"
+    if spec and case["merges"] > 50:
+        assert all(int(i[2]) > 0 for i in infos), "speculation must confirm guesses under the exchange"
+        assert len({tuple(i[2:]) for i in infos}) == 1, "every rank must make the same guesses"
     for r in range(world):
         assert open(tmp_path / f"trace_r{r}.txt").read() == case["trace"]
     assert open(tmp_path / "mr.model", "rb").read() == case["model_bytes"]
     assert open(tmp_path / "mr.vocab", "rb").read() == case["vocab_bytes"]
+
+
+def test_empty_shard_rank_joins_exchange(oracle_bin, tmp_path):
+    """More ranks than words: a rank with no tiles still takes part in every exchange (an empty
+    bucket) and the output stays the single-rank reference's."""
+    corpus = tmp_path / "tiny.txt"
+    corpus.write_text("abab abab abab cdcd cdcd\n" * 3)
+    world = 4
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
+               OMP_NUM_THREADS="1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(TESTS, "multirank_worker.py"), str(corpus), "262", "0",
+                               "0.995", "2", "types", str(tmp_path), "1", "1"],
+                              env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(world)]
+    outs = [p.communicate(timeout=300)[0].decode(errors="replace") for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+    infos = [open(tmp_path / f"info_r{r}.txt").read().split() for r in range(world)]
+    assert any(int(i[1]) == 0 for i in infos), "the case needs a rank without tiles"
+    subprocess.run([oracle_bin, str(corpus), "262", "0", "0.995", "2", str(tmp_path / "o.model"),
+                    str(tmp_path / "o.vocab")], check=True, stderr=subprocess.DEVNULL)
+    assert (tmp_path / "mr.model").read_bytes() == (tmp_path / "o.model").read_bytes()
+    assert (tmp_path / "mr.vocab").read_bytes() == (tmp_path / "o.vocab").read_bytes()
