@@ -122,6 +122,45 @@ def pmc_traffic(cfg_name, layout):
     return None
 
 
+def pair_count_leg(cfg, path, reps, device=0):
+    """K1 at HBM scale: the same corpus in the stream layout (every occurrence as int32 tokens,
+    the north-star data layout), `reps` x (reset + bpe_init).  k_pair_hist counts the bulk of the
+    stream (every occurrence past each type's first) and is timed alone with HIP events on the
+    trainer's stream; algorithmic bytes = 4 B per token (word headers are the boundaries) + 12 B
+    per tile descriptor (stream mode)."""
+    from shredword.cbase import lib
+    from shredword.trainer import BPETrainer
+    t = BPETrainer(vocab_size=cfg["vocab"], unk_id=cfg["unk"], character_coverage=cfg["cov"], min_pair_freq=cfg["mpf"])
+    t.set_option("log", 0)
+    t.set_option("device", device)
+    t.set_option("layout", "stream")
+    t0 = time.time()
+    t.load_corpus(path)
+    load_s = time.time() - t0
+    lib.bpe_init(t.trainer)  # warm-up
+    t.set_option("timing", 1)
+    t.set_option("clear_stats", 1)
+    for _ in range(reps):
+        t.reset()
+        lib.bpe_init(t.trainer)
+    st = t.stats()
+    t.destroy()
+    n = max(1, st["hist_launches"])
+    us = 1e3 * st["hist_kernel_ms"] / n
+    b = st["hist_kernel_bytes"] / n
+    achieved = b / (us * 1e-6) / 1e9 if us > 0 else None
+    k1_us = 1e3 * st["count_kernel_ms"] / max(1, st["count_launches"])
+    return {
+        "kernel": "k_pair_hist (K1 bulk, stream layout: packed 16-bit LDS pair table, one workgroup per CU)",
+        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS if achieved else None,
+        "avg_launch_us": us, "bytes_per_launch": b, "launches": st["hist_launches"],
+        "k1_total_us": k1_us,
+        "k1_total_GBps": (st["count_kernel_bytes"] / max(1, st["count_launches"])) / (k1_us * 1e-6) / 1e9 if k1_us > 0 else None,
+        "stream_tokens": st["live_tokens"], "tiles": st["num_tiles"], "load_s": load_s,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)

@@ -112,6 +112,9 @@ typedef struct ShredStats {
   uint64_t apply_cycles_combine, apply_cycles_order, apply_cycles_walk;
   uint64_t spec_hits, spec_misses;
   uint64_t exchange_overflows; /* multi-GPU: merges whose records needed a second all-gather */
+  /* stream layout K1 bulk (k_pair_hist, counts of every occurrence past the first of each type) */
+  double hist_kernel_ms, hist_kernel_bytes;
+  uint64_t hist_launches;
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

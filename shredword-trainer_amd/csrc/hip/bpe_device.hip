@@ -1444,6 +1444,90 @@ __global__ __launch_bounds__(kThreads) void k_pair_dense_collect(const u64* cnt,
 }
 
 // ------------------------------------------------------------------------------------------
+// K1 bulk (stream layout, every id a byte): pair counts only, over the tiles past the ft tiles
+// (the first occurrence of every type is packed into tiles [0, ft_tiles), where k_pair_dense
+// takes first touch; every other occurrence repeats a type, so only its counts matter).
+//
+// One 1024-thread workgroup per CU keeps the whole 256 x 256 table in LDS as packed 16-bit
+// counters (two pairs per dword, 128 KiB): a pair occurrence is one ds_add_rtn_u32 at a fixed
+// address, no hashing, no probing, nothing in HBM until the end.  A counter never wraps: the one
+// atomic that takes a half from 0x7FFF to 0x8000 (exactly one per crossing, increments are 1)
+// moves 0x8000 to the HBM table and takes it back off the half; meanwhile at most 16 K other
+// increments can land, so a half stays below 0xC000 and never carries into its neighbour.
+// Each lane streams 2 tiles x 16 tokens per iteration (8 x 16 B loads in flight), and the final
+// flush adds the non-zero halves to the HBM table (one u64 atomic per pair per workgroup).
+constexpr int kHistThreads = 1024;
+constexpr int kHistWaves = kHistThreads / 64;
+constexpr int kHistWords = kDensePairs / 2;
+
+__device__ __forceinline__ void hist_tile(uint32_t* h, const int32_t (&v)[kPer], int32_t nx, int32_t unk, u64* cnt) {
+  uint32_t old[kPer];
+  uint32_t key[kPer];
+  bool on[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int32_t x = v[j];
+    const int32_t y = j + 1 < kPer ? v[j + 1] : nx;
+    on[j] = !is_hdr(x) && !is_hdr(y) && x != unk && y != unk;
+    key[j] = ((uint32_t)x << 8) | ((uint32_t)y & 255u);
+    old[j] = 0;
+    if (on[j]) old[j] = atomicAdd(&h[key[j] >> 1], (key[j] & 1u) ? 0x10000u : 1u);
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint32_t half = (key[j] & 1u) ? (old[j] >> 16) : (old[j] & 0xFFFFu);
+    if (on[j] && half == 0x7FFFu) {
+      atomicSub(&h[key[j] >> 1], (key[j] & 1u) ? 0x80000000u : 0x8000u);
+      atomicAdd(&cnt[key[j]], (u64)0x8000);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kHistThreads) void k_pair_hist(const int32_t* tok, const uint64_t* tile_off,
+                                                             const uint32_t* tile_len, uint32_t t0, uint32_t t1,
+                                                             int32_t unk, u64* cnt) {
+  __shared__ uint32_t h[kHistWords];
+  for (int i = threadIdx.x; i < kHistWords; i += kHistThreads) h[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int p0 = lane * kPer;
+  const uint32_t stride = gridDim.x * kHistWaves;
+  for (uint32_t t = t0 + blockIdx.x * kHistWaves + wid; t < t1; t += 2 * stride) {
+    const uint32_t u = t + stride;
+    const bool two = u < t1;
+    const uint32_t lt = tile_len[t], lu = two ? tile_len[u] : 0u;
+    const int32_t* bt = tok + tile_off[t];
+    const int32_t* bu = tok + (two ? tile_off[u] : tile_off[t]);
+    if (lt <= (uint32_t)kWaveTok && lu <= (uint32_t)kWaveTok) {
+      // both tiles are one wave chunk: all 8 loads in flight together
+      int32_t va[kPer], vb[kPer];
+      load_chunk(bt, 0, lt, p0, va);
+      load_chunk(bu, 0, lu, p0, vb);
+      const int32_t na = next_token(bt, 0, lt, p0, va[0]);
+      const int32_t nb = next_token(bu, 0, lu, p0, vb[0]);
+      hist_tile(h, va, na, unk, cnt);
+      hist_tile(h, vb, nb, unk, cnt);
+      continue;
+    }
+    for (int k = 0; k < 2; ++k) {  // a tile holding one long word: chunk by chunk
+      const uint32_t len = k ? lu : lt;
+      const int32_t* base = k ? bu : bt;
+      for (uint32_t cs = 0; cs < len; cs += kWaveTok) {
+        int32_t v[kPer];
+        load_chunk(base, cs, min((uint32_t)kWaveTok, len - cs), p0, v);
+        hist_tile(h, v, next_token(base, cs, len, p0, v[0]), unk, cnt);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHistWords; i += kHistThreads) {
+    const uint32_t w = h[i];
+    if (w & 0xFFFFu) atomicAdd(&cnt[2 * i], (u64)(w & 0xFFFFu));
+    if (w >> 16) atomicAdd(&cnt[2 * i + 1], (u64)(w >> 16));
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // K6: final token histogram over ids [0, T) (the unk count lands on unk_id when it is in range)
 template <bool kWeighted>
 __global__ __launch_bounds__(kThreads) void k_token_freq(const int32_t* tok, const uint64_t* tile_off,
@@ -1646,6 +1730,9 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
   live_tokens0_ = ts.live;
   live_tokens_est_ = ts.live;
   nentries_ = ts.entries;
+  ft_tiles_ = ts.ft_tiles;
+  ft_live_tokens_ = 0;
+  for (size_t t = 0; t < ft_tiles_; ++t) ft_live_tokens_ += ts.len[t];
   tok_ = dalloc<int32_t>(ts.elems + 4 + kStreamPad, &bytes_alloc_);
   tok0_ = dalloc<int32_t>(ts.elems + 4 + kStreamPad, &bytes_alloc_);
   tile_off_ = dalloc<uint64_t>(ntiles_, &bytes_alloc_);
@@ -1836,18 +1923,31 @@ void Device::count_pairs_dense(int32_t unk_id, uint64_t live, std::vector<PairCo
   HIP_OK(hipMemsetAsync(cnt, 0, kDensePairs * sizeof(u64), S(stream_)));
   HIP_OK(hipMemsetAsync(ft, 0xFF, kDensePairs * sizeof(u64), S(stream_)));
   HIP_OK(hipMemsetAsync(n, 0, sizeof(uint32_t), S(stream_)));
-  DenseCountParams dp{tok_, tile_off_, tile_len_, (uint32_t)ntiles_, weight_, unk_id, cnt, ft};
+  // stream layout: first touch (and counts) from the ft tiles, counts alone from the rest
+  const size_t ft_tiles = layout_ == Layout::kStream ? ft_tiles_ : ntiles_;
+  DenseCountParams dp{tok_, tile_off_, tile_len_, (uint32_t)ft_tiles, weight_, unk_id, cnt, ft};
   int per_cu = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_pair_dense<true>),
                                                       kDenseThreads, 0));
   // >= 32 K tokens per workgroup: each one flushes its LDS table with HBM atomics at the end
-  const size_t by_tokens = (size_t)(live / 32768) + 1;
-  const int grid = (int)std::min<size_t>(std::min<size_t>((ntiles_ + kDenseWaves - 1) / kDenseWaves, by_tokens),
+  const uint64_t ft_live = ft_tiles == ntiles_ ? live : ft_live_tokens_;
+  const size_t by_tokens = (size_t)(ft_live / 32768) + 1;
+  const int grid = (int)std::min<size_t>(std::min<size_t>((ft_tiles + kDenseWaves - 1) / kDenseWaves, by_tokens),
                                          (size_t)cu_count_ * (size_t)std::max(1, per_cu));
   if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[2], S(stream_)));
-  if (layout_ == Layout::kStream) k_pair_dense<false><<<grid, kDenseThreads, 0, S(stream_)>>>(dp);
-  else k_pair_dense<true><<<grid, kDenseThreads, 0, S(stream_)>>>(dp);
-  HIP_OK(hipGetLastError());
+  if (ft_tiles > 0) {
+    if (layout_ == Layout::kStream) k_pair_dense<false><<<grid, kDenseThreads, 0, S(stream_)>>>(dp);
+    else k_pair_dense<true><<<grid, kDenseThreads, 0, S(stream_)>>>(dp);
+    HIP_OK(hipGetLastError());
+  }
+  const bool bulk = ft_tiles < ntiles_;
+  if (bulk) {
+    if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[4], S(stream_)));
+    const size_t hist_grid = std::min<size_t>((ntiles_ - ft_tiles + kHistWaves - 1) / kHistWaves, (size_t)cu_count_);
+    k_pair_hist<<<(int)hist_grid, kHistThreads, 0, S(stream_)>>>(tok_, tile_off_, tile_len_, (uint32_t)ft_tiles,
+                                                                (uint32_t)ntiles_, unk_id, cnt);
+    HIP_OK(hipGetLastError());
+  }
   if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[3], S(stream_)));
   k_pair_dense_collect<<<64, kThreads, 0, S(stream_)>>>(cnt, ft, dout, n);
   HIP_OK(hipGetLastError());
@@ -1865,6 +1965,12 @@ void Device::count_pairs_dense(int32_t unk_id, uint64_t live, std::vector<PairCo
     // layout, 12 B of tile descriptor per tile
     times_.count_bytes += 4.0 * (double)live + 12.0 * (double)ntiles_ +
                           (layout_ == Layout::kTypes ? 8.0 * (double)nentries_ : 0.0);
+    if (bulk) {  // k_pair_hist alone: 4 B per token (headers = word boundaries) + 12 B per tile
+      HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[4], (hipEvent_t)ev_[3]));
+      times_.hist_ms += ms;
+      times_.hist_launches += 1;
+      times_.hist_bytes += 4.0 * (double)(live - ft_live) + 12.0 * (double)(ntiles_ - ft_tiles);
+    }
   }
   for (void* q : {(void*)cnt, (void*)ft, (void*)n, (void*)dout}) HIP_OK(hipFree(q));
 }

@@ -33,6 +33,9 @@ struct KernelTimes {
   uint64_t count_launches = 0;
   double merge_bytes = 0;  // Σ algorithmic bytes of k_merge launches (4 B per live token read)
   double count_bytes = 0;  // Σ algorithmic bytes of k_pair_count (tokens + boundaries + weights)
+  double hist_ms = 0;      // Σ k_pair_hist durations (stream layout K1 bulk: counts only)
+  double hist_bytes = 0;   // Σ its algorithmic bytes (4 B per token + 12 B per tile)
+  uint64_t hist_launches = 0;
 };
 
 class Device : public Backend {
@@ -176,7 +179,7 @@ class Device : public Backend {
   int ordinal_ = 0;
   void* stream_ = nullptr;
   void* aux_stream_ = nullptr;  // wide collect of a slot while the other slot's merge runs
-  void* ev_[4] = {};            // [2],[3]: pair count
+  void* ev_[6] = {};            // [2],[3]: pair count, [4]: k_pair_hist start
   // sampled k_merge launch timing: a ring of event pairs read back without blocking
   static constexpr int kEvPairs = 16;
   void* mev_[kEvPairs][2] = {};
@@ -210,6 +213,8 @@ class Device : public Backend {
   uint32_t* sig_ = nullptr;    // per-tile pair signature (Bloom filter), see k_merge
   unsigned long long* stamps_ = nullptr;  // SHRED_STAMPS diagnostic build only
   uint64_t nentries_ = 0;
+  size_t ft_tiles_ = 0;         // tiles holding one occurrence of every type (TiledStream::ft_tiles)
+  uint64_t ft_live_tokens_ = 0;
   uint64_t live_tokens_est_ = 0;
 
   MergeSlot slot_[2];

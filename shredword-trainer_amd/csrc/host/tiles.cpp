@@ -43,24 +43,55 @@ void pack_tiles(const WordTable& wt, Layout layout, size_t begin, size_t end, Ti
   if (stream && nent == 0 && wt.total_occurrences > 0) fatal("stream layout requested without occurrence ranks");
   end = std::min(end, nent);
   begin = std::min(begin, end);
-  auto rank_of = [&](size_t e) -> uint32_t { return stream ? wt.occurrence_rank[e] : (uint32_t)e; };
+  const size_t n = end - begin;
+  // Stream layout: the first occurrence of every word type in [begin, end) is packed first, in
+  // corpus order, and that block ends on a tile boundary (ft_tiles); the other occurrences follow
+  // in corpus order.  Pair counts and merges are sums over occurrences (order-free), and every
+  // occurrence of a type has the same first touch (rank, position), so K1 takes first touch from
+  // the ft tiles alone and the bulk of the stream only has to be counted.
+  std::vector<uint32_t> order;
+  size_t nfirst = n;
+  if (stream && n > 0) {
+    order.resize(n);
+    std::vector<uint8_t> seen(wt.num_words(), 0);
+    size_t k = 0;
+    for (size_t e = begin; e < end; ++e) {
+      const uint32_t r = wt.occurrence_rank[e];
+      if (!seen[r]) {
+        seen[r] = 1;
+        order[k++] = r;
+      }
+    }
+    nfirst = k;
+    std::fill(seen.begin(), seen.end(), 0);
+    for (size_t e = begin; e < end; ++e) {
+      const uint32_t r = wt.occurrence_rank[e];
+      if (!seen[r]) {
+        seen[r] = 1;
+        continue;
+      }
+      order[k++] = r;
+    }
+  }
+  auto rank_of = [&](size_t i) -> uint32_t { return stream ? order[i] : (uint32_t)(begin + i); };
   auto len_of = [&](uint32_t r) -> uint64_t { return wt.offset[r + 1] - wt.offset[r]; };
 
   TiledStream& ts = *out;
   ts = TiledStream();
   std::vector<size_t> first;
   uint64_t pos = 0, fill = 0;
-  for (size_t e = begin; e < end; ++e) {
-    const uint64_t need = len_of(rank_of(e)) + 1;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t need = len_of(rank_of(i)) + 1;
     if (need >= (1ull << 31)) fatal("word longer than 2^31 tokens");
-    if (fill > 0 && fill + need > (uint64_t)kTileTokens) {
+    if (fill > 0 && (fill + need > (uint64_t)kTileTokens || i == nfirst)) {
       ts.len.push_back((uint32_t)fill);
       pos += (fill + 3) & ~3ull;
       fill = 0;
     }
+    if (i == nfirst) ts.ft_tiles = ts.len.size();
     if (fill == 0) {
       ts.off.push_back(pos);
-      first.push_back(e);
+      first.push_back(i);
     }
     fill += need;
   }
@@ -68,7 +99,8 @@ void pack_tiles(const WordTable& wt, Layout layout, size_t begin, size_t end, Ti
     ts.len.push_back((uint32_t)fill);
     pos += (fill + 3) & ~3ull;
   }
-  first.push_back(end);
+  if (nfirst == n) ts.ft_tiles = ts.len.size();
+  first.push_back(n);
   ts.elems = pos;
   ts.entries = end - begin;
   ts.tok.assign(pos + 4, kHeaderBase);
@@ -76,8 +108,8 @@ void pack_tiles(const WordTable& wt, Layout layout, size_t begin, size_t end, Ti
   auto fill_tiles = [&](size_t t0, size_t t1) {
     for (size_t t = t0; t < t1; ++t) {
       int32_t* dst = ts.tok.data() + ts.off[t];
-      for (size_t e = first[t]; e < first[t + 1]; ++e) {
-        const uint32_t r = rank_of(e);
+      for (size_t i = first[t]; i < first[t + 1]; ++i) {
+        const uint32_t r = rank_of(i);
         *dst++ = (int32_t)((uint32_t)kHeaderBase + r);
         const uint64_t o = wt.offset[r], l = len_of(r);
         std::memcpy(dst, wt.symbols.data() + o, l * sizeof(int32_t));

@@ -2,7 +2,8 @@
 //
 // Entries (distinct words in the "types" layout, word occurrences in corpus order in the
 // "stream" layout) are packed whole into tiles of at most kTileTokens tokens; a word longer than
-// that gets a tile of its own.  Each entry is written as an in-band header INT32_MIN + rank
+// that gets a tile of its own (the stream layout packs the first occurrence of every type
+// first, see pack_tiles).  Each entry is written as an in-band header INT32_MIN + rank
 // followed by its symbol ids.  Tiles start 16-byte aligned.
 #pragma once
 
@@ -25,6 +26,8 @@ struct TiledStream {
   uint64_t elems = 0;
   uint64_t live = 0;           // Σ len
   size_t entries = 0;
+  size_t ft_tiles = 0;         // tiles [0, ft_tiles) hold one occurrence of every type (all tiles in
+                               // the types layout); K1 takes first touch from them alone
   size_t num_tiles() const { return len.size(); }
 };
 

@@ -310,6 +310,9 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
     s->count_kernel_bytes = k.count_bytes;
     s->merge_launches = k.merge_launches;
     s->count_launches = k.count_launches;
+    s->hist_kernel_ms = k.hist_ms;
+    s->hist_kernel_bytes = k.hist_bytes;
+    s->hist_launches = k.hist_launches;
     s->device_bytes = t->dev->device_bytes();
     s->num_tiles = t->dev->num_tiles();
     s->live_tokens = t->dev->live_tokens();
