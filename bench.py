@@ -122,7 +122,7 @@ def pmc_traffic(cfg_name, layout):
     return None
 
 
-def pair_count_leg(cfg, path, reps, device=0):
+def pair_count_leg(cfg, path, reps, device=0, layout="stream"):
     """K1 at HBM scale: the same corpus in the stream layout (every occurrence as int32 tokens,
     the north-star data layout), `reps` x (reset + bpe_init).  k_pair_hist counts the bulk of the
     stream (every occurrence past each type's first) and is timed alone with HIP events on the
@@ -133,7 +133,7 @@ def pair_count_leg(cfg, path, reps, device=0):
     t = BPETrainer(vocab_size=cfg["vocab"], unk_id=cfg["unk"], character_coverage=cfg["cov"], min_pair_freq=cfg["mpf"])
     t.set_option("log", 0)
     t.set_option("device", device)
-    t.set_option("layout", "stream")
+    t.set_option("layout", layout)
     t0 = time.time()
     t.load_corpus(path)
     load_s = time.time() - t0
@@ -171,6 +171,8 @@ def main():
     ap.add_argument("--bytes", type=int, default=0, help="override the corpus size (testing)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pair-count-reps", type=int, default=10,
+                    help="K1 roofline leg on the stream layout of the same corpus (0: skip)")
     args = ap.parse_args()
 
     cfg = dict(CONFIGS[args.config])
@@ -277,8 +279,9 @@ def main():
                 "avg_launch_us": 1e3 * mk_ms, "avg_bytes_per_launch": mk_bytes,
                 "launches_sampled": st["merge_launches"], "launches": merges,
             },
-            "pair_count": {
-                "kernel": "k_pair_count (K1)", "avg_launch_us": 1e3 * k1_ms, "bytes_per_launch": k1_bytes,
+            "pair_count_types": {
+                "kernel": "k_pair_dense (K1 of this train(): types layout, weighted, first touch)",
+                "avg_launch_us": 1e3 * k1_ms, "bytes_per_launch": k1_bytes,
                 "achieved_GBps": (k1_bytes / (k1_ms * 1e-3)) / 1e9 if k1_ms > 0 else None,
             },
             "load_s": load_s, "corpus_gen_s": gen_s,
@@ -293,6 +296,11 @@ def main():
             "speculation": {"hits": st["spec_hits"], "misses": st["spec_misses"],
                             "hit_rate": st["spec_hits"] / max(1, st["spec_hits"] + st["spec_misses"])},
         }
+        if world == 1 and args.pair_count_reps > 0:
+            try:
+                result["pair_count"] = pair_count_leg(cfg, path, args.pair_count_reps, device=local)
+            except Exception as e:
+                result["pair_count"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(cfg, path, args.cpu_seconds)

@@ -22,6 +22,9 @@
 #ifndef SHRED_DELTA_LDS
 #define SHRED_DELTA_LDS 2048
 #endif
+#ifndef SHRED_DENSE_TOK
+#define SHRED_DENSE_TOK 32768
+#endif
 #ifndef SHRED_SIG_BITS
 #define SHRED_SIG_BITS 8192
 #endif
@@ -1456,42 +1459,99 @@ __global__ __launch_bounds__(kThreads) void k_pair_dense_collect(const u64* cnt,
 // increments can land, so a half stays below 0xC000 and never carries into its neighbour.
 // Each lane streams 2 tiles x 16 tokens per iteration (8 x 16 B loads in flight), and the final
 // flush adds the non-zero halves to the HBM table (one u64 atomic per pair per workgroup).
+#ifndef SHRED_HIST_CO
+#define SHRED_HIST_CO 1
+#endif
+#ifndef SHRED_HIST_MODE
+#define SHRED_HIST_MODE 0  // diagnostic 1: no LDS atomics (read ceiling of the access pattern)
+#endif
 constexpr int kHistThreads = 1024;
 constexpr int kHistWaves = kHistThreads / 64;
 constexpr int kHistWords = kDensePairs / 2;
 
-__device__ __forceinline__ void hist_tile(uint32_t* h, const int32_t (&v)[kPer], int32_t nx, int32_t unk, u64* cnt) {
-  uint32_t old[kPer];
-  uint32_t key[kPer];
+// One pair occurrence (x, y) per element: add 1 to its 16-bit half; `old` gets the dword before
+// the add.  Branch-free so that a lane's 16 atomics issue back to back behind one wait: an
+// inactive element adds 0 to a per-lane dummy word past the table (distinct banks).
+__device__ __forceinline__ void hist_add(uint32_t* h, int32_t x, int32_t y, int32_t unk, int lane, uint32_t& key,
+                                         uint32_t& old, bool& on, uint32_t& sink) {
+  // bitwise, not &&: short-circuit evaluation compiles to a branch per element
+  on = (bool)((unsigned)(x >= kHeaderLimit) & (unsigned)(y >= kHeaderLimit) & (unsigned)(x != unk) &
+              (unsigned)(y != unk));
+  key = ((uint32_t)x << 8) | ((uint32_t)y & 255u);
+#if SHRED_HIST_MODE == 1
+  old = 0;
+  if (on) sink += key;
+#else
+  const uint32_t a = on ? key >> 1 : (uint32_t)(kHistWords + lane);
+  const uint32_t inc = on ? ((key & 1u) ? 0x10000u : 1u) : 0u;
+  old = __hip_atomic_fetch_add(&h[a], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+}
+__device__ __forceinline__ void hist_fix(uint32_t* h, uint32_t key, uint32_t old, bool on, u64* cnt) {
+  const uint32_t half = (key & 1u) ? (old >> 16) : (old & 0xFFFFu);
+  if (on && half == 0x7FFFu) {
+    atomicSub(&h[key >> 1], (key & 1u) ? 0x80000000u : 0x8000u);
+    atomicAdd(&cnt[key], (u64)0x8000);
+  }
+}
+
+// 16 tokens per lane, lane-contiguous (load_chunk order): pairs (v[j], v[j+1]), then (v[15], nx).
+__device__ __forceinline__ void hist_tile(uint32_t* h, const int32_t (&v)[kPer], int32_t nx, int32_t unk, u64* cnt,
+                                          uint32_t& sink) {
+  uint32_t old[kPer], key[kPer];
   bool on[kPer];
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int32_t x = v[j];
-    const int32_t y = j + 1 < kPer ? v[j + 1] : nx;
-    on[j] = !is_hdr(x) && !is_hdr(y) && x != unk && y != unk;
-    key[j] = ((uint32_t)x << 8) | ((uint32_t)y & 255u);
-    old[j] = 0;
-    if (on[j]) old[j] = atomicAdd(&h[key[j] >> 1], (key[j] & 1u) ? 0x10000u : 1u);
-  }
+  for (int j = 0; j < kPer; ++j)
+    hist_add(h, v[j], j + 1 < kPer ? v[j + 1] : nx, unk, threadIdx.x & 63, key[j], old[j], on[j], sink);
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const uint32_t half = (key[j] & 1u) ? (old[j] >> 16) : (old[j] & 0xFFFFu);
-    if (on[j] && half == 0x7FFFu) {
-      atomicSub(&h[key[j] >> 1], (key[j] & 1u) ? 0x80000000u : 0x8000u);
-      atomicAdd(&cnt[key[j]], (u64)0x8000);
+  for (int j = 0; j < kPer; ++j) hist_fix(h, key[j], old[j], on[j], cnt);
+}
+
+// Coalesced order for a tile of <= 1024 tokens: quad k of lane l holds tokens 256 k + 4 l .. +3,
+// so each 16-B load instruction reads 1 KiB contiguous.  The token after a quad is lane l+1's
+// first of the same quad (DPP), or for lane 63 lane 0's first of quad k+1.
+__device__ __forceinline__ void load_tile_co(const int32_t* base, uint32_t len, int lane, int32_t (&v)[kPer]) {
+  const int4* q = reinterpret_cast<const int4*>(base) + lane;
+  int4 x[kPer / 4];
+#pragma unroll
+  for (int k = 0; k < kPer / 4; ++k) x[k] = q[64 * k];
+#pragma unroll
+  for (int k = 0; k < kPer / 4; ++k) {
+    const int p = 256 * k + 4 * lane;
+    v[4 * k] = p < (int)len ? x[k].x : kPad;
+    v[4 * k + 1] = p + 1 < (int)len ? x[k].y : kPad;
+    v[4 * k + 2] = p + 2 < (int)len ? x[k].z : kPad;
+    v[4 * k + 3] = p + 3 < (int)len ? x[k].w : kPad;
+  }
+}
+__device__ __forceinline__ void hist_tile_co(uint32_t* h, const int32_t (&v)[kPer], int lane, int32_t unk, u64* cnt,
+                                             uint32_t& sink) {
+  uint32_t old[kPer], key[kPer];
+  bool on[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer / 4; ++k) {
+    int32_t nx = wave_next(v[4 * k]);
+    if (lane == 63) nx = k + 1 < kPer / 4 ? (int32_t)lane_read((uint32_t)v[4 * k + 4], 0) : kPad;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = 4 * k + e;
+      hist_add(h, v[j], e < 3 ? v[j + 1] : nx, unk, lane, key[j], old[j], on[j], sink);
     }
   }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) hist_fix(h, key[j], old[j], on[j], cnt);
 }
 
 __global__ __launch_bounds__(kHistThreads) void k_pair_hist(const int32_t* tok, const uint64_t* tile_off,
                                                              const uint32_t* tile_len, uint32_t t0, uint32_t t1,
                                                              int32_t unk, u64* cnt) {
-  __shared__ uint32_t h[kHistWords];
-  for (int i = threadIdx.x; i < kHistWords; i += kHistThreads) h[i] = 0;
+  __shared__ uint32_t h[kHistWords + 64];  // + per-lane dummy words
+  for (int i = threadIdx.x; i < kHistWords + 64; i += kHistThreads) h[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int p0 = lane * kPer;
   const uint32_t stride = gridDim.x * kHistWaves;
+  uint32_t sink = 0;
   for (uint32_t t = t0 + blockIdx.x * kHistWaves + wid; t < t1; t += 2 * stride) {
     const uint32_t u = t + stride;
     const bool two = u < t1;
@@ -1501,12 +1561,19 @@ __global__ __launch_bounds__(kHistThreads) void k_pair_hist(const int32_t* tok, 
     if (lt <= (uint32_t)kWaveTok && lu <= (uint32_t)kWaveTok) {
       // both tiles are one wave chunk: all 8 loads in flight together
       int32_t va[kPer], vb[kPer];
+#if SHRED_HIST_CO
+      load_tile_co(bt, lt, lane, va);
+      load_tile_co(bu, lu, lane, vb);
+      hist_tile_co(h, va, lane, unk, cnt, sink);
+      hist_tile_co(h, vb, lane, unk, cnt, sink);
+#else
       load_chunk(bt, 0, lt, p0, va);
       load_chunk(bu, 0, lu, p0, vb);
       const int32_t na = next_token(bt, 0, lt, p0, va[0]);
       const int32_t nb = next_token(bu, 0, lu, p0, vb[0]);
-      hist_tile(h, va, na, unk, cnt);
-      hist_tile(h, vb, nb, unk, cnt);
+      hist_tile(h, va, na, unk, cnt, sink);
+      hist_tile(h, vb, nb, unk, cnt, sink);
+#endif
       continue;
     }
     for (int k = 0; k < 2; ++k) {  // a tile holding one long word: chunk by chunk
@@ -1515,10 +1582,13 @@ __global__ __launch_bounds__(kHistThreads) void k_pair_hist(const int32_t* tok, 
       for (uint32_t cs = 0; cs < len; cs += kWaveTok) {
         int32_t v[kPer];
         load_chunk(base, cs, min((uint32_t)kWaveTok, len - cs), p0, v);
-        hist_tile(h, v, next_token(base, cs, len, p0, v[0]), unk, cnt);
+        hist_tile(h, v, next_token(base, cs, len, p0, v[0]), unk, cnt, sink);
       }
     }
   }
+#if SHRED_HIST_MODE == 1
+  if (sink == 0x12345678u) h[0] = sink;  // keeps the loads alive in the diagnostic build
+#endif
   __syncthreads();
   for (int i = threadIdx.x; i < kHistWords; i += kHistThreads) {
     const uint32_t w = h[i];
@@ -1929,9 +1999,9 @@ void Device::count_pairs_dense(int32_t unk_id, uint64_t live, std::vector<PairCo
   int per_cu = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_pair_dense<true>),
                                                       kDenseThreads, 0));
-  // >= 32 K tokens per workgroup: each one flushes its LDS table with HBM atomics at the end
+  // >= SHRED_DENSE_TOK tokens per workgroup: each one flushes its LDS table with HBM atomics
   const uint64_t ft_live = ft_tiles == ntiles_ ? live : ft_live_tokens_;
-  const size_t by_tokens = (size_t)(ft_live / 32768) + 1;
+  const size_t by_tokens = (size_t)(ft_live / SHRED_DENSE_TOK) + 1;
   const int grid = (int)std::min<size_t>(std::min<size_t>((ft_tiles + kDenseWaves - 1) / kDenseWaves, by_tokens),
                                          (size_t)cu_count_ * (size_t)std::max(1, per_cu));
   if (timing_) HIP_OK(hipEventRecord((hipEvent_t)ev_[2], S(stream_)));

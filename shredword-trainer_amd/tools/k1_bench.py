@@ -21,13 +21,14 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--bytes", type=int, default=0)
+    ap.add_argument("--layout", default="stream")
     args = ap.parse_args()
     cfg = dict(bench.CONFIGS[args.config])
     if args.bytes:
         cfg["bytes"] = args.bytes
     path = bench.corpus_path(cfg, args.config)
     bench.ensure_corpus(cfg, path)
-    print(json.dumps(bench.pair_count_leg(cfg, path, args.reps)), flush=True)
+    print(json.dumps(bench.pair_count_leg(cfg, path, args.reps, layout=args.layout)), flush=True)
 
 
 if __name__ == "__main__":
