@@ -108,13 +108,16 @@ PMC_NOTE = ("HBM bytes per k_merge launch from rocprofv3 --pmc FETCH_SIZE / WRIT
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def pmc_traffic(cfg_name, layout):
-    """Measured HBM bytes per k_merge launch for this workload, from the committed PMC summary."""
+def pmc_traffic(cfg_name, layout, kernel=None):
+    """Measured HBM bytes per launch of `kernel` (default k_merge) for this workload, from the
+    committed PMC summaries (profiles/*_<config>_<layout>*_pmc_traffic.json)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(HERE, "profiles", f"*_{cfg_name}_{layout}_pmc_traffic.json")), reverse=True):
+    if kernel is None:
+        kernel = "k_merge<true>" if layout == "types" else "k_merge<false>"
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", f"*_{cfg_name}_{layout}*_pmc_traffic.json")), reverse=True):
         try:
             k = json.load(open(path))["kernels"]
-            ent = k.get("k_merge<true>" if layout == "types" else "k_merge<false>")
+            ent = k.get(kernel)
             if ent:
                 return ent["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
@@ -154,6 +157,9 @@ def pair_count_leg(cfg, path, reps, device=0, layout="stream"):
         "kernel": "k_pair_hist (K1 bulk, stream layout: packed 16-bit LDS pair table, one workgroup per CU)",
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS if achieved else None,
+        "traffic": pmc_traffic(cfg.get("name", "c2"), "stream", "k_pair_hist"),
+        "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/k1_bench.py, "
+                          "profiles/r01_<config>_stream_k1_pmc_traffic.json",
         "avg_launch_us": us, "bytes_per_launch": b, "launches": st["hist_launches"],
         "k1_total_us": k1_us,
         "k1_total_GBps": (st["count_kernel_bytes"] / max(1, st["count_launches"])) / (k1_us * 1e-6) / 1e9 if k1_us > 0 else None,
@@ -175,7 +181,7 @@ def main():
                     help="K1 roofline leg on the stream layout of the same corpus (0: skip)")
     args = ap.parse_args()
 
-    cfg = dict(CONFIGS[args.config])
+    cfg = dict(CONFIGS[args.config], name=args.config)
     if args.bytes:
         cfg["bytes"] = args.bytes
     rank = int(os.environ.get("RANK", "0"))

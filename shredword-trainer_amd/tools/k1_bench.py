@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--bytes", type=int, default=0)
     ap.add_argument("--layout", default="stream")
     args = ap.parse_args()
-    cfg = dict(bench.CONFIGS[args.config])
+    cfg = dict(bench.CONFIGS[args.config], name=args.config)
     if args.bytes:
         cfg["bytes"] = args.bytes
     path = bench.corpus_path(cfg, args.config)
