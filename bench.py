@@ -10,9 +10,10 @@ vocab_size=8192 (min_pair_freq 2000, coverage 0.995, unk 0 = the reference Pytho
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--layout types|stream]
 
 N > 1 runs under torch.distributed.run, one process per GPU: the word table is sharded by
-contiguous word ranges and each merge all-reduces the neighbour-delta tables over RCCL.  Every
-rank performs the same merges, so ``value`` = merges / max-over-ranks time (fixed corpus:
-strong scaling).  Rank 0 prints one JSON line.
+contiguous word ranges and each merge all-gathers the ranks' compacted neighbour-delta records
+over RCCL.  Every rank performs the same merges, so ``value`` = merges / max-over-ranks time
+(fixed corpus: strong scaling).  The K1 leg (``pair_count``) runs on every rank over its shard of
+the stream layout and reports aggregate HBM GB/s.  Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -97,7 +98,19 @@ def cpu_baseline(cfg, path, seconds):
         "sample": (f"first {merges} merges (train() capped at {seconds:.0f} s, load {float(fields['load']):.1f} s "
                    f"excluded) of the same corpus/config, oracle/bpe_oracle.c pinned to 1 core of {cpu} "
                    f"(nproc={os.cpu_count()})"),
+        "calibration": calibration_note(),
     }
+
+
+def calibration_note():
+    """The port's speed relative to the reference itself (tests/golden/cpu_calibration.json)."""
+    try:
+        rows = json.load(open(os.path.join(REPO, "tests", "golden", "cpu_calibration.json")))["rows"]
+        ratios = ", ".join(f"{r['train_time_ratio_port_over_reference']:.2f}" for r in rows)
+        return (f"port train time / reference train time = {ratios} on C1 and 100 MB "
+                f"(same outputs, 1 core each): the reference itself is slower than this baseline")
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 PMC_NOTE = ("HBM bytes per k_merge launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, "
@@ -125,12 +138,14 @@ def pmc_traffic(cfg_name, layout, kernel=None):
     return None
 
 
-def pair_count_leg(cfg, path, reps, device=0, layout="stream"):
+def pair_count_leg(cfg, path, reps, device=0, layout="stream", dist=None):
     """K1 at HBM scale: the same corpus in the stream layout (every occurrence as int32 tokens,
     the north-star data layout), `reps` x (reset + bpe_init).  k_pair_hist counts the bulk of the
     stream (every occurrence past each type's first) and is timed alone with HIP events on the
     trainer's stream; algorithmic bytes = 4 B per token (word headers are the boundaries) + 12 B
-    per tile descriptor (stream mode)."""
+    per tile descriptor (stream mode).  Under N ranks every rank counts its own
+    shard of the stream (the per-rank lists are merged over RCCL inside bpe_init) and the leg
+    reports the aggregate: sum over ranks of bytes per launch / the slowest rank's launch time."""
     from shredword.cbase import lib
     from shredword.trainer import BPETrainer
     t = BPETrainer(vocab_size=cfg["vocab"], unk_id=cfg["unk"], character_coverage=cfg["cov"], min_pair_freq=cfg["mpf"])
@@ -151,6 +166,13 @@ def pair_count_leg(cfg, path, reps, device=0, layout="stream"):
     n = max(1, st["hist_launches"])
     us = 1e3 * st["hist_kernel_ms"] / n
     b = st["hist_kernel_bytes"] / n
+    if dist is not None:
+        import torch
+        tb = torch.tensor([b], dtype=torch.float64)
+        dist.all_reduce(tb, op=dist.ReduceOp.SUM)
+        tu = torch.tensor([us], dtype=torch.float64)
+        dist.all_reduce(tu, op=dist.ReduceOp.MAX)
+        b, us = float(tb.item()), float(tu.item())
     achieved = b / (us * 1e-6) / 1e9 if us > 0 else None
     k1_us = 1e3 * st["count_kernel_ms"] / max(1, st["count_launches"])
     return {
@@ -164,7 +186,22 @@ def pair_count_leg(cfg, path, reps, device=0, layout="stream"):
         "k1_total_us": k1_us,
         "k1_total_GBps": (st["count_kernel_bytes"] / max(1, st["count_launches"])) / (k1_us * 1e-6) / 1e9 if k1_us > 0 else None,
         "stream_tokens": st["live_tokens"], "tiles": st["num_tiles"], "load_s": load_s,
+        "ranks": 1 if dist is None else dist.get_world_size(),
+        "aggregate": "sum of per-rank bytes / slowest rank's avg launch" if dist is not None else None,
     }
+
+
+def hbm_probe_leg(device=0, nbytes=4 << 30, reps=10):
+    """Achievable HBM bandwidth on this box: streaming read and copy kernels
+    of the library (shred_hbm_probe), beside the nominal 8 TB/s peak."""
+    import ctypes
+    from shredword.cbase import lib
+    r, c = ctypes.c_double(), ctypes.c_double()
+    if lib.shred_hbm_probe(device, nbytes, reps, ctypes.byref(r), ctypes.byref(c)) != 0:
+        return {"error": "shred_hbm_probe failed"}
+    return {"read_GBps": r.value, "copy_GBps": c.value, "bytes": nbytes, "reps": reps,
+            "read_frac_of_nominal": r.value / HBM_PEAK_GBS,
+            "kernels": "k_hbm_read (4 x 16 B nontemporal loads per lane in flight), k_hbm_copy"}
 
 
 def main():
@@ -247,6 +284,14 @@ def main():
             os.path.join(tmpd, f"bench_r{rank}.vocab").encode())
     t.destroy()
 
+    # K1 HBM leg (the metric's "pair-count HBM GB/s"): every rank counts its stream shard
+    pair_count = None
+    if args.pair_count_reps > 0:
+        try:
+            pair_count = pair_count_leg(cfg, path, args.pair_count_reps, device=local, dist=dist)
+        except Exception as e:
+            pair_count = {"error": repr(e)}
+
     if rank == 0:
         mk_ms = st["merge_kernel_ms"] / max(1, st["merge_launches"])
         mk_bytes = st["merge_kernel_bytes"] / max(1, st["merge_launches"])
@@ -302,11 +347,15 @@ def main():
             "speculation": {"hits": st["spec_hits"], "misses": st["spec_misses"],
                             "hit_rate": st["spec_hits"] / max(1, st["spec_hits"] + st["spec_misses"])},
         }
-        if world == 1 and args.pair_count_reps > 0:
-            try:
-                result["pair_count"] = pair_count_leg(cfg, path, args.pair_count_reps, device=local)
-            except Exception as e:
-                result["pair_count"] = {"error": repr(e)}
+        if pair_count is not None:
+            result["pair_count"] = pair_count
+        try:
+            result["hbm_achievable"] = hbm_probe_leg(device=local)
+            if (result.get("pair_count") or {}).get("achieved"):
+                result["pair_count"]["frac_of_achievable_read"] = (
+                    result["pair_count"]["achieved"] / world / result["hbm_achievable"]["read_GBps"])
+        except Exception as e:
+            result["hbm_achievable"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 result["cpu_baseline"] = cpu_baseline(cfg, path, args.cpu_seconds)

@@ -121,6 +121,11 @@ int shred_get_stats(const Trainer* trainer, ShredStats* out);
 /* Number of usable HIP devices (0 without a GPU); never initialises more than the runtime. */
 int shred_device_count(void);
 
+/* Measurement: achievable HBM bandwidth of `device`, a streaming read and a
+ * streaming copy of `bytes`, `reps` timed launches each; GB/s of bytes moved (copy counts read +
+ * write).  Returns 0, or -1 without a device / on allocation failure. */
+int shred_hbm_probe(int device, size_t bytes, int reps, double* read_gbps, double* copy_gbps);
+
 /* Multi-GPU (one process per GPU, RCCL over xGMI): rank 0 calls shred_dist_unique_id, the
  * bytes are broadcast out of band (torch.distributed), then every rank calls shred_dist_init
  * before create_trainer.  Trainers then shard the word table and all-reduce the per-merge

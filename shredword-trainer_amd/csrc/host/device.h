@@ -42,6 +42,9 @@ class Device : public Backend {
  public:
   // True when a HIP device is usable; otherwise *why says what is missing.
   static bool available(std::string* why);
+  // Achievable HBM bandwidth on `ordinal` (streaming read and copy of `bytes`, `reps` timed
+  // launches each, HIP events); GB/s of bytes moved.  0, or -1 without a device.
+  static int hbm_probe(int ordinal, size_t bytes, int reps, double* read_gbps, double* copy_gbps);
 
   explicit Device(int device_ordinal);
   ~Device();

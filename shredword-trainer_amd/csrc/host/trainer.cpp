@@ -345,6 +345,10 @@ int shred_device_count(void) {
   return n;
 }
 
+int shred_hbm_probe(int device, size_t bytes, int reps, double* read_gbps, double* copy_gbps) {
+  return Device::hbm_probe(device, bytes, reps, read_gbps, copy_gbps);
+}
+
 int shred_dist_unique_id(void* out, size_t cap) { return dist_unique_id(out, cap); }
 int shred_dist_init(int rank, int world, const void* id, size_t len, int device) {
   return dist_init(rank, world, id, len, device);

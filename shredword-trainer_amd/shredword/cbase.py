@@ -101,6 +101,8 @@ if hasattr(lib, "shred_probe_rollback"):  # diagnostics (absent from older build
     lib.shred_debug_tokens.argtypes, lib.shred_debug_tokens.restype = [Trainer, POINTER(c_int32), c_size_t], c_int64
 lib.shred_get_stats.argtypes, lib.shred_get_stats.restype = [Trainer, POINTER(ShredStats)], c_int
 lib.shred_device_count.argtypes, lib.shred_device_count.restype = [], c_int
+lib.shred_hbm_probe.argtypes = [c_int, c_size_t, c_int, POINTER(c_double), POINTER(c_double)]
+lib.shred_hbm_probe.restype = c_int
 lib.shred_dist_unique_id.argtypes, lib.shred_dist_unique_id.restype = [c_void_p, c_size_t], c_int
 lib.shred_dist_init.argtypes, lib.shred_dist_init.restype = [c_int, c_int, c_void_p, c_size_t, c_int], c_int
 lib.shred_dist_finalize.argtypes, lib.shred_dist_finalize.restype = [], c_int
