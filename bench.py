@@ -321,7 +321,9 @@ def main():
                 "symbols": st["num_symbols"], "occurrences": st["num_occurrences"], "tiles": st["num_tiles"],
             },
             "roofline": {
-                "kernel": "k_merge (signature filter + fused match/delta/compaction, K2+K3)",
+                "kernel": ("k_resident (LDS-resident merge loop, K2+K3: per-merge device time from the "
+                           "leader's dispatch to the host flag, s_memrealtime)" if st["resident_launches"]
+                           else "k_merge (signature filter + fused match/delta/compaction, K2+K3)"),
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": pmc_traffic(args.config, args.layout),
@@ -335,6 +337,8 @@ def main():
                 "avg_launch_us": 1e3 * k1_ms, "bytes_per_launch": k1_bytes,
                 "achieved_GBps": (k1_bytes / (k1_ms * 1e-3)) / 1e9 if k1_ms > 0 else None,
             },
+            "resident": {"launches": st["resident_launches"], "ms": st["resident_ms"],
+                         "note": "k_resident launch durations (HIP events): one persistent launch per train()"},
             "load_s": load_s, "corpus_gen_s": gen_s,
             "us_per_merge": 1e6 * elapsed / max(1, merges),
             "merge_kernel_share": (mk_ms * 1e-3 * merges) / elapsed if elapsed > 0 else None,

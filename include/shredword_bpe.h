@@ -82,6 +82,9 @@ int loadVocab(void* trainer, const char* path);
  *                               most 8)
  *   exchange = local | off      test: run the multi-GPU records exchange over a single-rank RCCL
  *                               communicator (before load_corpus)
+ *   resident = 0 | 1            LDS-resident merge loop (default 1): when the distinct-word
+ *                               table fits the chip's LDS, the merge loop runs as one persistent
+ *                               launch holding the table in LDS (results are identical either way)
  *   exchange_bucket = <n>       multi-GPU: records per rank in the fixed all-gather bucket
  *                               (default 1024; larger record sets take a second round)
  * Returns 0, or -1 for an unknown key/value. */
@@ -115,6 +118,9 @@ typedef struct ShredStats {
   /* stream layout K1 bulk (k_pair_hist, counts of every occurrence past the first of each type) */
   double hist_kernel_ms, hist_kernel_bytes;
   uint64_t hist_launches;
+  /* LDS-resident merge loop: k_resident launches and their summed durations (HIP events) */
+  uint64_t resident_launches;
+  double resident_ms;
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

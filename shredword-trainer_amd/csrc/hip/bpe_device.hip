@@ -382,7 +382,8 @@ struct DeltaLds {
   uint32_t spill;  // some delta went to the global tables
 };
 
-__device__ __forceinline__ void delta_global(const MergeParams& p, uint32_t key, u64 w, u64 ft) {
+template <class P>
+__device__ __forceinline__ void delta_global(const P& p, uint32_t key, u64 w, u64 ft) {
   atomicAdd(&p.dsum[key], w);
   const u64 old = atomicMin(&p.dft[key], ft);
   if (old == kEmpty64) {  // exactly one toucher sees MAX
@@ -390,7 +391,8 @@ __device__ __forceinline__ void delta_global(const MergeParams& p, uint32_t key,
   }
 }
 
-__device__ __forceinline__ void delta_emit(DeltaLds& h, const MergeParams& p, uint32_t key, u64 w, u64 ft) {
+template <class P>
+__device__ __forceinline__ void delta_emit(DeltaLds& h, const P& p, uint32_t key, u64 w, u64 ft) {
   uint32_t s = (key * 2654435761u) >> (32 - __builtin_ctz(kDeltaLdsW));
   for (int probe = 0; probe < 16; ++probe) {
     const uint32_t prev = atomicCAS(&h.key[s], kEmpty32, key);
@@ -947,6 +949,796 @@ __global__ __launch_bounds__(kThreads) void k_merge(MergeParams p) {
       sys_flag(&p.hcount[1], p.seq);
     }
     STAMP(7);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K2+K3 resident: the merge loop as ONE persistent launch with the word table held in LDS.
+//
+// When the types table fits the chip's LDS (256 CUs x ~100 KB: C2's 17 MB), workgroup w (one
+// per CU) copies its contiguous range of tiles and their word weights into LDS once and keeps
+// them there for the whole merge loop, so a merge never reads the table from HBM.  The host
+// posts each merge in a mailbox in pinned host memory; workgroup 0 (the leader) is the only
+// poller of host memory (pollers of one host line serialise over PCIe: 256 of them cost 200 us
+// per command on MI355X, one costs ~3 us) and hands the merge to its participants — the owners
+// of the merge's candidate tiles from the host tile index, or every workgroup — through one
+// 8-byte go word per workgroup on a 128-B line of its own (sc1 store after the sc1 command
+// stores and a vmcnt drain; each workgroup polls only its own word).  A participant applies the
+// merge to its tiles in LDS exactly as k_merge does to a single-chunk tile, reduces the
+// neighbour deltas in an LDS hash, publishes them to its region, and takes a ticket among the
+// participants; the last one gathers the regions into the host-visible records and raises the
+// host flag, as k_merge's fused completion does.  A STOP command (or a poll time-out) writes the
+// tiles back to HBM and ends the launch, so the HBM stream is current whenever the host uses it.
+constexpr int kResDeltaW = 1024;         // LDS delta slots per workgroup (spills go to HBM)
+constexpr int kResSigBits = 4096;        // per-tile pair signature held in LDS (Bloom, 2 hashes)
+constexpr int kResSigWords = kResSigBits / 32;
+constexpr uint32_t kResSigRebuild = 192;  // pairs added to a tile's signature before it is rebuilt
+constexpr uint32_t kResMaxTiles = 256;   // tiles one workgroup may own
+constexpr uint32_t kOpMerge = 1, kOpStop = 2, kOpTimeout = 3;
+
+constexpr uint32_t kResRing = 8;         // host command ring, device command ring, per-workgroup queues
+constexpr uint32_t kOpUnmerge = 4;
+
+// One host command (pinned host memory, written by the host; only the leader reads it).
+struct ResCmd {
+  uint32_t seq;     // written last (release): the command number; the entry is cmd[seq % kResRing]
+  uint32_t op;      // kOpMerge, kOpUnmerge (expand X -> a b where the last merge matched), kOpStop
+  int32_t a, b, X;
+  uint32_t slot;    // merge: which of the two record slots completes it
+  uint32_t nparts;  // participants; == grid: every workgroup (parts[] unused)
+  uint32_t pad;
+  uint32_t parts[kMaxMergeGroups];
+};
+struct ResMbox {
+  ResCmd cmd[kResRing];
+};
+
+// The per-merge device tables and host-visible buffers of one slot (as k_merge's MergeSlot).
+struct ResSlot {
+  u64* dsum;
+  u64* dft;
+  uint32_t* dlist;
+  uint32_t* dcount;   // [0] touched global slots
+  uint32_t* done;     // tickets: [0..7] shards, [8] top
+  DeltaRecord* out;   // host-visible records
+  uint32_t* hcount;   // host-visible: [0] records, [1] flag = seq, [2] matched tiles
+  u64* hstats;        // host-visible: [0] occurrences, [1] tokens rewritten, [2] device ticks of the merge
+  uint32_t* hmlist;   // host-visible matched tiles
+  uint32_t* rhdr;     // per-participant regions (as k_merge's)
+  u64* rrec;
+  uint32_t* rtile;
+};
+
+struct ResParams {
+  int32_t* tok;
+  const uint64_t* tile_off;
+  uint32_t* tile_len;
+  const uint64_t* weight;
+  const uint32_t* wg_tiles;  // grid + 1: workgroup w owns tiles [wg_tiles[w], wg_tiles[w+1])
+  const uint32_t* wg_rank;   // grid + 1: ... and the weights of ranks [wg_rank[w], wg_rank[w+1])
+  const uint32_t* tile_lofs; // per tile: word offset in its owner's LDS token area (multiple of 4)
+  uint32_t tok_words;        // LDS token area (words, multiple of 4, incl. one chunk of read slack)
+  uint32_t w_words;          // LDS weight area (u64 entries, even)
+  const ResMbox* mbox;
+  uint32_t* cmd;             // device command ring: kResRing x 8 words [a, b, X, nparts, slot, op, stamp lo, hi]
+  u64* q;                    // per-workgroup queues: kResRing entries each (zeroed before the launch)
+  uint32_t* status;          // host-visible: [0] kOpTimeout once the leader gave up waiting
+  uint32_t seq0;             // first command number of this launch
+  uint32_t leader_polls;     // idle leader iterations before the launch ends itself
+  uint32_t keys_per_merge, slot_cap;
+  ResSlot sl[2];
+  uint32_t* dbg;      // diagnostic (SHREDWORD_RESIDENT_DEBUG): per workgroup [phase, last seq, pi, T]
+  u64* stamps;        // diagnostic: per participant [go seen, work done, loop cycles, -] (s_memrealtime)
+};
+
+struct ResDelta {
+  uint32_t key[kResDeltaW];
+  u64 sum[kResDeltaW];
+  u64 ft[kResDeltaW];
+  uint32_t spill;
+};
+
+// Queue entry: seq (32) | count (16, this workgroup's entry number, 1-based) | pi (8) | op (8).
+__device__ __forceinline__ u64 q_entry(uint32_t seq, uint32_t cnt, uint32_t pi, uint32_t op) {
+  return (u64)seq | ((u64)(cnt & 0xFFFFu) << 32) | ((u64)(pi & 0xFFu) << 48) | ((u64)op << 56);
+}
+
+__device__ __forceinline__ void res_sig_bits(int32_t x, int32_t y, uint32_t* h1, uint32_t* h2) {
+  uint32_t k = (uint32_t)x * 0x9E3779B1u ^ ((uint32_t)y + 0x7F4A7C15u) * 0x85EBCA77u;
+  k ^= k >> 15;
+  k *= 0x2C1B3C6Du;
+  k ^= k >> 12;
+  k *= 0x297A2D39u;
+  k ^= k >> 15;
+  *h1 = k & (kResSigBits - 1);
+  *h2 = (k >> 16) & (kResSigBits - 1);
+}
+__device__ __forceinline__ bool res_sig_test(const uint32_t* sg, int32_t x, int32_t y) {
+  uint32_t h1, h2;
+  res_sig_bits(x, y, &h1, &h2);
+  return ((sg[h1 >> 5] >> (h1 & 31)) & 1u) && ((sg[h2 >> 5] >> (h2 & 31)) & 1u);
+}
+// Rebuilds a tile's LDS signature from its tokens t[0, len) (one wave).
+__device__ __forceinline__ void res_sig_build(uint32_t* sg, const int32_t* t, uint32_t len, int lane) {
+  for (int w = lane; w < kResSigWords; w += 64) sg[w] = 0;
+  wave_lds_sync();
+  for (uint32_t i = (uint32_t)lane; i + 1 < len; i += 64) {
+    const int32_t x = t[i], y = t[i + 1];
+    if (!is_hdr(x) && !is_hdr(y)) {
+      uint32_t h1, h2;
+      res_sig_bits(x, y, &h1, &h2);
+      atomicOr(&sg[h1 >> 5], 1u << (h1 & 31));
+      atomicOr(&sg[h2 >> 5], 1u << (h2 & 31));
+    }
+  }
+  wave_lds_sync();
+}
+
+__device__ __forceinline__ uint32_t host_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One wave applies (a, b) -> X to a single-chunk tile held in LDS at tb (live length *len):
+// k_merge's per-chunk logic with no carries (the tile is its own first and last chunk).
+// Returns the occurrences merged; the tile is compacted in place and *len updated.
+template <bool kWeighted>
+__device__ __forceinline__ uint32_t res_merge_tile(int32_t* tb, uint32_t* lenp, uint32_t* sg, uint32_t* sgadd, int32_t* st,
+                                                   const u64* s_w,
+                                                   uint32_t r0, int32_t a, int32_t b, int32_t X, ResDelta& h,
+                                                   const ResSlot& p, uint32_t slot_cap, int lane, u64* n_written,
+                                                   u64* cy) {
+#define RCY(k) if (cy) cy[k] = __builtin_amdgcn_s_memtime()
+  if (!res_sig_test(sg, a, b)) return 0;  // the pair cannot be in this tile
+  const uint32_t len = *lenp;
+  const int p0 = lane * kPer;
+  int32_t v[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer / 4; ++q) {
+    const int4 x = *reinterpret_cast<const int4*>(tb + p0 + 4 * q);
+    v[4 * q] = x.x;
+    v[4 * q + 1] = x.y;
+    v[4 * q + 2] = x.z;
+    v[4 * q + 3] = x.w;
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if ((uint32_t)(p0 + j) >= len) v[j] = kPad;
+  int32_t nx = wave_next(v[0]);
+  if (lane == 63) nx = kPad;
+  bool any = false;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) any |= (v[j] == a) & ((j + 1 < kPer ? v[j + 1] : nx) == b);
+  if (!__any(any)) return 0;
+  RCY(0);
+  const bool same = (a == b);
+  const uint32_t cl = len;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) st[SK(2 + p0 + j)] = v[j];
+  if (lane == 0) {
+    st[SK(0)] = kPad;
+    st[SK(1)] = kPad;
+  }
+  if (lane == 63) {
+    st[SK(2 + kWaveTok)] = kPad;
+    st[SK(3 + kWaveTok)] = kPad;
+  }
+  wave_lds_sync();
+  uint32_t mask = 0;
+  if (same) {
+    u64 nl = 0;  // last index whose token != a, + 1 (0 = none)
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (v[j] != a) nl = (u64)(p0 + j) + 1;
+    const u64 inc = wave_scan_max64(nl);
+    long long last = (long long)wave_prev64(inc) - 1;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const long long gi = (long long)(p0 + j);
+      if (v[j] != a) last = gi;
+      else if ((j + 1 < kPer ? v[j + 1] : nx) == a && ((gi - last - 1) & 1) == 0) mask |= 1u << j;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (v[j] == a && (j + 1 < kPer ? v[j + 1] : nx) == b) mask |= 1u << j;
+  }
+  uint32_t prevm = wave_prev(mask);
+  if (lane == 0) prevm = 0;
+  const uint32_t m_ext = (mask << 2) | ((prevm >> 14) & 3u);  // bit k <-> position p0 - 2 + k
+  const uint32_t removed = (m_ext >> 1) & 0xFFFFu;           // bit j <-> match at p0 + j - 1
+  const int valid = max(0, min(kPer, (int)cl - p0));
+  const uint32_t vmask = valid >= kPer ? 0xFFFFu : ((1u << valid) - 1u);
+  const int kc = __popc(~removed & vmask);
+  const int nm = __popc(mask);
+  uint32_t hmask = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if (is_hdr(v[j])) hmask |= 1u << j;
+  hmask &= vmask;
+  u64 hl = 0;
+  if (hmask) {
+    const int j = 31 - __clz(hmask);
+    hl = ((u64)(p0 + j + 1) << 32) | hdr_rank(st[SK(2 + p0 + j)]);
+  }
+  const u64 hinc = wave_scan_max64(hl);
+  const u64 hdr_ex = wave_prev64(hinc);
+  const int cinc = wave_incl_sum(kc | (nm << 16));
+  const int ctot = (int)lane_read((uint32_t)cinc, 63);
+  const int kc_ex = (cinc - (kc | (nm << 16))) & 0xFFFF;
+  const int kept = ctot & 0xFFFF;
+  const int matches = ctot >> 16;
+  RCY(1);
+  if (mask) {
+    const u64 hdr_in = lane == 0 ? 0ull : hdr_ex;
+    for (uint32_t mrem = mask; mrem; mrem &= mrem - 1) {
+      const int j = __ffs(mrem) - 1;
+      const uint32_t hb = hmask & ((2u << j) - 1u);
+      u64 hdr = hdr_in;
+      if (hb) {
+        const int jh = 31 - __clz(hb);
+        hdr = ((u64)(p0 + jh + 1) << 32) | hdr_rank(st[SK(2 + p0 + jh)]);
+      }
+      const uint32_t hidx = (uint32_t)(hdr >> 32) - 1u;
+      const uint32_t rank = (uint32_t)hdr;
+      const uint32_t gi = p0 + j;
+      const u64 w = kWeighted ? s_w[rank - r0] : 1ull;
+      const u64 ftb = ((u64)rank << 32) | ((u64)(gi - hidx - 1u) << 2);
+      const bool vl = gi - 1u > hidx;  // a left neighbour inside the word (X if it was just merged)
+      const int32_t left = ((m_ext >> j) & 1u) ? X : st[SK(1 + p0 + j)];
+      const int32_t right = st[SK(4 + p0 + j)];  // the original token after b
+      const bool vr = !is_hdr(right);
+      const uint32_t sl = slot_of(left, slot_cap) << 2, sr = slot_of(right, slot_cap) << 2;
+      const uint32_t key[4] = {sl | kOldLeft, sl | kNewLeft, sr | kOldRight, sr | kNewRight};
+      const bool val[4] = {vl, vl, vr, vr};
+      // the four slots are probed together (their CAS round trips overlap), then summed
+      uint32_t slot[4];
+      bool pend[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        slot[k] = (key[k] * 2654435761u) >> (32 - __builtin_ctz(kResDeltaW));
+        pend[k] = val[k];
+      }
+      for (int probe = 0; probe < 16 && (pend[0] | pend[1] | pend[2] | pend[3]); ++probe) {
+        uint32_t prev[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) prev[k] = pend[k] ? atomicCAS(&h.key[slot[k]], kEmpty32, key[k]) : key[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (pend[k]) {
+            if (prev[k] == kEmpty32 || prev[k] == key[k]) pend[k] = false;
+            else slot[k] = (slot[k] + 1) & (kResDeltaW - 1);
+          }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!val[k]) continue;
+        if (pend[k]) {  // the LDS hash is full around these slots: the global tables take it
+          h.spill = 1;
+          delta_global(p, key[k], w, ftb | (u64)(k));
+        } else {
+          atomicAdd(&h.sum[slot[k]], w);
+          atomicMin(&h.ft[slot[k]], ftb | (u64)(k));
+        }
+      }
+      // the tile's signature gains the new pairs (a superset stays valid; rebuilt when loose)
+      uint32_t h1, h2, h3, h4;
+      res_sig_bits(left, X, &h1, &h2);
+      res_sig_bits(X, right, &h3, &h4);
+      atomicOr(&sg[h1 >> 5], vl ? 1u << (h1 & 31) : 0u);
+      atomicOr(&sg[h2 >> 5], vl ? 1u << (h2 & 31) : 0u);
+      atomicOr(&sg[h3 >> 5], vr ? 1u << (h3 & 31) : 0u);
+      atomicOr(&sg[h4 >> 5], vr ? 1u << (h4 & 31) : 0u);
+    }
+  }
+  wave_lds_sync();  // every neighbour read is done: compact in place
+  RCY(2);
+  // branch-free: a dropped position writes this lane's trash word past the staging area
+  int o = kc_ex;
+  const int trash = kStPad + lane;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const bool keep = j < valid && !((removed >> j) & 1u);
+    st[keep ? SK(2 + o) : trash] = ((mask >> j) & 1u) ? X : v[j];
+    o += keep ? 1 : 0;
+  }
+  // a tile whose signature gathered many added pairs since its last build is re-signed below
+  const uint32_t added = *sgadd + 2u * (uint32_t)matches;
+  const bool rebuild = added > kResSigRebuild;
+  if (rebuild)
+    for (int w = lane; w < kResSigWords; w += 64) sg[w] = 0;
+  wave_lds_sync();
+  int32_t c[kPer + 1];  // this lane's compacted tokens (kPad past the end) and the next one
+#pragma unroll
+  for (int j = 0; j <= kPer; ++j) {
+    const int32_t t = st[SK(2 + p0 + j)];
+    c[j] = p0 + j < kept ? t : kPad;
+  }
+#pragma unroll
+  for (int q = 0; q < kPer / 4; ++q) {
+    if (p0 + 4 * q < kept) {
+      int4 x;
+      x.x = c[4 * q];
+      x.y = c[4 * q + 1];
+      x.z = c[4 * q + 2];
+      x.w = c[4 * q + 3];
+      *reinterpret_cast<int4*>(tb + p0 + 4 * q) = x;
+    }
+  }
+  if (lane == 0) *lenp = (uint32_t)kept;
+  *n_written += (u64)kept;
+  RCY(3);
+  if (rebuild) {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {  // signature of the compacted tile (OR of 0 where no pair)
+      uint32_t h1, h2;
+      res_sig_bits(c[j], c[j + 1], &h1, &h2);
+      const bool pr = !is_hdr(c[j]) && !is_hdr(c[j + 1]);
+      atomicOr(&sg[h1 >> 5], pr ? 1u << (h1 & 31) : 0u);
+      atomicOr(&sg[h2 >> 5], pr ? 1u << (h2 & 31) : 0u);
+    }
+  }
+  if (lane == 0) *sgadd = rebuild ? 0u : added;
+  wave_lds_sync();
+  RCY(4);
+#undef RCY
+  return (uint32_t)matches;
+}
+
+// One wave expands every X in a single-chunk tile held in LDS back into (a, b) — the undo of a
+// speculative merge that the host did not confirm; the tile's length grows back, within its
+// original LDS capacity.  The signature is rebuilt exactly.
+__device__ __forceinline__ void res_unmerge_tile(int32_t* tb, uint32_t* lenp, uint32_t* sg, uint32_t* sgadd, int32_t* st,
+                                                 int32_t a, int32_t b, int32_t X, int lane) {
+  const uint32_t len = *lenp;
+  const int p0 = lane * kPer;
+  int32_t v[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer / 4; ++q) {
+    const int4 x = *reinterpret_cast<const int4*>(tb + p0 + 4 * q);
+    v[4 * q] = x.x;
+    v[4 * q + 1] = x.y;
+    v[4 * q + 2] = x.z;
+    v[4 * q + 3] = x.w;
+  }
+  int nx = 0;  // this lane's X count
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if ((uint32_t)(p0 + j) >= len) v[j] = kPad;
+    nx += v[j] == X ? 1 : 0;
+  }
+  if (!__any(nx != 0)) return;
+  const int inc = wave_incl_sum(nx);
+  const int total = (int)lane_read((uint32_t)inc, 63);
+  const int nlen = (int)len + total;  // <= the tile's LDS capacity: the merge removed these tokens
+  int o = p0 + inc - nx;              // this lane's first output position
+  const int trash = kStPad + lane;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const bool live = (uint32_t)(p0 + j) < len;
+    const bool isx = live && v[j] == X;
+    st[live ? SK(o) : trash] = isx ? a : v[j];
+    st[isx ? SK(o + 1) : trash] = b;
+    o += live ? (isx ? 2 : 1) : 0;
+  }
+  wave_lds_sync();
+  for (int i = lane; i < kResSigWords; i += 64) sg[i] = 0;
+  int32_t c[kPer + 1];
+#pragma unroll
+  for (int j = 0; j <= kPer; ++j) {
+    const int32_t t = st[SK(p0 + j)];
+    c[j] = p0 + j < nlen ? t : kPad;
+  }
+#pragma unroll
+  for (int q = 0; q < kPer / 4; ++q) {
+    if (p0 + 4 * q < nlen) {
+      int4 x;
+      x.x = c[4 * q];
+      x.y = c[4 * q + 1];
+      x.z = c[4 * q + 2];
+      x.w = c[4 * q + 3];
+      *reinterpret_cast<int4*>(tb + p0 + 4 * q) = x;
+    }
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    uint32_t h1, h2;
+    res_sig_bits(c[j], c[j + 1], &h1, &h2);
+    const bool pr = !is_hdr(c[j]) && !is_hdr(c[j + 1]);
+    atomicOr(&sg[h1 >> 5], pr ? 1u << (h1 & 31) : 0u);
+    atomicOr(&sg[h2 >> 5], pr ? 1u << (h2 & 31) : 0u);
+  }
+  if (lane == 0) {
+    *lenp = (uint32_t)nlen;
+    *sgadd = 0;
+  }
+  wave_lds_sync();
+}
+
+template <bool kWeighted>
+__global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
+  extern __shared__ __align__(16) int32_t s_dyn[];
+  int32_t* s_res = s_dyn;                                     // the tiles' tokens
+  u64* s_w = reinterpret_cast<u64*>(s_dyn + p.tok_words);     // the words' weights
+  uint32_t* s_sig = reinterpret_cast<uint32_t*>(s_dyn + p.tok_words + 2 * p.w_words);  // per-tile signatures
+  __shared__ int32_t s_tok[kWaves][kStPad + 64];  // + a trash word per lane (branch-free compaction)
+  __shared__ ResDelta h;
+  __shared__ uint32_t s_len[kResMaxTiles], s_lofs[kResMaxTiles], s_sigadd[kResMaxTiles];
+  __shared__ uint32_t s_mt[kResMaxTiles];
+  __shared__ uint8_t s_lm[kResMaxTiles];   // tiles where this workgroup's last merge matched
+  __shared__ uint32_t s_qc[kMaxMergeGroups];  // leader: entries written to each workgroup's queue
+  __shared__ uint32_t s_nmt, s_nrec, s_last;
+  __shared__ uint32_t s_cmd[8];
+  __shared__ u64 s_cnt[2];
+  __shared__ uint32_t s_pre[kMaxMergeGroups + 1], s_pmt[kMaxMergeGroups + 1];
+  __shared__ uint32_t s_wtot[2][kWaves];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t G = gridDim.x, me = blockIdx.x;
+  const uint32_t t0 = p.wg_tiles[me], nt = p.wg_tiles[me + 1] - t0;
+  const uint32_t r0 = p.wg_rank[me], nr = p.wg_rank[me + 1] - r0;
+  int32_t* st = s_tok[wid];
+
+  // ---- residency: tiles, weights and signatures into LDS
+  for (uint32_t i = threadIdx.x; i < nt; i += kThreads) {
+    s_len[i] = p.tile_len[t0 + i];
+    s_lofs[i] = p.tile_lofs[t0 + i];
+    s_sigadd[i] = 0;
+    s_lm[i] = 0;
+  }
+  for (uint32_t i = threadIdx.x; i < G; i += kThreads) s_qc[i] = 0;
+  for (int i = threadIdx.x; i < kResDeltaW; i += kThreads) {
+    h.key[i] = kEmpty32;
+    h.sum[i] = 0;
+    h.ft[i] = kEmpty64;
+  }
+  if (kWeighted)
+    for (uint32_t i = threadIdx.x; i < nr; i += kThreads) s_w[i] = p.weight[r0 + i];
+  if (threadIdx.x == 0) h.spill = 0;
+  __syncthreads();
+  for (uint32_t i = wid; i < nt; i += kWaves) {
+    const int32_t* src = p.tok + p.tile_off[t0 + i];
+    int32_t* dst = s_res + s_lofs[i];
+    const uint32_t n4 = (s_len[i] + 3u) >> 2;
+    for (uint32_t q = (uint32_t)lane; q < n4; q += 64)
+      *reinterpret_cast<int4*>(dst + 4 * q) = *reinterpret_cast<const int4*>(src + 4 * q);
+    wave_lds_sync();
+    res_sig_build(s_sig + (size_t)i * kResSigWords, dst, s_len[i], lane);
+  }
+  __syncthreads();
+
+  uint32_t expect = p.seq0;  // leader: the next host command
+  uint32_t idle = 0;         // leader: polls without a command
+  uint32_t consumed = 0;     // thread 0: entries taken from this workgroup's queue
+  uint32_t exit_op = kOpStop;
+  u64* myq = p.q + (size_t)me * kResRing;
+  for (;;) {
+    // ---- the leader hands out the next host command, if one is posted (one poll per pass)
+    if (me == 0 && wid == 0) {
+      const ResCmd* hc = &p.mbox->cmd[expect % kResRing];
+      uint32_t op = 0, np = 0, slot = 0;
+      int32_t a = 0, b = 0, X = 0;
+      if (lane == 0) {
+        if (host_load(&hc->seq) == expect) {
+          op = host_load(&hc->op);
+          np = host_load(&hc->nparts);
+          slot = host_load(&hc->slot);
+          a = (int32_t)host_load((const uint32_t*)&hc->a);
+          b = (int32_t)host_load((const uint32_t*)&hc->b);
+          X = (int32_t)host_load((const uint32_t*)&hc->X);
+          idle = 0;
+        } else if (++idle >= p.leader_polls) {
+          op = kOpTimeout;  // nobody posts any more: every workgroup writes back and leaves
+        }
+      }
+      op = (uint32_t)__shfl((int)op, 0, 64);
+      if (op) {
+        np = (uint32_t)__shfl((int)np, 0, 64);
+        if ((op != kOpMerge && op != kOpUnmerge) || np > G) np = G;
+        if (lane == 0 && (op == kOpMerge || op == kOpUnmerge)) {
+          uint32_t* dc = p.cmd + (expect % kResRing) * 8;
+          __hip_atomic_store(dc, (uint32_t)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dc + 1, (uint32_t)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dc + 2, (uint32_t)X, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dc + 3, np, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dc + 4, slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(reinterpret_cast<u64*>(dc + 6), (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+        uint32_t wgs[kMaxMergeGroups / 64];  // this lane's participants, all loads in flight together
+#pragma unroll
+        for (int k = 0; k < kMaxMergeGroups / 64; ++k) {
+          const uint32_t i = (uint32_t)lane + 64u * k;
+          wgs[k] = i >= np ? G : ((op == kOpMerge || op == kOpUnmerge) && np < G) ? host_load(&hc->parts[i]) : i;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the command lands before any queue entry
+#pragma unroll
+        for (int k = 0; k < kMaxMergeGroups / 64; ++k) {
+          const uint32_t i = (uint32_t)lane + 64u * k, wg = wgs[k];
+          if (wg < G) {  // distinct workgroups per lane: the counters need no atomics
+            const uint32_t c = ++s_qc[wg];
+            __hip_atomic_store(p.q + (size_t)wg * kResRing + ((c - 1) % kResRing), q_entry(expect, c, i, op),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        ++expect;
+      }
+      if (lane == 0) s_cmd[7] = op;
+    }
+    // ---- this workgroup's next queue entry (the leader's workgroup never blocks here)
+    if (threadIdx.x == 0) {
+      uint32_t got = 0;
+      u64 v = 0;
+      const uint32_t want = (consumed + 1) & 0xFFFFu;
+      if (me == 0) {
+        v = __hip_atomic_load(myq + consumed % kResRing, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        got = ((uint32_t)(v >> 32) & 0xFFFFu) == want;
+        if (!got && !s_cmd[7]) __builtin_amdgcn_s_sleep(2);
+      } else {
+        while (((uint32_t)((v = __hip_atomic_load(myq + consumed % kResRing, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) >> 32) & 0xFFFFu) != want)
+          __builtin_amdgcn_s_sleep(2);
+        got = 1;
+      }
+      s_cmd[0] = got ? (uint32_t)(v >> 56) : 0u;
+      if (got) {
+        ++consumed;
+        s_cmd[1] = (uint32_t)(v >> 48) & 0xFFu;
+        s_cmd[2] = (uint32_t)v;
+        const uint32_t op = s_cmd[0];
+        if (op == kOpMerge || op == kOpUnmerge) {
+          const uint32_t* dc = p.cmd + ((uint32_t)v % kResRing) * 8;
+          s_cmd[3] = __hip_atomic_load(dc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_cmd[4] = __hip_atomic_load(dc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_cmd[5] = __hip_atomic_load(dc + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_cmd[6] = __hip_atomic_load(dc + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                     (__hip_atomic_load(dc + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 16);
+        }
+      }
+      s_nmt = 0;
+      s_nrec = 0;
+      s_cnt[0] = 0;
+      s_cnt[1] = 0;
+    }
+    __syncthreads();
+    const uint32_t op = s_cmd[0];
+    if (op == 0) continue;  // the leader's workgroup: nothing queued for it yet
+    if (op != kOpMerge && op != kOpUnmerge) {
+      exit_op = op;
+      break;
+    }
+    const uint32_t pi = s_cmd[1], seq = s_cmd[2];
+    const int32_t a = (int32_t)s_cmd[3], b = (int32_t)s_cmd[4], X = (int32_t)s_cmd[5];
+    const uint32_t T = s_cmd[6] & 0xFFFFu, slot = s_cmd[6] >> 16;
+    if (p.dbg && threadIdx.x == 0) {
+      p.dbg[me * 4] = 2;
+      p.dbg[me * 4 + 1] = seq;
+      p.dbg[me * 4 + 2] = pi;
+      p.dbg[me * 4 + 3] = T;
+    }
+    if (op == kOpUnmerge) {  // undo this workgroup's last merge (the host's guess was wrong)
+      for (uint32_t i = wid; i < nt; i += kWaves)
+        if (s_lm[i]) res_unmerge_tile(s_res + s_lofs[i], &s_len[i], s_sig + (size_t)i * kResSigWords, &s_sigadd[i], st,
+                                      a, b, X, lane);
+      __syncthreads();
+      continue;
+    }
+    const ResSlot& sl = p.sl[slot];
+    u64 clk0 = 0;
+    if (p.stamps && threadIdx.x == 0) {
+      __hip_atomic_store(p.stamps + pi * 4, (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      clk0 = __builtin_amdgcn_s_memtime();
+    }
+
+    // ---- the merge over this workgroup's tiles (wave per tile)
+    u64 n_merged = 0, n_written = 0;
+    u64 cyc[5] = {0, 0, 0, 0, 0};
+    for (uint32_t i = wid; i < nt; i += kWaves) {
+      const uint32_t m = res_merge_tile<kWeighted>(s_res + s_lofs[i], &s_len[i], s_sig + (size_t)i * kResSigWords,
+                                                   &s_sigadd[i], st, s_w, r0, a, b, X, h, sl, p.slot_cap, lane,
+                                                   &n_written, p.stamps ? cyc : nullptr);
+      if (lane == 0) s_lm[i] = m ? 1 : 0;
+      if (m) {
+        n_merged += m;
+        if (lane == 0) s_mt[atomicAdd(&s_nmt, 1u)] = t0 + i;
+      }
+    }
+    if (lane == 0) {
+      if (n_merged) atomicAdd(&s_cnt[0], n_merged);
+      if (n_written) atomicAdd(&s_cnt[1], n_written);
+    }
+    __syncthreads();
+    if (p.stamps && lane == 0 && cyc[4]) {  // a wave that merged in a tile: its phase cycles
+      for (int k = 0; k < 4; ++k)
+        __hip_atomic_store(p.stamps + 4 * G + pi * 4 + k, cyc[k + 1] - cyc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (p.stamps && threadIdx.x == 0) {
+      __hip_atomic_store(p.stamps + pi * 4 + 1, (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.stamps + pi * 4 + 3, (u64)__builtin_amdgcn_s_memtime() - clk0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- publish this participant's region (write-through), clearing the LDS hash
+    {
+      u64* rr = sl.rrec + (size_t)pi * kDeltaLdsW * 3;
+      for (int i = threadIdx.x; i < kResDeltaW; i += kThreads) {
+        const uint32_t key = h.key[i];
+        if (key == kEmpty32) continue;
+        const uint32_t k = atomicAdd(&s_nrec, 1u);
+        __hip_atomic_store(rr + 3 * k, (u64)key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rr + 3 * k + 1, h.sum[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rr + 3 * k + 2, h.ft[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h.key[i] = kEmpty32;
+        h.sum[i] = 0;
+        h.ft[i] = kEmpty64;
+      }
+      const uint32_t nmt = s_nmt;
+      for (uint32_t i = threadIdx.x; i < nmt; i += kThreads)
+        __hip_atomic_store(sl.rtile + (size_t)pi * kMtLds + i, s_mt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t* hd = sl.rhdr + (size_t)pi * kRegHdr;
+        __hip_atomic_store(hd, s_nrec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hd + 1, nmt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hd + 2, h.spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<u64*>(hd + 4), s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<u64*>(hd + 6), s_cnt[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h.spill = 0;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // ---- ticket among the T participants (sharded by participant index above 32)
+    if (threadIdx.x == 0) {
+      bool last = false;
+      if (T <= 32u) {
+        last = atomicAdd(&sl.done[8], 1u) == T - 1u;
+      } else {
+        const uint32_t g = pi & 7u, in_group = (T - g + 7u) >> 3;
+        if (atomicAdd(&sl.done[g], 1u) == in_group - 1u) {
+          atomicExch(&sl.done[g], 0u);
+          last = atomicAdd(&sl.done[8], 1u) == 7u;
+        }
+      }
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) continue;
+    // ---- the last participant: gather the regions to the host, raise the slot's flag
+    uint32_t n = 0, nm = 0;
+    {
+      u64 merged = 0, written = 0;
+      uint32_t spill = 0, my_nrec = 0, my_nmt = 0;
+      if (threadIdx.x == 0) {
+        s_cnt[0] = 0;
+        s_cnt[1] = 0;
+        s_nrec = 0;
+      }
+      __syncthreads();
+      const uint32_t g = threadIdx.x;
+      if (g < T) {
+        const uint32_t* hd = sl.rhdr + (size_t)g * kRegHdr;
+        my_nrec = __hip_atomic_load(hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        my_nmt = __hip_atomic_load(hd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spill = __hip_atomic_load(hd + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        merged = __hip_atomic_load(reinterpret_cast<const u64*>(hd + 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        written = __hip_atomic_load(reinterpret_cast<const u64*>(hd + 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (merged) atomicAdd(&s_cnt[0], merged);
+      if (written) atomicAdd(&s_cnt[1], written);
+      if (spill) atomicOr(&s_nrec, 1u);
+      const uint32_t ir = wave_scan_add(my_nrec), im = wave_scan_add(my_nmt);
+      if (lane == 63) {
+        s_wtot[0][wid] = ir;
+        s_wtot[1][wid] = im;
+      }
+      __syncthreads();
+      uint32_t br = 0, bm = 0;
+      for (int w = 0; w < wid; ++w) {
+        br += s_wtot[0][w];
+        bm += s_wtot[1][w];
+      }
+      if (g < T) {
+        s_pre[g] = br + ir - my_nrec;
+        s_pmt[g] = bm + im - my_nmt;
+      }
+      if (g == T - 1) {
+        s_pre[T] = br + ir;
+        s_pmt[T] = bm + im;
+      }
+      __syncthreads();
+      n = s_pre[T];
+      nm = s_pmt[T];
+      auto owner = [&](const uint32_t* pre, uint32_t i) {
+        uint32_t lo = 0, hi = T;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pre[mid] <= i) lo = mid;
+          else hi = mid;
+        }
+        return lo;
+      };
+      for (uint32_t i0 = 0; i0 < n; i0 += kThreads * 4) {
+        u64 r[4][3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t i = i0 + k * kThreads + threadIdx.x;
+          if (i < n) {
+            const uint32_t o = owner(s_pre, i);
+            const u64* src = sl.rrec + ((size_t)o * kDeltaLdsW + (i - s_pre[o])) * 3;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) r[k][c] = __hip_atomic_load(src + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t i = i0 + k * kThreads + threadIdx.x;
+          if (i < n) sys_record(sl.out + i, (uint32_t)r[k][0], r[k][1], r[k][2]);
+        }
+      }
+      for (uint32_t i = threadIdx.x; i < nm; i += kThreads) {
+        const uint32_t o = owner(s_pmt, i);
+        sys_store(sl.hmlist + i,
+                  __hip_atomic_load(sl.rtile + (size_t)o * kMtLds + (i - s_pmt[o]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      if (s_nrec) {  // spilled deltas in the global tables: all of them follow the records
+        __syncthreads();
+        if (threadIdx.x == 0) s_cmd[7] = atomicAdd(sl.dcount, 0u);
+        __syncthreads();
+        const uint32_t ngl = s_cmd[7];
+        for (uint32_t i = threadIdx.x; i < ngl; i += kThreads) {
+          const uint32_t key = atomicOr(&sl.dlist[i], 0u);
+          const u64 sum = atomicExch(&sl.dsum[key], 0ull);
+          const u64 ft = atomicExch(&sl.dft[key], kEmpty64);
+          sys_record(sl.out + n + i, key, sum, ft);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) atomicExch(sl.dcount, 0u);
+        n += ngl;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const u64 t_leader = __hip_atomic_load(reinterpret_cast<const u64*>(p.cmd + (seq % kResRing) * 8 + 6),
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sys_store(&sl.hstats[0], s_cnt[0]);
+      sys_store(&sl.hstats[1], s_cnt[1]);
+      sys_store(&sl.hstats[2], (u64)__builtin_amdgcn_s_memrealtime() - t_leader);
+      if (p.stamps) {  // diagnostic: the slowest participant per phase, relative to the leader
+        u64 mx[3] = {0, 0, 0};
+        for (uint32_t g = 0; g < T; ++g)
+          for (int k = 0; k < 2; ++k) {
+            const u64 v = __hip_atomic_load(p.stamps + g * 4 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t_leader;
+            mx[k] = v > mx[k] ? v : mx[k];
+          }
+        sys_store(&sl.hstats[3], mx[0]);
+        sys_store(&sl.hstats[4], mx[1]);
+        sys_store(&sl.hstats[5], mx[2]);
+      }
+      sys_store(&sl.hcount[0], n);
+      sys_store(&sl.hcount[2], nm);
+      atomicExch(&sl.done[8], 0u);
+      sys_flag(&sl.hcount[1], seq);
+    }
+  }
+  // ---- STOP (or the leader's time-out): the tiles go back to HBM
+  for (uint32_t i = wid; i < nt; i += kWaves) {
+    int32_t* dst = p.tok + p.tile_off[t0 + i];
+    const int32_t* src = s_res + s_lofs[i];
+    const uint32_t len = s_len[i];
+    const uint32_t n4 = (len + 3u) >> 2;
+    for (uint32_t q = (uint32_t)lane; q < n4; q += 64) {
+      int4 x = *reinterpret_cast<const int4*>(src + 4 * q);
+      if (4 * q + 1 >= len) x.y = kPad;
+      if (4 * q + 2 >= len) x.z = kPad;
+      if (4 * q + 3 >= len) x.w = kPad;
+      *reinterpret_cast<int4*>(dst + 4 * q) = x;
+    }
+    if (lane == 0) p.tile_len[t0 + i] = len;
+  }
+  if (threadIdx.x == 0 && exit_op != kOpStop) {
+    __threadfence_system();
+    __hip_atomic_store(&p.status[0], exit_op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1782,6 +2574,7 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
   HIP_OK(hipMemset(stamps_, 0, (size_t)kMaxMergeGroups * 4 * kStamps * sizeof(u64)));
 #endif
   if (const char* e = std::getenv("SHREDWORD_TILE_SKIP")) skip_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SHREDWORD_RESIDENT")) resident_on_ = std::atoi(e) != 0;
   int nb = 0;  // resident workgroups of k_merge per CU
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_merge<true>), kThreads, 0));
   merge_blocks_per_cu_ = nb > 0 ? nb : 4;
@@ -1848,6 +2641,13 @@ void Device::free_all() {
 
 Device::~Device() {
   (void)hipSetDevice(ordinal_);
+  if (res_running_ && res_posted_.empty()) park();
+  (void)hipStreamSynchronize(S(stream_));
+  free_resident();
+  if (res_mbox_) (void)hipHostFree(res_mbox_);
+  if (res_status_) (void)hipHostFree(res_status_);
+  for (auto e : res_ev_)
+    if (e) (void)hipEventDestroy((hipEvent_t)e);
   (void)hipStreamSynchronize(S(stream_));
   (void)hipStreamSynchronize(S(aux_stream_));
   free_all();
@@ -1867,6 +2667,7 @@ Device::~Device() {
 
 void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint64_t>& weights, int32_t max_id) {
   HIP_OK(hipSetDevice(ordinal_));
+  park();
   HIP_OK(hipStreamSynchronize(S(stream_)));
   flush_timing(true);
   free_all();
@@ -1924,10 +2725,12 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
   max_id0_ = max_id;
   uploaded_ = true;
   reset_tokens();
+  plan_resident(ts);
 }
 
 void Device::reset_tokens() {
   HIP_OK(hipSetDevice(ordinal_));
+  park();
   if (!uploaded_) return;
   for (const MergeSlot& s : slot_)
     if (s.launched) fatal("reset_tokens with a merge in flight");
@@ -1945,6 +2748,7 @@ void Device::reset_tokens() {
 
 uint64_t Device::live_tokens() {
   HIP_OK(hipSetDevice(ordinal_));
+  park();
   if (!ntiles_) return 0;
   u64* d = dalloc<u64>(1, &bytes_alloc_);
   HIP_OK(hipMemsetAsync(d, 0, sizeof(u64), S(stream_)));
@@ -2002,6 +2806,7 @@ void Device::ensure_slots(MergeSlot& s, uint32_t need) {
 
 void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
   HIP_OK(hipSetDevice(ordinal_));
+  park();
   out->clear();
   if (!ntiles_) {
     dist_merge_pairs(out);
@@ -2150,6 +2955,24 @@ void Device::flush_timing(bool block) {
 void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   HIP_OK(hipSetDevice(ordinal_));
   if (n < 1 || n > kChainMax) fatal("merge_chain: bad chain length");
+  if (n == 1 && run_count_ == 0 && ntiles_ && resident_eligible()) {  // k_resident
+    if (res_posted_.size() >= 2) fatal("merge_chain: two resident merges are already in flight");
+    const int slot = X0 & 1;  // consecutive merges alternate slots
+    bool grow = false;
+    for (const MergeSlot& s2 : slot_) grow |= !s2.dsum || (uint32_t)X0 + 2 > s2.cap;
+    if (grow) {  // the delta tables grow: only between launches
+      if (!res_posted_.empty()) fatal("merge_chain: delta tables too small with a resident merge in flight");
+      park();
+      for (MergeSlot& s2 : slot_) ensure_slots(s2, (uint32_t)X0 + 2);
+      const uint32_t cap = std::max(slot_[0].cap, slot_[1].cap);
+      for (MergeSlot& s2 : slot_) ensure_slots(s2, cap);
+    }
+    max_id_seen_ = std::max(max_id_seen_, X0);
+    const uint32_t seq = post_resident(kOpMerge, ab[0], ab[1], X0, slot);
+    res_posted_.push_back({X0, ab[0], ab[1], seq, slot, (uint32_t)res_post_parts_[slot].size()});
+    return;
+  }
+  park();
   if (run_count_ >= 2) fatal("merge_chain: two launches are already in flight");
   ChainRun& run = run_at(run_count_);
   run.slot = (run_head_ + run_count_) & 1;
@@ -2448,6 +3271,7 @@ void Device::finish_launch(ChainRun& run_) {
 
 size_t Device::collect(int32_t X, const DeltaRecord** recs) {
   HIP_OK(hipSetDevice(ordinal_));
+  if (!res_posted_.empty()) return collect_resident(X, recs);
   if (run_count_ == 0) fatal("collect: no launch in flight");
   ChainRun& run = run_at(0);
   const int j = X - run.X0;
@@ -2466,6 +3290,17 @@ size_t Device::collect(int32_t X, const DeltaRecord** recs) {
 
 void Device::rollback(int32_t X) {
   HIP_OK(hipSetDevice(ordinal_));
+  if (!res_posted_.empty()) {  // resident: each wrong guess is expanded back where it matched
+    while (!res_posted_.empty() && res_posted_.back().X >= X) {
+      const ResPost rp = res_posted_.back();
+      res_posted_.pop_back();
+      wait_resident(slot_[rp.slot], rp.seq);  // its completion leaves the slot before the slot's next merge
+      post_resident(kOpUnmerge, rp.a, rp.b, rp.X, rp.slot);
+      ++rollbacks_;
+    }
+    return;
+  }
+  park();
   ++rollbacks_;
   // every uncollected merge >= X, newest launch first
   for (int k = run_count_ - 1; k >= 0; --k) {
@@ -2548,6 +3383,7 @@ void Device::unmerge_launch(ChainRun& run_, const uint32_t* tiles, size_t n_tile
 
 void Device::token_freq(size_t T, std::vector<uint64_t>* freq) {
   HIP_OK(hipSetDevice(ordinal_));
+  park();
   freq->assign(T, 0);
   if (!ntiles_ || !T) {
     dist_allreduce_host(freq->data(), T, false);
@@ -2570,6 +3406,7 @@ void Device::token_freq(size_t T, std::vector<uint64_t>* freq) {
 
 void Device::download_tokens(std::vector<int32_t>* out) {
   HIP_OK(hipSetDevice(ordinal_));
+  park();
   out->clear();
   if (!ntiles_) return;
   std::vector<int32_t> all(tok_elems_ + 4);
@@ -2580,6 +3417,342 @@ void Device::download_tokens(std::vector<int32_t>* out) {
   HIP_OK(hipMemcpyAsync(lens.data(), tile_len_, ntiles_ * sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
   HIP_OK(hipStreamSynchronize(S(stream_)));
   for (size_t t = 0; t < ntiles_; ++t) out->insert(out->end(), all.begin() + off[t], all.begin() + off[t] + lens[t]);
+}
+
+// ==========================================================================================
+// k_resident host side: plan (which workgroup holds which tiles in LDS), launch, post, collect,
+// roll back, park.  See the kernel's comment for the protocol.
+void Device::free_resident() {
+  for (void* p : {(void*)res_wg_tiles_, (void*)res_wg_rank_, (void*)res_tile_lofs_, (void*)res_cmd_, (void*)res_q_,
+                  (void*)res_dbg_, (void*)res_stamps_})
+    if (p) HIP_OK(hipFree(p));
+  res_wg_tiles_ = res_wg_rank_ = res_tile_lofs_ = res_cmd_ = nullptr;
+  res_q_ = nullptr;
+  res_dbg_ = nullptr;
+  res_stamps_ = nullptr;
+  resident_ok_ = false;
+}
+
+void Device::plan_resident(const TiledStream& ts) {
+  free_resident();
+  if (layout_ != Layout::kTypes || ntiles_ == 0) return;
+  const uint32_t G = (uint32_t)std::min(cu_count_, kMaxMergeGroups);
+  if (G < 2) return;
+  const uint32_t W = G - 1;  // workers 1 .. G-1; workgroup 0 dispatches
+  int max_lds = 0;
+  HIP_OK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, ordinal_));
+  hipFuncAttributes fa;
+  HIP_OK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_resident<true>)));
+  const long budget = (long)max_lds - (long)fa.sharedSizeBytes - 64;  // dynamic LDS per workgroup
+  if (budget <= 0) return;
+  // per tile: first and last word rank (tiles hold whole words in rank order), LDS words
+  const size_t T = ntiles_;
+  std::vector<uint32_t> rfirst(T), rlast(T), words(T);
+  double total = 0;
+  for (size_t t = 0; t < T; ++t) {
+    const uint32_t len = ts.len[t];
+    if (len > (uint32_t)kWaveTok || len == 0) return;  // a long word: k_merge handles those
+    const int32_t* tk = ts.tok.data() + ts.off[t];
+    if (tk[0] >= kHeaderLimit) return;
+    rfirst[t] = (uint32_t)(tk[0] - kHeaderBase);
+    uint32_t last = rfirst[t];
+    for (uint32_t i = 1; i < len; ++i)
+      if (tk[i] < kHeaderLimit) last = (uint32_t)(tk[i] - kHeaderBase);
+    rlast[t] = last;
+    if (t && rfirst[t] != rlast[t - 1] + 1) return;
+    words[t] = (len + 3u) & ~3u;
+    total += 4.0 * words[t] + 8.0 * (rlast[t] - rfirst[t] + 1) + 4.0 * kResSigWords;
+  }
+  // contiguous ranges balanced by LDS bytes: tile t goes to worker 1 + floor((prefix + cost/2) * W / total)
+  std::vector<uint32_t> wg_tiles(G + 1, 0), wg_rank(G + 1, 0), lofs(T);
+  res_owner_.assign(T, 0);
+  double pre = 0;
+  uint32_t w = 1;
+  for (size_t t = 0; t < T; ++t) {
+    const double c = 4.0 * words[t] + 8.0 * (rlast[t] - rfirst[t] + 1) + 4.0 * kResSigWords;
+    uint32_t want = 1 + (uint32_t)std::min<double>(W - 1, std::floor((pre + c / 2) * W / total));
+    if (want < w) want = w;
+    while (w < want) wg_tiles[++w] = (uint32_t)t;
+    res_owner_[t] = w;
+    pre += c;
+  }
+  while (w < G) wg_tiles[++w] = (uint32_t)T;
+  uint32_t tok_words = 0, nr_max = 0, nt_max = 0;
+  res_wg_ntiles_.assign(G, 0);
+  for (uint32_t g = 0; g < G; ++g) {
+    const uint32_t a = wg_tiles[g], b = wg_tiles[g + 1];
+    res_wg_ntiles_[g] = b - a;
+    if (b - a > kResMaxTiles) return;
+    nt_max = std::max(nt_max, b - a);
+    uint32_t o = 0;
+    for (uint32_t t = a; t < b; ++t) {
+      lofs[t] = o;
+      o += words[t];
+    }
+    tok_words = std::max(tok_words, o);
+    wg_rank[g] = a < b ? rfirst[a] : (a < T ? rfirst[a] : rlast[T - 1] + 1);
+    const uint32_t r_end = a < b ? rlast[b - 1] + 1 : wg_rank[g];
+    nr_max = std::max(nr_max, r_end - wg_rank[g]);
+  }
+  wg_rank[G] = rlast[T - 1] + 1;
+  tok_words += (uint32_t)kWaveTok;  // every lane reads its 16 tokens of a full chunk from any tile start
+  nr_max = (nr_max + 1u) & ~1u;
+  const size_t shm = (size_t)tok_words * 4 + (size_t)nr_max * 8 + (size_t)nt_max * kResSigWords * 4;
+  if ((long)shm > budget) return;
+  res_grid_ = G;
+  res_tok_words_ = tok_words;
+  res_w_words_ = nr_max;
+  res_shm_ = shm;
+  res_all_.clear();
+  for (uint32_t g = 1; g < G; ++g) res_all_.push_back(g);
+  res_wg_tiles_ = dalloc<uint32_t>(G + 1, &bytes_alloc_);
+  res_wg_rank_ = dalloc<uint32_t>(G + 1, &bytes_alloc_);
+  res_tile_lofs_ = dalloc<uint32_t>(T, &bytes_alloc_);
+  res_cmd_ = dalloc<uint32_t>(kResRing * 8, &bytes_alloc_);
+  res_q_ = dalloc<uint64_t>((size_t)G * kResRing, &bytes_alloc_);
+  HIP_OK(hipMemcpy(res_wg_tiles_, wg_tiles.data(), (G + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(res_wg_rank_, wg_rank.data(), (G + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(res_tile_lofs_, lofs.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_OK(hipMemset(res_cmd_, 0, kResRing * 8 * sizeof(uint32_t)));
+  if (std::getenv("SHREDWORD_RESIDENT_DEBUG")) {
+    res_dbg_ = dalloc<uint32_t>((size_t)G * 4, &bytes_alloc_);
+    HIP_OK(hipMemset(res_dbg_, 0, (size_t)G * 16));
+  }
+  if (const char* e = std::getenv("SHREDWORD_RESIDENT_STAMPS")) {
+    res_stamps_ = dalloc<uint64_t>((size_t)G * 8, &bytes_alloc_);
+    HIP_OK(hipMemset(res_stamps_, 0, (size_t)G * 64));
+    res_stamp_detail_ = std::atoi(e) >= 2;
+  }
+  if (!res_mbox_) {
+    const unsigned pin = hipHostMallocMapped | hipHostMallocCoherent;
+    HIP_OK(hipHostMalloc(&res_mbox_, sizeof(ResMbox), pin));
+    std::memset(res_mbox_, 0, sizeof(ResMbox));
+    HIP_OK(hipHostGetDevicePointer(&res_mbox_dev_, res_mbox_, 0));
+    HIP_OK(hipHostMalloc((void**)&res_status_, 64, pin));
+    std::memset(res_status_, 0, 64);
+    HIP_OK(hipHostGetDevicePointer(&res_status_dev_, res_status_, 0));
+    for (auto& e : res_ev_) {
+      hipEvent_t ev;
+      HIP_OK(hipEventCreate(&ev));
+      e = ev;
+    }
+  }
+  HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_resident<true>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  resident_ok_ = true;
+}
+
+void Device::set_resident(bool on) {
+  park();
+  resident_on_ = on;
+}
+
+// Both slots' delta tables cover ids up to max_id before a launch needs them (a launch holds
+// the table pointers, so they cannot grow under it).
+void Device::reserve_ids(int32_t max_id) {
+  HIP_OK(hipSetDevice(ordinal_));
+  const uint32_t need = (uint32_t)std::max<int32_t>(max_id, 0) + 2;
+  bool grow = false;
+  for (const MergeSlot& s : slot_) grow |= !s.dsum || need > s.cap;
+  if (!grow) return;
+  if (!res_posted_.empty() || run_count_ > 0) return;  // later: merge_chain grows on demand
+  park();
+  for (MergeSlot& s : slot_) ensure_slots(s, need);
+  // both slots share keys_per_merge_: size them alike
+  const uint32_t cap = std::max(slot_[0].cap, slot_[1].cap);
+  for (MergeSlot& s : slot_) ensure_slots(s, cap);
+}
+
+void Device::start_resident() {
+  ResParams rp;
+  rp.tok = tok_;
+  rp.tile_off = tile_off_;
+  rp.tile_len = tile_len_;
+  rp.weight = weight_;
+  rp.wg_tiles = res_wg_tiles_;
+  rp.wg_rank = res_wg_rank_;
+  rp.tile_lofs = res_tile_lofs_;
+  rp.tok_words = res_tok_words_;
+  rp.w_words = res_w_words_;
+  rp.mbox = (const ResMbox*)res_mbox_dev_;
+  rp.cmd = res_cmd_;
+  rp.q = reinterpret_cast<u64*>(res_q_);
+  rp.status = (uint32_t*)res_status_dev_;
+  rp.seq0 = seq_ + 1;
+  rp.leader_polls = 1u << 23;  // ~10 s without a command: the launch ends itself (the host relaunches)
+  rp.keys_per_merge = keys_per_merge_;
+  rp.slot_cap = std::min(slot_[0].cap, slot_[1].cap);
+  for (int k = 0; k < 2; ++k) {
+    MergeSlot& sl = slot_[k];
+    ResSlot& r = rp.sl[k];
+    r.dsum = U(sl.dsum);
+    r.dft = U(sl.dft);
+    r.dlist = sl.dlist;
+    r.dcount = sl.dcount;
+    r.done = sl.dcount + 1;
+    r.out = (DeltaRecord*)sl.dev_recs;
+    r.hcount = (uint32_t*)sl.dev_count;
+    r.hstats = (u64*)((char*)sl.dev_count + 16);
+    r.hmlist = (uint32_t*)sl.dev_mlist;
+    r.rhdr = sl.rhdr;
+    r.rrec = U(sl.rrec);
+    r.rtile = sl.rtile;
+  }
+  rp.dbg = res_dbg_;
+  rp.stamps = U(res_stamps_);
+  res_status_[0] = 0;
+  HIP_OK(hipMemsetAsync(res_q_, 0, (size_t)res_grid_ * kResRing * sizeof(uint64_t), S(stream_)));
+  HIP_OK(hipEventRecord((hipEvent_t)res_ev_[0], S(stream_)));
+  void* args[] = {&rp};
+  HIP_OK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_resident<true>), dim3(res_grid_), dim3(kThreads),
+                                    args, (unsigned)res_shm_, S(stream_)));
+  HIP_OK(hipEventRecord((hipEvent_t)res_ev_[1], S(stream_)));
+  res_running_ = true;
+  res_merges_ = 0;
+  ++res_launches_;
+}
+
+// Posts one command to the resident launch (relaunching it first if it ended on its time-out).
+// Merge and unmerge commands name their participants; a merge's are kept by slot for its undo.
+uint32_t Device::post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int slot) {
+  if (res_running_ && __atomic_load_n(&res_status_[0], __ATOMIC_ACQUIRE) == kOpTimeout) {
+    if (!res_posted_.empty()) fatal("k_resident ended on its time-out with merges in flight");
+    HIP_OK(hipStreamSynchronize(S(stream_)));
+    res_running_ = false;
+  }
+  if (!res_running_ && op != kOpStop) start_resident();
+  const uint32_t seq = ++seq_;
+  ResCmd* m = &static_cast<ResMbox*>(res_mbox_)->cmd[seq % kResRing];
+  const uint32_t* parts = nullptr;
+  uint32_t np = res_grid_;
+  if (op == kOpMerge) {
+    std::vector<uint32_t>& pp = res_post_parts_[slot];
+    pp.clear();
+    if (skip_ && index_.candidates(a, b, &cand_) && !cand_.empty()) {
+      for (uint32_t t : cand_) {  // ascending tiles -> ascending owners
+        const uint32_t o = res_owner_[t];
+        if (pp.empty() || pp.back() != o) pp.push_back(o);
+      }
+    } else {
+      pp = res_all_;
+    }
+    for (uint32_t o : pp) visited_tiles_ += res_wg_ntiles_[o];
+    parts = pp.data();
+    np = (uint32_t)pp.size();
+  } else if (op == kOpUnmerge) {
+    parts = res_post_parts_[slot].data();
+    np = (uint32_t)res_post_parts_[slot].size();
+  }
+  if (parts) std::memcpy(m->parts, parts, np * sizeof(uint32_t));
+  m->op = op;
+  m->a = a;
+  m->b = b;
+  m->X = X;
+  m->slot = (uint32_t)slot;
+  m->nparts = np;
+  __atomic_store_n(&m->seq, seq, __ATOMIC_RELEASE);
+  return seq;
+}
+
+void Device::wait_resident(const MergeSlot& sl, uint32_t seq) {
+  volatile uint32_t* flag = sl.host_count + 1;
+  const double t0 = now_seconds();
+  unsigned spins = 0;
+  while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+    __builtin_ia32_pause();
+    if (++spins % 4096 != 0) continue;
+    if (__atomic_load_n(&res_status_[0], __ATOMIC_ACQUIRE) == kOpTimeout)
+      fatal("k_resident ended on its time-out before a posted merge completed");
+    if (res_dbg_ && now_seconds() - t0 > 3.0) resident_dump("no flag after 3 s");
+    if (now_seconds() - t0 > 120.0) {
+      const hipError_t e = hipStreamQuery(S(stream_));
+      if (e != hipSuccess && e != hipErrorNotReady) HIP_OK(e);
+      if (now_seconds() - t0 > 600.0) fatal("k_resident did not signal completion within 600 s");
+    }
+  }
+}
+
+size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
+  if (res_posted_.empty() || res_posted_.front().X != X) fatal("collect: merge X is not the oldest posted merge");
+  const ResPost rp = res_posted_.front();
+  res_posted_.erase(res_posted_.begin());
+  MergeSlot& sl = slot_[rp.slot];
+  wait_resident(sl, rp.seq);
+  const u64* hs = (const u64*)(sl.host_count + 4);
+  const size_t n = sl.host_count[0];
+  const uint32_t nm = sl.host_count[2];
+  index_.set_tiles(X, sl.host_mlist, nm);
+  res_lat_us_ += 1e-2 * (double)hs[2];  // s_memrealtime: 100 MHz
+  res_lat_n_ += 1;
+  if (res_stamps_) {
+    for (int k = 0; k < 2; ++k) res_phase_[k] += 1e-2 * (double)hs[3 + k];
+    res_phase_[3] += 1e-2 * (double)hs[2];
+    res_phase_n_ += 1;
+  }
+  if (timing_) times_.merge_bytes += 4.0 * (double)live_tokens_est_;
+  ++res_merges_;
+  live_tokens_est_ -= hs[0];
+  records_total_ += n;
+  records_max_ = std::max<uint64_t>(records_max_, n);
+  *recs = sl.host_recs;
+  return n;
+}
+
+// Diagnostic (SHREDWORD_RESIDENT_DEBUG=1): the state of a stuck resident launch, then exit.
+void Device::resident_dump(const char* why) {
+  const uint32_t G = res_grid_;
+  hipStream_t s;
+  HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  std::vector<uint32_t> dbg(4 * G), cmd(kResRing * 8);
+  std::vector<uint64_t> q((size_t)G * kResRing);
+  HIP_OK(hipMemcpyAsync(dbg.data(), res_dbg_, dbg.size() * 4, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(cmd.data(), res_cmd_, cmd.size() * 4, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(q.data(), res_q_, q.size() * 8, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  std::fprintf(stderr, "[RESIDENT] %s: seq_=%u status=%u posted=%zu flags=%u/%u\n", why, seq_, res_status_[0],
+               res_posted_.size(), slot_[0].host_count[1], slot_[1].host_count[1]);
+  for (const ResPost& rp : res_posted_)
+    std::fprintf(stderr, "[RESIDENT]   posted X=%d seq=%u slot=%d np=%u\n", rp.X, rp.seq, rp.slot, rp.nparts);
+  for (uint32_t g = 0; g < G; ++g) {
+    std::fprintf(stderr, "[RESIDENT] wg %u: phase %u seq %u pi %u T %u | q", g, dbg[4 * g], dbg[4 * g + 1], dbg[4 * g + 2],
+                 dbg[4 * g + 3]);
+    for (uint32_t k = 0; k < kResRing; ++k) {
+      const uint64_t v = q[(size_t)g * kResRing + k];
+      std::fprintf(stderr, " %u:%u", (uint32_t)v, (uint32_t)(v >> 32) & 0xFFFF);
+    }
+    std::fprintf(stderr, "\n");
+  }
+  std::fflush(stderr);
+  std::_Exit(3);
+}
+
+void Device::park() {
+  if (!res_running_) return;
+  HIP_OK(hipSetDevice(ordinal_));
+  if (!res_posted_.empty()) fatal("park: a resident merge was not collected");
+  post_resident(kOpStop, 0, 0, 0, 0);
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  res_running_ = false;
+  res_status_[0] = 0;
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)res_ev_[0], (hipEvent_t)res_ev_[1]));
+  res_ms_ += ms;
+  if (timing_ && res_merges_) {  // one launch: its wall time is the merge loop's device time
+    times_.merge_ms += ms;
+    times_.merge_launches += res_merges_;
+  }
+  res_merges_ = 0;
+  if (res_stamps_ && res_phase_n_) {
+    std::fprintf(stderr, "[RESIDENT] %llu merges, mean us after dispatch: go %.2f work %.2f flag %.2f\n",
+                 (unsigned long long)res_phase_n_, res_phase_[0] / res_phase_n_, res_phase_[1] / res_phase_n_,
+                 res_phase_[3] / res_phase_n_);
+    res_phase_[0] = res_phase_[1] = res_phase_[3] = 0;
+    res_phase_n_ = 0;
+  }
+  // the tiles are back in HBM: their pair signatures for k_merge / k_unmerge
+  const int grid = (int)std::min<size_t>((ntiles_ + kWaves - 1) / kWaves, (size_t)cu_count_ * 8);
+  k_sig_build<<<grid, kThreads, 0, S(stream_)>>>(tok_, tile_off_, tile_len_, (uint32_t)ntiles_, sig_);
+  HIP_OK(hipGetLastError());
 }
 
 }  // namespace shred

@@ -12,6 +12,7 @@
 // No HIP type appears here so host C++ can include it; bpe_device.hip implements it.
 #pragma once
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdio>
 #include <cstdint>
@@ -80,11 +81,26 @@ class Device : public Backend {
   // K4: merge X's records (host memory); the first collect of a chain waits for the launch.
   size_t collect(int32_t X, const DeltaRecord** recs) override;
   static constexpr int kChainMax = 8;
-  int max_chain() const override { return speculate_ ? kChainMax : 1; }
-  bool can_overlap() const override { return speculate_; }
+  int max_chain() const override { return speculate_ && !resident_eligible() ? kChainMax : 1; }
+  bool can_overlap() const override {
+    return speculate_ && (!resident_eligible() || (uint32_t)max_id_seen_ + 3 < std::min(slot_[0].cap, slot_[1].cap));
+  }
+  void reserve_ids(int32_t max_id) override;
   uint64_t exchange_overflows() const { return x_overflows_; }
   // Undoes the chain's uncollected merges >= X with k_unmerge (newest first), host-free.
   void rollback(int32_t X) override;
+  // LDS-resident merge loop (k_resident): when the types table fits the chip's LDS, single
+  // merges run in one persistent launch that holds the table in LDS; quiesce() ends it and
+  // leaves the HBM stream current.  Results are identical with it on or off.
+  void quiesce() override { park(); }
+  void park();
+  void set_resident(bool on);
+  bool resident() const { return resident_on_; }
+  bool resident_eligible() const { return resident_on_ && resident_ok_ && !exchange_; }
+  uint64_t resident_launches() const { return res_launches_; }
+  double resident_ms() const { return res_ms_; }
+  // mean dispatch -> host flag time of a resident merge (device clock), us
+  double resident_latency_us() const { return res_lat_n_ ? res_lat_us_ / (double)res_lat_n_ : 0.0; }
   void set_speculation(bool on) { speculate_ = on; }
   uint64_t rollbacks() const { return rollbacks_; }
   // Tuning: k_merge grid cap.
@@ -248,6 +264,52 @@ class Device : public Backend {
   int merge_blocks_per_cu_ = 4;
 
   size_t bytes_alloc_ = 0;
+
+  // ---- k_resident state (bpe_device.hip "K2+K3 resident")
+  struct ResPost {          // a merge posted to the resident loop and not yet collected
+    int32_t X, a, b;
+    uint32_t seq;
+    int slot;
+    uint32_t nparts;
+  };
+  void plan_resident(const TiledStream& ts);
+  void free_resident();
+  void start_resident();
+  uint32_t post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int slot);
+  void wait_resident(const MergeSlot& sl, uint32_t seq);
+  size_t collect_resident(int32_t X, const DeltaRecord** recs);
+  [[noreturn]] void resident_dump(const char* why);
+  bool resident_on_ = true;       // option (SHREDWORD_RESIDENT / set_option resident)
+  bool resident_ok_ = false;      // the uploaded table fits (plan_resident)
+  bool res_running_ = false;      // a k_resident launch is live
+  std::vector<ResPost> res_posted_;  // oldest first (at most two: a merge and the guess after it)
+  std::vector<uint32_t> res_post_parts_[2];  // participants of the posted merges, by slot
+  uint32_t res_grid_ = 0, res_tok_words_ = 0, res_w_words_ = 0;
+  size_t res_shm_ = 0;
+  uint32_t* res_wg_tiles_ = nullptr;   // device: grid + 1
+  uint32_t* res_wg_rank_ = nullptr;    // device: grid + 1
+  uint32_t* res_tile_lofs_ = nullptr;  // device: per tile
+  std::vector<uint32_t> res_owner_;    // tile -> workgroup (workgroup 0 dispatches, owns none)
+  std::vector<uint32_t> res_wg_ntiles_;
+  std::vector<uint32_t> res_all_;      // every worker workgroup (1 .. grid-1)
+  std::vector<uint32_t> res_parts_;
+  void* res_mbox_ = nullptr;           // pinned host ResMbox (command ring)
+  void* res_mbox_dev_ = nullptr;
+  uint32_t* res_cmd_ = nullptr;        // device command ring
+  uint64_t* res_q_ = nullptr;          // device per-workgroup queues
+  uint32_t* res_dbg_ = nullptr;        // device: per-workgroup progress (SHREDWORD_RESIDENT_DEBUG)
+  uint64_t* res_stamps_ = nullptr;     // device: per-participant phase stamps (SHREDWORD_RESIDENT_STAMPS)
+  double res_phase_[4] = {};
+  uint64_t res_phase_n_ = 0;
+  bool res_stamp_detail_ = false;
+  uint32_t* res_status_ = nullptr;     // pinned host status
+  void* res_status_dev_ = nullptr;
+  void* res_ev_[2] = {};
+  uint64_t res_launches_ = 0;
+  uint64_t res_merges_ = 0;            // merges collected in the current launch
+  double res_ms_ = 0;                  // Σ k_resident launch durations (HIP events)
+  double res_lat_us_ = 0;              // Σ per-merge dispatch -> flag times (device clock)
+  uint64_t res_lat_n_ = 0;
 };
 
 }  // namespace shred

@@ -110,11 +110,15 @@ int Engine::merge_batch(Backend& be, int batch) {
     return 0;
   }
   int done = 0;
+  be.reserve_ids(kBaseVocab +
+                 (int32_t)std::min<size_t>(merge_a_.size() + (size_t)batch,
+                                           std::max<size_t>(target_vocab_, merge_a_.size() + kBaseVocab + 1)));
   while (done < batch && !sel_.heap_empty()) {
     if (!merge_one(be, batch - done)) break;
     ++done;
   }
   finish_speculation(be);
+  be.quiesce();
   return done;
 }
 
@@ -126,6 +130,7 @@ int Engine::train(Backend& be) {
   times_.init_s += now_seconds() - t0;
   int total = 0;
   const int target = (int)target_vocab_ - kBaseVocab;  // bpe.cpp:353
+  if (target > 0) be.reserve_ids((int32_t)target_vocab_);
   while (total < target) {
     if (sel_.heap_empty()) {
       if (log_ >= 1) std::printf("[INFO]\t Heap exhausted, stopping training\n");
@@ -150,6 +155,7 @@ int Engine::train(Backend& be) {
     total += merged;
   }
   finish_speculation(be);
+  be.quiesce();
   if (trace_) std::fflush(trace_);
   times_.train_s += now_seconds() - t0;
   if (log_ >= 1) std::printf("[INFO]\t Training completed. Performed %d merges\n", total);

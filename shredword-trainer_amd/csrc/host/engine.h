@@ -34,6 +34,10 @@ class Backend {
   // Undoes every launched merge with id >= X that was not collected, newest first (each
   // expands its X back into (a, b)), so the corpus is exactly as before those merges.
   virtual void rollback(int32_t X) {}
+  // Ends any persistent device work (the merge loop's end): the corpus is then current in HBM.
+  virtual void quiesce() {}
+  // The merge loop will create ids up to max_id (tables can be sized once, up front).
+  virtual void reserve_ids(int32_t max_id) {}
   // K6: final weighted token histogram over ids [0, T) (all ranks).
   virtual void token_freq(size_t T, std::vector<uint64_t>* freq) = 0;
 };

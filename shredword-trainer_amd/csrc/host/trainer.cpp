@@ -39,6 +39,7 @@ struct Trainer {
   int device = -1;
   bool local_exchange = false;   // test: the multi-GPU exchange over a single-rank communicator
   uint32_t exchange_bucket = 0;  // records per rank and exchange bucket (0: default)
+  int resident = -1;             // LDS-resident merge loop: -1 default (on), 0 off, 1 on
   double load_s = 0;
 };
 
@@ -86,6 +87,9 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
       if (b < 1) return -1;
       t->exchange_bucket = (uint32_t)b;
     }
+  } else if (key == "resident") {
+    t->resident = std::atoi(val.c_str()) != 0 ? 1 : 0;
+    if (t->dev) t->dev->set_resident(t->resident != 0);
   } else if (key == "device") {
     t->device = std::atoi(val.c_str());
   } else {
@@ -112,6 +116,7 @@ bool ensure_device(Trainer* t, const char* caller) {
     t->dev.reset(new Device(ord));
     t->dev->set_timing(t->timing);
     t->dev->set_unk(t->config.unk_id);
+    if (t->resident >= 0) t->dev->set_resident(t->resident != 0);
     if (dist_active() || t->local_exchange) {
       Device::Exchange x;
       if (dist_active()) {
@@ -262,6 +267,8 @@ int shred_reset(Trainer* t) {
 double shred_probe_merge(Trainer* t, int32_t a, int32_t b, int iters) {
   if (!t || iters <= 0 || !ensure_device(t, "shred_probe_merge")) return -1.0;
   const int32_t X = kBaseVocab + (int32_t)t->engine.num_merges();
+  const bool resident = t->dev->resident();  // probes time the launch path
+  t->dev->set_resident(false);
   double total = 0;
   for (int i = 0; i < iters; ++i) {
     const double t0 = now_seconds();
@@ -269,16 +276,23 @@ double shred_probe_merge(Trainer* t, int32_t a, int32_t b, int iters) {
     const DeltaRecord* recs = nullptr;
     const size_t n = t->dev->collect(X, &recs);
     total += now_seconds() - t0;
-    if (n != 0) return -1.0;  // the pair occurs: the probe would have changed the corpus
+    if (n != 0) {
+      t->dev->set_resident(resident);
+      return -1.0;  // the pair occurs: the probe would have changed the corpus
+    }
   }
+  t->dev->set_resident(resident);
   return 1e6 * total / iters;
 }
 
 int shred_probe_rollback(Trainer* t, int32_t a, int32_t b) {
   if (!t || !ensure_device(t, "shred_probe_rollback")) return -1;
   const int32_t X = kBaseVocab + (int32_t)t->engine.num_merges();
+  const bool resident = t->dev->resident();  // the undo path belongs to the launch path
+  t->dev->set_resident(false);
   t->dev->merge_scan(a, b, X);
   t->dev->rollback(X);
+  t->dev->set_resident(resident);
   return 0;
 }
 
@@ -316,6 +330,8 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
     s->device_bytes = t->dev->device_bytes();
     s->num_tiles = t->dev->num_tiles();
     s->live_tokens = t->dev->live_tokens();
+    s->resident_launches = t->dev->resident_launches();
+    s->resident_ms = t->dev->resident_ms();
   }
   s->num_words = t->wt.num_words();
   s->num_symbols = t->wt.num_symbols();

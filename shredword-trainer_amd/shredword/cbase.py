@@ -64,7 +64,8 @@ class ShredStats(Structure):
                 ("apply_cycles_walk", c_uint64),
                 ("spec_hits", c_uint64), ("spec_misses", c_uint64),
                 ("exchange_overflows", c_uint64),
-                ("hist_kernel_ms", c_double), ("hist_kernel_bytes", c_double), ("hist_launches", c_uint64)]
+                ("hist_kernel_ms", c_double), ("hist_kernel_bytes", c_double), ("hist_launches", c_uint64),
+                ("resident_launches", c_uint64), ("resident_ms", c_double)]
 
 
 Trainer = c_void_p

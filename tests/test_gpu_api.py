@@ -182,6 +182,7 @@ def test_speculation_lockstep(layout, medium_corpus):
         t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
         t.set_option("layout", layout)
         t.set_option("speculate", spec)
+        t.set_option("resident", 0)  # speculation belongs to the launch path
         t.load_corpus(medium_corpus)
         lib.bpe_init(t.trainer)
         ts.append(t)
@@ -199,6 +200,41 @@ def test_speculation_lockstep(layout, medium_corpus):
     assert st["spec_hits"] > 0 and st["spec_misses"] > 0
     for t in ts:
         t.destroy()
+
+
+def test_resident_lockstep(medium_corpus, tmp_path):
+    """The LDS-resident merge loop (k_resident) against the launch path, in bpe_merge_batch
+    chunks: identical merges and device token streams after every chunk (each chunk ends the
+    persistent launch and writes the tiles back; id 4096 regrows the delta tables mid-run)."""
+    from shredword.cbase import lib
+    ts = []
+    for res in (0, 1):
+        t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+        t.set_option("resident", res)
+        t.load_corpus(medium_corpus)
+        lib.bpe_init(t.trainer)
+        ts.append(t)
+    done = 0
+    for chunk in [1, 300, 7, 1000, 64] * 20:
+        na = lib.bpe_merge_batch(ts[0].trainer, chunk)
+        nb = lib.bpe_merge_batch(ts[1].trainer, chunk)
+        assert na == nb
+        xa, xb = ts[0].tokens(), ts[1].tokens()
+        assert xa.shape == xb.shape and (xa == xb).all(), f"streams differ after {done + na} merges"
+        done += na
+        if na < chunk:
+            break
+    assert done > 4000
+    st0, st1 = ts[0].stats(), ts[1].stats()
+    assert st0["resident_launches"] == 0 and st1["resident_launches"] > 10
+    assert st1["spec_hits"] > 0 and st1["spec_misses"] > 0  # guesses confirmed and undone in LDS
+    paths = []
+    for i, t in enumerate(ts):
+        m, v = str(tmp_path / f"r{i}.model"), str(tmp_path / f"r{i}.vocab")
+        t.save(m, v)
+        paths.append((open(m, "rb").read(), open(v, "rb").read()))
+        t.destroy()
+    assert paths[0] == paths[1]
 
 
 def _parse_vocab(vocab: bytes, ops):

@@ -11,7 +11,7 @@ from conftest import PKG, golden_cases
 pytestmark = pytest.mark.gpu
 
 
-def _train(case, corpus, tmp_path, layout="types"):
+def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None):
     from shredword.trainer import BPETrainer
 
     cfg = case["config"]
@@ -21,10 +21,13 @@ def _train(case, corpus, tmp_path, layout="types"):
     t.set_option("log", 0)
     t.set_option("layout", layout)
     t.set_option("trace", trace)
+    t.set_option("resident", resident)
     t.load_corpus(corpus)
     merges = t.train()
     model, vocab = str(tmp_path / "g.model"), str(tmp_path / "g.vocab")
     t.save(model, vocab)
+    if stats is not None:
+        stats.update(t.stats())
     t.destroy()
     return merges, open(model, "rb").read(), open(vocab, "rb").read(), open(trace).read()
 
@@ -34,12 +37,30 @@ API_CASES = [n for n in golden_cases() if not n.startswith("cli_")]
 
 @pytest.mark.parametrize("name", API_CASES)
 def test_types_layout_matches_reference(name, case_corpus, tmp_path):
+    """Default path: the LDS-resident merge loop (k_resident) wherever the table fits; the
+    adversarial corpora hold a word longer than one tile and take the launch path."""
     case, corpus = case_corpus(name)
-    merges, model, vocab, trace = _train(case, corpus, tmp_path, "types")
+    st = {}
+    merges, model, vocab, trace = _train(case, corpus, tmp_path, "types", stats=st)
     assert merges == case["merges"]
     assert trace == case["trace"]
     assert model == case["model_bytes"]
     assert vocab == case["vocab_bytes"]
+    if merges > 0 and not name.startswith("adv_"):
+        assert st["resident_launches"] > 0
+
+
+@pytest.mark.parametrize("name", API_CASES)
+def test_types_layout_launch_path_matches_reference(name, case_corpus, tmp_path):
+    """The per-merge launch path (k_merge + speculation + k_unmerge), resident loop off."""
+    case, corpus = case_corpus(name)
+    st = {}
+    merges, model, vocab, trace = _train(case, corpus, tmp_path, "types", resident=0, stats=st)
+    assert merges == case["merges"]
+    assert trace == case["trace"]
+    assert model == case["model_bytes"]
+    assert vocab == case["vocab_bytes"]
+    assert st["resident_launches"] == 0
 
 
 @pytest.mark.parametrize("name", ["c1_ascii10m_v8192", "ascii1m_v3000_mpf2", "adv_unk0", "adv_unkm1",
