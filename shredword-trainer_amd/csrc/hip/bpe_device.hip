@@ -30,6 +30,7 @@
 #endif
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 #include <cstring>
 #include <stdexcept>
@@ -980,14 +981,14 @@ constexpr uint32_t kResRing = 8;         // host command ring, device command ri
 constexpr uint32_t kOpUnmerge = 4;
 
 // One host command (pinned host memory, written by the host; only the leader reads it).
+// Every field is an 8-byte granule {seq, value} written by one aligned 8-byte store, so the
+// leader reads the whole command in ONE round trip (13 lanes, one granule each) and takes it
+// only when every granule carries the command number: no ordering between the host's stores or
+// the device's loads is needed.  The command for number s lives in cmd[s % kResRing].
+constexpr int kCmdOp = 0, kCmdA = 1, kCmdB = 2, kCmdX = 3, kCmdSlotN = 4, kCmdMask = 5;  // mask: 8 granules
+constexpr int kCmdGranules = 13;
 struct ResCmd {
-  uint32_t seq;     // written last (release): the command number; the entry is cmd[seq % kResRing]
-  uint32_t op;      // kOpMerge, kOpUnmerge (expand X -> a b where the last merge matched), kOpStop
-  int32_t a, b, X;
-  uint32_t slot;    // merge: which of the two record slots completes it
-  uint32_t nparts;  // participants; == grid: every workgroup (parts[] unused)
-  uint32_t pad;
-  uint32_t parts[kMaxMergeGroups];
+  uint64_t g[16];  // g[k] = seq | value << 32
 };
 struct ResMbox {
   ResCmd cmd[kResRing];
@@ -1038,9 +1039,15 @@ struct ResDelta {
   uint32_t spill;
 };
 
-// Queue entry: seq (32) | count (16, this workgroup's entry number, 1-based) | pi (8) | op (8).
-__device__ __forceinline__ u64 q_entry(uint32_t seq, uint32_t cnt, uint32_t pi, uint32_t op) {
-  return (u64)seq | ((u64)(cnt & 0xFFFFu) << 32) | ((u64)(pi & 0xFFu) << 48) | ((u64)op << 56);
+// Queue entry: two 8-byte halves, each tagged with this workgroup's entry number (count, 1-based,
+// 16 bits); a reader takes the entry when both halves carry the count it expects.
+//   half 0: count 16 | pi 8 | op 3 | slot 1 | T 9 | a 20     half 1: count 16 | b 20 | X 20
+__device__ __forceinline__ void q_pack(uint32_t cnt, uint32_t pi, uint32_t op, uint32_t slot, uint32_t T, int32_t a,
+                                       int32_t b, int32_t X, u64* h0, u64* h1) {
+  const u64 c = cnt & 0xFFFFu;
+  *h0 = c | ((u64)(pi & 0xFFu) << 16) | ((u64)(op & 7u) << 24) | ((u64)(slot & 1u) << 27) | ((u64)(T & 0x1FFu) << 28) |
+        ((u64)((uint32_t)a & 0xFFFFFu) << 37);
+  *h1 = c | ((u64)((uint32_t)b & 0xFFFFFu) << 16) | ((u64)((uint32_t)X & 0xFFFFFu) << 36);
 }
 
 __device__ __forceinline__ void res_sig_bits(int32_t x, int32_t y, uint32_t* h1, uint32_t* h2) {
@@ -1074,9 +1081,6 @@ __device__ __forceinline__ void res_sig_build(uint32_t* sg, const int32_t* t, ui
   wave_lds_sync();
 }
 
-__device__ __forceinline__ uint32_t host_load(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 // One wave applies (a, b) -> X to a single-chunk tile held in LDS at tb (live length *len):
 // k_merge's per-chunk logic with no carries (the tile is its own first and last chunk).
@@ -1370,6 +1374,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   __shared__ uint32_t s_nmt, s_nrec, s_last;
   __shared__ uint32_t s_cmd[8];
   __shared__ u64 s_cnt[2];
+  __shared__ u64 s_tlead;
   __shared__ uint32_t s_pre[kMaxMergeGroups + 1], s_pmt[kMaxMergeGroups + 1];
   __shared__ uint32_t s_wtot[2][kWaves];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1410,55 +1415,52 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   uint32_t idle = 0;         // leader: polls without a command
   uint32_t consumed = 0;     // thread 0: entries taken from this workgroup's queue
   uint32_t exit_op = kOpStop;
-  u64* myq = p.q + (size_t)me * kResRing;
+  const u64* myq = p.q + (size_t)me * kResRing * 2;
   for (;;) {
     // ---- the leader hands out the next host command, if one is posted (one poll per pass)
     if (me == 0 && wid == 0) {
-      const ResCmd* hc = &p.mbox->cmd[expect % kResRing];
-      uint32_t op = 0, np = 0, slot = 0;
-      int32_t a = 0, b = 0, X = 0;
-      if (lane == 0) {
-        if (host_load(&hc->seq) == expect) {
-          op = host_load(&hc->op);
-          np = host_load(&hc->nparts);
-          slot = host_load(&hc->slot);
-          a = (int32_t)host_load((const uint32_t*)&hc->a);
-          b = (int32_t)host_load((const uint32_t*)&hc->b);
-          X = (int32_t)host_load((const uint32_t*)&hc->X);
-          idle = 0;
-        } else if (++idle >= p.leader_polls) {
-          op = kOpTimeout;  // nobody posts any more: every workgroup writes back and leaves
-        }
+      const uint64_t* hc = p.mbox->cmd[expect % kResRing].g;
+      // lane k < kCmdGranules reads granule k: the whole command in one round trip
+      const u64 gv = lane < kCmdGranules ? __hip_atomic_load(hc + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+      const bool tagged = lane >= kCmdGranules || (uint32_t)gv == expect;
+      const bool ready = __all(tagged);
+      const uint32_t val = (uint32_t)(gv >> 32);
+      uint32_t op = 0;
+      if (ready) {
+        op = (uint32_t)__shfl((int)val, kCmdOp, 64);
+        idle = 0;
+      } else if (++idle >= p.leader_polls) {
+        op = kOpTimeout;  // nobody posts any more: every workgroup writes back and leaves
       }
-      op = (uint32_t)__shfl((int)op, 0, 64);
       if (op) {
-        np = (uint32_t)__shfl((int)np, 0, 64);
-        if ((op != kOpMerge && op != kOpUnmerge) || np > G) np = G;
-        if (lane == 0 && (op == kOpMerge || op == kOpUnmerge)) {
-          uint32_t* dc = p.cmd + (expect % kResRing) * 8;
-          __hip_atomic_store(dc, (uint32_t)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(dc + 1, (uint32_t)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(dc + 2, (uint32_t)X, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(dc + 3, np, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(dc + 4, slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int32_t a = __shfl((int)val, kCmdA, 64), b = __shfl((int)val, kCmdB, 64), X = __shfl((int)val, kCmdX, 64);
+        const uint32_t sn = (uint32_t)__shfl((int)val, kCmdSlotN, 64);
+        const bool merge_like = ready && (op == kOpMerge || op == kOpUnmerge);
+        // lane l covers workgroups 4l .. 4l+3: its mask nibble, participant indices by a wave scan
+        const uint32_t mw = (uint32_t)__shfl((int)val, kCmdMask + (lane >> 3), 64);
+        uint32_t nib = merge_like ? (mw >> ((lane & 7) * 4)) & 0xFu : 0xFu;
+        if (4u * (uint32_t)lane >= G) nib = 0;
+        for (int k = 0; k < 4; ++k)
+          if (4u * lane + k >= G) nib &= ~(1u << k);
+        const uint32_t cnt = __popc(nib);
+        const uint32_t incl = wave_scan_add(cnt);
+        const uint32_t T = merge_like ? lane_read(incl, 63) : G;
+        uint32_t pi = incl - cnt;
+        if (lane == 0 && merge_like) {
+          uint32_t* dc = p.cmd + ((uint32_t)X % kResRing) * 8;
           __hip_atomic_store(reinterpret_cast<u64*>(dc + 6), (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         }
-        uint32_t wgs[kMaxMergeGroups / 64];  // this lane's participants, all loads in flight together
 #pragma unroll
-        for (int k = 0; k < kMaxMergeGroups / 64; ++k) {
-          const uint32_t i = (uint32_t)lane + 64u * k;
-          wgs[k] = i >= np ? G : ((op == kOpMerge || op == kOpUnmerge) && np < G) ? host_load(&hc->parts[i]) : i;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the command lands before any queue entry
-#pragma unroll
-        for (int k = 0; k < kMaxMergeGroups / 64; ++k) {
-          const uint32_t i = (uint32_t)lane + 64u * k, wg = wgs[k];
-          if (wg < G) {  // distinct workgroups per lane: the counters need no atomics
-            const uint32_t c = ++s_qc[wg];
-            __hip_atomic_store(p.q + (size_t)wg * kResRing + ((c - 1) % kResRing), q_entry(expect, c, i, op),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
+        for (int k = 0; k < 4; ++k) {
+          if (!((nib >> k) & 1u)) continue;
+          const uint32_t wg = 4u * lane + k;  // distinct workgroups per lane: the counters need no atomics
+          const uint32_t c = ++s_qc[wg];
+          u64 h0, h1;
+          q_pack(c, pi++, op, sn & 1u, T, a, b, X, &h0, &h1);
+          u64* e = p.q + ((size_t)wg * kResRing + ((c - 1) % kResRing)) * 2;
+          __hip_atomic_store(e, h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(e + 1, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         ++expect;
       }
@@ -1466,33 +1468,27 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
     }
     // ---- this workgroup's next queue entry (the leader's workgroup never blocks here)
     if (threadIdx.x == 0) {
-      uint32_t got = 0;
-      u64 v = 0;
       const uint32_t want = (consumed + 1) & 0xFFFFu;
-      if (me == 0) {
-        v = __hip_atomic_load(myq + consumed % kResRing, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        got = ((uint32_t)(v >> 32) & 0xFFFFu) == want;
-        if (!got && !s_cmd[7]) __builtin_amdgcn_s_sleep(2);
-      } else {
-        while (((uint32_t)((v = __hip_atomic_load(myq + consumed % kResRing, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)) >> 32) & 0xFFFFu) != want)
-          __builtin_amdgcn_s_sleep(2);
-        got = 1;
+      const u64* e = myq + (consumed % kResRing) * 2;
+      u64 h0 = 0, h1 = 0;
+      bool got = false;
+      for (;;) {
+        h0 = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h1 = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        got = (uint32_t)(h0 & 0xFFFFu) == want && (uint32_t)(h1 & 0xFFFFu) == want;
+        if (got || me == 0) break;
+        __builtin_amdgcn_s_sleep(2);
       }
-      s_cmd[0] = got ? (uint32_t)(v >> 56) : 0u;
+      if (me == 0 && !got && !s_cmd[7]) __builtin_amdgcn_s_sleep(2);
+      s_cmd[0] = got ? (uint32_t)(h0 >> 24) & 7u : 0u;
       if (got) {
         ++consumed;
-        s_cmd[1] = (uint32_t)(v >> 48) & 0xFFu;
-        s_cmd[2] = (uint32_t)v;
-        const uint32_t op = s_cmd[0];
-        if (op == kOpMerge || op == kOpUnmerge) {
-          const uint32_t* dc = p.cmd + ((uint32_t)v % kResRing) * 8;
-          s_cmd[3] = __hip_atomic_load(dc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_cmd[4] = __hip_atomic_load(dc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_cmd[5] = __hip_atomic_load(dc + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_cmd[6] = __hip_atomic_load(dc + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
-                     (__hip_atomic_load(dc + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 16);
-        }
+        s_cmd[1] = (uint32_t)(h0 >> 16) & 0xFFu;
+        s_cmd[2] = (uint32_t)(h0 >> 27) & 1u;                     // slot
+        s_cmd[6] = (uint32_t)(h0 >> 28) & 0x1FFu;                 // T
+        s_cmd[3] = (uint32_t)(h0 >> 37) & 0xFFFFFu;               // a
+        s_cmd[4] = (uint32_t)(h1 >> 16) & 0xFFFFFu;               // b
+        s_cmd[5] = (uint32_t)(h1 >> 36) & 0xFFFFFu;               // X
       }
       s_nmt = 0;
       s_nrec = 0;
@@ -1506,12 +1502,12 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       exit_op = op;
       break;
     }
-    const uint32_t pi = s_cmd[1], seq = s_cmd[2];
+    const uint32_t pi = s_cmd[1], slot = s_cmd[2];
     const int32_t a = (int32_t)s_cmd[3], b = (int32_t)s_cmd[4], X = (int32_t)s_cmd[5];
-    const uint32_t T = s_cmd[6] & 0xFFFFu, slot = s_cmd[6] >> 16;
+    const uint32_t T = s_cmd[6];
     if (p.dbg && threadIdx.x == 0) {
       p.dbg[me * 4] = 2;
-      p.dbg[me * 4 + 1] = seq;
+      p.dbg[me * 4 + 1] = (uint32_t)X;
       p.dbg[me * 4 + 2] = pi;
       p.dbg[me * 4 + 3] = T;
     }
@@ -1605,6 +1601,9 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
     if (!s_last) continue;
     // ---- the last participant: gather the regions to the host, raise the slot's flag
     uint32_t n = 0, nm = 0;
+    if (threadIdx.x == 0)  // the dispatch stamp (per-merge device time), loaded beside the headers
+      s_tlead = __hip_atomic_load(reinterpret_cast<const u64*>(p.cmd + ((uint32_t)X % kResRing) * 8 + 6),
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     {
       u64 merged = 0, written = 0;
       uint32_t spill = 0, my_nrec = 0, my_nmt = 0;
@@ -1699,8 +1698,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      const u64 t_leader = __hip_atomic_load(reinterpret_cast<const u64*>(p.cmd + (seq % kResRing) * 8 + 6),
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const u64 t_leader = s_tlead;
       sys_store(&sl.hstats[0], s_cnt[0]);
       sys_store(&sl.hstats[1], s_cnt[1]);
       sys_store(&sl.hstats[2], (u64)__builtin_amdgcn_s_memrealtime() - t_leader);
@@ -1718,7 +1716,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       sys_store(&sl.hcount[0], n);
       sys_store(&sl.hcount[2], nm);
       atomicExch(&sl.done[8], 0u);
-      sys_flag(&sl.hcount[1], seq);
+      sys_flag(&sl.hcount[1], (uint32_t)X);  // the host clears the flag before posting to the slot
     }
   }
   // ---- STOP (or the leader's time-out): the tiles go back to HBM
@@ -2955,7 +2953,7 @@ void Device::flush_timing(bool block) {
 void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   HIP_OK(hipSetDevice(ordinal_));
   if (n < 1 || n > kChainMax) fatal("merge_chain: bad chain length");
-  if (n == 1 && run_count_ == 0 && ntiles_ && resident_eligible()) {  // k_resident
+  if (n == 1 && run_count_ == 0 && ntiles_ && resident_eligible() && X0 < (1 << 20)) {  // k_resident (ids: 20 bits)
     if (res_posted_.size() >= 2) fatal("merge_chain: two resident merges are already in flight");
     const int slot = X0 & 1;  // consecutive merges alternate slots
     bool grow = false;
@@ -2969,7 +2967,7 @@ void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
     }
     max_id_seen_ = std::max(max_id_seen_, X0);
     const uint32_t seq = post_resident(kOpMerge, ab[0], ab[1], X0, slot);
-    res_posted_.push_back({X0, ab[0], ab[1], seq, slot, (uint32_t)res_post_parts_[slot].size()});
+    res_posted_.push_back({X0, ab[0], ab[1], seq, slot, (uint32_t)res_post_parts_[slot].size(), now_seconds()});
     return;
   }
   park();
@@ -3294,7 +3292,7 @@ void Device::rollback(int32_t X) {
     while (!res_posted_.empty() && res_posted_.back().X >= X) {
       const ResPost rp = res_posted_.back();
       res_posted_.pop_back();
-      wait_resident(slot_[rp.slot], rp.seq);  // its completion leaves the slot before the slot's next merge
+      wait_resident(slot_[rp.slot], rp.X);  // its completion leaves the slot before the slot's next merge
       post_resident(kOpUnmerge, rp.a, rp.b, rp.X, rp.slot);
       ++rollbacks_;
     }
@@ -3509,7 +3507,7 @@ void Device::plan_resident(const TiledStream& ts) {
   res_wg_rank_ = dalloc<uint32_t>(G + 1, &bytes_alloc_);
   res_tile_lofs_ = dalloc<uint32_t>(T, &bytes_alloc_);
   res_cmd_ = dalloc<uint32_t>(kResRing * 8, &bytes_alloc_);
-  res_q_ = dalloc<uint64_t>((size_t)G * kResRing, &bytes_alloc_);
+  res_q_ = dalloc<uint64_t>((size_t)G * kResRing * 2, &bytes_alloc_);
   HIP_OK(hipMemcpy(res_wg_tiles_, wg_tiles.data(), (G + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(res_wg_rank_, wg_rank.data(), (G + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(res_tile_lofs_, lofs.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -3601,7 +3599,7 @@ void Device::start_resident() {
   rp.dbg = res_dbg_;
   rp.stamps = U(res_stamps_);
   res_status_[0] = 0;
-  HIP_OK(hipMemsetAsync(res_q_, 0, (size_t)res_grid_ * kResRing * sizeof(uint64_t), S(stream_)));
+  HIP_OK(hipMemsetAsync(res_q_, 0, (size_t)res_grid_ * kResRing * 2 * sizeof(uint64_t), S(stream_)));
   HIP_OK(hipEventRecord((hipEvent_t)res_ev_[0], S(stream_)));
   void* args[] = {&rp};
   HIP_OK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_resident<true>), dim3(res_grid_), dim3(kThreads),
@@ -3621,9 +3619,7 @@ uint32_t Device::post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int
     res_running_ = false;
   }
   if (!res_running_ && op != kOpStop) start_resident();
-  const uint32_t seq = ++seq_;
-  ResCmd* m = &static_cast<ResMbox*>(res_mbox_)->cmd[seq % kResRing];
-  const uint32_t* parts = nullptr;
+  uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t np = res_grid_;
   if (op == kOpMerge) {
     std::vector<uint32_t>& pp = res_post_parts_[slot];
@@ -3637,28 +3633,31 @@ uint32_t Device::post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int
       pp = res_all_;
     }
     for (uint32_t o : pp) visited_tiles_ += res_wg_ntiles_[o];
-    parts = pp.data();
-    np = (uint32_t)pp.size();
-  } else if (op == kOpUnmerge) {
-    parts = res_post_parts_[slot].data();
-    np = (uint32_t)res_post_parts_[slot].size();
+    slot_[slot].host_count[1] = 0xFFFFFFFFu;  // the merge raises X here
   }
-  if (parts) std::memcpy(m->parts, parts, np * sizeof(uint32_t));
-  m->op = op;
-  m->a = a;
-  m->b = b;
-  m->X = X;
-  m->slot = (uint32_t)slot;
-  m->nparts = np;
-  __atomic_store_n(&m->seq, seq, __ATOMIC_RELEASE);
+  if (op == kOpMerge || op == kOpUnmerge) {
+    const std::vector<uint32_t>& pp = res_post_parts_[slot];
+    for (uint32_t o : pp) mask[o >> 5] |= 1u << (o & 31);
+    np = (uint32_t)pp.size();
+  }
+  const uint32_t seq = ++seq_;
+  uint64_t* g = static_cast<ResMbox*>(res_mbox_)->cmd[seq % kResRing].g;
+  auto put = [&](int k, uint32_t v) { __atomic_store_n(&g[k], (uint64_t)seq | ((uint64_t)v << 32), __ATOMIC_RELAXED); };
+  put(kCmdOp, op);
+  put(kCmdA, (uint32_t)a);
+  put(kCmdB, (uint32_t)b);
+  put(kCmdX, (uint32_t)X);
+  put(kCmdSlotN, (uint32_t)slot | (np << 8));
+  for (int k = 0; k < 8; ++k) put(kCmdMask + k, mask[k]);
+  std::atomic_thread_fence(std::memory_order_release);
   return seq;
 }
 
-void Device::wait_resident(const MergeSlot& sl, uint32_t seq) {
+void Device::wait_resident(const MergeSlot& sl, int32_t X) {
   volatile uint32_t* flag = sl.host_count + 1;
   const double t0 = now_seconds();
   unsigned spins = 0;
-  while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+  while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != (uint32_t)X) {
     __builtin_ia32_pause();
     if (++spins % 4096 != 0) continue;
     if (__atomic_load_n(&res_status_[0], __ATOMIC_ACQUIRE) == kOpTimeout)
@@ -3677,7 +3676,14 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   const ResPost rp = res_posted_.front();
   res_posted_.erase(res_posted_.begin());
   MergeSlot& sl = slot_[rp.slot];
-  wait_resident(sl, rp.seq);
+  const double tw = now_seconds();
+  wait_resident(sl, rp.X);
+  {  // host clock: post -> flag seen, and the part of it spent waiting here
+    const double t1 = now_seconds();
+    res_post_flag_us_ += 1e6 * (t1 - rp.t_post);
+    res_host_wait_ += 1e6 * (t1 - tw);
+    res_parts_sum_ += rp.nparts;
+  }
   const u64* hs = (const u64*)(sl.host_count + 4);
   const size_t n = sl.host_count[0];
   const uint32_t nm = sl.host_count[2];
@@ -3704,7 +3710,7 @@ void Device::resident_dump(const char* why) {
   hipStream_t s;
   HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   std::vector<uint32_t> dbg(4 * G), cmd(kResRing * 8);
-  std::vector<uint64_t> q((size_t)G * kResRing);
+  std::vector<uint64_t> q((size_t)G * kResRing * 2);
   HIP_OK(hipMemcpyAsync(dbg.data(), res_dbg_, dbg.size() * 4, hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(cmd.data(), res_cmd_, cmd.size() * 4, hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(q.data(), res_q_, q.size() * 8, hipMemcpyDeviceToHost, s));
@@ -3717,8 +3723,8 @@ void Device::resident_dump(const char* why) {
     std::fprintf(stderr, "[RESIDENT] wg %u: phase %u seq %u pi %u T %u | q", g, dbg[4 * g], dbg[4 * g + 1], dbg[4 * g + 2],
                  dbg[4 * g + 3]);
     for (uint32_t k = 0; k < kResRing; ++k) {
-      const uint64_t v = q[(size_t)g * kResRing + k];
-      std::fprintf(stderr, " %u:%u", (uint32_t)v, (uint32_t)(v >> 32) & 0xFFFF);
+      const uint64_t v = q[((size_t)g * kResRing + k) * 2];
+      std::fprintf(stderr, " %u:%u", (uint32_t)(v & 0xFFFF), (uint32_t)(v >> 24) & 7u);
     }
     std::fprintf(stderr, "\n");
   }
@@ -3733,6 +3739,8 @@ void Device::park() {
   post_resident(kOpStop, 0, 0, 0, 0);
   HIP_OK(hipStreamSynchronize(S(stream_)));
   res_running_ = false;
+  for (MergeSlot& s2 : slot_)  // flags carried merge ids: the launch path compares launch numbers
+    if (s2.host_count) s2.host_count[1] = 0xFFFFFFFFu;
   res_status_[0] = 0;
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)res_ev_[0], (hipEvent_t)res_ev_[1]));
@@ -3741,14 +3749,18 @@ void Device::park() {
     times_.merge_ms += ms;
     times_.merge_launches += res_merges_;
   }
-  res_merges_ = 0;
-  if (res_stamps_ && res_phase_n_) {
-    std::fprintf(stderr, "[RESIDENT] %llu merges, mean us after dispatch: go %.2f work %.2f flag %.2f\n",
-                 (unsigned long long)res_phase_n_, res_phase_[0] / res_phase_n_, res_phase_[1] / res_phase_n_,
-                 res_phase_[3] / res_phase_n_);
-    res_phase_[0] = res_phase_[1] = res_phase_[3] = 0;
-    res_phase_n_ = 0;
+  if (res_merges_ && std::getenv("SHREDWORD_RESIDENT_REPORT")) {
+    const double n = (double)res_merges_;
+    std::fprintf(stderr, "[RESIDENT] %llu merges in %.2f ms | host: post->flag %.2f us, waited %.2f us | participants %.1f",
+                 (unsigned long long)res_merges_, ms, res_post_flag_us_ / n, res_host_wait_ / n, res_parts_sum_ / n);
+    if (res_phase_n_)
+      std::fprintf(stderr, " | device after dispatch: go %.2f work %.2f flag %.2f", res_phase_[0] / res_phase_n_,
+                   res_phase_[1] / res_phase_n_, res_phase_[3] / res_phase_n_);
+    std::fprintf(stderr, "\n");
   }
+  res_post_flag_us_ = res_host_wait_ = res_parts_sum_ = 0;
+  res_phase_[0] = res_phase_[1] = res_phase_[2] = res_phase_[3] = 0;
+  res_phase_n_ = 0;
   // the tiles are back in HBM: their pair signatures for k_merge / k_unmerge
   const int grid = (int)std::min<size_t>((ntiles_ + kWaves - 1) / kWaves, (size_t)cu_count_ * 8);
   k_sig_build<<<grid, kThreads, 0, S(stream_)>>>(tok_, tile_off_, tile_len_, (uint32_t)ntiles_, sig_);

@@ -271,12 +271,13 @@ class Device : public Backend {
     uint32_t seq;
     int slot;
     uint32_t nparts;
+    double t_post;
   };
   void plan_resident(const TiledStream& ts);
   void free_resident();
   void start_resident();
   uint32_t post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int slot);
-  void wait_resident(const MergeSlot& sl, uint32_t seq);
+  void wait_resident(const MergeSlot& sl, int32_t X);
   size_t collect_resident(int32_t X, const DeltaRecord** recs);
   [[noreturn]] void resident_dump(const char* why);
   bool resident_on_ = true;       // option (SHREDWORD_RESIDENT / set_option resident)
@@ -302,6 +303,7 @@ class Device : public Backend {
   double res_phase_[4] = {};
   uint64_t res_phase_n_ = 0;
   bool res_stamp_detail_ = false;
+  double res_host_wait_ = 0, res_parts_sum_ = 0, res_post_flag_us_ = 0;
   uint32_t* res_status_ = nullptr;     // pinned host status
   void* res_status_dev_ = nullptr;
   void* res_ev_[2] = {};
