@@ -1375,6 +1375,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   __shared__ uint32_t s_cmd[8];
   __shared__ u64 s_cnt[2];
   __shared__ u64 s_tlead;
+  __shared__ uint32_t s_nout;  // the last participant: records written to the host
   __shared__ uint32_t s_pre[kMaxMergeGroups + 1], s_pmt[kMaxMergeGroups + 1];
   __shared__ uint32_t s_wtot[2][kWaves];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1611,6 +1612,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
         s_cnt[0] = 0;
         s_cnt[1] = 0;
         s_nrec = 0;
+        s_nout = 0;
       }
       __syncthreads();
       const uint32_t g = threadIdx.x;
@@ -1669,11 +1671,36 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
           }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 4; ++k) {  // combine the participants' records per key in the LDS hash
           const uint32_t i = i0 + k * kThreads + threadIdx.x;
-          if (i < n) sys_record(sl.out + i, (uint32_t)r[k][0], r[k][1], r[k][2]);
+          if (i >= n) continue;
+          const uint32_t key = (uint32_t)r[k][0];
+          uint32_t hs = (key * 2654435761u) >> (32 - __builtin_ctz(kResDeltaW));
+          bool done = false;
+          for (int probe = 0; probe < 16 && !done; ++probe) {
+            const uint32_t prev = atomicCAS(&h.key[hs], kEmpty32, key);
+            if (prev == kEmpty32 || prev == key) {
+              atomicAdd(&h.sum[hs], r[k][1]);
+              atomicMin(&h.ft[hs], r[k][2]);
+              done = true;
+            } else {
+              hs = (hs + 1) & (kResDeltaW - 1);
+            }
+          }
+          if (!done) sys_record(sl.out + atomicAdd(&s_nout, 1u), key, r[k][1], r[k][2]);  // the host combines these
         }
       }
+      __syncthreads();
+      for (int i = threadIdx.x; i < kResDeltaW; i += kThreads) {
+        const uint32_t key = h.key[i];
+        if (key == kEmpty32) continue;
+        sys_record(sl.out + atomicAdd(&s_nout, 1u), key, h.sum[i], h.ft[i]);
+        h.key[i] = kEmpty32;
+        h.sum[i] = 0;
+        h.ft[i] = kEmpty64;
+      }
+      __syncthreads();
+      n = s_nout;
       for (uint32_t i = threadIdx.x; i < nm; i += kThreads) {
         const uint32_t o = owner(s_pmt, i);
         sys_store(sl.hmlist + i,
@@ -3503,6 +3530,7 @@ void Device::plan_resident(const TiledStream& ts) {
   res_shm_ = shm;
   res_all_.clear();
   for (uint32_t g = 1; g < G; ++g) res_all_.push_back(g);
+  res_wg_first_ = wg_tiles;
   res_wg_tiles_ = dalloc<uint32_t>(G + 1, &bytes_alloc_);
   res_wg_rank_ = dalloc<uint32_t>(G + 1, &bytes_alloc_);
   res_tile_lofs_ = dalloc<uint32_t>(T, &bytes_alloc_);
@@ -3623,15 +3651,8 @@ uint32_t Device::post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int
   uint32_t np = res_grid_;
   if (op == kOpMerge) {
     std::vector<uint32_t>& pp = res_post_parts_[slot];
-    pp.clear();
-    if (skip_ && index_.candidates(a, b, &cand_) && !cand_.empty()) {
-      for (uint32_t t : cand_) {  // ascending tiles -> ascending owners
-        const uint32_t o = res_owner_[t];
-        if (pp.empty() || pp.back() != o) pp.push_back(o);
-      }
-    } else {
-      pp = res_all_;
-    }
+    if (skip_) index_.owners(a, b, res_wg_first_, &pp);
+    if (!skip_ || pp.empty()) pp = res_all_;
     for (uint32_t o : pp) visited_tiles_ += res_wg_ntiles_[o];
     slot_[slot].host_count[1] = 0xFFFFFFFFu;  // the merge raises X here
   }

@@ -293,6 +293,7 @@ class Device : public Backend {
   std::vector<uint32_t> res_owner_;    // tile -> workgroup (workgroup 0 dispatches, owns none)
   std::vector<uint32_t> res_wg_ntiles_;
   std::vector<uint32_t> res_all_;      // every worker workgroup (1 .. grid-1)
+  std::vector<uint32_t> res_wg_first_; // grid + 1: first tile of each workgroup
   std::vector<uint32_t> res_parts_;
   void* res_mbox_ = nullptr;           // pinned host ResMbox (command ring)
   void* res_mbox_dev_ = nullptr;

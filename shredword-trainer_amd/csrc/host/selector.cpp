@@ -136,16 +136,26 @@ void Selector::add_counts(std::vector<PairCount> pairs) {
 }
 
 bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, int32_t* pb) const {
+  // The best valid entry sharing no token with (a, b) among the first `window` heap slots, by a
+  // walk from the root that skips every subtree whose root is below the best found so far (the
+  // heap property bounds the whole subtree), so it touches a handful of entries.
   const size_t n = std::min(window, heap_.size());
   uint64_t best_f = 0;
   size_t best = SIZE_MAX;
-  for (size_t i = 0; i < n; ++i) {
+  size_t stack[64];
+  int sp = 0;
+  if (n) stack[sp++] = 0;
+  while (sp) {
+    const size_t i = stack[--sp];
     const HeapEnt& e = heap_[i];
-    if (e.freq < best_f || e.freq < min_freq_) continue;
+    if (e.freq < best_f || e.freq < min_freq_ || (best != SIZE_MAX && e.freq == best_f && i > best)) continue;
+    const size_t l = 2 * i + 1;
+    if (l + 1 < n && sp < 63) stack[sp++] = l + 1;
+    if (l < n && sp < 63) stack[sp++] = l;
     if (e.a == a || e.a == b || e.b == a || e.b == b || e.a == unk_ || e.b == unk_) continue;
     const Info* in = find(pack_pair(e.a, e.b));
     if (!in || in->version != e.version || in->freq != e.freq) continue;
-    if (e.freq > best_f || best == SIZE_MAX) {
+    if (e.freq > best_f || best == SIZE_MAX || i < best) {
       best_f = e.freq;
       best = i;
     }

@@ -241,4 +241,50 @@ bool TileIndex::intersect(const Set* sa, const Set* sb, std::vector<uint32_t>* o
   return !out->empty();
 }
 
+void TileIndex::to_bits(const Set* s, std::vector<uint64_t>* bits) const {
+  const size_t nw = (ntiles_ + 63) / 64;
+  if (!s->bits.empty()) {
+    *bits = s->bits;
+    return;
+  }
+  bits->assign(nw, 0);
+  for (uint32_t t : s->list) (*bits)[t >> 6] |= 1ull << (t & 63);
+}
+
+void TileIndex::owners(int32_t a, int32_t b, const std::vector<uint32_t>& first, std::vector<uint32_t>* out) const {
+  out->clear();
+  const size_t W = first.size() - 1;
+  const size_t nw = (ntiles_ + 63) / 64;
+  const Set* sa = nullptr;
+  const Set* sb = nullptr;
+  if ((uint32_t)a < 256 && (uint32_t)b < 256 && !base_pairs_.empty()) {
+    sa = &base_pairs_[(uint32_t)a * 256 + (uint32_t)b];  // exact tiles of a pair of bytes
+  } else {
+    sa = get(a);
+    sb = get(b);
+  }
+  if (!sa || (sb == nullptr && !((uint32_t)a < 256 && (uint32_t)b < 256 && !base_pairs_.empty()))) {
+    for (size_t w = 0; w < W; ++w)  // unknown id: every owner
+      if (first[w + 1] > first[w]) out->push_back((uint32_t)w);
+    return;
+  }
+  to_bits(sa, &ba_);
+  if (sb) {
+    to_bits(sb, &bb_);
+    for (size_t i = 0; i < nw; ++i) ba_[i] &= bb_[i];
+  }
+  for (size_t w = 0; w < W; ++w) {
+    const uint32_t lo = first[w], hi = first[w + 1];  // [lo, hi)
+    if (lo >= hi) continue;
+    bool any = false;
+    for (uint32_t i = lo >> 6; i <= (hi - 1) >> 6 && !any; ++i) {
+      uint64_t m = ba_[i];
+      if (i == lo >> 6) m &= ~0ull << (lo & 63);
+      if (i == (hi - 1) >> 6 && ((hi - 1) & 63) != 63) m &= (2ull << ((hi - 1) & 63)) - 1;
+      any = m != 0;
+    }
+    if (any) out->push_back((uint32_t)w);
+  }
+}
+
 }  // namespace shred

@@ -55,6 +55,9 @@ class TileIndex {
   void reset();  // back to the state after build()
   // Candidate tiles of (a, b) in ascending order; false = visiting every tile is cheaper.
   bool candidates(int32_t a, int32_t b, std::vector<uint32_t>* out) const;
+  // The owners of (a, b)'s candidate tiles, where owner w holds tiles [first[w], first[w+1]):
+  // ascending workgroup ids in *out.  Computed on tile bitmaps without listing the tiles.
+  void owners(int32_t a, int32_t b, const std::vector<uint32_t>& first, std::vector<uint32_t>* out) const;
   void set_tiles(int32_t id, const uint32_t* tiles, size_t n);
   size_t num_tiles() const { return ntiles_; }
 
@@ -69,8 +72,10 @@ class TileIndex {
 
   bool intersect(const Set* sa, const Set* sb, std::vector<uint32_t>* out) const;
 
+  void to_bits(const Set* s, std::vector<uint64_t>* bits) const;
   uint32_t ntiles_ = 0;
   std::vector<Set> ids_, ids0_;
+  mutable std::vector<uint64_t> ba_, bb_;  // scratch bitmaps of owners()
   std::vector<Set> base_pairs_;  // [a * 256 + b] for a, b < 256 (immutable after build)
 };
 
