@@ -326,9 +326,18 @@ def main():
                            else "k_merge (signature filter + fused match/delta/compaction, K2+K3)"),
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": pmc_traffic(args.config, args.layout),
-                "traffic_source": PMC_NOTE,
+                "traffic": (pmc_traffic(args.config, args.layout, "k_resident<true>") / max(1.0, per_step_merges)
+                            if st["resident_launches"] and pmc_traffic(args.config, args.layout, "k_resident<true>")
+                            else None if st["resident_launches"] else pmc_traffic(args.config, args.layout)),
+                "traffic_source": (PMC_NOTE.replace("per k_merge launch", "per merge (k_resident launch bytes / merges "
+                                                    "per launch: one launch per train())")
+                                   if st["resident_launches"] else PMC_NOTE),
                 "algorithmic_bytes": "4 B x live tokens per merge (SURVEY.md §8 d4, K2)",
+                "note": ("k_resident is one persistent launch per train(); avg_launch_us = its duration (HIP events) / "
+                         "merges, i.e. device wall time per merge; the table is read from LDS, not HBM, so the bound "
+                         "in practice is the per-merge round-trip chain, not HBM bandwidth"
+                         if st["resident_launches"] else None),
+                "dispatch_to_flag_us": st.get("resident_latency_us"),
                 "avg_launch_us": 1e3 * mk_ms, "avg_bytes_per_launch": mk_bytes,
                 "launches_sampled": st["merge_launches"], "launches": merges,
             },

@@ -121,6 +121,7 @@ typedef struct ShredStats {
   /* LDS-resident merge loop: k_resident launches and their summed durations (HIP events) */
   uint64_t resident_launches;
   double resident_ms;
+  double resident_latency_us;  /* mean per-merge dispatch -> host flag time (device clock) */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -3565,6 +3565,10 @@ void Device::plan_resident(const TiledStream& ts) {
   }
   HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_resident<true>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  int per_cu = 0;  // the persistent grid must be co-resident: at least one workgroup per CU
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_resident<true>), kThreads,
+                                                      shm));
+  if (per_cu < 1 || (long)per_cu * cu_count_ < (long)G) return;
   resident_ok_ = true;
 }
 
@@ -3629,9 +3633,10 @@ void Device::start_resident() {
   res_status_[0] = 0;
   HIP_OK(hipMemsetAsync(res_q_, 0, (size_t)res_grid_ * kResRing * 2 * sizeof(uint64_t), S(stream_)));
   HIP_OK(hipEventRecord((hipEvent_t)res_ev_[0], S(stream_)));
-  void* args[] = {&rp};
-  HIP_OK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_resident<true>), dim3(res_grid_), dim3(kThreads),
-                                    args, (unsigned)res_shm_, S(stream_)));
+  // a plain launch: one workgroup per CU by its LDS footprint, checked against the occupancy
+  // query at plan time (plan_resident), so every workgroup is resident together
+  k_resident<true><<<res_grid_, kThreads, res_shm_, S(stream_)>>>(rp);
+  HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord((hipEvent_t)res_ev_[1], S(stream_)));
   res_running_ = true;
   res_merges_ = 0;

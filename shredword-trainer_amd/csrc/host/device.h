@@ -125,6 +125,9 @@ class Device : public Backend {
     times_ = KernelTimes();
     records_total_ = records_max_ = 0;
     visited_tiles_ = 0;
+    res_launches_ = 0;
+    res_ms_ = res_lat_us_ = 0;
+    res_lat_n_ = 0;
   }
   uint64_t live_tokens();  // Σ tile_len (headers included)
   size_t num_tiles() const { return ntiles_; }

@@ -332,6 +332,7 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
     s->live_tokens = t->dev->live_tokens();
     s->resident_launches = t->dev->resident_launches();
     s->resident_ms = t->dev->resident_ms();
+    s->resident_latency_us = t->dev->resident_latency_us();
   }
   s->num_words = t->wt.num_words();
   s->num_symbols = t->wt.num_symbols();
