@@ -1089,9 +1089,7 @@ template <bool kWeighted>
 __device__ __forceinline__ uint32_t res_merge_tile(int32_t* tb, uint32_t* lenp, uint32_t* sg, uint32_t* sgadd, int32_t* st,
                                                    const u64* s_w,
                                                    uint32_t r0, int32_t a, int32_t b, int32_t X, ResDelta& h,
-                                                   const ResSlot& p, uint32_t slot_cap, int lane, u64* n_written,
-                                                   u64* cy) {
-#define RCY(k) if (cy) cy[k] = __builtin_amdgcn_s_memtime()
+                                                   const ResSlot& p, uint32_t slot_cap, int lane, u64* n_written) {
   if (!res_sig_test(sg, a, b)) return 0;  // the pair cannot be in this tile
   const uint32_t len = *lenp;
   const int p0 = lane * kPer;
@@ -1113,7 +1111,6 @@ __device__ __forceinline__ uint32_t res_merge_tile(int32_t* tb, uint32_t* lenp, 
 #pragma unroll
   for (int j = 0; j < kPer; ++j) any |= (v[j] == a) & ((j + 1 < kPer ? v[j + 1] : nx) == b);
   if (!__any(any)) return 0;
-  RCY(0);
   const bool same = (a == b);
   const uint32_t cl = len;
 #pragma unroll
@@ -1171,7 +1168,6 @@ __device__ __forceinline__ uint32_t res_merge_tile(int32_t* tb, uint32_t* lenp, 
   const int kc_ex = (cinc - (kc | (nm << 16))) & 0xFFFF;
   const int kept = ctot & 0xFFFF;
   const int matches = ctot >> 16;
-  RCY(1);
   if (mask) {
     const u64 hdr_in = lane == 0 ? 0ull : hdr_ex;
     for (uint32_t mrem = mask; mrem; mrem &= mrem - 1) {
@@ -1235,7 +1231,6 @@ __device__ __forceinline__ uint32_t res_merge_tile(int32_t* tb, uint32_t* lenp, 
     }
   }
   wave_lds_sync();  // every neighbour read is done: compact in place
-  RCY(2);
   // branch-free: a dropped position writes this lane's trash word past the staging area
   int o = kc_ex;
   const int trash = kStPad + lane;
@@ -1270,7 +1265,6 @@ __device__ __forceinline__ uint32_t res_merge_tile(int32_t* tb, uint32_t* lenp, 
   }
   if (lane == 0) *lenp = (uint32_t)kept;
   *n_written += (u64)kept;
-  RCY(3);
   if (rebuild) {
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {  // signature of the compacted tile (OR of 0 where no pair)
@@ -1283,8 +1277,6 @@ __device__ __forceinline__ uint32_t res_merge_tile(int32_t* tb, uint32_t* lenp, 
   }
   if (lane == 0) *sgadd = rebuild ? 0u : added;
   wave_lds_sync();
-  RCY(4);
-#undef RCY
   return (uint32_t)matches;
 }
 
@@ -1359,7 +1351,10 @@ __device__ __forceinline__ void res_unmerge_tile(int32_t* tb, uint32_t* lenp, ui
   wave_lds_sync();
 }
 
-template <bool kWeighted>
+// kLdsTok: the tokens live in LDS (the table fits the chip's LDS); otherwise they stay in HBM
+// (read and rewritten in place by their owner workgroup only) and LDS holds the weights and the
+// tile signatures, which is what decides which tiles a merge reads at all.
+template <bool kWeighted, bool kLdsTok>
 __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   extern __shared__ __align__(16) int32_t s_dyn[];
   int32_t* s_res = s_dyn;                                     // the tiles' tokens
@@ -1368,6 +1363,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   __shared__ int32_t s_tok[kWaves][kStPad + 64];  // + a trash word per lane (branch-free compaction)
   __shared__ ResDelta h;
   __shared__ uint32_t s_len[kResMaxTiles], s_lofs[kResMaxTiles], s_sigadd[kResMaxTiles];
+  __shared__ u64 s_toff[kResMaxTiles];
   __shared__ uint32_t s_mt[kResMaxTiles];
   __shared__ uint8_t s_lm[kResMaxTiles];   // tiles where this workgroup's last merge matched
   __shared__ uint32_t s_qc[kMaxMergeGroups];  // leader: entries written to each workgroup's queue
@@ -1388,6 +1384,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   for (uint32_t i = threadIdx.x; i < nt; i += kThreads) {
     s_len[i] = p.tile_len[t0 + i];
     s_lofs[i] = p.tile_lofs[t0 + i];
+    s_toff[i] = p.tile_off[t0 + i];
     s_sigadd[i] = 0;
     s_lm[i] = 0;
   }
@@ -1401,14 +1398,20 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
     for (uint32_t i = threadIdx.x; i < nr; i += kThreads) s_w[i] = p.weight[r0 + i];
   if (threadIdx.x == 0) h.spill = 0;
   __syncthreads();
+  auto tile_ptr = [&](uint32_t i) -> int32_t* {
+    if constexpr (kLdsTok) return s_res + s_lofs[i];
+    else return p.tok + s_toff[i];
+  };
   for (uint32_t i = wid; i < nt; i += kWaves) {
-    const int32_t* src = p.tok + p.tile_off[t0 + i];
-    int32_t* dst = s_res + s_lofs[i];
-    const uint32_t n4 = (s_len[i] + 3u) >> 2;
-    for (uint32_t q = (uint32_t)lane; q < n4; q += 64)
-      *reinterpret_cast<int4*>(dst + 4 * q) = *reinterpret_cast<const int4*>(src + 4 * q);
-    wave_lds_sync();
-    res_sig_build(s_sig + (size_t)i * kResSigWords, dst, s_len[i], lane);
+    if constexpr (kLdsTok) {
+      const int32_t* src = p.tok + s_toff[i];
+      int32_t* dst = s_res + s_lofs[i];
+      const uint32_t n4 = (s_len[i] + 3u) >> 2;
+      for (uint32_t q = (uint32_t)lane; q < n4; q += 64)
+        *reinterpret_cast<int4*>(dst + 4 * q) = *reinterpret_cast<const int4*>(src + 4 * q);
+      wave_lds_sync();
+    }
+    res_sig_build(s_sig + (size_t)i * kResSigWords, tile_ptr(i), s_len[i], lane);
   }
   __syncthreads();
 
@@ -1514,7 +1517,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
     }
     if (op == kOpUnmerge) {  // undo this workgroup's last merge (the host's guess was wrong)
       for (uint32_t i = wid; i < nt; i += kWaves)
-        if (s_lm[i]) res_unmerge_tile(s_res + s_lofs[i], &s_len[i], s_sig + (size_t)i * kResSigWords, &s_sigadd[i], st,
+        if (s_lm[i]) res_unmerge_tile(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords, &s_sigadd[i], st,
                                       a, b, X, lane);
       __syncthreads();
       continue;
@@ -1528,11 +1531,10 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
 
     // ---- the merge over this workgroup's tiles (wave per tile)
     u64 n_merged = 0, n_written = 0;
-    u64 cyc[5] = {0, 0, 0, 0, 0};
     for (uint32_t i = wid; i < nt; i += kWaves) {
-      const uint32_t m = res_merge_tile<kWeighted>(s_res + s_lofs[i], &s_len[i], s_sig + (size_t)i * kResSigWords,
+      const uint32_t m = res_merge_tile<kWeighted>(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords,
                                                    &s_sigadd[i], st, s_w, r0, a, b, X, h, sl, p.slot_cap, lane,
-                                                   &n_written, p.stamps ? cyc : nullptr);
+                                                   &n_written);
       if (lane == 0) s_lm[i] = m ? 1 : 0;
       if (m) {
         n_merged += m;
@@ -1544,10 +1546,6 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       if (n_written) atomicAdd(&s_cnt[1], n_written);
     }
     __syncthreads();
-    if (p.stamps && lane == 0 && cyc[4]) {  // a wave that merged in a tile: its phase cycles
-      for (int k = 0; k < 4; ++k)
-        __hip_atomic_store(p.stamps + 4 * G + pi * 4 + k, cyc[k + 1] - cyc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     if (p.stamps && threadIdx.x == 0) {
       __hip_atomic_store(p.stamps + pi * 4 + 1, (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(p.stamps + pi * 4 + 3, (u64)__builtin_amdgcn_s_memtime() - clk0, __ATOMIC_RELAXED,
@@ -1748,16 +1746,18 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   }
   // ---- STOP (or the leader's time-out): the tiles go back to HBM
   for (uint32_t i = wid; i < nt; i += kWaves) {
-    int32_t* dst = p.tok + p.tile_off[t0 + i];
-    const int32_t* src = s_res + s_lofs[i];
     const uint32_t len = s_len[i];
-    const uint32_t n4 = (len + 3u) >> 2;
-    for (uint32_t q = (uint32_t)lane; q < n4; q += 64) {
-      int4 x = *reinterpret_cast<const int4*>(src + 4 * q);
-      if (4 * q + 1 >= len) x.y = kPad;
-      if (4 * q + 2 >= len) x.z = kPad;
-      if (4 * q + 3 >= len) x.w = kPad;
-      *reinterpret_cast<int4*>(dst + 4 * q) = x;
+    if constexpr (kLdsTok) {
+      int32_t* dst = p.tok + s_toff[i];
+      const int32_t* src = s_res + s_lofs[i];
+      const uint32_t n4 = (len + 3u) >> 2;
+      for (uint32_t q = (uint32_t)lane; q < n4; q += 64) {
+        int4 x = *reinterpret_cast<const int4*>(src + 4 * q);
+        if (4 * q + 1 >= len) x.y = kPad;
+        if (4 * q + 2 >= len) x.z = kPad;
+        if (4 * q + 3 >= len) x.w = kPad;
+        *reinterpret_cast<int4*>(dst + 4 * q) = x;
+      }
     }
     if (lane == 0) p.tile_len[t0 + i] = len;
   }
@@ -3467,9 +3467,10 @@ void Device::plan_resident(const TiledStream& ts) {
   int max_lds = 0;
   HIP_OK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, ordinal_));
   hipFuncAttributes fa;
-  HIP_OK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_resident<true>)));
+  HIP_OK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_resident<true, true>)));
   const long budget = (long)max_lds - (long)fa.sharedSizeBytes - 64;  // dynamic LDS per workgroup
-  if (budget <= 0) return;
+  // the dynamic region follows the statics unpadded: its 16-B LDS accesses need a 16-B base
+  if (budget <= 0 || fa.sharedSizeBytes % 16 != 0) return;
   // per tile: first and last word rank (tiles hold whole words in rank order), LDS words
   const size_t T = ntiles_;
   std::vector<uint32_t> rfirst(T), rlast(T), words(T);
@@ -3522,8 +3523,13 @@ void Device::plan_resident(const TiledStream& ts) {
   wg_rank[G] = rlast[T - 1] + 1;
   tok_words += (uint32_t)kWaveTok;  // every lane reads its 16 tokens of a full chunk from any tile start
   nr_max = (nr_max + 1u) & ~1u;
-  const size_t shm = (size_t)tok_words * 4 + (size_t)nr_max * 8 + (size_t)nt_max * kResSigWords * 4;
-  if ((long)shm > budget) return;
+  size_t shm = (size_t)tok_words * 4 + (size_t)nr_max * 8 + (size_t)nt_max * kResSigWords * 4;
+  res_lds_tok_ = (long)shm <= budget && !std::getenv("SHREDWORD_RESIDENT_HBM");
+  if (!res_lds_tok_) {  // the tokens stay in HBM; LDS holds weights and signatures
+    tok_words = 0;
+    shm = (size_t)nr_max * 8 + (size_t)nt_max * kResSigWords * 4;
+    if ((long)shm > budget) return;
+  }
   res_grid_ = G;
   res_tok_words_ = tok_words;
   res_w_words_ = nr_max;
@@ -3563,11 +3569,11 @@ void Device::plan_resident(const TiledStream& ts) {
       e = ev;
     }
   }
-  HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_resident<true>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  const void* kfn = res_lds_tok_ ? reinterpret_cast<const void*>(&k_resident<true, true>)
+                                 : reinterpret_cast<const void*>(&k_resident<true, false>);
+  HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   int per_cu = 0;  // the persistent grid must be co-resident: at least one workgroup per CU
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_resident<true>), kThreads,
-                                                      shm));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kThreads, shm));
   if (per_cu < 1 || (long)per_cu * cu_count_ < (long)G) return;
   resident_ok_ = true;
 }
@@ -3635,7 +3641,8 @@ void Device::start_resident() {
   HIP_OK(hipEventRecord((hipEvent_t)res_ev_[0], S(stream_)));
   // a plain launch: one workgroup per CU by its LDS footprint, checked against the occupancy
   // query at plan time (plan_resident), so every workgroup is resident together
-  k_resident<true><<<res_grid_, kThreads, res_shm_, S(stream_)>>>(rp);
+  if (res_lds_tok_) k_resident<true, true><<<res_grid_, kThreads, res_shm_, S(stream_)>>>(rp);
+  else k_resident<true, false><<<res_grid_, kThreads, res_shm_, S(stream_)>>>(rp);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord((hipEvent_t)res_ev_[1], S(stream_)));
   res_running_ = true;

@@ -98,6 +98,7 @@ class Device : public Backend {
   bool resident() const { return resident_on_; }
   bool resident_eligible() const { return resident_on_ && resident_ok_ && !exchange_; }
   uint64_t resident_launches() const { return res_launches_; }
+  bool resident_tokens_in_lds() const { return res_lds_tok_; }
   double resident_ms() const { return res_ms_; }
   // mean dispatch -> host flag time of a resident merge (device clock), us
   double resident_latency_us() const { return res_lat_n_ ? res_lat_us_ / (double)res_lat_n_ : 0.0; }
@@ -286,6 +287,7 @@ class Device : public Backend {
   bool resident_on_ = true;       // option (SHREDWORD_RESIDENT / set_option resident)
   bool resident_ok_ = false;      // the uploaded table fits (plan_resident)
   bool res_running_ = false;      // a k_resident launch is live
+  bool res_lds_tok_ = true;       // the tokens are in LDS (else in HBM, LDS holds weights + signatures)
   std::vector<ResPost> res_posted_;  // oldest first (at most two: a merge and the guess after it)
   std::vector<uint32_t> res_post_parts_[2];  // participants of the posted merges, by slot
   uint32_t res_grid_ = 0, res_tok_words_ = 0, res_w_words_ = 0;

@@ -202,11 +202,15 @@ def test_speculation_lockstep(layout, medium_corpus):
         t.destroy()
 
 
-def test_resident_lockstep(medium_corpus, tmp_path):
-    """The LDS-resident merge loop (k_resident) against the launch path, in bpe_merge_batch
+@pytest.mark.parametrize("tokens", ["lds", "hbm"])
+def test_resident_lockstep(tokens, medium_corpus, tmp_path, monkeypatch):
+    """The resident merge loop (k_resident) against the launch path, in bpe_merge_batch
     chunks: identical merges and device token streams after every chunk (each chunk ends the
-    persistent launch and writes the tiles back; id 4096 regrows the delta tables mid-run)."""
+    persistent launch and writes the tiles back).  tokens=hbm keeps the tokens in HBM (the mode
+    of tables larger than the chip's LDS)."""
     from shredword.cbase import lib
+    if tokens == "hbm":
+        monkeypatch.setenv("SHREDWORD_RESIDENT_HBM", "1")
     ts = []
     for res in (0, 1):
         t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
