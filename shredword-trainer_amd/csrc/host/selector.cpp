@@ -25,7 +25,8 @@ void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
   table_.assign(1 << 20, Info{kEmptyKey, 0, 0, 0});  // 24 MB: no rehash below 512 k pairs
   mask_ = table_.size() - 1;
   count_ = 0;
-  heap_.clear();
+  hf_.clear();
+  hp_.clear();
 }
 
 void Selector::grow() {
@@ -77,36 +78,44 @@ bool Selector::lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) c
 
 void Selector::push(int32_t a, int32_t b, uint64_t freq, uint32_t version) {
   ++ctr_.pushes;
-  size_t i = heap_.size();
-  heap_.push_back({});
-  const HeapEnt x{a, b, freq, version};
+  size_t i = hf_.size();
+  hf_.push_back(0);
+  hp_.push_back({});
   while (i > 0) {
     size_t p = (i - 1) >> 1;
-    if (heap_[p].freq >= freq) break;  // sift up only while parent < child (heap.cpp:76)
-    heap_[i] = heap_[p];
+    if (hf_[p] >= freq) break;  // sift up only while parent < child (heap.cpp:76)
+    hf_[i] = hf_[p];
+    hp_[i] = hp_[p];
     i = p;
   }
-  heap_[i] = x;
+  hf_[i] = freq;
+  hp_[i] = {a, b, version};
 }
 
 Selector::HeapEnt Selector::pop() {
   ++ctr_.pops;
-  HeapEnt top = heap_[0];
-  HeapEnt x = heap_.back();
-  heap_.pop_back();
-  const size_t n = heap_.size();
+  const HeapEnt top{hp_[0].a, hp_[0].b, hf_[0], hp_[0].version};
+  const uint64_t xf = hf_.back();
+  const HeapPay xp = hp_.back();
+  hf_.pop_back();
+  hp_.pop_back();
+  const size_t n = hf_.size();
   if (n == 0) return top;
   size_t i = 0;
+  const uint64_t* f = hf_.data();
   for (;;) {  // left child if strictly greater, then right if strictly greater (heap.cpp:101-106)
     size_t l = 2 * i + 1, r = l + 1, best = i;
-    uint64_t bf = x.freq;
-    if (l < n && heap_[l].freq > bf) { best = l; bf = heap_[l].freq; }
-    if (r < n && heap_[r].freq > bf) best = r;
+    if (4 * i + 3 < n) __builtin_prefetch(f + 4 * i + 3);  // the grandchildren of both sides
+    uint64_t bf = xf;
+    if (l < n && f[l] > bf) { best = l; bf = f[l]; }
+    if (r < n && f[r] > bf) best = r;
     if (best == i) break;
-    heap_[i] = heap_[best];
+    hf_[i] = f[best];
+    hp_[i] = hp_[best];
     i = best;
   }
-  heap_[i] = x;
+  hf_[i] = xf;
+  hp_[i] = xp;
   return top;
 }
 
@@ -139,7 +148,7 @@ bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, in
   // The best valid entry sharing no token with (a, b) among the first `window` heap slots, by a
   // walk from the root that skips every subtree whose root is below the best found so far (the
   // heap property bounds the whole subtree), so it touches a handful of entries.
-  const size_t n = std::min(window, heap_.size());
+  const size_t n = std::min(window, hf_.size());
   uint64_t best_f = 0;
   size_t best = SIZE_MAX;
   size_t stack[64];
@@ -147,7 +156,7 @@ bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, in
   if (n) stack[sp++] = 0;
   while (sp) {
     const size_t i = stack[--sp];
-    const HeapEnt& e = heap_[i];
+    const HeapEnt e{hp_[i].a, hp_[i].b, hf_[i], hp_[i].version};
     if (e.freq < best_f || e.freq < min_freq_ || (best != SIZE_MAX && e.freq == best_f && i > best)) continue;
     const size_t l = 2 * i + 1;
     if (l + 1 < n && sp < 63) stack[sp++] = l + 1;
@@ -161,16 +170,16 @@ bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, in
     }
   }
   if (best == SIZE_MAX) return false;
-  *pa = heap_[best].a;
-  *pb = heap_[best].b;
+  *pa = hp_[best].a;
+  *pb = hp_[best].b;
   return true;
 }
 
 size_t Selector::predict_chain(int32_t a, int32_t b, size_t window, size_t k, int32_t* out) const {
-  const size_t n = std::min(window, heap_.size());
+  const size_t n = std::min(window, hf_.size());
   std::vector<std::pair<uint64_t, size_t>> cand;  // (freq, heap slot) of the valid entries
   for (size_t i = 0; i < n; ++i) {
-    const HeapEnt& e = heap_[i];
+    const HeapEnt e{hp_[i].a, hp_[i].b, hf_[i], hp_[i].version};
     if (e.freq < min_freq_ || e.a == unk_ || e.b == unk_) continue;
     const Info* in = find(pack_pair(e.a, e.b));
     if (!in || in->version != e.version || in->freq != e.freq) continue;
@@ -181,7 +190,7 @@ size_t Selector::predict_chain(int32_t a, int32_t b, size_t window, size_t k, in
   size_t m = 0;
   for (const auto& c : cand) {
     if (m == k) break;
-    const HeapEnt& e = heap_[c.second];
+    const HeapPay& e = hp_[c.second];
     bool clash = false;
     for (int32_t u : used) clash |= e.a == u || e.b == u;
     if (clash) continue;
@@ -195,8 +204,10 @@ size_t Selector::predict_chain(int32_t a, int32_t b, size_t window, size_t k, in
 }
 
 bool Selector::select(int32_t* a, int32_t* b, uint64_t* freq) {
-  while (!heap_.empty()) {
+  while (!hf_.empty()) {
     HeapEnt top = pop();
+    if (!hf_.empty())  // the next top's pair info, fetched while this one is checked
+      __builtin_prefetch(&table_[mix64(pack_pair(hp_[0].a, hp_[0].b)) & mask_]);
     Info& in = get(top.a, top.b);
     if (top.version != in.version) {  // stale entry
       ++ctr_.stale;

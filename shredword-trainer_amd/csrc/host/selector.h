@@ -69,9 +69,9 @@ class Selector {
   // share no token with (a, b) or with each other, by frequency.  out: k (a, b) pairs.
   size_t predict_chain(int32_t a, int32_t b, size_t window, size_t k, int32_t* out) const;
 
-  size_t heap_size() const { return heap_.size(); }
-  bool heap_empty() const { return heap_.empty(); }
-  uint64_t heap_top_freq() const { return heap_.empty() ? 0 : heap_[0].freq; }
+  size_t heap_size() const { return hf_.size(); }
+  bool heap_empty() const { return hf_.empty(); }
+  uint64_t heap_top_freq() const { return hf_.empty() ? 0 : hf_[0]; }
   size_t num_pairs() const { return count_; }
   // freq/version of a pair (0/0 when absent); for tests.
   bool lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) const;
@@ -87,6 +87,7 @@ class Selector {
   // pair (INT32_MIN, INT32_MIN), which no token pair can be (ids are >= -2^30).
   struct Info { uint64_t key; uint64_t freq; uint32_t version; uint32_t seq; };
   struct HeapEnt { int32_t a, b; uint64_t freq; uint32_t version; };
+  struct HeapPay { int32_t a, b; uint32_t version; };
   struct Change { uint64_t hk; int64_t delta; uint64_t ft; };
   static constexpr uint64_t kEmptyKey = 0x8000000080000000ull;
 
@@ -101,7 +102,10 @@ class Selector {
   std::vector<Info> table_;
   size_t count_ = 0;
   uint64_t mask_ = 0;
-  std::vector<HeapEnt> heap_;
+  // The reference's binary heap (heap.cpp), struct-of-arrays: the sifts compare frequencies only,
+  // so they walk a dense u64 array (8 children per cache line pair) and move the payload beside.
+  std::vector<uint64_t> hf_;
+  std::vector<HeapPay> hp_;
   std::vector<Change> changes_;
   std::vector<uint32_t> change_index_;
   std::vector<uint32_t> bucket_start_;
