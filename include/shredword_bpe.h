@@ -85,6 +85,8 @@ int loadVocab(void* trainer, const char* path);
  *   resident = 0 | 1            LDS-resident merge loop (default 1): when the distinct-word
  *                               table fits the chip's LDS, the merge loop runs as one persistent
  *                               launch holding the table in LDS (results are identical either way)
+ *   gpu_load = 0 | 1            count the corpus words on the device at load_corpus (default 1;
+ *                               types layout, files without NUL bytes; same table either way)
  *   exchange_bucket = <n>       multi-GPU: records per rank in the fixed all-gather bucket
  *                               (default 1024; larger record sets take a second round)
  * Returns 0, or -1 for an unknown key/value. */
@@ -122,6 +124,7 @@ typedef struct ShredStats {
   uint64_t resident_launches;
   double resident_ms;
   double resident_latency_us;  /* mean per-merge dispatch -> host flag time (device clock) */
+  uint64_t load_on_gpu;        /* 1: the last load_corpus counted its words on the device */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -168,11 +168,85 @@ void scan_words(const uint8_t* d, Range r, F&& f) {
   }
 }
 
+// The word table from the distinct words in reference word order (rank order): spellings,
+// counts, the coverage cut and the symbols (bpe.cpp:156-172, histogram.cpp:7-53).
+void finish_table(const uint8_t* d, const std::vector<WordRec>& recs, const LoadOptions& opt, int threads,
+                  WordTable* out) {
+  const size_t W = recs.size();
+  if (W > (size_t)kMaxRank) fatal("corpus has more than 2^30 distinct words");
+  WordTable& wt = *out;
+  wt = WordTable();
+  wt.offset.resize(W + 1);
+  wt.count.resize(W);
+  uint64_t S = 0;
+  for (size_t r = 0; r < W; ++r) {
+    wt.offset[r] = S;
+    wt.count[r] = recs[r].count;
+    S += recs[r].len;
+  }
+  wt.offset[W] = S;
+  wt.bytes.resize(S);
+  parallel_for(threads, (W + 4095) / 4096, [&](size_t blk, int) {
+    size_t r1 = std::min(W, (blk + 1) * 4096);
+    for (size_t r = blk * 4096; r < r1; ++r) std::memcpy(wt.bytes.data() + wt.offset[r], d + recs[r].first, recs[r].len);
+  });
+  uint64_t occ = 0;
+  for (uint64_t c : wt.count) occ += c;
+  wt.total_occurrences = occ;
+
+  // Coverage (bpe.cpp:156-172): unweighted histogram over distinct words.
+  std::vector<std::array<uint64_t, 256>> hist(threads);
+  for (auto& h : hist) h.fill(0);
+  const size_t chunk = 1 << 20;
+  parallel_for(threads, (S + chunk - 1) / chunk, [&](size_t c, int t) {
+    size_t e = std::min<size_t>(S, (c + 1) * chunk);
+    for (size_t i = c * chunk; i < e; ++i) hist[t][wt.bytes[i]]++;
+  });
+  uint64_t cnt[256] = {};
+  for (auto& h : hist)
+    for (int c = 0; c < 256; ++c) cnt[c] += h[c];
+  std::vector<std::pair<int, uint64_t>> cand;
+  for (int bk = 0; bk < 256; ++bk) {
+    int c = (bk - 165) & 255;  // StrMap(256) bucket of the 1-byte key c is (5381*33 + c) & 255
+    if (cnt[c]) cand.push_back({c, cnt[c]});
+  }
+  std::stable_sort(cand.begin(), cand.end(),
+                   [](const std::pair<int, uint64_t>& a, const std::pair<int, uint64_t>& b) { return a.second > b.second; });
+  wt.distinct_bytes = cand.size();
+  wt.kept_bytes = (size_t)((float)cand.size() * opt.coverage);
+  for (size_t i = 0; i < wt.kept_bytes && i < cand.size(); ++i) wt.keep[cand[i].first] = true;
+
+  int32_t map[256];
+  for (int c = 0; c < 256; ++c) map[c] = wt.keep[c] ? c : opt.unk_id;
+  wt.symbols.resize(S);
+  parallel_for(threads, (S + chunk - 1) / chunk, [&](size_t c, int) {
+    size_t e = std::min<size_t>(S, (c + 1) * chunk);
+    for (size_t i = c * chunk; i < e; ++i) wt.symbols[i] = map[wt.bytes[i]];
+  });
+}
+
 }  // namespace
 
 void load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordTable* out) {
   int threads = opt.threads > 0 ? opt.threads : (int)std::thread::hardware_concurrency();
   threads = std::max(1, std::min(threads, 32));
+  // the device count (types layout, NUL-free files: every line is read whole, so the words are
+  // the maximal runs of non-delimiters of the whole file)
+  if (opt.gpu_device >= 0 && !opt.want_stream && n >= opt.gpu_min_bytes && !std::memchr(d, 0, n)) {
+    std::vector<WordRec> recs;
+    std::string why;
+    const double t0 = now_seconds();
+    if (gpu_count_words(opt.gpu_device, d, n, &recs, &why)) {
+      const double t1 = now_seconds();
+      finish_table(d, recs, opt, threads, out);
+      out->counted_on_gpu = true;
+      if (std::getenv("SHREDWORD_LOAD_REPORT"))
+        std::fprintf(stderr, "[LOAD] device count %.1f ms, host table %.1f ms\n", 1e3 * (t1 - t0),
+                     1e3 * (now_seconds() - t1));
+      return;
+    }
+    std::fprintf(stderr, "[WARNING]\t GPU word count unavailable (%s): counting on the host\n", why.c_str());
+  }
   std::vector<Range> vis = visible_ranges(d, n);
   uint64_t vis_bytes = 0;
   for (auto& r : vis) vis_bytes += r.end - r.begin;
@@ -221,59 +295,13 @@ void load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordT
   });
   std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) { return a.order < b.order; });
 
-  WordTable& wt = *out;
-  wt = WordTable();
-  wt.offset.resize(W + 1);
-  wt.count.resize(W);
-  uint64_t S = 0;
+  std::vector<WordRec> recs(W);
   for (size_t r = 0; r < W; ++r) {
     const Entry& e = merged[keys[r].part].ents[keys[r].idx];
-    wt.offset[r] = S;
-    wt.count[r] = e.count;
-    S += e.len;
+    recs[r] = WordRec{e.first, e.count, e.len, 0};
   }
-  wt.offset[W] = S;
-  wt.bytes.resize(S);
-  parallel_for(threads, (W + 4095) / 4096, [&](size_t blk, int) {
-    size_t r1 = std::min(W, (blk + 1) * 4096);
-    for (size_t r = blk * 4096; r < r1; ++r) {
-      const Entry& e = merged[keys[r].part].ents[keys[r].idx];
-      std::memcpy(wt.bytes.data() + wt.offset[r], d + e.first, e.len);
-    }
-  });
-  uint64_t occ = 0;
-  for (uint64_t c : wt.count) occ += c;
-  wt.total_occurrences = occ;
-
-  // Coverage (bpe.cpp:156-172): unweighted histogram over distinct words.
-  std::vector<std::array<uint64_t, 256>> hist(threads);
-  for (auto& h : hist) h.fill(0);
-  const size_t chunk = 1 << 20;
-  parallel_for(threads, (S + chunk - 1) / chunk, [&](size_t c, int t) {
-    size_t e = std::min<size_t>(S, (c + 1) * chunk);
-    for (size_t i = c * chunk; i < e; ++i) hist[t][wt.bytes[i]]++;
-  });
-  uint64_t cnt[256] = {};
-  for (auto& h : hist)
-    for (int c = 0; c < 256; ++c) cnt[c] += h[c];
-  std::vector<std::pair<int, uint64_t>> cand;
-  for (int bk = 0; bk < 256; ++bk) {
-    int c = (bk - 165) & 255;  // StrMap(256) bucket of the 1-byte key c is (5381*33 + c) & 255
-    if (cnt[c]) cand.push_back({c, cnt[c]});
-  }
-  std::stable_sort(cand.begin(), cand.end(),
-                   [](const std::pair<int, uint64_t>& a, const std::pair<int, uint64_t>& b) { return a.second > b.second; });
-  wt.distinct_bytes = cand.size();
-  wt.kept_bytes = (size_t)((float)cand.size() * opt.coverage);
-  for (size_t i = 0; i < wt.kept_bytes && i < cand.size(); ++i) wt.keep[cand[i].first] = true;
-
-  int32_t map[256];
-  for (int c = 0; c < 256; ++c) map[c] = wt.keep[c] ? c : opt.unk_id;
-  wt.symbols.resize(S);
-  parallel_for(threads, (S + chunk - 1) / chunk, [&](size_t c, int) {
-    size_t e = std::min<size_t>(S, (c + 1) * chunk);
-    for (size_t i = c * chunk; i < e; ++i) wt.symbols[i] = map[wt.bytes[i]];
-  });
+  finish_table(d, recs, opt, threads, out);
+  WordTable& wt = *out;
 
   if (opt.want_stream) {
     // rank of every distinct word, addressable through the merged counters

@@ -31,6 +31,7 @@ struct WordTable {
   bool keep[256] = {};
   // Stream layout (optional): the type rank of every word occurrence, in corpus order.
   std::vector<uint32_t> occurrence_rank;
+  bool counted_on_gpu = false;   // the distinct words were counted on the device (load_device.hip)
 
   size_t num_words() const { return count.size(); }
   size_t num_symbols() const { return symbols.size(); }
@@ -41,7 +42,23 @@ struct LoadOptions {
   float coverage = 0.995f;
   bool want_stream = false;  // also fill occurrence_rank
   int threads = 0;           // 0: hardware concurrency (capped at 32)
+  int gpu_device = -1;       // >= 0: count words on this HIP device (types layout, NUL-free files)
+  size_t gpu_min_bytes = 1 << 20;  // smaller files take the host path
 };
+
+// One distinct word found by the device count: its first offset in the file, its occurrence
+// count and its length (hip/load_device.hip).
+struct WordRec {
+  uint64_t first;
+  uint64_t count;
+  uint32_t len;
+  uint32_t pad;
+};
+
+// GPU word count: the distinct words of d[0, n) in reference word order
+// (djb2(word) & 4095, first occurrence).  d must not contain NUL bytes (those files keep the
+// host's fgets/strlen path).  False (reason in *why) when no device is usable.
+bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec>* out, std::string* why);
 
 // Returns 0 on success, -1 if the file cannot be opened/mapped (message in *err).
 int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::string* err);

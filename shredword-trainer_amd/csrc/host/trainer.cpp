@@ -40,6 +40,7 @@ struct Trainer {
   bool local_exchange = false;   // test: the multi-GPU exchange over a single-rank communicator
   uint32_t exchange_bucket = 0;  // records per rank and exchange bucket (0: default)
   int resident = -1;             // LDS-resident merge loop: -1 default (on), 0 off, 1 on
+  bool gpu_load = true;          // count the corpus words on the device (types layout)
   double load_s = 0;
 };
 
@@ -87,6 +88,8 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
       if (b < 1) return -1;
       t->exchange_bucket = (uint32_t)b;
     }
+  } else if (key == "gpu_load") {
+    t->gpu_load = std::atoi(val.c_str()) != 0;
   } else if (key == "resident") {
     t->resident = std::atoi(val.c_str()) != 0 ? 1 : 0;
     if (t->dev) t->dev->set_resident(t->resident != 0);
@@ -165,6 +168,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   t->engine.configure(t->config.target_vocab_size, t->config.unk_id, t->config.min_pair_freq);
   t->engine.set_log(env_int("SHREDWORD_LOG", 1));
   t->timing = env_int("SHREDWORD_TIMING", 0) != 0;
+  t->gpu_load = env_int("SHREDWORD_GPU_LOAD", 1) != 0;
   t->device = env_int("SHREDWORD_DEVICE", -1);
   if (const char* v = std::getenv("SHREDWORD_LAYOUT")) set_option(t, "layout", v);
   if (const char* v = std::getenv("SHREDWORD_TRACE")) set_option(t, "trace", v);
@@ -190,6 +194,12 @@ int bpe_load_corpus(Trainer* t, const char* path) {
   opt.unk_id = t->config.unk_id;
   opt.coverage = t->config.character_coverage;
   opt.want_stream = t->layout == Layout::kStream;
+  if (t->gpu_load && !opt.want_stream && shred_device_count() > 0) {  // the ordinal ensure_device will use
+    int ord = t->device;
+    if (ord < 0) ord = dist_active() ? dist_state().device : env_int("LOCAL_RANK", 0);
+    opt.gpu_device = ord % shred_device_count();
+    opt.gpu_min_bytes = (size_t)env_int("SHREDWORD_GPU_LOAD_MIN", 1 << 20);
+  }
   std::string err;
   WordTable wt;
   if (load_corpus(path, opt, &wt, &err) != 0) {
@@ -333,6 +343,9 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
     s->resident_launches = t->dev->resident_launches();
     s->resident_ms = t->dev->resident_ms();
     s->resident_latency_us = t->dev->resident_latency_us();
+  }
+  {
+    s->load_on_gpu = t->wt.counted_on_gpu ? 1 : 0;
   }
   s->num_words = t->wt.num_words();
   s->num_symbols = t->wt.num_symbols();

@@ -65,7 +65,8 @@ class ShredStats(Structure):
                 ("spec_hits", c_uint64), ("spec_misses", c_uint64),
                 ("exchange_overflows", c_uint64),
                 ("hist_kernel_ms", c_double), ("hist_kernel_bytes", c_double), ("hist_launches", c_uint64),
-                ("resident_launches", c_uint64), ("resident_ms", c_double), ("resident_latency_us", c_double)]
+                ("resident_launches", c_uint64), ("resident_ms", c_double), ("resident_latency_us", c_double),
+                ("load_on_gpu", c_uint64)]
 
 
 Trainer = c_void_p

@@ -289,3 +289,33 @@ def test_full_size_c2_invariants(tmp_path):
     assert len(freqs) == n
     assert all(x >= y for x, y in zip(freqs, freqs[1:])), "merge frequencies must not increase"
     assert freqs[-1] >= 2000
+
+
+@pytest.mark.parametrize("kind", ["medium", "adversarial_no_nul", "utf8"])
+def test_gpu_word_count_matches_host(kind, medium_corpus, tmp_path, monkeypatch):
+    """load_corpus counting words on the device (load_device.hip) against the host count: the
+    same word table, so the same training bytes.  The adversarial corpus (CR/TAB runs, 10 kB
+    lines, a 10,333-byte word, no final newline) is taken without its NUL bytes, which keep the
+    host's fgets/strlen path."""
+    monkeypatch.setenv("SHREDWORD_GPU_LOAD_MIN", "1")
+    if kind == "medium":
+        corpus = medium_corpus
+    elif kind == "utf8":
+        corpus = str(tmp_path / "u.txt")
+        corpora.gen_synthetic(corpus, 3_000_000, 77, "utf8")
+    else:
+        corpus = str(tmp_path / "adv.txt")
+        with open(corpus, "wb") as f:
+            f.write(corpora.adversarial_bytes(5).replace(b"\0", b""))
+    outs = []
+    for gpu in (0, 1):
+        t = _trainer(vocab_size=3000, unk_id=0, character_coverage=0.9995, min_pair_freq=2)
+        t.set_option("gpu_load", gpu)
+        t.load_corpus(corpus)
+        n, model, vocab = _train_bytes(t, tmp_path, f"w{gpu}")
+        st = t.stats()
+        t.destroy()
+        assert st["load_on_gpu"] == gpu
+        outs.append((n, model, vocab, st["num_words"], st["num_symbols"], st["num_occurrences"]))
+    assert outs[0] == outs[1]
+
