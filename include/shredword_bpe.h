@@ -85,6 +85,9 @@ int loadVocab(void* trainer, const char* path);
  *   resident = 0 | 1            LDS-resident merge loop (default 1): when the distinct-word
  *                               table fits the chip's LDS, the merge loop runs as one persistent
  *                               launch holding the table in LDS (results are identical either way)
+ *   spec_depth = 1 | 2 | 3      resident loop: guessed merges in flight behind the current merge
+ *                               (default 1, or env SHREDWORD_SPEC_DEPTH; a wrong guess undoes every
+ *                               guess after it; results are identical at any depth)
  *   gpu_load = 0 | 1            count the corpus words on the device at load_corpus (default 1;
  *                               types layout, files without NUL bytes; same table either way)
  *   exchange_bucket = <n>       multi-GPU: records per rank in the fixed all-gather bucket

@@ -977,7 +977,14 @@ constexpr uint32_t kResSigRebuild = 192;  // pairs added to a tile's signature b
 constexpr uint32_t kResMaxTiles = 256;   // tiles one workgroup may own
 constexpr uint32_t kOpMerge = 1, kOpStop = 2, kOpTimeout = 3;
 
-constexpr uint32_t kResRing = 8;         // host command ring, device command ring, per-workgroup queues
+// host command ring, device command ring, per-workgroup queues: at most 10 commands are ever
+// outstanding (Device::rollback), so no entry is overwritten before it is read
+constexpr uint32_t kResRing = 16;
+// Workgroup roles: 0 dispatches the host's commands, 1 completes every merge (gathers the
+// participants' records to the host), 2 .. grid-1 own the tiles.
+constexpr uint32_t kResGatherWg = 1, kResFirstWorker = 2;
+constexpr int kResGatherBatch = 16;  // records per gatherer thread per round trip
+static_assert(kResDeltaW < (1 << 12) && kResMaxTiles * kWaveTok < (1u << 22), "region header fields (k_resident)");
 constexpr uint32_t kOpUnmerge = 4;
 
 // One host command (pinned host memory, written by the host; only the leader reads it).
@@ -1000,7 +1007,7 @@ struct ResSlot {
   u64* dft;
   uint32_t* dlist;
   uint32_t* dcount;   // [0] touched global slots
-  uint32_t* done;     // tickets: [0..7] shards, [8] top
+  uint32_t* done;     // [8]: participants that published their region (the gatherer resets it)
   DeltaRecord* out;   // host-visible records
   uint32_t* hcount;   // host-visible: [0] records, [1] flag = seq, [2] matched tiles
   u64* hstats;        // host-visible: [0] occurrences, [1] tokens rewritten, [2] device ticks of the merge
@@ -1027,7 +1034,7 @@ struct ResParams {
   uint32_t seq0;             // first command number of this launch
   uint32_t leader_polls;     // idle leader iterations before the launch ends itself
   uint32_t keys_per_merge, slot_cap;
-  ResSlot sl[2];
+  ResSlot sl[Device::kResSlots];  // merge X uses sl[X % kResSlots]
   uint32_t* dbg;      // diagnostic (SHREDWORD_RESIDENT_DEBUG): per workgroup [phase, last seq, pi, T]
   u64* stamps;        // diagnostic: per participant [go seen, work done, loop cycles, -] (s_memrealtime)
 };
@@ -1041,12 +1048,12 @@ struct ResDelta {
 
 // Queue entry: two 8-byte halves, each tagged with this workgroup's entry number (count, 1-based,
 // 16 bits); a reader takes the entry when both halves carry the count it expects.
-//   half 0: count 16 | pi 8 | op 3 | slot 1 | T 9 | a 20     half 1: count 16 | b 20 | X 20
+//   half 0: count 16 | pi 8 | op 3 | slot 2 | T 9 | a 20     half 1: count 16 | b 20 | X 20
 __device__ __forceinline__ void q_pack(uint32_t cnt, uint32_t pi, uint32_t op, uint32_t slot, uint32_t T, int32_t a,
                                        int32_t b, int32_t X, u64* h0, u64* h1) {
   const u64 c = cnt & 0xFFFFu;
-  *h0 = c | ((u64)(pi & 0xFFu) << 16) | ((u64)(op & 7u) << 24) | ((u64)(slot & 1u) << 27) | ((u64)(T & 0x1FFu) << 28) |
-        ((u64)((uint32_t)a & 0xFFFFFu) << 37);
+  *h0 = c | ((u64)(pi & 0xFFu) << 16) | ((u64)(op & 7u) << 24) | ((u64)(slot & 3u) << 27) | ((u64)(T & 0x1FFu) << 29) |
+        ((u64)((uint32_t)a & 0xFFFFFu) << 38);
   *h1 = c | ((u64)((uint32_t)b & 0xFFFFFu) << 16) | ((u64)((uint32_t)X & 0xFFFFFu) << 36);
 }
 
@@ -1365,12 +1372,13 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   __shared__ uint32_t s_len[kResMaxTiles], s_lofs[kResMaxTiles], s_sigadd[kResMaxTiles];
   __shared__ u64 s_toff[kResMaxTiles];
   __shared__ uint32_t s_mt[kResMaxTiles];
-  __shared__ uint8_t s_lm[kResMaxTiles];   // tiles where this workgroup's last merge matched
+  __shared__ uint8_t s_lm[kResMaxTiles];   // per tile: bit X % 8 set when merge X matched there
   __shared__ uint32_t s_qc[kMaxMergeGroups];  // leader: entries written to each workgroup's queue
-  __shared__ uint32_t s_nmt, s_nrec, s_last;
+  __shared__ uint32_t s_nmt, s_nrec;
   __shared__ uint32_t s_cmd[8];
   __shared__ u64 s_cnt[2];
   __shared__ u64 s_tlead;
+  __shared__ u64 s_ts[4];      // diagnostic (stamps): the gatherer's phase ends
   __shared__ uint32_t s_nout;  // the last participant: records written to the host
   __shared__ uint32_t s_pre[kMaxMergeGroups + 1], s_pmt[kMaxMergeGroups + 1];
   __shared__ uint32_t s_wtot[2][kWaves];
@@ -1454,6 +1462,8 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
           uint32_t* dc = p.cmd + ((uint32_t)X % kResRing) * 8;
           __hip_atomic_store(reinterpret_cast<u64*>(dc + 6), (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+          if (p.stamps)  // diagnostic: the host times post -> dispatch (write-through)
+            __hip_atomic_store(p.status + 1, expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1461,7 +1471,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
           const uint32_t wg = 4u * lane + k;  // distinct workgroups per lane: the counters need no atomics
           const uint32_t c = ++s_qc[wg];
           u64 h0, h1;
-          q_pack(c, pi++, op, sn & 1u, T, a, b, X, &h0, &h1);
+          q_pack(c, pi++, op, sn & 3u, T, a, b, X, &h0, &h1);
           u64* e = p.q + ((size_t)wg * kResRing + ((c - 1) % kResRing)) * 2;
           __hip_atomic_store(e, h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(e + 1, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1488,9 +1498,9 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       if (got) {
         ++consumed;
         s_cmd[1] = (uint32_t)(h0 >> 16) & 0xFFu;
-        s_cmd[2] = (uint32_t)(h0 >> 27) & 1u;                     // slot
-        s_cmd[6] = (uint32_t)(h0 >> 28) & 0x1FFu;                 // T
-        s_cmd[3] = (uint32_t)(h0 >> 37) & 0xFFFFFu;               // a
+        s_cmd[2] = (uint32_t)(h0 >> 27) & 3u;                     // slot
+        s_cmd[6] = (uint32_t)(h0 >> 29) & 0x1FFu;                 // T
+        s_cmd[3] = (uint32_t)(h0 >> 38) & 0xFFFFFu;               // a
         s_cmd[4] = (uint32_t)(h1 >> 16) & 0xFFFFFu;               // b
         s_cmd[5] = (uint32_t)(h1 >> 36) & 0xFFFFFu;               // X
       }
@@ -1515,19 +1525,15 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       p.dbg[me * 4 + 2] = pi;
       p.dbg[me * 4 + 3] = T;
     }
-    if (op == kOpUnmerge) {  // undo this workgroup's last merge (the host's guess was wrong)
+    const uint32_t lm_bit = 1u << ((uint32_t)X & 7u);
+    if (op == kOpUnmerge) {  // undo merge X, a wrong guess (the host undoes them newest first)
       for (uint32_t i = wid; i < nt; i += kWaves)
-        if (s_lm[i]) res_unmerge_tile(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords, &s_sigadd[i], st,
+        if (s_lm[i] & lm_bit) res_unmerge_tile(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords, &s_sigadd[i], st,
                                       a, b, X, lane);
       __syncthreads();
       continue;
     }
     const ResSlot& sl = p.sl[slot];
-    u64 clk0 = 0;
-    if (p.stamps && threadIdx.x == 0) {
-      __hip_atomic_store(p.stamps + pi * 4, (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      clk0 = __builtin_amdgcn_s_memtime();
-    }
 
     // ---- the merge over this workgroup's tiles (wave per tile)
     u64 n_merged = 0, n_written = 0;
@@ -1535,7 +1541,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       const uint32_t m = res_merge_tile<kWeighted>(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords,
                                                    &s_sigadd[i], st, s_w, r0, a, b, X, h, sl, p.slot_cap, lane,
                                                    &n_written);
-      if (lane == 0) s_lm[i] = m ? 1 : 0;
+      if (lane == 0) s_lm[i] = m ? (s_lm[i] | lm_bit) : (s_lm[i] & ~lm_bit);
       if (m) {
         n_merged += m;
         if (lane == 0) s_mt[atomicAdd(&s_nmt, 1u)] = t0 + i;
@@ -1546,11 +1552,6 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       if (n_written) atomicAdd(&s_cnt[1], n_written);
     }
     __syncthreads();
-    if (p.stamps && threadIdx.x == 0) {
-      __hip_atomic_store(p.stamps + pi * 4 + 1, (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.stamps + pi * 4 + 3, (u64)__builtin_amdgcn_s_memtime() - clk0, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
     // ---- publish this participant's region (write-through), clearing the LDS hash
     {
       u64* rr = sl.rrec + (size_t)pi * kDeltaLdsW * 3;
@@ -1568,37 +1569,24 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       const uint32_t nmt = s_nmt;
       for (uint32_t i = threadIdx.x; i < nmt; i += kThreads)
         __hip_atomic_store(sl.rtile + (size_t)pi * kMtLds + i, s_mt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      u64* hd = reinterpret_cast<u64*>(sl.rhdr + (size_t)pi * kRegHdr);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's region stores (and spills) are done
       __syncthreads();
+      // the header: two 8-byte words, each tagged with X, stored last; the gatherer polls them
+      // (so no ticket and no second drain: the workgroup goes straight on to its next command)
+      //   word 0: X 20 | records 12 | matched tiles 16 | spill 1   word 1: X 20 | merged 22 | written 22
       if (threadIdx.x == 0) {
-        uint32_t* hd = sl.rhdr + (size_t)pi * kRegHdr;
-        __hip_atomic_store(hd, s_nrec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(hd + 1, nmt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(hd + 2, h.spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(reinterpret_cast<u64*>(hd + 4), s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(reinterpret_cast<u64*>(hd + 6), s_cnt[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 x20 = (u64)(uint32_t)X & 0xFFFFFu;
+        const u64 w0 = x20 | ((u64)s_nrec << 20) | ((u64)nmt << 32) | ((u64)(h.spill ? 1u : 0u) << 48);
+        const u64 w1 = x20 | ((s_cnt[0] & 0x3FFFFFull) << 20) | ((s_cnt[1] & 0x3FFFFFull) << 42);
+        __hip_atomic_store(hd, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hd + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         h.spill = 0;
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (me != kResGatherWg) continue;
     __syncthreads();
-    // ---- ticket among the T participants (sharded by participant index above 32)
-    if (threadIdx.x == 0) {
-      bool last = false;
-      if (T <= 32u) {
-        last = atomicAdd(&sl.done[8], 1u) == T - 1u;
-      } else {
-        const uint32_t g = pi & 7u, in_group = (T - g + 7u) >> 3;
-        if (atomicAdd(&sl.done[g], 1u) == in_group - 1u) {
-          atomicExch(&sl.done[g], 0u);
-          last = atomicAdd(&sl.done[8], 1u) == 7u;
-        }
-      }
-      s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) continue;
-    // ---- the last participant: gather the regions to the host, raise the slot's flag
+    // ---- the gatherer: gather the regions to the host, raise the slot's flag
     uint32_t n = 0, nm = 0;
     if (threadIdx.x == 0)  // the dispatch stamp (per-merge device time), loaded beside the headers
       s_tlead = __hip_atomic_load(reinterpret_cast<const u64*>(p.cmd + ((uint32_t)X % kResRing) * 8 + 6),
@@ -1614,19 +1602,38 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       }
       __syncthreads();
       const uint32_t g = threadIdx.x;
-      if (g < T) {
-        const uint32_t* hd = sl.rhdr + (size_t)g * kRegHdr;
-        my_nrec = __hip_atomic_load(hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        my_nmt = __hip_atomic_load(hd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        spill = __hip_atomic_load(hd + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        merged = __hip_atomic_load(reinterpret_cast<const u64*>(hd + 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        written = __hip_atomic_load(reinterpret_cast<const u64*>(hd + 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (g < T) {  // thread g waits for participant g's header, then takes its counts and resets it
+        u64* hd = reinterpret_cast<u64*>(sl.rhdr + (size_t)g * kRegHdr);
+        const uint32_t x20 = (uint32_t)X & 0xFFFFFu;
+        u64 v0, v1;
+        for (;;) {
+          v0 = __hip_atomic_load(hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v1 = __hip_atomic_load(hd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (((uint32_t)v0 & 0xFFFFFu) == x20 && ((uint32_t)v1 & 0xFFFFFu) == x20) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        my_nrec = (uint32_t)(v0 >> 20) & 0xFFFu;
+        my_nmt = (uint32_t)(v0 >> 32) & 0xFFFFu;
+        spill = (uint32_t)(v0 >> 48) & 1u;
+        merged = (v1 >> 20) & 0x3FFFFFull;
+        written = (v1 >> 42) & 0x3FFFFFull;
+        __hip_atomic_store(hd, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // drained before the flag
+        __hip_atomic_store(hd + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (merged) atomicAdd(&s_cnt[0], merged);
-      if (written) atomicAdd(&s_cnt[1], written);
-      if (spill) atomicOr(&s_nrec, 1u);
+      if (p.stamps) {  // diagnostic: all regions published
+        __syncthreads();
+        if (threadIdx.x == 0) s_ts[0] = __builtin_amdgcn_s_memrealtime();
+      }
+      // per-wave totals first (each participant's counts fit 22 bits): one LDS atomic per wave,
+      // not one per participant on the same address
+      const uint32_t wm = wave_scan_add((uint32_t)merged), ww = wave_scan_add((uint32_t)written);
+      const bool any_spill = __any(spill != 0);
       const uint32_t ir = wave_scan_add(my_nrec), im = wave_scan_add(my_nmt);
       if (lane == 63) {
+        if (wm) atomicAdd(&s_cnt[0], (u64)wm);
+        if (ww) atomicAdd(&s_cnt[1], (u64)ww);
+        if (any_spill) atomicOr(&s_nrec, 1u);
         s_wtot[0][wid] = ir;
         s_wtot[1][wid] = im;
       }
@@ -1647,6 +1654,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       __syncthreads();
       n = s_pre[T];
       nm = s_pmt[T];
+      if (p.stamps && threadIdx.x == 0) s_ts[1] = __builtin_amdgcn_s_memrealtime();
       auto owner = [&](const uint32_t* pre, uint32_t i) {
         uint32_t lo = 0, hi = T;
         while (hi - lo > 1) {
@@ -1656,10 +1664,10 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
         }
         return lo;
       };
-      for (uint32_t i0 = 0; i0 < n; i0 += kThreads * 4) {
-        u64 r[4][3];
+      for (uint32_t i0 = 0; i0 < n; i0 += kThreads * kResGatherBatch) {
+        u64 r[kResGatherBatch][3];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kResGatherBatch; ++k) {
           const uint32_t i = i0 + k * kThreads + threadIdx.x;
           if (i < n) {
             const uint32_t o = owner(s_pre, i);
@@ -1668,8 +1676,13 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
             for (int c = 0; c < 3; ++c) r[k][c] = __hip_atomic_load(src + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
+        if (p.stamps && i0 == 0) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (threadIdx.x == 0) s_ts[2] = __builtin_amdgcn_s_memrealtime();
+        }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {  // combine the participants' records per key in the LDS hash
+        for (int k = 0; k < kResGatherBatch; ++k) {  // combine the participants' records per key in the LDS hash
           const uint32_t i = i0 + k * kThreads + threadIdx.x;
           if (i >= n) continue;
           const uint32_t key = (uint32_t)r[k][0];
@@ -1688,6 +1701,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
           if (!done) sys_record(sl.out + atomicAdd(&s_nout, 1u), key, r[k][1], r[k][2]);  // the host combines these
         }
       }
+      if (p.stamps && threadIdx.x == 0) s_ts[3] = __builtin_amdgcn_s_memrealtime();
       __syncthreads();
       for (int i = threadIdx.x; i < kResDeltaW; i += kThreads) {
         const uint32_t key = h.key[i];
@@ -1727,20 +1741,12 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       sys_store(&sl.hstats[0], s_cnt[0]);
       sys_store(&sl.hstats[1], s_cnt[1]);
       sys_store(&sl.hstats[2], (u64)__builtin_amdgcn_s_memrealtime() - t_leader);
-      if (p.stamps) {  // diagnostic: the slowest participant per phase, relative to the leader
-        u64 mx[3] = {0, 0, 0};
-        for (uint32_t g = 0; g < T; ++g)
-          for (int k = 0; k < 2; ++k) {
-            const u64 v = __hip_atomic_load(p.stamps + g * 4 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t_leader;
-            mx[k] = v > mx[k] ? v : mx[k];
-          }
-        sys_store(&sl.hstats[3], mx[0]);
-        sys_store(&sl.hstats[4], mx[1]);
-        sys_store(&sl.hstats[5], mx[2]);
+      if (p.stamps) {  // diagnostic: the gatherer's phases, relative to the leader's dispatch
+        for (int k = 0; k < 4; ++k) sys_store(&sl.hstats[3 + k], s_ts[k] - t_leader);
+        sys_store(&sl.hstats[7], (u64)s_pre[T]);  // records before the combine
       }
       sys_store(&sl.hcount[0], n);
       sys_store(&sl.hcount[2], nm);
-      atomicExch(&sl.done[8], 0u);
       sys_flag(&sl.hcount[1], (uint32_t)X);  // the host clears the flag before posting to the slot
     }
   }
@@ -2585,7 +2591,7 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
   cu_count_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   const unsigned pin = hipHostMallocMapped | hipHostMallocCoherent;
   for (MergeSlot& sl : slot_) {
-    HIP_OK(hipHostMalloc((void**)&sl.host_count, 64, pin));
+    HIP_OK(hipHostMalloc((void**)&sl.host_count, 128, pin));
     std::memset(sl.host_count, 0, 64);
     HIP_OK(hipHostGetDevicePointer(&sl.dev_count, sl.host_count, 0));
   }
@@ -2609,7 +2615,7 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
 void Device::set_merge_groups(int groups) { max_groups_ = std::max(1, std::min(kMaxMergeGroups, groups)); }
 
 void Device::set_exchange(const Exchange& x) {
-  if (slot_[0].dsum || slot_[1].dsum) fatal("set_exchange: merge buffers already exist");
+  if (slot_[0].dsum || slot_[1].dsum || slot_[2].dsum || slot_[3].dsum) fatal("set_exchange: merge buffers already exist");
   if (x.world < 1 || x.world > 64 || !x.allgather || x.bucket_records < 1) fatal("set_exchange: bad exchange");
   xchg_ = x;
   exchange_ = true;
@@ -2981,15 +2987,16 @@ void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   HIP_OK(hipSetDevice(ordinal_));
   if (n < 1 || n > kChainMax) fatal("merge_chain: bad chain length");
   if (n == 1 && run_count_ == 0 && ntiles_ && resident_eligible() && X0 < (1 << 20)) {  // k_resident (ids: 20 bits)
-    if (res_posted_.size() >= 2) fatal("merge_chain: two resident merges are already in flight");
-    const int slot = X0 & 1;  // consecutive merges alternate slots
+    if (res_posted_.size() >= (size_t)kResSlots) fatal("merge_chain: every resident slot has a merge in flight");
+    const int slot = pick_resident_slot();
     bool grow = false;
     for (const MergeSlot& s2 : slot_) grow |= !s2.dsum || (uint32_t)X0 + 2 > s2.cap;
     if (grow) {  // the delta tables grow: only between launches
       if (!res_posted_.empty()) fatal("merge_chain: delta tables too small with a resident merge in flight");
       park();
       for (MergeSlot& s2 : slot_) ensure_slots(s2, (uint32_t)X0 + 2);
-      const uint32_t cap = std::max(slot_[0].cap, slot_[1].cap);
+      uint32_t cap = 0;
+      for (const MergeSlot& s2 : slot_) cap = std::max(cap, s2.cap);
       for (MergeSlot& s2 : slot_) ensure_slots(s2, cap);
     }
     max_id_seen_ = std::max(max_id_seen_, X0);
@@ -3319,8 +3326,10 @@ void Device::rollback(int32_t X) {
     while (!res_posted_.empty() && res_posted_.back().X >= X) {
       const ResPost rp = res_posted_.back();
       res_posted_.pop_back();
-      wait_resident(slot_[rp.slot], rp.X);  // its completion leaves the slot before the slot's next merge
+      // no wait: every workgroup takes its commands in order, so the undo follows the guess; the
+      // slot stays out of use until the guess's completion is seen (pick_resident_slot)
       post_resident(kOpUnmerge, rp.a, rp.b, rp.X, rp.slot);
+      res_abandoned_[rp.slot] = rp.X;
       ++rollbacks_;
     }
     return;
@@ -3462,8 +3471,8 @@ void Device::plan_resident(const TiledStream& ts) {
   free_resident();
   if (layout_ != Layout::kTypes || ntiles_ == 0) return;
   const uint32_t G = (uint32_t)std::min(cu_count_, kMaxMergeGroups);
-  if (G < 2) return;
-  const uint32_t W = G - 1;  // workers 1 .. G-1; workgroup 0 dispatches
+  if (G < kResFirstWorker + 1) return;
+  const uint32_t W = G - kResFirstWorker;  // workers 2 .. G-1 (0 dispatches, 1 gathers)
   int max_lds = 0;
   HIP_OK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, ordinal_));
   hipFuncAttributes fa;
@@ -3489,14 +3498,14 @@ void Device::plan_resident(const TiledStream& ts) {
     words[t] = (len + 3u) & ~3u;
     total += 4.0 * words[t] + 8.0 * (rlast[t] - rfirst[t] + 1) + 4.0 * kResSigWords;
   }
-  // contiguous ranges balanced by LDS bytes: tile t goes to worker 1 + floor((prefix + cost/2) * W / total)
+  // contiguous ranges balanced by LDS bytes: tile t goes to worker 2 + floor((prefix + cost/2) * W / total)
   std::vector<uint32_t> wg_tiles(G + 1, 0), wg_rank(G + 1, 0), lofs(T);
   res_owner_.assign(T, 0);
   double pre = 0;
-  uint32_t w = 1;
+  uint32_t w = kResFirstWorker;
   for (size_t t = 0; t < T; ++t) {
     const double c = 4.0 * words[t] + 8.0 * (rlast[t] - rfirst[t] + 1) + 4.0 * kResSigWords;
-    uint32_t want = 1 + (uint32_t)std::min<double>(W - 1, std::floor((pre + c / 2) * W / total));
+    uint32_t want = kResFirstWorker + (uint32_t)std::min<double>(W - 1, std::floor((pre + c / 2) * W / total));
     if (want < w) want = w;
     while (w < want) wg_tiles[++w] = (uint32_t)t;
     res_owner_[t] = w;
@@ -3535,7 +3544,7 @@ void Device::plan_resident(const TiledStream& ts) {
   res_w_words_ = nr_max;
   res_shm_ = shm;
   res_all_.clear();
-  for (uint32_t g = 1; g < G; ++g) res_all_.push_back(g);
+  for (uint32_t g = kResFirstWorker; g < G; ++g) res_all_.push_back(g);
   res_wg_first_ = wg_tiles;
   res_wg_tiles_ = dalloc<uint32_t>(G + 1, &bytes_alloc_);
   res_wg_rank_ = dalloc<uint32_t>(G + 1, &bytes_alloc_);
@@ -3594,8 +3603,9 @@ void Device::reserve_ids(int32_t max_id) {
   if (!res_posted_.empty() || run_count_ > 0) return;  // later: merge_chain grows on demand
   park();
   for (MergeSlot& s : slot_) ensure_slots(s, need);
-  // both slots share keys_per_merge_: size them alike
-  const uint32_t cap = std::max(slot_[0].cap, slot_[1].cap);
+  // the slots share keys_per_merge_: size them alike
+  uint32_t cap = 0;
+  for (const MergeSlot& s : slot_) cap = std::max(cap, s.cap);
   for (MergeSlot& s : slot_) ensure_slots(s, cap);
 }
 
@@ -3617,8 +3627,8 @@ void Device::start_resident() {
   rp.seq0 = seq_ + 1;
   rp.leader_polls = 1u << 23;  // ~10 s without a command: the launch ends itself (the host relaunches)
   rp.keys_per_merge = keys_per_merge_;
-  rp.slot_cap = std::min(slot_[0].cap, slot_[1].cap);
-  for (int k = 0; k < 2; ++k) {
+  rp.slot_cap = min_slot_cap();
+  for (int k = 0; k < kResSlots; ++k) {
     MergeSlot& sl = slot_[k];
     ResSlot& r = rp.sl[k];
     r.dsum = U(sl.dsum);
@@ -3633,7 +3643,10 @@ void Device::start_resident() {
     r.rhdr = sl.rhdr;
     r.rrec = U(sl.rrec);
     r.rtile = sl.rtile;
+    // region headers carry the merge id k_resident polls for: none may hold a stale one
+    if (sl.rhdr) HIP_OK(hipMemsetAsync(sl.rhdr, 0, (size_t)kMaxMergeGroups * kRegHdr * sizeof(uint32_t), S(stream_)));
   }
+  for (int32_t& x : res_abandoned_) x = -1;
   rp.dbg = res_dbg_;
   rp.stamps = U(res_stamps_);
   res_status_[0] = 0;
@@ -3672,6 +3685,10 @@ uint32_t Device::post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int
     const std::vector<uint32_t>& pp = res_post_parts_[slot];
     for (uint32_t o : pp) mask[o >> 5] |= 1u << (o & 31);
     np = (uint32_t)pp.size();
+    if (op == kOpMerge) {  // the gatherer completes every merge
+      mask[0] |= 1u << kResGatherWg;
+      ++np;
+    }
   }
   const uint32_t seq = ++seq_;
   uint64_t* g = static_cast<ResMbox*>(res_mbox_)->cmd[seq % kResRing].g;
@@ -3684,6 +3701,32 @@ uint32_t Device::post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int
   for (int k = 0; k < 8; ++k) put(kCmdMask + k, mask[k]);
   std::atomic_thread_fence(std::memory_order_release);
   return seq;
+}
+
+// A slot for the next resident merge: none with a posted merge, and none whose undone guess has
+// not completed yet (its completion still writes the slot and raises the slot's flag with the
+// same merge id the next merge may carry).
+int Device::pick_resident_slot() {
+  for (;;) {
+    int wait_slot = -1;
+    for (int k = 0; k < kResSlots; ++k) {
+      const int s = (res_next_slot_ + k) % kResSlots;
+      bool used = false;
+      for (const ResPost& rp : res_posted_) used |= rp.slot == s;
+      if (used) continue;
+      if (res_abandoned_[s] >= 0) {
+        if (__atomic_load_n(slot_[s].host_count + 1, __ATOMIC_ACQUIRE) != (uint32_t)res_abandoned_[s]) {
+          if (wait_slot < 0) wait_slot = s;
+          continue;
+        }
+        res_abandoned_[s] = -1;
+      }
+      res_next_slot_ = (s + 1) % kResSlots;
+      return s;
+    }
+    if (wait_slot < 0) fatal("k_resident: no free merge slot");
+    wait_resident(slot_[wait_slot], res_abandoned_[wait_slot]);
+  }
 }
 
 void Device::wait_resident(const MergeSlot& sl, int32_t X) {
@@ -3710,6 +3753,10 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   res_posted_.erase(res_posted_.begin());
   MergeSlot& sl = slot_[rp.slot];
   const double tw = now_seconds();
+  if (res_stamps_) {  // diagnostic: when the leader's dispatch of this merge becomes visible here
+    while ((int32_t)(__atomic_load_n(&res_status_[1], __ATOMIC_ACQUIRE) - rp.seq) < 0) __builtin_ia32_pause();
+    res_phase_[2] += 1e6 * (now_seconds() - rp.t_post);
+  }
   wait_resident(sl, rp.X);
   {  // host clock: post -> flag seen, and the part of it spent waiting here
     const double t1 = now_seconds();
@@ -3724,7 +3771,8 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   res_lat_us_ += 1e-2 * (double)hs[2];  // s_memrealtime: 100 MHz
   res_lat_n_ += 1;
   if (res_stamps_) {
-    for (int k = 0; k < 2; ++k) res_phase_[k] += 1e-2 * (double)hs[3 + k];
+    for (int k = 0; k < 4; ++k) res_ph_[k] += 1e-2 * (double)hs[3 + k];
+    res_phase_[4] += (double)hs[7];
     res_phase_[3] += 1e-2 * (double)hs[2];
     res_phase_n_ += 1;
   }
@@ -3750,6 +3798,7 @@ void Device::resident_dump(const char* why) {
   HIP_OK(hipStreamSynchronize(s));
   std::fprintf(stderr, "[RESIDENT] %s: seq_=%u status=%u posted=%zu flags=%u/%u\n", why, seq_, res_status_[0],
                res_posted_.size(), slot_[0].host_count[1], slot_[1].host_count[1]);
+  for (int k = 2; k < kResSlots; ++k) std::fprintf(stderr, "[RESIDENT] flag[%d]=%u\n", k, slot_[k].host_count[1]);
   for (const ResPost& rp : res_posted_)
     std::fprintf(stderr, "[RESIDENT]   posted X=%d seq=%u slot=%d np=%u\n", rp.X, rp.seq, rp.slot, rp.nparts);
   for (uint32_t g = 0; g < G; ++g) {
@@ -3772,6 +3821,7 @@ void Device::park() {
   post_resident(kOpStop, 0, 0, 0, 0);
   HIP_OK(hipStreamSynchronize(S(stream_)));
   res_running_ = false;
+  for (int32_t& x : res_abandoned_) x = -1;  // every command ran
   for (MergeSlot& s2 : slot_)  // flags carried merge ids: the launch path compares launch numbers
     if (s2.host_count) s2.host_count[1] = 0xFFFFFFFFu;
   res_status_[0] = 0;
@@ -3787,12 +3837,17 @@ void Device::park() {
     std::fprintf(stderr, "[RESIDENT] %llu merges in %.2f ms | host: post->flag %.2f us, waited %.2f us | participants %.1f",
                  (unsigned long long)res_merges_, ms, res_post_flag_us_ / n, res_host_wait_ / n, res_parts_sum_ / n);
     if (res_phase_n_)
-      std::fprintf(stderr, " | device after dispatch: go %.2f work %.2f flag %.2f", res_phase_[0] / res_phase_n_,
-                   res_phase_[1] / res_phase_n_, res_phase_[3] / res_phase_n_);
+      std::fprintf(stderr,
+                   " | host: post -> dispatch seen %.2f | device after dispatch: all published %.2f prefix %.2f loaded %.2f "
+                   "combined %.2f flag %.2f",
+                   res_phase_[2] / res_phase_n_, res_ph_[0] / res_phase_n_, res_ph_[1] / res_phase_n_,
+                   res_ph_[2] / res_phase_n_, res_ph_[3] / res_phase_n_, res_phase_[3] / res_phase_n_);
+    if (res_phase_n_) std::fprintf(stderr, " | records before combine %.1f", res_phase_[4] / res_phase_n_);
     std::fprintf(stderr, "\n");
   }
   res_post_flag_us_ = res_host_wait_ = res_parts_sum_ = 0;
-  res_phase_[0] = res_phase_[1] = res_phase_[2] = res_phase_[3] = 0;
+  res_phase_[0] = res_phase_[1] = res_phase_[2] = res_phase_[3] = res_phase_[4] = 0;
+  for (double& x : res_ph_) x = 0;
   res_phase_n_ = 0;
   // the tiles are back in HBM: their pair signatures for k_merge / k_unmerge
   const int grid = (int)std::min<size_t>((ntiles_ + kWaves - 1) / kWaves, (size_t)cu_count_ * 8);

@@ -83,7 +83,17 @@ class Device : public Backend {
   static constexpr int kChainMax = 8;
   int max_chain() const override { return speculate_ && !resident_eligible() ? kChainMax : 1; }
   bool can_overlap() const override {
-    return speculate_ && (!resident_eligible() || (uint32_t)max_id_seen_ + 3 < std::min(slot_[0].cap, slot_[1].cap));
+    return speculate_ && (!resident_eligible() || (uint32_t)max_id_seen_ + 3 < min_slot_cap());
+  }
+  // k_resident takes up to kResSlots merges in flight (the current one and the guesses behind
+  // it); the launch path two launches.
+  static constexpr int kResSlots = 4;
+  int overlap_depth() const override { return resident_eligible() ? spec_depth_ : 1; }
+  void set_spec_depth(int d) { spec_depth_ = std::max(1, std::min(d, kResSlots - 1)); }
+  uint32_t min_slot_cap() const {
+    uint32_t c = UINT32_MAX;
+    for (const MergeSlot& s : slot_) c = std::min(c, s.cap);
+    return c;
   }
   void reserve_ids(int32_t max_id) override;
   uint64_t exchange_overflows() const { return x_overflows_; }
@@ -240,7 +250,7 @@ class Device : public Backend {
   uint64_t ft_live_tokens_ = 0;
   uint64_t live_tokens_est_ = 0;
 
-  MergeSlot slot_[2];
+  MergeSlot slot_[kResSlots];  // the launch path uses slots 0 and 1
   ChainRun runs_[2];
   int run_head_ = 0, run_count_ = 0;  // runs_[run_head_] is the oldest in flight
   ChainRun& run_at(int k) { return runs_[(run_head_ + k) & 1]; }
@@ -282,20 +292,24 @@ class Device : public Backend {
   void start_resident();
   uint32_t post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int slot);
   void wait_resident(const MergeSlot& sl, int32_t X);
+  int pick_resident_slot();
   size_t collect_resident(int32_t X, const DeltaRecord** recs);
   [[noreturn]] void resident_dump(const char* why);
   bool resident_on_ = true;       // option (SHREDWORD_RESIDENT / set_option resident)
   bool resident_ok_ = false;      // the uploaded table fits (plan_resident)
   bool res_running_ = false;      // a k_resident launch is live
   bool res_lds_tok_ = true;       // the tokens are in LDS (else in HBM, LDS holds weights + signatures)
-  std::vector<ResPost> res_posted_;  // oldest first (at most two: a merge and the guess after it)
-  std::vector<uint32_t> res_post_parts_[2];  // participants of the posted merges, by slot
+  std::vector<ResPost> res_posted_;  // oldest first (a merge and the guesses behind it)
+  std::vector<uint32_t> res_post_parts_[kResSlots];  // participants of the posted merges, by slot
+  int spec_depth_ = 1;               // guesses in flight behind the current merge (resident)
+  int32_t res_abandoned_[kResSlots] = {-1, -1, -1, -1};  // by slot: an undone guess not yet completed
+  int res_next_slot_ = 0;
   uint32_t res_grid_ = 0, res_tok_words_ = 0, res_w_words_ = 0;
   size_t res_shm_ = 0;
   uint32_t* res_wg_tiles_ = nullptr;   // device: grid + 1
   uint32_t* res_wg_rank_ = nullptr;    // device: grid + 1
   uint32_t* res_tile_lofs_ = nullptr;  // device: per tile
-  std::vector<uint32_t> res_owner_;    // tile -> workgroup (workgroup 0 dispatches, owns none)
+  std::vector<uint32_t> res_owner_;    // tile -> workgroup (0 dispatches and 1 gathers: they own none)
   std::vector<uint32_t> res_wg_ntiles_;
   std::vector<uint32_t> res_all_;      // every worker workgroup (1 .. grid-1)
   std::vector<uint32_t> res_wg_first_; // grid + 1: first tile of each workgroup
@@ -306,7 +320,8 @@ class Device : public Backend {
   uint64_t* res_q_ = nullptr;          // device per-workgroup queues
   uint32_t* res_dbg_ = nullptr;        // device: per-workgroup progress (SHREDWORD_RESIDENT_DEBUG)
   uint64_t* res_stamps_ = nullptr;     // device: per-participant phase stamps (SHREDWORD_RESIDENT_STAMPS)
-  double res_phase_[4] = {};
+  double res_phase_[5] = {};
+  double res_ph_[4] = {};  // diagnostic: the gatherer's phases
   uint64_t res_phase_n_ = 0;
   bool res_stamp_detail_ = false;
   double res_host_wait_ = 0, res_parts_sum_ = 0, res_post_flag_us_ = 0;

@@ -84,10 +84,18 @@ bool Engine::merge_one(Backend& be, int remaining) {
     ++launches_;
     be.merge_chain(chain_ab_.data(), n, X);
   }
-  // overlap: the next merge's guess runs while this one is consumed
-  if (speculate_ && chain == 1 && pending_.empty() && remaining > 1 && be.can_overlap()) {
-    Guess g{0, 0, X + 1};
-    if (sel_.predict_next(a, b, pred_window_, &g.a, &g.b)) {
+  // overlap: the next merges' guesses run while this one is consumed (up to the backend's depth;
+  // each guess shares no token with this merge or the guesses before it)
+  if (speculate_ && chain == 1) {
+    const size_t depth = (size_t)std::max(1, be.overlap_depth());
+    while (pending_.size() < depth && (int)pending_.size() + 1 < remaining && be.can_overlap()) {
+      used_.assign({a, b});
+      for (const Guess& p : pending_) {
+        used_.push_back(p.a);
+        used_.push_back(p.b);
+      }
+      Guess g{0, 0, X + 1 + (int32_t)pending_.size()};
+      if (!sel_.predict_avoid(used_.data(), used_.size(), pred_window_, &g.a, &g.b)) break;
       pending_.push_back(g);
       ++launches_;
       be.merge_scan(g.a, g.b, g.X);

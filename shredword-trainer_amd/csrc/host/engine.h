@@ -31,6 +31,8 @@ class Backend {
   // True when a second launch may be issued before the first is collected (its merges run
   // after the first launch's on the device).
   virtual bool can_overlap() const { return false; }
+  // How many guessed merges may be in flight behind the current one (overlap mode).
+  virtual int overlap_depth() const { return 1; }
   // Undoes every launched merge with id >= X that was not collected, newest first (each
   // expands its X back into (a, b)), so the corpus is exactly as before those merges.
   virtual void rollback(int32_t X) {}
@@ -105,6 +107,7 @@ class Engine {
     int32_t a, b, X;
   };
   std::vector<Guess> pending_;  // launched guesses awaiting confirmation, oldest first
+  std::vector<int32_t> used_;
   std::vector<int32_t> chain_ab_;
   uint64_t spec_hits_ = 0, spec_misses_ = 0, launches_ = 0;
   size_t probe_k_ = 0, probe_window_ = 256;

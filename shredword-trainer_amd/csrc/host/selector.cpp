@@ -145,9 +145,15 @@ void Selector::add_counts(std::vector<PairCount> pairs) {
 }
 
 bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, int32_t* pb) const {
-  // The best valid entry sharing no token with (a, b) among the first `window` heap slots, by a
+  const int32_t used[2] = {a, b};
+  return predict_avoid(used, 2, window, pa, pb);
+}
+
+bool Selector::predict_avoid(const int32_t* used, size_t n_used, size_t window, int32_t* pa, int32_t* pb) const {
+  // The best valid entry sharing no token with `used` among the first `window` heap slots, by a
   // walk from the root that skips every subtree whose root is below the best found so far (the
-  // heap property bounds the whole subtree), so it touches a handful of entries.
+  // heap property bounds the whole subtree), so it touches a handful of entries.  Ties: the
+  // lowest heap slot, as a scan in slot order would pick.
   const size_t n = std::min(window, hf_.size());
   uint64_t best_f = 0;
   size_t best = SIZE_MAX;
@@ -156,16 +162,20 @@ bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, in
   if (n) stack[sp++] = 0;
   while (sp) {
     const size_t i = stack[--sp];
-    const HeapEnt e{hp_[i].a, hp_[i].b, hf_[i], hp_[i].version};
-    if (e.freq < best_f || e.freq < min_freq_ || (best != SIZE_MAX && e.freq == best_f && i > best)) continue;
+    const uint64_t f = hf_[i];
+    if (f < best_f || f < min_freq_ || (best != SIZE_MAX && f == best_f && i > best)) continue;
     const size_t l = 2 * i + 1;
     if (l + 1 < n && sp < 63) stack[sp++] = l + 1;
     if (l < n && sp < 63) stack[sp++] = l;
-    if (e.a == a || e.a == b || e.b == a || e.b == b || e.a == unk_ || e.b == unk_) continue;
+    const HeapPay& e = hp_[i];
+    if (e.a == unk_ || e.b == unk_) continue;
+    bool clash = false;
+    for (size_t k = 0; k < n_used; ++k) clash |= e.a == used[k] || e.b == used[k];
+    if (clash) continue;
     const Info* in = find(pack_pair(e.a, e.b));
-    if (!in || in->version != e.version || in->freq != e.freq) continue;
-    if (e.freq > best_f || best == SIZE_MAX || i < best) {
-      best_f = e.freq;
+    if (!in || in->version != e.version || in->freq != f) continue;
+    if (f > best_f || best == SIZE_MAX || i < best) {
+      best_f = f;
       best = i;
     }
   }

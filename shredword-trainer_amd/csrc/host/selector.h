@@ -65,6 +65,9 @@ class Selector {
   // entry among the first `window` heap slots that shares no token with (a, b).  Used only to
   // run the next merge speculatively; the exact replay decides.
   bool predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, int32_t* pb) const;
+  // The same with every token in used[0, n_used) avoided (deeper speculation: the guess after
+  // the guesses already in flight).
+  bool predict_avoid(const int32_t* used, size_t n_used, size_t window, int32_t* pa, int32_t* pb) const;
   // Up to k further merges guessed from the heap after (a, b): the best valid entries that
   // share no token with (a, b) or with each other, by frequency.  out: k (a, b) pairs.
   size_t predict_chain(int32_t a, int32_t b, size_t window, size_t k, int32_t* out) const;

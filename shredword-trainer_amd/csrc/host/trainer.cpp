@@ -40,6 +40,7 @@ struct Trainer {
   bool local_exchange = false;   // test: the multi-GPU exchange over a single-rank communicator
   uint32_t exchange_bucket = 0;  // records per rank and exchange bucket (0: default)
   int resident = -1;             // LDS-resident merge loop: -1 default (on), 0 off, 1 on
+  int spec_depth = 0;            // resident guesses in flight (0: env SHREDWORD_SPEC_DEPTH or default)
   bool gpu_load = true;          // count the corpus words on the device (types layout)
   double load_s = 0;
 };
@@ -93,6 +94,11 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
   } else if (key == "resident") {
     t->resident = std::atoi(val.c_str()) != 0 ? 1 : 0;
     if (t->dev) t->dev->set_resident(t->resident != 0);
+  } else if (key == "spec_depth") {
+    const int d = std::atoi(val.c_str());
+    if (d < 1 || d > Device::kResSlots - 1) return -1;
+    t->spec_depth = d;
+    if (t->dev) t->dev->set_spec_depth(d);
   } else if (key == "device") {
     t->device = std::atoi(val.c_str());
   } else {
@@ -120,6 +126,7 @@ bool ensure_device(Trainer* t, const char* caller) {
     t->dev->set_timing(t->timing);
     t->dev->set_unk(t->config.unk_id);
     if (t->resident >= 0) t->dev->set_resident(t->resident != 0);
+    t->dev->set_spec_depth(t->spec_depth ? t->spec_depth : env_int("SHREDWORD_SPEC_DEPTH", 1));
     if (dist_active() || t->local_exchange) {
       Device::Exchange x;
       if (dist_active()) {

@@ -202,12 +202,13 @@ def test_speculation_lockstep(layout, medium_corpus):
         t.destroy()
 
 
-@pytest.mark.parametrize("tokens", ["lds", "hbm"])
-def test_resident_lockstep(tokens, medium_corpus, tmp_path, monkeypatch):
+@pytest.mark.parametrize("tokens,depth", [("lds", 1), ("hbm", 1), ("lds", 2), ("hbm", 3)])
+def test_resident_lockstep(tokens, depth, medium_corpus, tmp_path, monkeypatch):
     """The resident merge loop (k_resident) against the launch path, in bpe_merge_batch
     chunks: identical merges and device token streams after every chunk (each chunk ends the
     persistent launch and writes the tiles back).  tokens=hbm keeps the tokens in HBM (the mode
-    of tables larger than the chip's LDS)."""
+    of tables larger than the chip's LDS); depth = guessed merges in flight behind the current
+    one (a wrong guess undoes every guess after it, newest first)."""
     from shredword.cbase import lib
     if tokens == "hbm":
         monkeypatch.setenv("SHREDWORD_RESIDENT_HBM", "1")
@@ -215,6 +216,7 @@ def test_resident_lockstep(tokens, medium_corpus, tmp_path, monkeypatch):
     for res in (0, 1):
         t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
         t.set_option("resident", res)
+        t.set_option("spec_depth", depth)
         t.load_corpus(medium_corpus)
         lib.bpe_init(t.trainer)
         ts.append(t)

@@ -65,6 +65,19 @@ def test_types_layout_resident_hbm_matches_reference(name, case_corpus, tmp_path
         assert st["resident_launches"] > 0
 
 
+@pytest.mark.parametrize("name", [n for n in API_CASES if not n.startswith("adv_")])
+def test_types_layout_resident_deep_speculation_matches_reference(name, case_corpus, tmp_path, monkeypatch):
+    """k_resident with three guessed merges in flight behind the current one."""
+    monkeypatch.setenv("SHREDWORD_SPEC_DEPTH", "3")
+    case, corpus = case_corpus(name)
+    st = {}
+    merges, model, vocab, trace = _train(case, corpus, tmp_path, "types", stats=st)
+    assert merges == case["merges"]
+    assert trace == case["trace"]
+    assert model == case["model_bytes"]
+    assert vocab == case["vocab_bytes"]
+
+
 @pytest.mark.parametrize("name", API_CASES)
 def test_types_layout_launch_path_matches_reference(name, case_corpus, tmp_path):
     """The per-merge launch path (k_merge + speculation + k_unmerge), resident loop off."""
