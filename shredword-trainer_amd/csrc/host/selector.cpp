@@ -106,6 +106,10 @@ Selector::HeapEnt Selector::pop() {
   for (;;) {  // left child if strictly greater, then right if strictly greater (heap.cpp:101-106)
     size_t l = 2 * i + 1, r = l + 1, best = i;
     if (4 * i + 3 < n) __builtin_prefetch(f + 4 * i + 3);  // the grandchildren of both sides
+    if (8 * i + 7 < n) {                                  // and their children (one 64-B line)
+      __builtin_prefetch(f + 8 * i + 7);
+      __builtin_prefetch(f + 8 * i + 14);
+    }
     uint64_t bf = xf;
     if (l < n && f[l] > bf) { best = l; bf = f[l]; }
     if (r < n && f[r] > bf) best = r;
@@ -282,13 +286,25 @@ void Selector::apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, s
   const uint64_t c1 = __builtin_ia32_rdtsc();
   ctr_.cyc_combine += c1 - c0;
   // 2. reference application order: bucket (hk % 1024) ascending, latest first touch first.
-  //    Counting sort by bucket, then insertion sort inside the (almost always tiny) buckets.
-  bucket_start_.assign(kDeltaBuckets + 1, 0);
-  for (const Change& c : changes_) bucket_start_[(c.hk % kDeltaBuckets) + 1]++;
-  for (int k = 0; k < kDeltaBuckets; ++k) bucket_start_[k + 1] += bucket_start_[k];
-  ordered_.resize(changes_.size());
-  for (const Change& c : changes_) ordered_[bucket_start_[c.hk % kDeltaBuckets]++] = c;
-  for (size_t i = 1; i < ordered_.size(); ++i) {
+  //    Two stable 5-bit counting passes by bucket (the usual ~100 changes never pay for a
+  //    1024-entry prefix), then insertion sort inside the (almost always tiny) buckets.
+  static_assert(kDeltaBuckets == 1024, "two 5-bit passes");
+  const size_t nc = changes_.size();
+  staged_.resize(nc);
+  ordered_.resize(nc);
+  {
+    uint32_t cnt[33] = {};
+    for (const Change& c : changes_) cnt[(c.hk & 31u) + 1]++;
+    for (int k = 0; k < 32; ++k) cnt[k + 1] += cnt[k];
+    for (const Change& c : changes_) staged_[cnt[c.hk & 31u]++] = c;
+  }
+  {
+    uint32_t cnt[33] = {};
+    for (const Change& c : staged_) cnt[((c.hk >> 5) & 31u) + 1]++;
+    for (int k = 0; k < 32; ++k) cnt[k + 1] += cnt[k];
+    for (const Change& c : staged_) ordered_[cnt[(c.hk >> 5) & 31u]++] = c;
+  }
+  for (size_t i = 1; i < nc; ++i) {
     const Change c = ordered_[i];
     const uint64_t bk = c.hk % kDeltaBuckets;
     size_t j = i;

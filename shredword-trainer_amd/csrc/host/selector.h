@@ -111,7 +111,7 @@ class Selector {
   std::vector<HeapPay> hp_;
   std::vector<Change> changes_;
   std::vector<uint32_t> change_index_;
-  std::vector<uint32_t> bucket_start_;
+  std::vector<Change> staged_;  // apply: the first counting pass
   std::vector<Change> ordered_;
   Counters ctr_;
 };
