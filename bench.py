@@ -191,6 +191,50 @@ def pair_count_leg(cfg, path, reps, device=0, layout="stream", dist=None):
     }
 
 
+def encode_leg(model, vocab, unk, path, reps, device=0):
+    """Encoder: the model this run trained applied to its own HBM-resident corpus
+    (k_encode_words + k_encode_scan + k_encode_emit, HIP events on the encoder's stream).  Checks
+    the size-independent property that the id counts equal the .vocab frequency column."""
+    import numpy as np
+    import torch
+    from shredword.encoder import BPEEncoder
+    enc = BPEEncoder(model, vocab, unk_id=unk, device=device)
+    text = torch.from_numpy(np.fromfile(path, dtype=np.uint8)).to(f"cuda:{device}")
+    n = text.numel()
+    out = torch.empty(n, dtype=torch.int32, device=text.device)
+    ids, _ = enc.encode_device(text, out)  # warm-up (scratch allocation)
+    times = []
+    for _ in range(reps):
+        ids, ms = enc.encode_device(text, out)
+        times.append(ms)
+    ms = sorted(times)[len(times) // 2]
+    nids = ids.numel()
+    # .vocab frequency column: record i = token i (C string) + " " + freq + "\n" (bpe.cpp:417)
+    raw = open(model, "rb").read()
+    merges = np.frombuffer(raw, dtype=np.int32).reshape(-1, 3)
+    toks = [bytes([b]) for b in range(256)]
+    for a, b, _ in merges:
+        toks.append(toks[a] + toks[b])
+    vb, pos, freq = open(vocab, "rb").read(), 0, []
+    for t in toks:
+        pos += len(t.replace(b"\0", b"")) + 1
+        end = vb.index(b"\n", pos)
+        freq.append(int(vb[pos:end]))
+        pos = end + 1
+    valid = ids[(ids >= 0) & (ids < len(toks))].long()
+    counts = torch.bincount(valid, minlength=len(toks)).cpu().numpy()
+    alg = n + 4.0 * nids
+    enc.destroy()
+    del text, out
+    torch.cuda.empty_cache()
+    return {"kernel": "k_encode_words + k_encode_scan + k_encode_emit (median of reps, HIP events)",
+            "text_bytes": n, "ids": nids, "ms": ms, "text_GBps": n / (ms * 1e-3) / 1e9,
+            "algorithmic_bytes": alg, "achieved_GBps": alg / (ms * 1e-3) / 1e9,
+            "frac_of_hbm_peak": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "counts_match_vocab": bool(np.array_equal(counts, np.array(freq, dtype=np.int64))),
+            "note": "bound by dependent L2 probes of the merge-rank table (one per pair per merge step), not HBM"}
+
+
 def hbm_probe_leg(device=0, nbytes=4 << 30, reps=10):
     """Achievable HBM bandwidth on this box: streaming read and copy kernels
     of the library (shred_hbm_probe), beside the nominal 8 TB/s peak."""
@@ -214,6 +258,7 @@ def main():
     ap.add_argument("--bytes", type=int, default=0, help="override the corpus size (testing)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--encode-reps", type=int, default=5, help="encoder leg repetitions (0 = skip)")
     ap.add_argument("--pair-count-reps", type=int, default=10,
                     help="K1 roofline leg on the stream layout of the same corpus (0: skip)")
     args = ap.parse_args()
@@ -292,6 +337,14 @@ def main():
         except Exception as e:
             pair_count = {"error": repr(e)}
 
+    encode = None
+    if args.encode_reps > 0 and rank == 0:
+        try:
+            encode = encode_leg(os.path.join(tmpd, f"bench_r{rank}.model"), os.path.join(tmpd, f"bench_r{rank}.vocab"),
+                                cfg["unk"], path, args.encode_reps, device=local)
+        except Exception as e:
+            encode = {"error": repr(e)}
+
     if rank == 0:
         mk_ms = st["merge_kernel_ms"] / max(1, st["merge_launches"])
         mk_bytes = st["merge_kernel_bytes"] / max(1, st["merge_launches"])
@@ -362,6 +415,8 @@ def main():
         }
         if pair_count is not None:
             result["pair_count"] = pair_count
+        if encode is not None:
+            result["encode"] = encode
         try:
             result["hbm_achievable"] = hbm_probe_leg(device=local)
             if (result.get("pair_count") or {}).get("achieved"):

@@ -1,0 +1,371 @@
+// BPE encoder on gfx950 (C ABI include/shredword_encode.h).
+//
+// Applies a trained merge list to text.  The replay the trainer performs (merge m over every word
+// left to right, reference bpe.cpp:265-296, for m = 0, 1, ...) equals, per word, "merge the
+// leftmost adjacent pair of lowest rank until no pair has a rank": a pair created by merge m
+// involves the new id 256 + m, so its rank is > m, and no earlier rank can reappear.  The
+// kernels therefore encode every word independently:
+//
+//   k_encode_words  one thread per 32-byte span takes the words that START in it (maximal runs
+//                   outside "\t\r\n ", found with a 32-bit delimiter mask of the span), maps
+//                   bytes through the byte map, and runs the lowest-rank loop on a per-thread
+//                   LDS strip of tokens and cached pair ranks (words <= 32 bytes), or in global
+//                   scratch (longer words, <= kEncMaxWord).  Pair ranks come from a read-only
+//                   open-addressing table of u64 slots (L2-resident: 16 K slots = 128 KB for
+//                   8 K merges).  A thread packs its words' ids at its first word start, so the
+//                   spans of different threads never overlap; per-thread and per-block counts.
+//   k_encode_scan   one workgroup scans the block counts (exclusive, in place) and the total.
+//   k_encode_emit   one workgroup per block copies its threads' runs to the output in text
+//                   order: each output slot finds its thread by binary search over the block's
+//                   inclusive scan, so the stores are coalesced.
+// Traffic per text byte: 1 B read + 4 B x (ids / byte) x 3 (pack write, emit read, emit write)
+// + 0.125 B of counts; algorithmic: 1 B + 4 B x ids / byte.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../host/encoder.h"
+
+namespace shred {
+namespace {
+
+typedef uint64_t u64;
+
+constexpr int kThreads = 128;              // threads per workgroup
+constexpr int kSpan = 32;                  // bytes whose word starts one thread owns
+constexpr int kChunk = kThreads * kSpan;   // bytes per workgroup
+constexpr int kStrip = 32;                 // tokens a word keeps in LDS (32 KB per workgroup)
+constexpr int kInf = 0x7fffffff;
+constexpr int kScanThreads = 1024;
+
+__device__ __forceinline__ uint32_t is_delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }
+
+__device__ __forceinline__ int pair_rank(const u64* __restrict__ tab, u64 mask, int a, int b) {
+  if ((uint32_t)a >= (uint32_t)kEncIdLimit || (uint32_t)b >= (uint32_t)kEncIdLimit) return kInf;
+  const u64 key = (u64)(uint32_t)a << 20 | (u64)(uint32_t)b;
+  for (u64 i = ((key * 0x9E3779B97F4A7C15ull) >> 24) & mask;; i = (i + 1) & mask) {
+    const u64 e = tab[i];
+    if (e == kEncEmpty) return kInf;
+    if ((e >> 20) == key) return (int)(e & 0xFFFFFu);
+  }
+}
+
+// Lowest-rank merging of tok[0..m) with cached ranks rk[0..m-1) (LDS strip or global scratch).
+// Returns the final length.
+template <typename Tok>
+__device__ __forceinline__ int merge_word(Tok tok, Tok rk, int m, const u64* __restrict__ tab, u64 mask) {
+  for (int j = 0; j + 1 < m; ++j) rk(j) = pair_rank(tab, mask, tok(j), tok(j + 1));
+  while (m > 1) {
+    int best = kInf, p = -1;
+    for (int j = 0; j + 1 < m; ++j) {
+      const int r = rk(j);
+      if (r < best) { best = r; p = j; }
+    }
+    if (best == kInf) break;
+    tok(p) = 256 + best;
+    for (int j = p + 1; j + 1 < m; ++j) tok(j) = tok(j + 1);
+    for (int j = p + 1; j + 2 < m; ++j) rk(j) = rk(j + 1);
+    --m;
+    if (p > 0) rk(p - 1) = pair_rank(tab, mask, tok(p - 1), tok(p));
+    if (p + 1 < m) rk(p) = pair_rank(tab, mask, tok(p), tok(p + 1));
+  }
+  return m;
+}
+
+struct LdsRef {
+  int* base;
+  __device__ __forceinline__ int& operator()(int j) const { return base[j * kThreads]; }
+};
+struct GlobalRef {
+  int* base;
+  __device__ __forceinline__ int& operator()(int j) const { return base[j]; }
+};
+
+template <bool kAligned>
+__global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __restrict__ text, u64 n,
+                                                           const int32_t* __restrict__ byte_map,
+                                                           const u64* __restrict__ tab, u64 mask,
+                                                           int32_t* __restrict__ pad, int32_t* __restrict__ rank,
+                                                           uint32_t* __restrict__ tcnt, u64* __restrict__ bcnt,
+                                                           u64* __restrict__ misc) {
+  __shared__ int s_map[256];
+  __shared__ int s_tok[kStrip * kThreads];
+  __shared__ int s_rk[kStrip * kThreads];
+  __shared__ uint32_t s_sum;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 256; i += kThreads) s_map[i] = byte_map[i];
+  if (tid == 0) s_sum = 0;
+  __syncthreads();
+
+  const u64 base = (u64)blockIdx.x * kChunk + (u64)tid * kSpan;
+  uint32_t cnt = 0, j0 = 0;
+  if (base < n) {
+    const u64 lim = n - base < (u64)kSpan ? n - base : (u64)kSpan;
+    uint32_t dm = 0;  // bit k: byte base + k is a delimiter (or past the end)
+    if (kAligned && lim == (u64)kSpan) {
+      const uint4* p = reinterpret_cast<const uint4*>(text + base);
+      const uint4 v0 = p[0], v1 = p[1];
+      const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int k = 0; k < kSpan; ++k) dm |= is_delim((w[k >> 2] >> (8 * (k & 3))) & 255u) << k;
+    } else {
+      for (int k = 0; k < kSpan; ++k) dm |= ((u64)k < lim ? is_delim(text[base + k]) : 1u) << k;
+    }
+    const uint32_t prevd = base == 0 ? 1u : is_delim(text[base - 1]);
+    uint32_t starts = ~dm & ((dm << 1) | prevd);
+    if (starts) j0 = __ffs(starts) - 1;
+    u64 wpos = base + j0;
+    LdsRef tok{s_tok + tid}, rk{s_rk + tid};
+    while (starts) {
+      const int j = __ffs(starts) - 1;
+      starts &= starts - 1;
+      const u64 s = base + j;
+      const uint32_t above = dm >> j;  // bit 0 is clear: s starts a word
+      u64 L;
+      if (above) {
+        L = __ffs(above) - 1;
+      } else {  // runs past the span
+        u64 e = base + kSpan;
+        while (e < n && e - s <= (u64)kEncMaxWord && !is_delim(text[e])) ++e;
+        L = e - s;
+      }
+      if (L > (u64)kEncMaxWord) {
+        atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), 1ull);
+        continue;
+      }
+      int m;
+      if (L <= (u64)kStrip) {
+        for (int k = 0; k < (int)L; ++k) tok(k) = s_map[text[s + k]];
+        m = merge_word(tok, rk, (int)L, tab, mask);
+        for (int k = 0; k < m; ++k) pad[wpos + k] = tok(k);
+      } else {
+        GlobalRef gt{pad + s}, gr{rank + s};
+        for (int k = 0; k < (int)L; ++k) gt(k) = s_map[text[s + k]];
+        m = merge_word(gt, gr, (int)L, tab, mask);
+        for (int k = 0; k < m; ++k) pad[wpos + k] = gt(k);  // wpos <= s: ascending copy is safe
+      }
+      wpos += m;
+      cnt += m;
+    }
+  }
+  tcnt[(u64)blockIdx.x * kThreads + tid] = cnt << 5 | j0;
+  if (cnt) atomicAdd(&s_sum, cnt);
+  __syncthreads();
+  if (tid == 0) bcnt[blockIdx.x] = s_sum;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_encode_scan(u64* __restrict__ bcnt, u64 nb, u64* __restrict__ misc) {
+  __shared__ u64 s[kScanThreads];
+  const int tid = threadIdx.x;
+  const u64 per = (nb + kScanThreads - 1) / kScanThreads;
+  const u64 lo = (u64)tid * per, hi = lo + per < nb ? lo + per : nb;
+  u64 sum = 0;
+  for (u64 i = lo; i < hi; ++i) sum += bcnt[i];
+  s[tid] = sum;
+  __syncthreads();
+  for (int d = 1; d < kScanThreads; d <<= 1) {
+    const u64 v = tid >= d ? s[tid - d] : 0;
+    __syncthreads();
+    s[tid] += v;
+    __syncthreads();
+  }
+  u64 run = s[tid] - sum;  // exclusive
+  for (u64 i = lo; i < hi; ++i) {
+    const u64 v = bcnt[i];
+    bcnt[i] = run;
+    run += v;
+  }
+  if (tid == kScanThreads - 1) misc[0] = s[tid];
+}
+
+__global__ __launch_bounds__(kThreads) void k_encode_emit(const int32_t* __restrict__ pad, const uint32_t* __restrict__ tcnt,
+                                                          const u64* __restrict__ bcnt, int32_t* __restrict__ out) {
+  __shared__ uint32_t s_inc[kThreads];
+  __shared__ uint32_t s_src[kThreads];  // pad offset of each thread's run, relative to the block
+  const int tid = threadIdx.x;
+  const uint32_t t = tcnt[(u64)blockIdx.x * kThreads + tid];
+  const uint32_t cnt = t >> 5;
+  s_inc[tid] = cnt;
+  s_src[tid] = (uint32_t)tid * kSpan + (t & 31u);
+  __syncthreads();
+  for (int d = 1; d < kThreads; d <<= 1) {
+    const uint32_t v = tid >= d ? s_inc[tid - d] : 0;
+    __syncthreads();
+    s_inc[tid] += v;
+    __syncthreads();
+  }
+  const uint32_t total = s_inc[kThreads - 1];
+  const u64 base = (u64)blockIdx.x * kChunk;
+  int32_t* dst = out + bcnt[blockIdx.x];
+  for (uint32_t i = tid; i < total; i += kThreads) {
+    int lo = 0, hi = kThreads - 1;  // first thread whose inclusive count exceeds i
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_inc[mid] > i) hi = mid; else lo = mid + 1;
+    }
+    const uint32_t excl = s_inc[lo] - (tcnt[(u64)blockIdx.x * kThreads + lo] >> 5);
+    dst[i] = pad[base + s_src[lo] + (i - excl)];
+  }
+}
+
+#define ENC_OK(expr)                                                                            \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) {                                                                     \
+      std::fprintf(stderr, "[ERROR]\t encoder: %s: %s\n", #expr, hipGetErrorString(e_));        \
+      return -1;                                                                                \
+    }                                                                                           \
+  } while (0)
+
+}  // namespace
+
+EncodeDevice* EncodeDevice::create(int device, const std::vector<uint64_t>& table, const int32_t* byte_map,
+                                   std::string* why) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    *why = "no HIP device visible";
+    return nullptr;
+  }
+  if (device < 0 || device >= count) {
+    *why = "device ordinal " + std::to_string(device) + " out of range";
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    *why = "hipSetDevice failed";
+    return nullptr;
+  }
+  EncodeDevice* d = new EncodeDevice();
+  d->device_ = device;
+  d->mask_ = table.size() - 1;
+  hipStream_t st = nullptr;
+  bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+  d->stream_ = st;
+  ok = ok && hipMalloc(&d->table_, table.size() * 8) == hipSuccess;
+  ok = ok && hipMalloc(&d->byte_map_, 256 * 4) == hipSuccess;
+  ok = ok && hipMalloc(&d->misc_, 16) == hipSuccess;
+  ok = ok && hipHostMalloc(&d->host_misc_, 16, hipHostMallocDefault) == hipSuccess;
+  ok = ok && hipMemcpy(d->table_, table.data(), table.size() * 8, hipMemcpyHostToDevice) == hipSuccess;
+  ok = ok && hipMemcpy(d->byte_map_, byte_map, 256 * 4, hipMemcpyHostToDevice) == hipSuccess;
+  for (int i = 0; i < 4 && ok; ++i) {
+    hipEvent_t e;
+    ok = hipEventCreate(&e) == hipSuccess;
+    d->ev_[i] = e;
+  }
+  if (!ok) {
+    *why = "device allocation failed";
+    delete d;
+    return nullptr;
+  }
+  return d;
+}
+
+EncodeDevice::~EncodeDevice() {
+  (void)hipSetDevice(device_);
+  if (stream_) (void)hipStreamSynchronize((hipStream_t)stream_);
+  for (void* p : {(void*)table_, (void*)byte_map_, (void*)misc_, (void*)pad_, (void*)rank_, (void*)tcnt_,
+                  (void*)bcnt_, (void*)dtext_, (void*)dout_})
+    if (p) (void)hipFree(p);
+  if (host_misc_) (void)hipHostFree(host_misc_);
+  for (void* e : ev_)
+    if (e) (void)hipEventDestroy((hipEvent_t)e);
+  if (stream_) (void)hipStreamDestroy((hipStream_t)stream_);
+}
+
+bool EncodeDevice::reserve(size_t n, std::string* why) {
+  if (n <= cap_bytes_) return true;
+  for (void* p : {(void*)pad_, (void*)rank_, (void*)tcnt_, (void*)bcnt_})
+    if (p) (void)hipFree(p);
+  pad_ = rank_ = nullptr;
+  tcnt_ = nullptr;
+  bcnt_ = nullptr;
+  cap_bytes_ = 0;
+  const size_t nb = (n + kChunk - 1) / kChunk, cap = nb * kChunk;  // every later n <= cap fits
+  if (hipMalloc(&pad_, cap * 4) != hipSuccess || hipMalloc(&rank_, cap * 4) != hipSuccess ||
+      hipMalloc(&tcnt_, nb * kThreads * 4) != hipSuccess || hipMalloc(&bcnt_, nb * 8) != hipSuccess) {
+    *why = "scratch allocation failed";
+    return false;
+  }
+  cap_bytes_ = cap;
+  return true;
+}
+
+int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t cap, void* stream, double* kernel_ms) {
+  if (kernel_ms) *kernel_ms = 0;
+  if (n == 0) return 0;
+  if (!text || !out) return -1;
+  ENC_OK(hipSetDevice(device_));
+  std::string why;
+  if (!reserve(n, &why)) {
+    std::fprintf(stderr, "[ERROR]\t encoder: %s (%zu bytes)\n", why.c_str(), n);
+    return -1;
+  }
+  hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)stream_;
+  const u64 nb = (n + kChunk - 1) / kChunk;
+  hipEvent_t* ev = reinterpret_cast<hipEvent_t*>(ev_);
+  ENC_OK(hipMemsetAsync(misc_, 0, 16, st));
+  ENC_OK(hipEventRecord(ev[0], st));
+  if ((reinterpret_cast<uintptr_t>(text) & 15) == 0)
+    k_encode_words<true><<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, pad_, rank_,
+                                                                        tcnt_, bcnt_, misc_);
+  else
+    k_encode_words<false><<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, pad_, rank_,
+                                                                         tcnt_, bcnt_, misc_);
+  ENC_OK(hipGetLastError());
+  k_encode_scan<<<1, kScanThreads, 0, st>>>(bcnt_, nb, misc_);
+  ENC_OK(hipGetLastError());
+  ENC_OK(hipEventRecord(ev[1], st));
+  ENC_OK(hipMemcpyAsync(host_misc_, misc_, 16, hipMemcpyDeviceToHost, st));
+  ENC_OK(hipStreamSynchronize(st));
+  if (host_misc_[1]) return -3;
+  const u64 total = host_misc_[0];
+  if (total > cap) return -2;
+  ENC_OK(hipEventRecord(ev[2], st));
+  if (total) k_encode_emit<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(pad_, tcnt_, bcnt_, out);
+  ENC_OK(hipGetLastError());
+  ENC_OK(hipEventRecord(ev[3], st));
+  ENC_OK(hipStreamSynchronize(st));
+  if (kernel_ms) {
+    float a = 0, b = 0;
+    ENC_OK(hipEventElapsedTime(&a, ev[0], ev[1]));
+    ENC_OK(hipEventElapsedTime(&b, ev[2], ev[3]));
+    *kernel_ms = (double)a + (double)b;
+  }
+  return (int64_t)total;
+}
+
+bool EncodeDevice::reserve_host(size_t n) {
+  if (n <= host_cap_) return true;
+  if (dtext_) (void)hipFree(dtext_);
+  if (dout_) (void)hipFree(dout_);
+  dtext_ = nullptr;
+  dout_ = nullptr;
+  host_cap_ = 0;
+  if (hipMalloc(&dtext_, n) != hipSuccess || hipMalloc(&dout_, n * 4) != hipSuccess) return false;
+  host_cap_ = n;
+  return true;
+}
+
+int64_t EncodeDevice::encode_host(const uint8_t* text, size_t n, int32_t* out, size_t cap) {
+  if (n == 0) return 0;
+  if (!text || !out) return -1;
+  ENC_OK(hipSetDevice(device_));
+  if (!reserve_host(n)) {
+    std::fprintf(stderr, "[ERROR]\t encoder: staging allocation failed (%zu bytes)\n", n);
+    return -1;
+  }
+  hipStream_t st = (hipStream_t)stream_;
+  ENC_OK(hipMemcpyAsync(dtext_, text, n, hipMemcpyHostToDevice, st));
+  const int64_t r = encode(dtext_, n, dout_, cap, nullptr, nullptr);
+  if (r > 0) {
+    ENC_OK(hipMemcpyAsync(out, dout_, (size_t)r * 4, hipMemcpyDeviceToHost, st));
+    ENC_OK(hipStreamSynchronize(st));
+  }
+  return r;
+}
+
+}  // namespace shred

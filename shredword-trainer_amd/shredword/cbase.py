@@ -35,6 +35,26 @@ def _get_lib_path():
     raise FileNotFoundError(f"Could not find trainer library in {search}. Available files: {available}")
 
 
+def _share_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64.so (SONAME
+    libamdhip64.so.7) and its libraries ask for it by the unversioned name, so a process that loads
+    /opt/rocm's copy first (through libtrainer.so) and imports torch later ends up with two
+    runtimes, and frees their shared state twice at exit.  Loading torch's copy first, by path,
+    makes libtrainer.so's libamdhip64.so.7 and torch's libamdhip64.so resolve to the same object
+    (same SONAME / same file).  Nothing is imported from torch here."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    for d in (spec.submodule_search_locations or []) if spec else []:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            ctypes.CDLL(p, mode=getattr(ctypes, "RTLD_GLOBAL", 0))
+            return
+
+
+_share_hip_runtime()
 _lib_path = _get_lib_path()
 lib = ctypes.CDLL(_lib_path, mode=getattr(ctypes, "RTLD_GLOBAL", 0))
 
@@ -108,3 +128,18 @@ lib.shred_hbm_probe.restype = c_int
 lib.shred_dist_unique_id.argtypes, lib.shred_dist_unique_id.restype = [c_void_p, c_size_t], c_int
 lib.shred_dist_init.argtypes, lib.shred_dist_init.restype = [c_int, c_int, c_void_p, c_size_t, c_int], c_int
 lib.shred_dist_finalize.argtypes, lib.shred_dist_finalize.restype = [], c_int
+
+# encoder (include/shredword_encode.h)
+Encoder = c_void_p
+lib.shred_encoder_create.argtypes = [POINTER(c_int32), c_size_t, POINTER(c_int32), c_int]
+lib.shred_encoder_create.restype = Encoder
+lib.shred_encoder_load.argtypes, lib.shred_encoder_load.restype = [c_char_p, c_char_p, c_int32, c_int], Encoder
+lib.shred_encoder_destroy.argtypes, lib.shred_encoder_destroy.restype = [Encoder], None
+lib.shred_encoder_info.argtypes = [Encoder, POINTER(c_size_t), POINTER(c_int32)]
+lib.shred_encoder_info.restype = c_int
+lib.shred_encode.argtypes = [Encoder, c_void_p, c_size_t, c_void_p, c_size_t]
+lib.shred_encode.restype = c_int64
+lib.shred_encode_device.argtypes = [Encoder, c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, POINTER(c_double)]
+lib.shred_encode_device.restype = c_int64
+lib.shred_decode.argtypes = [Encoder, c_void_p, c_size_t, c_void_p, c_size_t]
+lib.shred_decode.restype = c_int64

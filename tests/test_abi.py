@@ -1,5 +1,5 @@
 """The drop-in boundary without a GPU: libtrainer.so loads, exports every symbol that
-include/shredword_bpe.h declares (the reference's 8 BPE + 13 Unigram symbols bound by
+include/shredword_bpe.h and include/shredword_encode.h declare (the reference's 8 BPE + 13 Unigram symbols bound by
 cbase.py:50-71, plus extensions), keeps the reference BPEConfig layout, and fails loudly — never
 silently on the CPU — when no GPU is present."""
 import ctypes
@@ -11,7 +11,7 @@ import pytest
 
 from conftest import PKG, REPO
 
-HEADER = os.path.join(REPO, "include", "shredword_bpe.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("shredword_bpe.h", "shredword_encode.h")]
 REFERENCE_BPE = ["create_trainer", "bpe_trainer_destroy", "bpe_init", "bpe_count_bigrams", "bpe_load_corpus",
                  "bpe_merge_batch", "bpe_train", "bpe_save"]
 REFERENCE_UNIGRAM = ["trainerCreate", "trainerDestroy", "addTextToTrainer", "preprocessTexts",
@@ -20,7 +20,7 @@ REFERENCE_UNIGRAM = ["trainerCreate", "trainerDestroy", "addTextToTrainer", "pre
 
 
 def declared_functions():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{}]*\)\s*;", text)
     return sorted(set(n for n in names if n not in ("if", "while", "sizeof")))
@@ -98,3 +98,16 @@ def test_cli_usage_and_argument_errors(tmp_path):
     r = subprocess.run([CLI, f"input={tmp_path / 'missing.txt'}", "model_type=bpe", f"output_model={tmp_path}/m",
                         f"output_vocab={tmp_path}/v", "ignored", "unknown_key=1"], capture_output=True, text=True)
     assert r.returncode == 255 and "Failed to load corpus" in r.stderr
+
+
+def test_encoder_without_gpu_fails_loudly(tmp_path):
+    from shredword.cbase import lib
+    from shredword.encoder import BPEEncoder
+    if lib.shred_device_count() > 0:
+        pytest.skip("a GPU is present")
+    model = tmp_path / "m.model"
+    model.write_bytes(b"")
+    with pytest.raises(RuntimeError):
+        BPEEncoder(str(model))
+    with pytest.raises(RuntimeError):
+        BPEEncoder.from_merges([[97, 98, 256]])
