@@ -77,6 +77,36 @@ __device__ __forceinline__ int merge_word(Tok tok, Tok rk, int m, const u64* __r
   return m;
 }
 
+// Packed form for vocabularies below 2^16 ids: LDS entry j = tok_j << 16 | rank of (tok_j, tok_j+1)
+// (0xFFFF: none), one word per position, so a strip takes half the LDS (twice the occupancy) and
+// a shift moves token and rank together.  e points at the thread's column (stride kThreads).
+__device__ __forceinline__ uint32_t rank16(const u64* __restrict__ tab, u64 mask, uint32_t a, uint32_t b) {
+  const int r = pair_rank(tab, mask, (int)a, (int)b);
+  return r == kInf ? 0xFFFFu : (uint32_t)r;
+}
+
+__device__ __forceinline__ int merge_word_packed(uint32_t* e, int m, const u64* __restrict__ tab, u64 mask) {
+#define E(j) e[(j) * kThreads]
+  for (int j = 0; j + 1 < m; ++j) E(j) |= rank16(tab, mask, E(j) >> 16, E(j + 1) >> 16);
+  E(m - 1) |= 0xFFFFu;
+  while (m > 1) {
+    uint32_t best = 0xFFFFu;
+    int p = -1;
+    for (int j = 0; j + 1 < m; ++j) {
+      const uint32_t r = E(j) & 0xFFFFu;
+      if (r < best) { best = r; p = j; }
+    }
+    if (p < 0) break;
+    const uint32_t x = 256u + best;
+    for (int j = p + 1; j + 1 < m; ++j) E(j) = E(j + 1);
+    --m;
+    E(p) = x << 16 | (p + 1 < m ? rank16(tab, mask, x, E(p + 1) >> 16) : 0xFFFFu);
+    if (p > 0) E(p - 1) = (E(p - 1) & 0xFFFF0000u) | rank16(tab, mask, E(p - 1) >> 16, x);
+  }
+#undef E
+  return m;
+}
+
 struct LdsRef {
   int* base;
   __device__ __forceinline__ int& operator()(int j) const { return base[j * kThreads]; }
@@ -86,7 +116,7 @@ struct GlobalRef {
   __device__ __forceinline__ int& operator()(int j) const { return base[j]; }
 };
 
-template <bool kAligned>
+template <bool kAligned, bool kPacked>
 __global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __restrict__ text, u64 n,
                                                            const int32_t* __restrict__ byte_map,
                                                            const u64* __restrict__ tab, u64 mask,
@@ -94,8 +124,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __rest
                                                            uint32_t* __restrict__ tcnt, u64* __restrict__ bcnt,
                                                            u64* __restrict__ misc) {
   __shared__ int s_map[256];
-  __shared__ int s_tok[kStrip * kThreads];
-  __shared__ int s_rk[kStrip * kThreads];
+  __shared__ int s_strip[(kPacked ? 1 : 2) * kStrip * kThreads];
   __shared__ uint32_t s_sum;
   const int tid = threadIdx.x;
   for (int i = tid; i < 256; i += kThreads) s_map[i] = byte_map[i];
@@ -120,7 +149,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __rest
     uint32_t starts = ~dm & ((dm << 1) | prevd);
     if (starts) j0 = __ffs(starts) - 1;
     u64 wpos = base + j0;
-    LdsRef tok{s_tok + tid}, rk{s_rk + tid};
+    LdsRef tok{s_strip + tid}, rk{s_strip + kStrip * kThreads + tid};
     while (starts) {
       const int j = __ffs(starts) - 1;
       starts &= starts - 1;
@@ -140,9 +169,16 @@ __global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __rest
       }
       int m;
       if (L <= (u64)kStrip) {
-        for (int k = 0; k < (int)L; ++k) tok(k) = s_map[text[s + k]];
-        m = merge_word(tok, rk, (int)L, tab, mask);
-        for (int k = 0; k < m; ++k) pad[wpos + k] = tok(k);
+        if (kPacked) {
+          uint32_t* e = reinterpret_cast<uint32_t*>(s_strip) + tid;
+          for (int k = 0; k < (int)L; ++k) e[k * kThreads] = (uint32_t)s_map[text[s + k]] << 16;
+          m = merge_word_packed(e, (int)L, tab, mask);
+          for (int k = 0; k < m; ++k) pad[wpos + k] = (int)(e[k * kThreads] >> 16);
+        } else {
+          for (int k = 0; k < (int)L; ++k) tok(k) = s_map[text[s + k]];
+          m = merge_word(tok, rk, (int)L, tab, mask);
+          for (int k = 0; k < m; ++k) pad[wpos + k] = tok(k);
+        }
       } else {
         GlobalRef gt{pad + s}, gr{rank + s};
         for (int k = 0; k < (int)L; ++k) gt(k) = s_map[text[s + k]];
@@ -242,6 +278,11 @@ EncodeDevice* EncodeDevice::create(int device, const std::vector<uint64_t>& tabl
   EncodeDevice* d = new EncodeDevice();
   d->device_ = device;
   d->mask_ = table.size() - 1;
+  // 16-bit packing needs every id (bytes' symbols and 256 + rank) below 0xFFFF
+  size_t merges = 0;
+  for (uint64_t e : table) merges += e != kEncEmpty;
+  d->packed_ = 256 + merges < 0xFFFFu;
+  for (int b = 0; b < 256; ++b) d->packed_ = d->packed_ && byte_map[b] >= 0 && byte_map[b] < 0xFFFF;
   hipStream_t st = nullptr;
   bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
   d->stream_ = st;
@@ -309,12 +350,11 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
   hipEvent_t* ev = reinterpret_cast<hipEvent_t*>(ev_);
   ENC_OK(hipMemsetAsync(misc_, 0, 16, st));
   ENC_OK(hipEventRecord(ev[0], st));
-  if ((reinterpret_cast<uintptr_t>(text) & 15) == 0)
-    k_encode_words<true><<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, pad_, rank_,
-                                                                        tcnt_, bcnt_, misc_);
-  else
-    k_encode_words<false><<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, pad_, rank_,
-                                                                         tcnt_, bcnt_, misc_);
+  const bool aligned = (reinterpret_cast<uintptr_t>(text) & 15) == 0;
+  auto kern = aligned ? (packed_ ? k_encode_words<true, true> : k_encode_words<true, false>)
+                      : (packed_ ? k_encode_words<false, true> : k_encode_words<false, false>);
+  kern<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, pad_, rank_, tcnt_, bcnt_,
+                                                      misc_);
   ENC_OK(hipGetLastError());
   k_encode_scan<<<1, kScanThreads, 0, st>>>(bcnt_, nb, misc_);
   ENC_OK(hipGetLastError());

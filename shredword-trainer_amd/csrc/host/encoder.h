@@ -43,6 +43,7 @@ class EncodeDevice {
   void* stream_ = nullptr;      // hipStream_t
   uint64_t* table_ = nullptr;
   uint64_t mask_ = 0;
+  bool packed_ = false;         // 16-bit LDS strips (ids < 0xFFFF)
   int32_t* byte_map_ = nullptr;
   // scratch sized for the largest text seen: ids per word span, rank cache of long words,
   // per-thread counts, per-block counts / offsets, total + error word

@@ -36,22 +36,16 @@ def _get_lib_path():
 
 
 def _share_hip_runtime():
-    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64.so (SONAME
-    libamdhip64.so.7) and its libraries ask for it by the unversioned name, so a process that loads
-    /opt/rocm's copy first (through libtrainer.so) and imports torch later ends up with two
-    runtimes, and frees their shared state twice at exit.  Loading torch's copy first, by path,
-    makes libtrainer.so's libamdhip64.so.7 and torch's libamdhip64.so resolve to the same object
-    (same SONAME / same file).  Nothing is imported from torch here."""
-    import importlib.util
+    """One HIP stack per process.  PyTorch-ROCm ships its own HIP/HSA/rocprofiler-register
+    libraries and asks for them by unversioned names; a process whose first HIP call came from
+    libtrainer.so (/opt/rocm's stack) and that imports torch later holds two copies and aborts at
+    exit (measured: even hipGetDeviceCount before `import torch` does it).  Importing torch first,
+    when it is installed, makes libtrainer.so bind to torch's already-loaded runtime (same SONAME),
+    as in bench.py.  torch is plumbing only; nothing here uses it."""
     try:
-        spec = importlib.util.find_spec("torch")
-    except (ImportError, ValueError):
-        return
-    for d in (spec.submodule_search_locations or []) if spec else []:
-        p = os.path.join(d, "lib", "libamdhip64.so")
-        if os.path.exists(p):
-            ctypes.CDLL(p, mode=getattr(ctypes, "RTLD_GLOBAL", 0))
-            return
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 
 
 _share_hip_runtime()
