@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -195,6 +196,165 @@ __global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __rest
   if (tid == 0) bcnt[blockIdx.x] = s_sum;
 }
 
+// ---- word cache: every distinct word is encoded once -------------------------------------
+// A corpus repeats its words (C2: 121 M occurrences of 380 K distinct words), so the default path
+// encodes each distinct word once and copies its ids to every occurrence:
+//   k_cache_insert  per occurrence: 64-bit hash of (bytes, length) into an open-addressing table
+//                   (key, min first offset); a full probe window flags an overflow;
+//   k_cache_encode  per used slot: the lowest-rank loop on the word's first occurrence, ids kept
+//                   at store[first ..);
+//   k_cache_words   per occurrence: find the slot, compare the bytes with the first occurrence
+//                   (a 64-bit collision is flagged, never trusted), copy the ids into the thread's
+//                   packed run — the same per-thread / per-block counts k_encode_emit consumes.
+// An overflow or a collision reruns the call on the direct path (k_encode_words): exact always.
+constexpr int kCacheProbes = 128;
+
+__device__ __forceinline__ u64 word_hash(const uint8_t* __restrict__ p, uint32_t L) {
+  u64 h = 1469598103934665603ull;
+  for (uint32_t k = 0; k < L; ++k) h = (h ^ p[k]) * 1099511628211ull;
+  h ^= (u64)L * 0x9E3779B97F4A7C15ull;
+  // FNV's multiplier barely mixes the middle bits the slot index uses: murmur3's fmix64 does
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 33;
+  return h | 1ull;  // 0 marks an empty slot
+}
+
+// Calls f(s, L) for every word starting in this thread's span (L may exceed kEncMaxWord).
+template <typename F>
+__device__ __forceinline__ void for_each_word(const uint8_t* __restrict__ text, u64 n, u64 base, F f) {
+  if (base >= n) return;
+  const u64 lim = n - base < (u64)kSpan ? n - base : (u64)kSpan;
+  uint32_t dm = 0;
+  for (int k = 0; k < kSpan; ++k) dm |= ((u64)k < lim ? is_delim(text[base + k]) : 1u) << k;
+  const uint32_t prevd = base == 0 ? 1u : is_delim(text[base - 1]);
+  uint32_t starts = ~dm & ((dm << 1) | prevd);
+  while (starts) {
+    const int j = __ffs(starts) - 1;
+    starts &= starts - 1;
+    const u64 s = base + j;
+    const uint32_t above = dm >> j;
+    u64 L;
+    if (above) {
+      L = __ffs(above) - 1;
+    } else {
+      u64 e = base + kSpan;
+      while (e < n && e - s <= (u64)kEncMaxWord && !is_delim(text[e])) ++e;
+      L = e - s;
+    }
+    f(s, L, j);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_cache_insert(const uint8_t* __restrict__ text, u64 n,
+                                                           u64* __restrict__ key, u64* __restrict__ first,
+                                                           u64 cmask, u64* __restrict__ misc) {
+  const u64 base = (u64)blockIdx.x * kChunk + (u64)threadIdx.x * kSpan;
+  for_each_word(text, n, base, [&](u64 s, u64 L, int) {
+    if (L > (u64)kEncMaxWord) {
+      atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), 1ull);
+      return;
+    }
+    const u64 h = word_hash(text + s, (uint32_t)L);
+    u64 i = (h >> 17) & cmask;
+    for (int p = 0; p < kCacheProbes; ++p, i = (i + 1) & cmask) {
+      u64 k = key[i];
+      if (k == 0) {
+        k = atomicCAS(reinterpret_cast<unsigned long long*>(key + i), 0ull, (unsigned long long)h);
+        if (k == 0) k = h;
+      }
+      if (k == h) {
+        // hot words hit one slot from every wave: only an earlier occurrence needs the atomic
+        if (s < __hip_atomic_load(first + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+          atomicMin(reinterpret_cast<unsigned long long*>(first + i), (unsigned long long)s);
+        return;
+      }
+    }
+    atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), 2ull);  // window full
+  });
+}
+
+template <bool kPacked>
+__global__ __launch_bounds__(kThreads) void k_cache_encode(const uint8_t* __restrict__ text, u64 n,
+                                                           const int32_t* __restrict__ byte_map,
+                                                           const u64* __restrict__ tab, u64 mask,
+                                                           const u64* __restrict__ key, const u64* __restrict__ first,
+                                                           uint32_t* __restrict__ nids, u64 cap,
+                                                           int32_t* __restrict__ store, int32_t* __restrict__ rank) {
+  __shared__ int s_map[256];
+  __shared__ int s_strip[(kPacked ? 1 : 2) * kStrip * kThreads];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 256; i += kThreads) s_map[i] = byte_map[i];
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * kThreads + tid;
+  if (i >= cap || key[i] == 0) return;
+  const u64 s = first[i];
+  u64 e = s;
+  while (e < n && !is_delim(text[e])) ++e;  // <= kEncMaxWord (insert checked)
+  const int L = (int)(e - s);
+  int m;
+  if (L <= kStrip) {
+    if (kPacked) {
+      uint32_t* q = reinterpret_cast<uint32_t*>(s_strip) + tid;
+      for (int k = 0; k < L; ++k) q[k * kThreads] = (uint32_t)s_map[text[s + k]] << 16;
+      m = merge_word_packed(q, L, tab, mask);
+      for (int k = 0; k < m; ++k) store[s + k] = (int)(q[k * kThreads] >> 16);
+    } else {
+      LdsRef tok{s_strip + tid}, rk{s_strip + kStrip * kThreads + tid};
+      for (int k = 0; k < L; ++k) tok(k) = s_map[text[s + k]];
+      m = merge_word(tok, rk, L, tab, mask);
+      for (int k = 0; k < m; ++k) store[s + k] = tok(k);
+    }
+  } else {
+    GlobalRef gt{store + s}, gr{rank + s};
+    for (int k = 0; k < L; ++k) gt(k) = s_map[text[s + k]];
+    m = merge_word(gt, gr, L, tab, mask);
+  }
+  nids[i] = (uint32_t)m;
+}
+
+__global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restrict__ text, u64 n,
+                                                          const u64* __restrict__ key, const u64* __restrict__ first,
+                                                          const uint32_t* __restrict__ nids, u64 cmask,
+                                                          const int32_t* __restrict__ store, int32_t* __restrict__ pad,
+                                                          uint32_t* __restrict__ tcnt, u64* __restrict__ bcnt,
+                                                          u64* __restrict__ misc) {
+  __shared__ uint32_t s_sum;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_sum = 0;
+  __syncthreads();
+  const u64 base = (u64)blockIdx.x * kChunk + (u64)tid * kSpan;
+  uint32_t cnt = 0, j0 = 0xFFFFFFFFu;
+  u64 wpos = 0;
+  for_each_word(text, n, base, [&](u64 s, u64 L, int j) {
+    if (j0 == 0xFFFFFFFFu) { j0 = (uint32_t)j; wpos = s; }
+    if (L > (u64)kEncMaxWord) return;  // flagged by k_cache_insert
+    const u64 h = word_hash(text + s, (uint32_t)L);
+    u64 i = (h >> 17) & cmask;
+    int p = 0;
+    for (; p < kCacheProbes && key[i] != h; ++p) i = (i + 1) & cmask;
+    if (p == kCacheProbes) return;  // flagged by k_cache_insert (overflow)
+    const u64 f = first[i];
+    bool same = f + L <= n && (f + L == n || is_delim(text[f + L]));
+    for (u64 k = 0; same && k < L && f != s; ++k) same = text[f + k] == text[s + k];
+    if (!same) {
+      atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), 4ull);  // 64-bit collision
+      return;
+    }
+    const uint32_t m = nids[i];
+    for (uint32_t k = 0; k < m; ++k) pad[wpos + k] = store[f + k];
+    wpos += m;
+    cnt += m;
+  });
+  if (j0 == 0xFFFFFFFFu) j0 = 0;
+  tcnt[(u64)blockIdx.x * kThreads + tid] = cnt << 5 | j0;
+  if (cnt) atomicAdd(&s_sum, cnt);
+  __syncthreads();
+  if (tid == 0) bcnt[blockIdx.x] = s_sum;
+}
+
 __global__ __launch_bounds__(kScanThreads) void k_encode_scan(u64* __restrict__ bcnt, u64 nb, u64* __restrict__ misc) {
   __shared__ u64 s[kScanThreads];
   const int tid = threadIdx.x;
@@ -309,7 +469,7 @@ EncodeDevice::~EncodeDevice() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize((hipStream_t)stream_);
   for (void* p : {(void*)table_, (void*)byte_map_, (void*)misc_, (void*)pad_, (void*)rank_, (void*)tcnt_,
-                  (void*)bcnt_, (void*)dtext_, (void*)dout_})
+                  (void*)bcnt_, (void*)dtext_, (void*)dout_, (void*)ckey_, (void*)cfirst_, (void*)cnids_})
     if (p) (void)hipFree(p);
   if (host_misc_) (void)hipHostFree(host_misc_);
   for (void* e : ev_)
@@ -319,13 +479,22 @@ EncodeDevice::~EncodeDevice() {
 
 bool EncodeDevice::reserve(size_t n, std::string* why) {
   if (n <= cap_bytes_) return true;
-  for (void* p : {(void*)pad_, (void*)rank_, (void*)tcnt_, (void*)bcnt_})
+  for (void* p : {(void*)pad_, (void*)rank_, (void*)tcnt_, (void*)bcnt_, (void*)ckey_, (void*)cfirst_, (void*)cnids_})
     if (p) (void)hipFree(p);
   pad_ = rank_ = nullptr;
+  ckey_ = cfirst_ = nullptr;
+  cnids_ = nullptr;
   tcnt_ = nullptr;
   bcnt_ = nullptr;
   cap_bytes_ = 0;
   const size_t nb = (n + kChunk - 1) / kChunk, cap = nb * kChunk;  // every later n <= cap fits
+  ccap_ = 1 << 20;  // word-cache slots: >= 1 M and >= one per 64 text bytes (overflow -> direct path)
+  while (ccap_ < cap / 64) ccap_ <<= 1;
+  if (hipMalloc(&ckey_, ccap_ * 8) != hipSuccess || hipMalloc(&cfirst_, ccap_ * 8) != hipSuccess ||
+      hipMalloc(&cnids_, ccap_ * 4) != hipSuccess) {
+    *why = "word-cache allocation failed";
+    return false;
+  }
   if (hipMalloc(&pad_, cap * 4) != hipSuccess || hipMalloc(&rank_, cap * 4) != hipSuccess ||
       hipMalloc(&tcnt_, nb * kThreads * 4) != hipSuccess || hipMalloc(&bcnt_, nb * 8) != hipSuccess) {
     *why = "scratch allocation failed";
@@ -348,20 +517,43 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
   hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)stream_;
   const u64 nb = (n + kChunk - 1) / kChunk;
   hipEvent_t* ev = reinterpret_cast<hipEvent_t*>(ev_);
-  ENC_OK(hipMemsetAsync(misc_, 0, 16, st));
+  const char* env = std::getenv("SHREDWORD_ENCODE_CACHE");
+  bool cached = !(env && env[0] == '0');
   ENC_OK(hipEventRecord(ev[0], st));
-  const bool aligned = (reinterpret_cast<uintptr_t>(text) & 15) == 0;
-  auto kern = aligned ? (packed_ ? k_encode_words<true, true> : k_encode_words<true, false>)
-                      : (packed_ ? k_encode_words<false, true> : k_encode_words<false, false>);
-  kern<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, pad_, rank_, tcnt_, bcnt_,
-                                                      misc_);
-  ENC_OK(hipGetLastError());
-  k_encode_scan<<<1, kScanThreads, 0, st>>>(bcnt_, nb, misc_);
-  ENC_OK(hipGetLastError());
+  for (;;) {
+    ENC_OK(hipMemsetAsync(misc_, 0, 16, st));
+    if (cached) {
+      ENC_OK(hipMemsetAsync(ckey_, 0, ccap_ * 8, st));
+      ENC_OK(hipMemsetAsync(cfirst_, 0xFF, ccap_ * 8, st));
+      k_cache_insert<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, ckey_, cfirst_, ccap_ - 1, misc_);
+      ENC_OK(hipGetLastError());
+      auto enck = packed_ ? k_cache_encode<true> : k_cache_encode<false>;
+      enck<<<dim3((unsigned)(ccap_ / kThreads)), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, ckey_,
+                                                                          cfirst_, cnids_, ccap_, rank_, pad_);
+      ENC_OK(hipGetLastError());
+      k_cache_words<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, ckey_, cfirst_, cnids_, ccap_ - 1, rank_,
+                                                                   pad_, tcnt_, bcnt_, misc_);
+    } else {
+      const bool aligned = (reinterpret_cast<uintptr_t>(text) & 15) == 0;
+      auto kern = aligned ? (packed_ ? k_encode_words<true, true> : k_encode_words<true, false>)
+                          : (packed_ ? k_encode_words<false, true> : k_encode_words<false, false>);
+      kern<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, pad_, rank_, tcnt_,
+                                                          bcnt_, misc_);
+    }
+    ENC_OK(hipGetLastError());
+    k_encode_scan<<<1, kScanThreads, 0, st>>>(bcnt_, nb, misc_);
+    ENC_OK(hipGetLastError());
+    ENC_OK(hipMemcpyAsync(host_misc_, misc_, 16, hipMemcpyDeviceToHost, st));
+    ENC_OK(hipStreamSynchronize(st));
+    if (host_misc_[1] & 1) return -3;
+    if (!(host_misc_[1] & 6)) break;
+    cached = false;  // cache overflow or a 64-bit word-hash collision: redo on the direct path
+    if (std::getenv("SHREDWORD_ENCODE_DEBUG"))
+      std::fprintf(stderr, "[DEBUG]\t encoder: word cache %s (%zu slots); direct path\n",
+                   host_misc_[1] & 4 ? "hash collision" : "overflow", ccap_);
+    ++fallbacks_;
+  }
   ENC_OK(hipEventRecord(ev[1], st));
-  ENC_OK(hipMemcpyAsync(host_misc_, misc_, 16, hipMemcpyDeviceToHost, st));
-  ENC_OK(hipStreamSynchronize(st));
-  if (host_misc_[1]) return -3;
   const u64 total = host_misc_[0];
   if (total > cap) return -2;
   ENC_OK(hipEventRecord(ev[2], st));

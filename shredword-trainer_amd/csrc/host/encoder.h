@@ -34,6 +34,8 @@ class EncodeDevice {
   int64_t encode(const uint8_t* text, size_t n, int32_t* out, size_t cap, void* stream, double* kernel_ms);
   // Host buffers: staged through cached device buffers.
   int64_t encode_host(const uint8_t* text, size_t n, int32_t* out, size_t cap);
+  // Calls that fell back from the word cache to the direct path (overflow or hash collision).
+  uint64_t fallbacks() const { return fallbacks_; }
 
  private:
   EncodeDevice() = default;
@@ -52,13 +54,19 @@ class EncodeDevice {
   int32_t* rank_ = nullptr;
   uint32_t* tcnt_ = nullptr;
   uint64_t* bcnt_ = nullptr;
-  uint64_t* misc_ = nullptr;    // [0] total ids, [1] error flags
+  uint64_t* misc_ = nullptr;    // [0] total ids, [1] flags: 1 long word, 2 cache overflow, 4 collision
+  // word cache (one slot per distinct word): 64-bit word hash, first occurrence, id count
+  size_t ccap_ = 0;
+  uint64_t* ckey_ = nullptr;
+  uint64_t* cfirst_ = nullptr;
+  uint32_t* cnids_ = nullptr;
   uint64_t* host_misc_ = nullptr;  // pinned
   // host-path staging
   size_t host_cap_ = 0;
   uint8_t* dtext_ = nullptr;
   int32_t* dout_ = nullptr;
   void* ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t fallbacks_ = 0;
 };
 
 }  // namespace shred

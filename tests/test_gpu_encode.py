@@ -4,6 +4,8 @@
   corpus with the reference's own .model, and id counts equal to the reference's .vocab column;
 * the encoder fed a model the GPU trainer just wrote (train -> save -> encode the training
   corpus -> counts == .vocab), at 32 MB;
+* the word cache (default) and the direct kernel on the same inputs; a cache overflow (more
+  distinct words than slots) reruns exactly on the direct path;
 * edge cases: empty text, delimiters only, no trailing delimiter, word lengths around the LDS
   strip (31/32/33) and the limit (1024 ok, 1025 rejected), random bytes incl. NUL and 0x80-0xFF,
   unaligned device text, a too-small output, the coverage byte map, decode round trips.
@@ -98,7 +100,10 @@ def _random_merges(rng, alphabet, M):
     return np.array(out, dtype=np.int32)
 
 
-def test_edge_cases_against_oracle():
+@pytest.mark.parametrize("cache", ["1", "0"])
+def test_edge_cases_against_oracle(cache, monkeypatch):
+    """Both paths: the word cache (default) and the direct per-occurrence kernel."""
+    monkeypatch.setenv("SHREDWORD_ENCODE_CACHE", cache)
     rng = np.random.default_rng(5)
     alpha = [97, 98, 99, 100]
     merges = _random_merges(rng, alpha, 300)
@@ -133,7 +138,9 @@ def test_edge_cases_against_oracle():
     enc.destroy()
 
 
-def test_unaligned_device_text_and_byte_map():
+@pytest.mark.parametrize("cache", ["1", "0"])
+def test_unaligned_device_text_and_byte_map(cache, monkeypatch):
+    monkeypatch.setenv("SHREDWORD_ENCODE_CACHE", cache)
     import torch
     rng = np.random.default_rng(9)
     alpha = list(range(0x61, 0x6b))
@@ -170,3 +177,16 @@ def test_invalid_models_are_rejected(tmp_path):
     e = BPEEncoder(str(tmp_path / "m.model"))              # identity byte map without a .vocab
     assert e.encode(b"abab ba").tolist() == [256, 256, 98, 97]
     e.destroy()
+
+
+def test_word_cache_overflow_falls_back_exactly():
+    """1.5 M distinct words overflow the 1 M-slot word cache: the call reruns on the direct path."""
+    rng = np.random.default_rng(3)
+    alpha = list(range(0x30, 0x3a))
+    merges = _random_merges(rng, alpha, 300)
+    words = rng.permutation(1_500_000)
+    text = ("\n".join(f"{w:07d}" for w in words) + "\n").encode()
+    enc = _enc_from(merges)
+    want = oracle_encode(merges, None, text)
+    assert np.array_equal(enc.encode(text), want)
+    enc.destroy()
