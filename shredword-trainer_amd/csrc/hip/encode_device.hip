@@ -209,9 +209,37 @@ __global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __rest
 // An overflow or a collision reruns the call on the direct path (k_encode_words): exact always.
 constexpr int kCacheProbes = 128;
 
-__device__ __forceinline__ u64 word_hash(const uint8_t* __restrict__ p, uint32_t L) {
+// The workgroup's chunk of text staged in LDS (coalesced 4-byte loads), with a few bytes before
+// it and kOverhang after: word scans, hashes and compares read LDS, and global memory only for
+// bytes outside the staged window.
+constexpr int kOverhang = 256;
+constexpr int kStageBytes = 4 + kChunk + kOverhang;
+
+struct TextView {
+  const uint8_t* __restrict__ g;
+  const uint8_t* l;  // LDS copy of [lo, hi)
+  u64 lo, hi;
+  __device__ __forceinline__ uint32_t operator[](u64 i) const { return (i >= lo && i < hi) ? l[i - lo] : g[i]; }
+};
+
+__device__ __forceinline__ TextView stage_chunk(const uint8_t* __restrict__ text, u64 n, uint32_t* lds) {
+  const u64 cbase = (u64)blockIdx.x * kChunk;
+  const u64 lo = cbase >= 4 ? cbase - 4 : 0;
+  u64 hi = lo + kStageBytes;
+  if (hi > n) hi = n;
+  const u64 words = (hi - lo) / 4;
+  for (u64 w = threadIdx.x; w < words; w += kThreads) {
+    const uint8_t* p = text + lo + 4 * w;  // lo is 4-aligned; the text base may not be
+    lds[w] = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+  }
+  __syncthreads();
+  return TextView{text, reinterpret_cast<const uint8_t*>(lds), lo, lo + 4 * words};
+}
+
+template <typename T>
+__device__ __forceinline__ u64 word_hash(const T& t, u64 s, uint32_t L) {
   u64 h = 1469598103934665603ull;
-  for (uint32_t k = 0; k < L; ++k) h = (h ^ p[k]) * 1099511628211ull;
+  for (uint32_t k = 0; k < L; ++k) h = (h ^ t[s + k]) * 1099511628211ull;
   h ^= (u64)L * 0x9E3779B97F4A7C15ull;
   // FNV's multiplier barely mixes the middle bits the slot index uses: murmur3's fmix64 does
   h ^= h >> 33;
@@ -223,8 +251,8 @@ __device__ __forceinline__ u64 word_hash(const uint8_t* __restrict__ p, uint32_t
 }
 
 // Calls f(s, L) for every word starting in this thread's span (L may exceed kEncMaxWord).
-template <typename F>
-__device__ __forceinline__ void for_each_word(const uint8_t* __restrict__ text, u64 n, u64 base, F f) {
+template <typename T, typename F>
+__device__ __forceinline__ void for_each_word(const T& text, u64 n, u64 base, F f) {
   if (base >= n) return;
   const u64 lim = n - base < (u64)kSpan ? n - base : (u64)kSpan;
   uint32_t dm = 0;
@@ -251,13 +279,15 @@ __device__ __forceinline__ void for_each_word(const uint8_t* __restrict__ text, 
 __global__ __launch_bounds__(kThreads) void k_cache_insert(const uint8_t* __restrict__ text, u64 n,
                                                            u64* __restrict__ key, u64* __restrict__ first,
                                                            u64 cmask, u64* __restrict__ misc) {
+  __shared__ uint32_t s_text[kStageBytes / 4];
+  const TextView tv = stage_chunk(text, n, s_text);
   const u64 base = (u64)blockIdx.x * kChunk + (u64)threadIdx.x * kSpan;
-  for_each_word(text, n, base, [&](u64 s, u64 L, int) {
+  for_each_word(tv, n, base, [&](u64 s, u64 L, int) {
     if (L > (u64)kEncMaxWord) {
       atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), 1ull);
       return;
     }
-    const u64 h = word_hash(text + s, (uint32_t)L);
+    const u64 h = word_hash(tv, s, (uint32_t)L);
     u64 i = (h >> 17) & cmask;
     for (int p = 0; p < kCacheProbes; ++p, i = (i + 1) & cmask) {
       u64 k = key[i];
@@ -322,23 +352,28 @@ __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restr
                                                           uint32_t* __restrict__ tcnt, u64* __restrict__ bcnt,
                                                           u64* __restrict__ misc) {
   __shared__ uint32_t s_sum;
+  __shared__ uint32_t s_text[kStageBytes / 4];
   const int tid = threadIdx.x;
   if (tid == 0) s_sum = 0;
-  __syncthreads();
+  const TextView tv = stage_chunk(text, n, s_text);  // synchronises
   const u64 base = (u64)blockIdx.x * kChunk + (u64)tid * kSpan;
   uint32_t cnt = 0, j0 = 0xFFFFFFFFu;
   u64 wpos = 0;
-  for_each_word(text, n, base, [&](u64 s, u64 L, int j) {
+  for_each_word(tv, n, base, [&](u64 s, u64 L, int j) {
     if (j0 == 0xFFFFFFFFu) { j0 = (uint32_t)j; wpos = s; }
     if (L > (u64)kEncMaxWord) return;  // flagged by k_cache_insert
-    const u64 h = word_hash(text + s, (uint32_t)L);
+    const u64 h = word_hash(tv, s, (uint32_t)L);
     u64 i = (h >> 17) & cmask;
     int p = 0;
     for (; p < kCacheProbes && key[i] != h; ++p) i = (i + 1) & cmask;
     if (p == kCacheProbes) return;  // flagged by k_cache_insert (overflow)
     const u64 f = first[i];
     bool same = f + L <= n && (f + L == n || is_delim(text[f + L]));
-    for (u64 k = 0; same && k < L && f != s; ++k) same = text[f + k] == text[s + k];
+    if (same && f != s) {  // branch-free compare: the loads are independent and pipeline
+      uint32_t diff = 0;
+      for (u64 k = 0; k < L; ++k) diff |= text[f + k] ^ tv[s + k];
+      same = diff == 0;
+    }
     if (!same) {
       atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), 4ull);  // 64-bit collision
       return;
@@ -488,8 +523,8 @@ bool EncodeDevice::reserve(size_t n, std::string* why) {
   bcnt_ = nullptr;
   cap_bytes_ = 0;
   const size_t nb = (n + kChunk - 1) / kChunk, cap = nb * kChunk;  // every later n <= cap fits
-  ccap_ = 1 << 20;  // word-cache slots: >= 1 M and >= one per 64 text bytes (overflow -> direct path)
-  while (ccap_ < cap / 64) ccap_ <<= 1;
+  ccap_ = 1 << 20;  // word-cache slots: >= 1 M and >= one per 256 text bytes (overflow -> direct path)
+  while (ccap_ < cap / 256) ccap_ <<= 1;
   if (hipMalloc(&ckey_, ccap_ * 8) != hipSuccess || hipMalloc(&cfirst_, ccap_ * 8) != hipSuccess ||
       hipMalloc(&cnids_, ccap_ * 4) != hipSuccess) {
     *why = "word-cache allocation failed";
