@@ -102,6 +102,39 @@ def cpu_baseline(cfg, path, seconds):
     }
 
 
+def encode_cpu_baseline(model, vocab, unk, path, sample_bytes=200_000_000):
+    """The encoder's CPU port (oracle/encode_oracle.c: the literal merge replay with a per-word
+    cache) on one core over the first `sample_bytes` of the corpus (cut at a newline), with the
+    same byte map the GPU encoder derives; checks that the ids equal the GPU encoder's."""
+    import ctypes
+    import numpy as np
+    from shredword.encoder import BPEEncoder
+    lib_path = os.path.join(REPO, "oracle", "_build", "libbpe_oracle.so")
+    if not os.path.exists(lib_path):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "port"], check=True)
+    lib = ctypes.CDLL(lib_path)
+    lib.or_encode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                              ctypes.c_void_p, ctypes.c_size_t]
+    lib.or_encode.restype = ctypes.c_int64
+    with open(path, "rb") as f:
+        text = f.read(sample_bytes)
+    text = text[:text.rfind(b"\n") + 1] or text
+    merges = np.fromfile(model, dtype=np.int32).reshape(-1, 3).copy()
+    enc = BPEEncoder(model, vocab, unk_id=unk)
+    bm = enc.byte_map
+    gpu_ids = enc.encode(text)
+    enc.destroy()
+    buf = np.frombuffer(text, dtype=np.uint8)
+    out = np.empty(len(text), dtype=np.int32)
+    t0 = time.perf_counter()
+    r = lib.or_encode(merges.ctypes.data, merges.shape[0], bm.ctypes.data, buf.ctypes.data, len(text),
+                      out.ctypes.data, out.size)
+    dt = time.perf_counter() - t0
+    return {"value": len(text) / dt / 1e9, "unit": "GB/s of text", "cores": 1, "kind": "port",
+            "sample": f"first {len(text)} bytes of the same corpus, oracle/encode_oracle.c (word-cached replay), 1 thread",
+            "ids_equal_gpu": bool(r == gpu_ids.size and np.array_equal(out[:max(r, 0)], gpu_ids))}
+
+
 def calibration_note():
     """The port's speed relative to the reference itself (tests/golden/cpu_calibration.json)."""
     try:
@@ -435,6 +468,13 @@ def main():
                 result["cpu_baseline"] = cpu_baseline(cfg, path, args.cpu_seconds)
             except Exception as e:  # the GPU number stands on its own
                 result["cpu_baseline"] = {"value": None, "error": repr(e)}
+            if isinstance(encode, dict) and "ms" in encode:
+                try:
+                    encode["cpu_baseline"] = encode_cpu_baseline(os.path.join(tmpd, f"bench_r{rank}.model"),
+                                                                 os.path.join(tmpd, f"bench_r{rank}.vocab"),
+                                                                 cfg["unk"], path)
+                except Exception as e:
+                    encode["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(result), flush=True)
     if world > 1:
         sdist.finalize()
