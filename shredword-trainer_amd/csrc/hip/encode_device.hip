@@ -417,12 +417,11 @@ __global__ __launch_bounds__(kScanThreads) void k_encode_scan(u64* __restrict__ 
 __global__ __launch_bounds__(kThreads) void k_encode_emit(const int32_t* __restrict__ pad, const uint32_t* __restrict__ tcnt,
                                                           const u64* __restrict__ bcnt, int32_t* __restrict__ out) {
   __shared__ uint32_t s_inc[kThreads];
-  __shared__ uint32_t s_src[kThreads];  // pad offset of each thread's run, relative to the block
+  __shared__ int s_src[kThreads];  // pad offset of each thread's run (block-relative) minus its exclusive count
   const int tid = threadIdx.x;
   const uint32_t t = tcnt[(u64)blockIdx.x * kThreads + tid];
   const uint32_t cnt = t >> 5;
   s_inc[tid] = cnt;
-  s_src[tid] = (uint32_t)tid * kSpan + (t & 31u);
   __syncthreads();
   for (int d = 1; d < kThreads; d <<= 1) {
     const uint32_t v = tid >= d ? s_inc[tid - d] : 0;
@@ -430,6 +429,8 @@ __global__ __launch_bounds__(kThreads) void k_encode_emit(const int32_t* __restr
     s_inc[tid] += v;
     __syncthreads();
   }
+  s_src[tid] = tid * kSpan + (int)(t & 31u) - (int)(s_inc[tid] - cnt);
+  __syncthreads();
   const uint32_t total = s_inc[kThreads - 1];
   const u64 base = (u64)blockIdx.x * kChunk;
   int32_t* dst = out + bcnt[blockIdx.x];
@@ -439,8 +440,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_emit(const int32_t* __restr
       const int mid = (lo + hi) >> 1;
       if (s_inc[mid] > i) hi = mid; else lo = mid + 1;
     }
-    const uint32_t excl = s_inc[lo] - (tcnt[(u64)blockIdx.x * kThreads + lo] >> 5);
-    dst[i] = pad[base + s_src[lo] + (i - excl)];
+    dst[i] = pad[(int64_t)base + s_src[lo] + (int64_t)i];
   }
 }
 
