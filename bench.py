@@ -226,7 +226,7 @@ def pair_count_leg(cfg, path, reps, device=0, layout="stream", dist=None):
 
 def encode_leg(model, vocab, unk, path, reps, device=0):
     """Encoder: the model this run trained applied to its own HBM-resident corpus
-    (word-cache kernels + k_encode_scan + k_encode_emit, HIP events on the encoder's stream).  Checks
+    (word-cache kernels + hipCUB scan + k_encode_emit, HIP events on the encoder's stream).  Checks
     the size-independent property that the id counts equal the .vocab frequency column."""
     import numpy as np
     import torch
@@ -261,8 +261,8 @@ def encode_leg(model, vocab, unk, path, reps, device=0):
     del text, out
     torch.cuda.empty_cache()
     traffic = sum(pmc_traffic("c2", "types", k) or 0.0 for k in
-                  ("k_cache_insert", "k_cache_encode<true>", "k_cache_words", "k_encode_scan", "k_encode_emit"))
-    return {"kernel": ("k_cache_insert + k_cache_encode + k_cache_words + k_encode_scan + k_encode_emit "
+                  ("k_cache_insert", "k_cache_encode<true>", "k_cache_words", "k_encode_emit"))
+    return {"kernel": ("k_cache_insert + k_cache_encode + k_cache_words + hipCUB scan + k_encode_emit "
                        "(word cache; median of reps, HIP events)"),
             "traffic_bytes": traffic or None,
             "text_bytes": n, "ids": nids, "ms": ms, "text_GBps": n / (ms * 1e-3) / 1e9,

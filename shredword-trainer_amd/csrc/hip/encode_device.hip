@@ -14,13 +14,15 @@
 //                   open-addressing table of u64 slots (L2-resident: 16 K slots = 128 KB for
 //                   8 K merges).  A thread packs its words' ids at its first word start, so the
 //                   spans of different threads never overlap; per-thread and per-block counts.
-//   k_encode_scan   one workgroup scans the block counts (exclusive, in place) and the total.
+//   hipCUB scan     inclusive block sums (the last is the total).
 //   k_encode_emit   one workgroup per block copies its threads' runs to the output in text
 //                   order: each output slot finds its thread by binary search over the block's
 //                   inclusive scan, so the stores are coalesced.
 // Traffic per text byte: 1 B read + 4 B x (ids / byte) x 3 (pack write, emit read, emit write)
 // + 0.125 B of counts; algorithmic: 1 B + 4 B x ids / byte.
 #include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdint>
@@ -42,7 +44,6 @@ constexpr int kSpan = 32;                  // bytes whose word starts one thread
 constexpr int kChunk = kThreads * kSpan;   // bytes per workgroup
 constexpr int kStrip = 32;                 // tokens a word keeps in LDS (32 KB per workgroup)
 constexpr int kInf = 0x7fffffff;
-constexpr int kScanThreads = 1024;
 
 __device__ __forceinline__ uint32_t is_delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }
 
@@ -390,30 +391,6 @@ __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restr
   if (tid == 0) bcnt[blockIdx.x] = s_sum;
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_encode_scan(u64* __restrict__ bcnt, u64 nb, u64* __restrict__ misc) {
-  __shared__ u64 s[kScanThreads];
-  const int tid = threadIdx.x;
-  const u64 per = (nb + kScanThreads - 1) / kScanThreads;
-  const u64 lo = (u64)tid * per, hi = lo + per < nb ? lo + per : nb;
-  u64 sum = 0;
-  for (u64 i = lo; i < hi; ++i) sum += bcnt[i];
-  s[tid] = sum;
-  __syncthreads();
-  for (int d = 1; d < kScanThreads; d <<= 1) {
-    const u64 v = tid >= d ? s[tid - d] : 0;
-    __syncthreads();
-    s[tid] += v;
-    __syncthreads();
-  }
-  u64 run = s[tid] - sum;  // exclusive
-  for (u64 i = lo; i < hi; ++i) {
-    const u64 v = bcnt[i];
-    bcnt[i] = run;
-    run += v;
-  }
-  if (tid == kScanThreads - 1) misc[0] = s[tid];
-}
-
 __global__ __launch_bounds__(kThreads) void k_encode_emit(const int32_t* __restrict__ pad, const uint32_t* __restrict__ tcnt,
                                                           const u64* __restrict__ bcnt, int32_t* __restrict__ out) {
   __shared__ uint32_t s_inc[kThreads];
@@ -433,7 +410,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_emit(const int32_t* __restr
   __syncthreads();
   const uint32_t total = s_inc[kThreads - 1];
   const u64 base = (u64)blockIdx.x * kChunk;
-  int32_t* dst = out + bcnt[blockIdx.x];
+  int32_t* dst = out + (bcnt[blockIdx.x] - total);  // bcnt: inclusive block sums
   for (uint32_t i = tid; i < total; i += kThreads) {
     int lo = 0, hi = kThreads - 1;  // first thread whose inclusive count exceeds i
     while (lo < hi) {
@@ -504,7 +481,7 @@ EncodeDevice::~EncodeDevice() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize((hipStream_t)stream_);
   for (void* p : {(void*)table_, (void*)byte_map_, (void*)misc_, (void*)pad_, (void*)rank_, (void*)tcnt_,
-                  (void*)bcnt_, (void*)dtext_, (void*)dout_, (void*)ckey_, (void*)cfirst_, (void*)cnids_})
+                  (void*)bcnt_, (void*)dtext_, (void*)dout_, (void*)ckey_, (void*)cfirst_, (void*)cnids_, scan_tmp_})
     if (p) (void)hipFree(p);
   if (host_misc_) (void)hipHostFree(host_misc_);
   for (void* e : ev_)
@@ -514,8 +491,10 @@ EncodeDevice::~EncodeDevice() {
 
 bool EncodeDevice::reserve(size_t n, std::string* why) {
   if (n <= cap_bytes_) return true;
-  for (void* p : {(void*)pad_, (void*)rank_, (void*)tcnt_, (void*)bcnt_, (void*)ckey_, (void*)cfirst_, (void*)cnids_})
+  for (void* p : {(void*)pad_, (void*)rank_, (void*)tcnt_, (void*)bcnt_, (void*)ckey_, (void*)cfirst_, (void*)cnids_,
+                  scan_tmp_})
     if (p) (void)hipFree(p);
+  scan_tmp_ = nullptr;
   pad_ = rank_ = nullptr;
   ckey_ = cfirst_ = nullptr;
   cnids_ = nullptr;
@@ -531,7 +510,9 @@ bool EncodeDevice::reserve(size_t n, std::string* why) {
     return false;
   }
   if (hipMalloc(&pad_, cap * 4) != hipSuccess || hipMalloc(&rank_, cap * 4) != hipSuccess ||
-      hipMalloc(&tcnt_, nb * kThreads * 4) != hipSuccess || hipMalloc(&bcnt_, nb * 8) != hipSuccess) {
+      hipMalloc(&tcnt_, nb * kThreads * 4) != hipSuccess || hipMalloc(&bcnt_, 2 * nb * 8) != hipSuccess ||
+      hipcub::DeviceScan::InclusiveSum(nullptr, scan_tmp_bytes_, bcnt_, bcnt_ + nb, (int)nb) != hipSuccess ||
+      hipMalloc(&scan_tmp_, scan_tmp_bytes_ ? scan_tmp_bytes_ : 16) != hipSuccess) {
     *why = "scratch allocation failed";
     return false;
   }
@@ -576,8 +557,9 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
                                                           bcnt_, misc_);
     }
     ENC_OK(hipGetLastError());
-    k_encode_scan<<<1, kScanThreads, 0, st>>>(bcnt_, nb, misc_);
-    ENC_OK(hipGetLastError());
+    // inclusive block sums into bcnt_[nb, 2 nb); the last one is the total
+    ENC_OK(hipcub::DeviceScan::InclusiveSum(scan_tmp_, scan_tmp_bytes_, bcnt_, bcnt_ + nb, (int)nb, st));
+    ENC_OK(hipMemcpyAsync(misc_, bcnt_ + 2 * nb - 1, 8, hipMemcpyDeviceToDevice, st));
     ENC_OK(hipMemcpyAsync(host_misc_, misc_, 16, hipMemcpyDeviceToHost, st));
     ENC_OK(hipStreamSynchronize(st));
     if (host_misc_[1] & 1) return -3;
@@ -592,7 +574,7 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
   const u64 total = host_misc_[0];
   if (total > cap) return -2;
   ENC_OK(hipEventRecord(ev[2], st));
-  if (total) k_encode_emit<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(pad_, tcnt_, bcnt_, out);
+  if (total) k_encode_emit<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(pad_, tcnt_, bcnt_ + nb, out);
   ENC_OK(hipGetLastError());
   ENC_OK(hipEventRecord(ev[3], st));
   ENC_OK(hipStreamSynchronize(st));

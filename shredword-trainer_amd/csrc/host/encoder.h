@@ -53,7 +53,9 @@ class EncodeDevice {
   int32_t* pad_ = nullptr;
   int32_t* rank_ = nullptr;
   uint32_t* tcnt_ = nullptr;
-  uint64_t* bcnt_ = nullptr;
+  uint64_t* bcnt_ = nullptr;    // [0, nb) block counts, [nb, 2 nb) inclusive sums
+  void* scan_tmp_ = nullptr;     // hipCUB scan scratch
+  size_t scan_tmp_bytes_ = 0;
   uint64_t* misc_ = nullptr;    // [0] total ids, [1] flags: 1 long word, 2 cache overflow, 4 collision
   // word cache (one slot per distinct word): 64-bit word hash, first occurrence, id count
   size_t ccap_ = 0;
