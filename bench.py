@@ -1,19 +1,32 @@
 #!/usr/bin/env python3
-"""Benchmark of the BPE merge path on MI355X (BASELINE.json metric: BPE merges/sec).
+"""Benchmark of the BPE merge path on MI355X (BASELINE.json metric: BPE merges/sec to vocab=32k +
+pair-count HBM GB/s).
 
 A step is one full ``train()`` of the HBM-resident corpus (pair count K1 + heap build + every
 merge to the target vocab or heap exhaustion), preceded by ``reset()`` which restores the
-unmerged token stream on the device.  The default workload is BASELINE.json configs[1] (C2):
-vocab_size=8192 (min_pair_freq 2000, coverage 0.995, unk 0 = the reference Python defaults) on a
-1 GB synthetic UTF-8 corpus from the committed generator (seed 2).
+unmerged word table on the device.  The default workload is BASELINE.json configs[2] (C3), the
+config the metric is quoted on ("to vocab=32k") and which fits one GPU: vocab_size=32000,
+min_pair_freq=2 (coverage 0.995, unk 0 = the reference Python defaults) on a 10 GB synthetic
+UTF-8 corpus from the committed generator (seed 3).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--layout types|stream]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|...] [--layout types|stream]
 
-N > 1 runs under torch.distributed.run, one process per GPU: the word table is sharded by
-contiguous word ranges and each merge all-gathers the ranks' compacted neighbour-delta records
-over RCCL.  Every rank performs the same merges, so ``value`` = merges / max-over-ranks time
-(fixed corpus: strong scaling).  The K1 leg (``pair_count``) runs on every rank over its shard of
-the stream layout and reports aggregate HBM GB/s.  Rank 0 prints one JSON line.
+Legs beside the timed steps (all on the same corpus):
+* ``roofline``: K1 ``k_pair_hist`` over the corpus in the stream layout (every occurrence as
+  int32 tokens, the north star's flat token array; 4 B/token + 12 B/tile), HIP events on the
+  trainer stream, against the 8 TB/s HBM peak; ``traffic`` from the committed PMC passes.
+* ``merge_loop``: the dominant kernel of the timed step (the persistent merge loop), which is
+  bound by the per-merge round trip, not by bandwidth: µs per merge, device dispatch -> flag.
+* ``cpu_baseline``: oracle/bpe_oracle (the reference-faithful CPU restatement) on one host core,
+  run concurrently with the GPU legs on another core, train() capped at --cpu-seconds and
+  extrapolated to the full run along the measured cost curve committed in
+  tests/golden/fullsize/<config>/case.json.
+
+N > 1 runs under torch.distributed.run, one process per GPU.  Each rank trains its own replica
+of the word table (the merge loop is a serial chain of dependent merges: "replicas only", see
+DESIGN.md §5), so ``value`` = merges per step x ranks / max-over-ranks time and ``scaling`` is
+"weak"; the K1 leg counts every rank's shard of the stream and reports aggregate GB/s.
+Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -65,41 +78,105 @@ def ensure_corpus(cfg, path):
     return time.time() - t0
 
 
-def cpu_baseline(cfg, path, seconds):
-    """The CPU port (oracle/bpe_oracle.c, reference-faithful merge loop) on one host core,
-    bounded to `seconds` of train time on the same corpus and config."""
-    exe = os.path.join(REPO, "oracle", "_build", "bpe_oracle")
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "port"], check=True)
-    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), "shredword_cpu_baseline")
-
-    def pin():
-        try:
-            os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
-        except OSError:
-            pass
-
-    proc = subprocess.run([exe, path, str(cfg["vocab"]), str(cfg["unk"]), repr(cfg["cov"]), str(cfg["mpf"]),
-                           out + ".model", out + ".vocab", "--max-seconds", str(seconds)],
-                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, preexec_fn=pin, check=True)
-    fields = dict(kv.split("=") for kv in proc.stderr.decode().split("TIMING", 1)[1].split())
-    merges, train_s = int(fields["merges"]), float(fields["train"])
-    cpu = "unknown"
+def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {
+    return "unknown"
+
+
+def cpu_baseline_start(cfg, path, seconds):
+    """Starts the CPU port (oracle/bpe_oracle.c: the reference-faithful merge loop, SURVEY.md §8
+    d5) on ONE host core — the last core of this process's affinity set, away from the core
+    the GPU host loop runs on — with train() capped at `seconds`.  It runs while the GPU legs
+    run; cpu_baseline_finish() collects it."""
+    exe = os.path.join(REPO, "oracle", "_build", "bpe_oracle")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "port"], check=True)
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), "shredword_cpu_baseline")
+    cores = sorted(os.sched_getaffinity(0))
+    core = cores[-1]
+
+    def pin():
+        try:
+            os.sched_setaffinity(0, {core})
+        except OSError:
+            pass
+
+    errf = open(out + ".err", "w+b")
+    proc = subprocess.Popen([exe, path, str(cfg["vocab"]), str(cfg["unk"]), repr(cfg["cov"]), str(cfg["mpf"]),
+                             out + ".model", out + ".vocab", "--max-seconds", str(seconds), "--progress", "256"],
+                            stdout=subprocess.DEVNULL, stderr=errf, preexec_fn=pin)
+    return {"proc": proc, "err": errf, "core": core, "seconds": seconds, "t0": time.time()}
+
+
+def fullsize_case(cfg_name):
+    """The committed full-size oracle run of this config (tests/golden/make_fullsize.py)."""
+    try:
+        return json.load(open(os.path.join(REPO, "tests", "golden", "fullsize", cfg_name, "case.json")))
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline_finish(h, cfg_name, target_merges, gpu_merges, timeout=600):
+    """merges/s of the capped CPU run.  When it stopped early, the full train() time is
+    extrapolated along the measured cost curve of the committed full-size run of the same
+    corpus and config (the oracle's cumulative train seconds every 256 merges, measured in the
+    build container): T_full = t_cap(k) x curve(full) / curve(k), k = merges the capped run
+    reached.  The merge loop's per-merge cost falls as the word table shrinks, so this is the
+    reference cost model of SURVEY.md §8 d5 (~c x S_live per merge) taken from measurement."""
+    try:
+        h["proc"].wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        h["proc"].kill()
+        raise
+    h["err"].seek(0)
+    err = h["err"].read().decode()
+    h["err"].close()
+    if h["proc"].returncode != 0 or "TIMING" not in err:
+        raise RuntimeError(f"bpe_oracle failed (rc {h['proc'].returncode}): {err[-300:]}")
+    fields = dict(kv.split("=") for kv in err.split("TIMING", 1)[1].split())
+    merges, train_s, load_s = int(fields["merges"]), float(fields["train"]), float(fields["load"])
+    res = {
         "value": merges / train_s if train_s > 0 else None, "unit": "merges/s", "cores": 1, "kind": "port",
-        "sample": (f"first {merges} merges (train() capped at {seconds:.0f} s, load {float(fields['load']):.1f} s "
-                   f"excluded) of the same corpus/config, oracle/bpe_oracle.c pinned to 1 core of {cpu} "
-                   f"(nproc={os.cpu_count()})"),
+        "sample": (f"train() of the same corpus/config capped at {h['seconds']:.0f} s: {merges} of "
+                   f"{target_merges} merges in {train_s:.1f} s (load {load_s:.1f} s excluded); "
+                   f"oracle/bpe_oracle.c pinned to core {h['core']} of {cpu_model()} (nproc={os.cpu_count()}), "
+                   f"run concurrently with the GPU legs"),
+        "capped_merges": merges, "capped_train_s": train_s, "load_s": load_s,
         "calibration": calibration_note(),
     }
+    case = fullsize_case(cfg_name)
+    if merges < target_merges and case and case.get("oracle", {}).get("progress"):
+        curve = case["oracle"]["progress"]
+        full_m, full_s = case["merges"], case["oracle"]["train_s"]
+        # the container's time to reach `merges`, interpolated on the curve (0 at 0 merges)
+        pts = [(0, 0.0)] + [(m, t) for m, t in curve]
+        at = None
+        for (m0, t0), (m1, t1) in zip(pts, pts[1:]):
+            if m0 <= merges <= m1:
+                at = t0 + (t1 - t0) * (merges - m0) / max(1, m1 - m0)
+                break
+        if at and at > 0:
+            est = train_s * full_s / at
+            res.update({
+                "value": full_m / est, "extrapolated": True,
+                "extrapolated_train_s": est,
+                "sample": res["sample"] + (f"; extrapolated to all {full_m} merges along the measured cost curve of the "
+                                           f"full run (tests/golden/fullsize/{cfg_name}/case.json: {full_s:.0f} s on "
+                                           f"{case['oracle'].get('cpu', 'the build container')}, x{train_s / at:.2f} "
+                                           f"on this host)"),
+            })
+    elif merges < target_merges:
+        res["extrapolated"] = False
+        res["note"] = "capped run, no committed full-run curve for this config: value = merges/s of the capped prefix"
+    if gpu_merges:
+        res["gpu_merges_per_step"] = gpu_merges
+    return res
 
 
 def encode_cpu_baseline(model, vocab, unk, path, sample_bytes=200_000_000):
@@ -291,7 +368,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--layout", default="types", choices=["types", "stream"])
     ap.add_argument("--bytes", type=int, default=0, help="override the corpus size (testing)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
@@ -323,6 +400,12 @@ def main():
     path = corpus_path(cfg, args.config)
     gen_s = ensure_corpus(cfg, path) if local == 0 else 0.0
     barrier()
+    cpu_h = None
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu_h = cpu_baseline_start(cfg, path, args.cpu_seconds)
+        except Exception as e:  # the GPU number stands on its own
+            cpu_h = {"error": repr(e)}
 
     from shredword import dist as sdist
     from shredword.trainer import BPETrainer
@@ -392,6 +475,22 @@ def main():
         k1_ms = st["count_kernel_ms"] / max(1, st["count_launches"])
         k1_bytes = st["count_kernel_bytes"] / max(1, st["count_launches"])
         per_step_merges = merges / max(1, args.steps)
+        merge_loop = {
+            "kernel": ("k_resident (persistent merge loop, K2+K3: match, neighbour deltas, in-place compaction)"
+                       if st["resident_launches"] else "k_merge (per-merge launches, K2+K3)"),
+            "bound": "latency",
+            "us_per_merge": 1e6 * elapsed / max(1, merges),
+            "device_us_per_merge": 1e3 * mk_ms,
+            "dispatch_to_flag_us": st.get("resident_latency_us"),
+            "algorithmic_bytes_per_merge": mk_bytes,
+            "hbm_GBps_equiv": achieved, "frac_of_hbm_peak": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic_per_merge": (res_traffic / max(1.0, per_step_merges) if st["resident_launches"] and res_traffic
+                                  else None if st["resident_launches"] else pmc_traffic(args.config, args.layout)),
+            "note": ("a serial chain of dependent merges: each needs the previous one's exact heap replay on the "
+                     "host, so the bound is the per-merge round trip (host select/apply + device dispatch -> flag), "
+                     "not bandwidth; the HBM fraction is shown for completeness only"),
+            "launches": merges,
+        }
         result = {
             "metric": "BPE merges/sec",
             "value": merges / elapsed,
@@ -413,26 +512,8 @@ def main():
                 "merges_per_step": per_step_merges, "distinct_words": st["num_words"],
                 "symbols": st["num_symbols"], "occurrences": st["num_occurrences"], "tiles": st["num_tiles"],
             },
-            "roofline": {
-                "kernel": ("k_resident (LDS-resident merge loop, K2+K3: per-merge device time from the "
-                           "leader's dispatch to the host flag, s_memrealtime)" if st["resident_launches"]
-                           else "k_merge (signature filter + fused match/delta/compaction, K2+K3)"),
-                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": (res_traffic / max(1.0, per_step_merges) if st["resident_launches"] and res_traffic
-                            else None if st["resident_launches"] else pmc_traffic(args.config, args.layout)),
-                "traffic_source": (PMC_NOTE.replace("per k_merge launch", "per merge (k_resident launch bytes / merges "
-                                                    "per launch: one launch per train())")
-                                   if st["resident_launches"] else PMC_NOTE),
-                "algorithmic_bytes": "4 B x live tokens per merge (SURVEY.md §8 d4, K2)",
-                "note": ("k_resident is one persistent launch per train(); avg_launch_us = its duration (HIP events) / "
-                         "merges, i.e. device wall time per merge; the table is read from LDS, not HBM, so the bound "
-                         "in practice is the per-merge round-trip chain, not HBM bandwidth"
-                         if st["resident_launches"] else None),
-                "dispatch_to_flag_us": st.get("resident_latency_us"),
-                "avg_launch_us": 1e3 * mk_ms, "avg_bytes_per_launch": mk_bytes,
-                "launches_sampled": st["merge_launches"], "launches": merges,
-            },
+            "roofline": None,
+            "merge_loop": merge_loop,
             "pair_count_types": {
                 "kernel": "k_pair_dense (K1 of this train(): types layout, weighted, first touch)",
                 "avg_launch_us": 1e3 * k1_ms, "bytes_per_launch": k1_bytes,
@@ -441,8 +522,6 @@ def main():
             "resident": {"launches": st["resident_launches"], "ms": st["resident_ms"],
                          "note": "k_resident launch durations (HIP events): one persistent launch per train()"},
             "load_s": load_s, "corpus_gen_s": gen_s,
-            "us_per_merge": 1e6 * elapsed / max(1, merges),
-            "merge_kernel_share": (mk_ms * 1e-3 * merges) / elapsed if elapsed > 0 else None,
             "host_breakdown_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
             "init_s_last_step": st["init_seconds"],
             "selector_last_step": {k: st[k] for k in ("heap_pops", "heap_stale_pops", "heap_pushes", "delta_records",
@@ -452,8 +531,29 @@ def main():
             "speculation": {"hits": st["spec_hits"], "misses": st["spec_misses"],
                             "hit_rate": st["spec_hits"] / max(1, st["spec_hits"] + st["spec_misses"])},
         }
+        case = fullsize_case(args.config)
+        if case and not args.bytes:
+            result["config"]["corpus_md5_expected"] = case["corpus_md5"]
+            result["config"]["unique_bytes"] = case["unique_bytes"]
+            # size-independent parity at full size: the bench's own .model/.vocab against the
+            # committed full-run oracle output of this corpus (tests/golden/fullsize/)
+            import hashlib
+            mm = hashlib.md5(open(os.path.join(tmpd, f"bench_r{rank}.model"), "rb").read()).hexdigest()
+            vm = hashlib.md5(open(os.path.join(tmpd, f"bench_r{rank}.vocab"), "rb").read()).hexdigest()
+            result["parity_fullsize"] = {"model_md5_equal": mm == case["model_md5"],
+                                         "vocab_md5_equal": vm == case["vocab_md5"],
+                                         "reference": f"tests/golden/fullsize/{args.config}/case.json"}
         if pair_count is not None:
             result["pair_count"] = pair_count
+            if pair_count.get("achieved"):
+                result["roofline"] = {k: pair_count[k] for k in ("kernel", "bound", "achieved", "peak", "unit", "frac",
+                                                                 "traffic")}
+                result["roofline"]["traffic_unit"] = "HBM bytes per launch (PMC)"
+                result["roofline"]["algorithmic_bytes_per_launch"] = pair_count["bytes_per_launch"]
+                result["roofline"]["avg_launch_us"] = pair_count["avg_launch_us"]
+                result["roofline"]["note"] = ("K1, the pair-count scan the north star sets the HBM-roofline target on; "
+                                              "the timed step's dominant kernel is the latency-bound merge loop "
+                                              "(merge_loop)")
         if encode is not None:
             result["encode"] = encode
         try:
@@ -463,9 +563,11 @@ def main():
                     result["pair_count"]["achieved"] / world / result["hbm_achievable"]["read_GBps"])
         except Exception as e:
             result["hbm_achievable"] = {"error": repr(e)}
-        if world == 1 and not args.no_cpu_baseline:
+        if cpu_h is not None:
             try:
-                result["cpu_baseline"] = cpu_baseline(cfg, path, args.cpu_seconds)
+                if "error" in cpu_h:
+                    raise RuntimeError(cpu_h["error"])
+                result["cpu_baseline"] = cpu_baseline_finish(cpu_h, args.config, cfg["vocab"] - 256, per_step_merges)
             except Exception as e:  # the GPU number stands on its own
                 result["cpu_baseline"] = {"value": None, "error": repr(e)}
             if isinstance(encode, dict) and "ms" in encode:

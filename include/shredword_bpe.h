@@ -128,6 +128,15 @@ typedef struct ShredStats {
   double resident_ms;
   double resident_latency_us;  /* mean per-merge dispatch -> host flag time (device clock) */
   uint64_t load_on_gpu;        /* 1: the last load_corpus counted its words on the device */
+  /* indexed merge loop (k_word_loop, the default for the types layout on one GPU) */
+  uint64_t index_on;           /* 1: merges run through the pair -> words index */
+  uint64_t index_merges, index_undos, index_launches;
+  uint64_t index_candidates;   /* Σ listed words scanned by collected merges */
+  uint64_t index_changed;      /* Σ words a collected merge changed */
+  uint64_t index_occurrences;  /* Σ occurrences merged */
+  double index_ms;             /* Σ k_word_loop launch durations (HIP events) */
+  double index_dev_us;         /* Σ per-merge device time, command seen -> flag (device clock) */
+  double index_wait_us;        /* Σ per-merge host time, post -> flag seen */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

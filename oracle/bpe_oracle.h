@@ -38,6 +38,7 @@ void or_save(const OrTrainer* t, const char* model_path, const char* vocab_path)
 /* Trace file: "M a b freq new_id" per merge (bpe.cpp:260) and
  * "B batch done heap_size top_freq" per batch (bpe.cpp:369).  NULL disables. */
 void or_set_trace(OrTrainer* t, const char* path);
+void or_set_progress(OrTrainer* t, long every);  /* > 0: PROGRESS lines on stderr every `every` merges */
 
 /* Introspection for unit tests. */
 size_t or_num_words(const OrTrainer* t);

@@ -2606,6 +2606,7 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
 #endif
   if (const char* e = std::getenv("SHREDWORD_TILE_SKIP")) skip_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_RESIDENT")) resident_on_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SHREDWORD_INDEX")) index_on_ = std::atoi(e) != 0;
   int nb = 0;  // resident workgroups of k_merge per CU
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_merge<true>), kThreads, 0));
   merge_blocks_per_cu_ = nb > 0 ? nb : 4;
@@ -2673,6 +2674,8 @@ void Device::free_all() {
 Device::~Device() {
   (void)hipSetDevice(ordinal_);
   if (res_running_ && res_posted_.empty()) park();
+  delete wl_;  // ends its launch first
+  wl_ = nullptr;
   (void)hipStreamSynchronize(S(stream_));
   free_resident();
   if (res_mbox_) (void)hipHostFree(res_mbox_);
@@ -2755,8 +2758,62 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
   max_id_seen_ = max_id;
   max_id0_ = max_id;
   uploaded_ = true;
+  words_stale_ = false;
+  wl_pristine_index_ = true;
+  if (wl_ && (layout != Layout::kTypes || exchange_ || !index_on_)) {
+    delete wl_;
+    wl_ = nullptr;
+  }
+  if (layout == Layout::kTypes && !exchange_ && index_on_) {
+    if (!wl_) wl_ = new WordLoop(ordinal_, stream_, unk_);
+    if (!wl_->upload(ts, weight_)) {
+      delete wl_;
+      wl_ = nullptr;
+    }
+  }
   reset_tokens();
   plan_resident(ts);
+}
+
+void Device::set_index(bool on) {
+  park();
+  index_on_ = on;
+}
+
+// The indexed loop's launch ends and the tile stream catches up with its words (the tile
+// kernels — K1, K6, k_merge, downloads — read the tiles).
+void Device::index_sync() {
+  if (!wl_) return;
+  if (wl_->running()) wl_->stop();
+  const WordLoopStats& ws = wl_->stats();
+  if (timing_ && ws.merges > wl_ms_seen_) {  // the launch's wall time is the merge loop's device time
+    times_.merge_launches += ws.merges - wl_ms_seen_;
+    times_.merge_ms += ws.kernel_ms - wl_kms_seen_;
+  }
+  wl_ms_seen_ = ws.merges;
+  wl_kms_seen_ = ws.kernel_ms;
+  if (wl_->tiles_dirty() && ntiles_) {
+    wl_->sync_tiles(tok_, tile_off_, tile_len_);
+    const int grid = (int)std::min<size_t>((ntiles_ + kWaves - 1) / kWaves, (size_t)cu_count_ * 8);
+    k_sig_build<<<grid, kThreads, 0, S(stream_)>>>(tok_, tile_off_, tile_len_, (uint32_t)ntiles_, sig_);
+    HIP_OK(hipGetLastError());
+  }
+}
+
+// A tile-path merge ran after the loop's last merge: the loop takes the tiles' words.
+void Device::index_refresh() {
+  std::vector<int32_t> all(tok_elems_ + 4);
+  TiledStream ts;
+  ts.off.resize(ntiles_);
+  ts.len.resize(ntiles_);
+  HIP_OK(hipMemcpyAsync(all.data(), tok_, all.size() * sizeof(int32_t), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipMemcpyAsync(ts.off.data(), tile_off_, ntiles_ * sizeof(uint64_t), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipMemcpyAsync(ts.len.data(), tile_len_, ntiles_ * sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  ts.tok = std::move(all);
+  if (!wl_->load_current(ts)) fatal("index_refresh: the tile stream no longer matches the word table");
+  words_stale_ = false;
+  wl_pristine_index_ = false;
 }
 
 void Device::reset_tokens() {
@@ -2775,6 +2832,12 @@ void Device::reset_tokens() {
   live_tokens_est_ = live_tokens0_;
   max_id_seen_ = max_id0_;
   index_.reset();
+  if (wl_) {
+    wl_->reset();
+    if (!wl_pristine_index_) wl_->rebuild();
+    wl_pristine_index_ = true;
+    words_stale_ = false;
+  }
 }
 
 uint64_t Device::live_tokens() {
@@ -2986,6 +3049,18 @@ void Device::flush_timing(bool block) {
 void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   HIP_OK(hipSetDevice(ordinal_));
   if (n < 1 || n > kChainMax) fatal("merge_chain: bad chain length");
+  if (n == 1 && index_eligible() && run_count_ == 0 && res_posted_.empty()) {  // the indexed loop
+    if (words_stale_) index_refresh();
+    if (!wl_->in_flight()) wl_->reserve(X0);
+    max_id_seen_ = std::max(max_id_seen_, X0);
+    wl_->post_merge(ab[0], ab[1], X0);
+    return;
+  }
+  if (wl_) {
+    if (wl_->in_flight()) fatal("merge_chain: a tile-path merge while indexed merges are in flight");
+    index_sync();
+    words_stale_ = true;  // the tile path changes the tiles behind the loop's words
+  }
   if (n == 1 && run_count_ == 0 && ntiles_ && resident_eligible() && X0 < (1 << 20)) {  // k_resident (ids: 20 bits)
     if (res_posted_.size() >= (size_t)kResSlots) fatal("merge_chain: every resident slot has a merge in flight");
     const int slot = pick_resident_slot();
@@ -3303,6 +3378,12 @@ void Device::finish_launch(ChainRun& run_) {
 
 size_t Device::collect(int32_t X, const DeltaRecord** recs) {
   HIP_OK(hipSetDevice(ordinal_));
+  if (wl_ && wl_->in_flight()) {
+    const size_t n = wl_->collect(X, recs);
+    records_total_ += n;
+    records_max_ = std::max<uint64_t>(records_max_, n);
+    return n;
+  }
   if (!res_posted_.empty()) return collect_resident(X, recs);
   if (run_count_ == 0) fatal("collect: no launch in flight");
   ChainRun& run = run_at(0);
@@ -3322,6 +3403,11 @@ size_t Device::collect(int32_t X, const DeltaRecord** recs) {
 
 void Device::rollback(int32_t X) {
   HIP_OK(hipSetDevice(ordinal_));
+  if (wl_ && wl_->in_flight()) {
+    wl_->rollback(X);
+    ++rollbacks_;
+    return;
+  }
   if (!res_posted_.empty()) {  // resident: each wrong guess is expanded back where it matched
     while (!res_posted_.empty() && res_posted_.back().X >= X) {
       const ResPost rp = res_posted_.back();
@@ -3596,6 +3682,7 @@ void Device::set_resident(bool on) {
 // the table pointers, so they cannot grow under it).
 void Device::reserve_ids(int32_t max_id) {
   HIP_OK(hipSetDevice(ordinal_));
+  if (index_eligible() && !wl_->in_flight()) wl_->reserve(max_id);
   const uint32_t need = (uint32_t)std::max<int32_t>(max_id, 0) + 2;
   bool grow = false;
   for (const MergeSlot& s : slot_) grow |= !s.dsum || need > s.cap;
@@ -3815,6 +3902,7 @@ void Device::resident_dump(const char* why) {
 }
 
 void Device::park() {
+  index_sync();
   if (!res_running_) return;
   HIP_OK(hipSetDevice(ordinal_));
   if (!res_posted_.empty()) fatal("park: a resident merge was not collected");

@@ -23,6 +23,7 @@
 #include "engine.h"
 #include "selector.h"
 #include "tiles.h"
+#include "word_loop.h"
 
 namespace shred {
 
@@ -81,14 +82,17 @@ class Device : public Backend {
   // K4: merge X's records (host memory); the first collect of a chain waits for the launch.
   size_t collect(int32_t X, const DeltaRecord** recs) override;
   static constexpr int kChainMax = 8;
-  int max_chain() const override { return speculate_ && !resident_eligible() ? kChainMax : 1; }
+  int max_chain() const override {
+    return speculate_ && !resident_eligible() && !index_eligible() ? kChainMax : 1;
+  }
   bool can_overlap() const override {
+    if (index_eligible()) return speculate_;
     return speculate_ && (!resident_eligible() || (uint32_t)max_id_seen_ + 3 < min_slot_cap());
   }
   // k_resident takes up to kResSlots merges in flight (the current one and the guesses behind
   // it); the launch path two launches.
   static constexpr int kResSlots = 4;
-  int overlap_depth() const override { return resident_eligible() ? spec_depth_ : 1; }
+  int overlap_depth() const override { return resident_eligible() || index_eligible() ? spec_depth_ : 1; }
   void set_spec_depth(int d) { spec_depth_ = std::max(1, std::min(d, kResSlots - 1)); }
   uint32_t min_slot_cap() const {
     uint32_t c = UINT32_MAX;
@@ -106,7 +110,12 @@ class Device : public Backend {
   void park();
   void set_resident(bool on);
   bool resident() const { return resident_on_; }
-  bool resident_eligible() const { return resident_on_ && resident_ok_ && !exchange_; }
+  bool resident_eligible() const { return resident_on_ && resident_ok_ && !exchange_ && !index_eligible(); }
+  // The indexed merge loop (word_loop.h): the default for the types layout on one GPU.
+  void set_index(bool on);
+  bool index_on() const { return index_on_; }
+  bool index_eligible() const { return index_on_ && wl_ && wl_->ready() && !exchange_; }
+  const WordLoop* word_loop() const { return wl_; }
   uint64_t resident_launches() const { return res_launches_; }
   bool resident_tokens_in_lds() const { return res_lds_tok_; }
   double resident_ms() const { return res_ms_; }
@@ -139,6 +148,11 @@ class Device : public Backend {
     res_launches_ = 0;
     res_ms_ = res_lat_us_ = 0;
     res_lat_n_ = 0;
+    if (wl_) {
+      wl_->clear_stats();
+      wl_ms_seen_ = 0;
+      wl_kms_seen_ = 0;
+    }
   }
   uint64_t live_tokens();  // Σ tile_len (headers included)
   size_t num_tiles() const { return ntiles_; }
@@ -278,6 +292,16 @@ class Device : public Backend {
   int merge_blocks_per_cu_ = 4;
 
   size_t bytes_alloc_ = 0;
+
+  // ---- the indexed merge loop (word_loop.h)
+  void index_sync();               // ends the loop's launch, brings the tiles up to date
+  void index_refresh();            // words_stale_: rebuild the loop's table from the tiles
+  WordLoop* wl_ = nullptr;
+  bool index_on_ = true;           // option (SHREDWORD_INDEX / set_option index)
+  bool words_stale_ = false;       // a tile-path merge changed the tiles after the words
+  bool wl_pristine_index_ = true;  // the loop's initial index is the uploaded table's
+  uint64_t wl_ms_seen_ = 0;        // merges already folded into times_
+  double wl_kms_seen_ = 0;         // launch time already folded into times_
 
   // ---- k_resident state (bpe_device.hip "K2+K3 resident")
   struct ResPost {          // a merge posted to the resident loop and not yet collected

@@ -40,6 +40,7 @@ struct Trainer {
   bool local_exchange = false;   // test: the multi-GPU exchange over a single-rank communicator
   uint32_t exchange_bucket = 0;  // records per rank and exchange bucket (0: default)
   int resident = -1;             // LDS-resident merge loop: -1 default (on), 0 off, 1 on
+  int index = -1;                // indexed merge loop: -1 default (on), 0 off, 1 on
   int spec_depth = 0;            // resident guesses in flight (0: env SHREDWORD_SPEC_DEPTH or default)
   bool gpu_load = true;          // count the corpus words on the device (types layout)
   double load_s = 0;
@@ -94,6 +95,9 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
   } else if (key == "resident") {
     t->resident = std::atoi(val.c_str()) != 0 ? 1 : 0;
     if (t->dev) t->dev->set_resident(t->resident != 0);
+  } else if (key == "index") {
+    t->index = std::atoi(val.c_str()) != 0 ? 1 : 0;
+    if (t->dev) t->dev->set_index(t->index != 0);
   } else if (key == "spec_depth") {
     const int d = std::atoi(val.c_str());
     if (d < 1 || d > Device::kResSlots - 1) return -1;
@@ -126,6 +130,7 @@ bool ensure_device(Trainer* t, const char* caller) {
     t->dev->set_timing(t->timing);
     t->dev->set_unk(t->config.unk_id);
     if (t->resident >= 0) t->dev->set_resident(t->resident != 0);
+    if (t->index >= 0) t->dev->set_index(t->index != 0);
     t->dev->set_spec_depth(t->spec_depth ? t->spec_depth : env_int("SHREDWORD_SPEC_DEPTH", 1));
     if (dist_active() || t->local_exchange) {
       Device::Exchange x;
@@ -350,6 +355,19 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
     s->resident_launches = t->dev->resident_launches();
     s->resident_ms = t->dev->resident_ms();
     s->resident_latency_us = t->dev->resident_latency_us();
+    if (const WordLoop* wl = t->dev->word_loop()) {
+      const WordLoopStats& w = wl->stats();
+      s->index_on = t->dev->index_eligible() ? 1 : 0;
+      s->index_merges = w.merges;
+      s->index_undos = w.undos;
+      s->index_launches = w.launches;
+      s->index_candidates = w.candidates;
+      s->index_changed = w.changed;
+      s->index_occurrences = w.occurrences;
+      s->index_ms = w.kernel_ms;
+      s->index_dev_us = w.dev_us;
+      s->index_wait_us = w.wait_us;
+    }
   }
   {
     s->load_on_gpu = t->wt.counted_on_gpu ? 1 : 0;

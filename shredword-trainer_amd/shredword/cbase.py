@@ -80,7 +80,11 @@ class ShredStats(Structure):
                 ("exchange_overflows", c_uint64),
                 ("hist_kernel_ms", c_double), ("hist_kernel_bytes", c_double), ("hist_launches", c_uint64),
                 ("resident_launches", c_uint64), ("resident_ms", c_double), ("resident_latency_us", c_double),
-                ("load_on_gpu", c_uint64)]
+                ("load_on_gpu", c_uint64),
+                ("index_on", c_uint64), ("index_merges", c_uint64), ("index_undos", c_uint64),
+                ("index_launches", c_uint64), ("index_candidates", c_uint64), ("index_changed", c_uint64),
+                ("index_occurrences", c_uint64), ("index_ms", c_double), ("index_dev_us", c_double),
+                ("index_wait_us", c_double)]
 
 
 Trainer = c_void_p

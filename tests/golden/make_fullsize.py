@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Full-size parity fixtures for the bench configs.
+
+The reference itself cannot train a 1-10 GB corpus here: its word counter is a fixed 4096-bucket
+chained map (hash.cpp:29-53), O(tokens x W / 4096) — days at C3.  These fixtures therefore come
+from the CPU restatement ``oracle/bpe_oracle`` run to completion, which is pinned to the reference
+by every golden in tests/golden/*/ (tests/test_oracle.py), including the reference's own deep
+31,744- and 63,744-merge runs.  Per config this writes ``tests/golden/fullsize/<name>/``:
+
+* ``case.json``     — generator recipe, corpus md5 + unique-byte count + W + S (SURVEY.md §8 d2
+                      "record W, S, corpus md5 and unique-byte count per config"), the trainer
+                      config, merges, .model/.vocab md5s, oracle load/train seconds;
+* ``model.bin.gz``  — the oracle's .model (so a GPU mismatch names its first differing merge);
+* ``trace.txt.gz``  — "M a b freq new_id" per merge and "B batch completed heap top" per batch.
+
+Corpora are regenerated from the recipe (bin/gen_corpus) and their md5 is checked.  Usage:
+    python tests/golden/make_fullsize.py c2 [c3 ...]       (minutes for c2, ~1 h for c3)
+"""
+from __future__ import annotations
+
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import corpora  # noqa: E402
+
+REPO = corpora.REPO
+ORACLE_EXE = os.path.join(REPO, "oracle", "_build", "bpe_oracle")
+OUT = os.path.join(HERE, "fullsize")
+
+# name: (bytes, seed, script, (vocab, unk, coverage, min_pair_freq)) — bench.py CONFIGS
+CASES = {
+    "c2": (1_000_000_000, 2, "utf8", (8192, 0, 0.995, 2000)),
+    "c3": (10_000_000_000, 3, "utf8", (32000, 0, 0.995, 2)),
+}
+
+
+def corpus_file(name: str, nbytes: int, seed: int, script: str) -> str:
+    d = os.environ.get("SHREDWORD_BENCH_DIR", os.path.join(os.environ.get("TMPDIR", "/tmp"), "shredword_bench"))
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, f"{name}_{script}_{nbytes}_s{seed}.txt")
+    if not (os.path.exists(path) and os.path.getsize(path) == nbytes):
+        corpora.gen_synthetic(path, nbytes, seed, script)
+    return path
+
+
+def corpus_stats(path: str):
+    """md5 and the number of distinct byte values."""
+    import numpy as np
+    h = hashlib.md5()
+    seen = np.zeros(256, dtype=bool)
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 26), b""):
+            h.update(chunk)
+            seen |= np.bincount(np.frombuffer(chunk, dtype=np.uint8), minlength=256) > 0
+    return h.hexdigest(), int(seen.sum())
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def md5_bytes(b: bytes) -> str:
+    return hashlib.md5(b).hexdigest()
+
+
+def make(name: str) -> None:
+    nbytes, seed, script, (vocab, unk, cov, mpf) = CASES[name]
+    path = corpus_file(name, nbytes, seed, script)
+    md5, nbyte = corpus_stats(path)
+    d = os.path.join(OUT, name)
+    os.makedirs(d, exist_ok=True)
+    tmp = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"fullsize_{name}")
+    t0 = time.time()
+    proc = subprocess.run([ORACLE_EXE, path, str(vocab), str(unk), repr(cov), str(mpf), tmp + ".model",
+                           tmp + ".vocab", "--trace", tmp + ".trace", "--progress", "256"],
+                          stderr=subprocess.PIPE, check=True)
+    wall = time.time() - t0
+    err = proc.stderr.decode()
+    fields = dict(kv.split("=") for kv in err.split("TIMING", 1)[1].split())
+    # measured cost curve: cumulative train seconds after every 256 merges (bench.py extrapolates
+    # its capped CPU baseline along this curve)
+    curve = [[int(l.split()[1]), float(l.split()[2])] for l in err.splitlines() if l.startswith("PROGRESS ")]
+    model = open(tmp + ".model", "rb").read()
+    vocabb = open(tmp + ".vocab", "rb").read()
+    with gzip.GzipFile(os.path.join(d, "model.bin.gz"), "wb", mtime=0) as f:
+        f.write(model)
+    with open(tmp + ".trace", "rb") as src, gzip.GzipFile(os.path.join(d, "trace.txt.gz"), "wb", mtime=0) as f:
+        f.write(src.read())
+    case = {
+        "recipe": {"kind": "synthetic", "bytes": nbytes, "seed": seed, "script": script},
+        "corpus_md5": md5, "unique_bytes": nbyte,
+        "distinct_words": int(fields["words"]), "symbols": int(fields["symbols"]),
+        "config": {"vocab_size": vocab, "unk_id": unk, "character_coverage": cov, "min_pair_freq": mpf},
+        "merges": int(fields["merges"]),
+        "model_md5": md5_bytes(model), "vocab_md5": md5_bytes(vocabb), "vocab_bytes": len(vocabb),
+        "oracle": {"exe": "oracle/_build/bpe_oracle", "load_s": float(fields["load"]),
+                   "train_s": float(fields["train"]), "wall_s": wall,
+                   "cpu": cpu_model(), "progress": curve},
+    }
+    with open(os.path.join(d, "case.json"), "w") as f:
+        json.dump(case, f, indent=1)
+        f.write("\n")
+    for ext in (".model", ".vocab", ".trace"):
+        os.unlink(tmp + ext)
+    print(name, json.dumps(case), flush=True)
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or ["c2"]:
+        make(n)

@@ -58,6 +58,16 @@ CASES = {
     "small_v50_zero": ({"kind": "small"}, (50, 0, 0.995, 1000), "api"),
     "small_v256_zero": ({"kind": "small"}, (256, 0, 0.995, 2), "api"),
     "small_cov0_mpf0": ({"kind": "small"}, (400, 0, 0.0, 0), "api"),
+    # deep runs (VERDICT r1 "pin parity at the untested configs"): the C3 vocab/min_pair_freq to the
+    # full 31,744 merges, and vocab 64000 / coverage 0.9995 on a mixed-script corpus with > 4,000
+    # distinct code points, deep (ids past 32,767, all 63,744 merges) and at min_pair_freq 2000
+    # (heap exhaustion).
+    "utf8_24m_v32000_mpf2": ({"kind": "synthetic", "bytes": 24_000_000, "seed": 21, "script": "utf8"},
+                             (32000, 0, 0.995, 2), "api"),
+    "mixed24m_v64000_cov9995_mpf2": ({"kind": "synthetic", "bytes": 24_000_000, "seed": 22, "script": "mixed"},
+                                     (64000, 0, 0.9995, 2), "api"),
+    "mixed24m_v64000_cov9995": ({"kind": "synthetic", "bytes": 24_000_000, "seed": 22, "script": "mixed"},
+                                (64000, 0, 0.9995, 2000), "api"),
     "cli_ascii10m": ({"kind": "synthetic", "bytes": 10_000_000, "seed": 1, "script": "ascii"},
                      (8192, -1, 0.9995, 2000), "cli"),
     "cli_utf8_2m_mpf20": ({"kind": "synthetic", "bytes": 2_000_000, "seed": 18, "script": "utf8"},

@@ -172,17 +172,19 @@ def test_rollback_restores_stream(medium_corpus):
     t.destroy()
 
 
-@pytest.mark.parametrize("layout", ["stream", "types"])
-def test_speculation_lockstep(layout, medium_corpus):
+@pytest.mark.parametrize("layout,index", [("stream", 0), ("types", 0), ("types", 1)])
+def test_speculation_lockstep(layout, index, medium_corpus):
     """Speculative pipelining on vs off, in bpe_merge_batch chunks: identical merges and an
-    identical device token stream after every chunk (rollbacks included)."""
+    identical device token stream after every chunk (rollbacks included).  index=1: the indexed
+    loop (guesses undone by UNMERGE); index=0: the launch path."""
     from shredword.cbase import lib
     ts = []
     for spec in (0, 1):
         t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
         t.set_option("layout", layout)
         t.set_option("speculate", spec)
-        t.set_option("resident", 0)  # speculation belongs to the launch path
+        t.set_option("resident", 0)
+        t.set_option("index", index)
         t.load_corpus(medium_corpus)
         lib.bpe_init(t.trainer)
         ts.append(t)
@@ -216,6 +218,7 @@ def test_resident_lockstep(tokens, depth, medium_corpus, tmp_path, monkeypatch):
     for res in (0, 1):
         t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
         t.set_option("resident", res)
+        t.set_option("index", 0)
         t.set_option("spec_depth", depth)
         t.load_corpus(medium_corpus)
         lib.bpe_init(t.trainer)
@@ -243,6 +246,77 @@ def test_resident_lockstep(tokens, depth, medium_corpus, tmp_path, monkeypatch):
     assert paths[0] == paths[1]
 
 
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_index_lockstep(depth, medium_corpus, tmp_path):
+    """The indexed loop (k_word_loop) against the launch path, in bpe_merge_batch chunks: the
+    same merges and the same device token stream after every chunk (each chunk ends the
+    persistent launch and writes the words back into the tiles), with `depth` guesses in flight."""
+    from shredword.cbase import lib
+    ts = []
+    for idx in (0, 1):
+        t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+        t.set_option("resident", 0)
+        t.set_option("index", idx)
+        t.set_option("spec_depth", depth)
+        t.load_corpus(medium_corpus)
+        lib.bpe_init(t.trainer)
+        ts.append(t)
+    done = 0
+    for chunk in [1, 300, 7, 1000, 64] * 20:
+        na = lib.bpe_merge_batch(ts[0].trainer, chunk)
+        nb = lib.bpe_merge_batch(ts[1].trainer, chunk)
+        assert na == nb
+        xa, xb = ts[0].tokens(), ts[1].tokens()
+        assert xa.shape == xb.shape and (xa == xb).all(), f"streams differ after {done + na} merges"
+        done += na
+        if na < chunk:
+            break
+    assert done > 4000
+    st0, st1 = ts[0].stats(), ts[1].stats()
+    assert st0["index_merges"] == 0 and st1["index_merges"] >= done
+    assert st1["spec_hits"] > 0 and st1["index_undos"] > 0
+    paths = []
+    for i, t in enumerate(ts):
+        m, v = str(tmp_path / f"i{i}.model"), str(tmp_path / f"i{i}.vocab")
+        t.save(m, v)
+        paths.append((open(m, "rb").read(), open(v, "rb").read()))
+        t.destroy()
+    assert paths[0] == paths[1]
+
+
+def test_index_after_tile_path_merges(medium_corpus, tmp_path):
+    """Merges on the tile path (index off) followed by indexed merges (index on) on the same
+    trainer: the loop re-reads the merged tiles and re-indexes them; then reset() returns to the
+    uploaded table and its initial index, and a full retrain matches a fresh trainer."""
+    from shredword.cbase import lib
+    ref = _trainer(vocab_size=3000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+    ref.set_option("index", 0)
+    ref.set_option("resident", 0)
+    ref.load_corpus(medium_corpus)
+    n_ref, model_ref, vocab_ref = _train_bytes(ref, tmp_path, "ref")
+    ref.destroy()
+    t = _trainer(vocab_size=3000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+    t.load_corpus(medium_corpus)
+    lib.bpe_init(t.trainer)
+    t.set_option("index", 0)
+    t.set_option("resident", 0)
+    assert lib.bpe_merge_batch(t.trainer, 500) == 500
+    t.set_option("index", 1)
+    done = 500
+    while done < n_ref:
+        k = lib.bpe_merge_batch(t.trainer, min(777, n_ref - done))
+        assert k > 0
+        done += k
+    m, v = tmp_path / "mix.model", tmp_path / "mix.vocab"
+    t.save(str(m), str(v))
+    assert m.read_bytes() == model_ref and v.read_bytes() == vocab_ref
+    assert t.stats()["index_merges"] >= n_ref - 500
+    t.reset()
+    n2, model2, vocab2 = _train_bytes(t, tmp_path, "again")
+    t.destroy()
+    assert (n2, model2, vocab2) == (n_ref, model_ref, vocab_ref)
+
+
 def _parse_vocab(vocab: bytes, ops):
     """(spelling, freq) per id, walking the file with spellings derived from the merges:
     a spelling may contain any byte (token 10 is a newline), so lines cannot be split blindly."""
@@ -259,6 +333,50 @@ def _parse_vocab(vocab: bytes, ops):
         pos = end + 1
     assert pos == len(vocab)
     return out
+
+
+def _fullsize(name):
+    import gzip
+    import json
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize", name)
+    if not os.path.exists(os.path.join(d, "case.json")):
+        pytest.skip(f"no full-size fixture for {name}")
+    case = json.load(open(os.path.join(d, "case.json")))
+    with gzip.open(os.path.join(d, "model.bin.gz"), "rb") as f:
+        case["model_bytes"] = f.read()
+    with gzip.open(os.path.join(d, "trace.txt.gz"), "rt") as f:
+        case["trace"] = f.read()
+    r = case["recipe"]
+    corpus = os.path.join(os.environ.get("TMPDIR", "/tmp"), "shredword_bench",
+                          f"{name}_{r['script']}_{r['bytes']}_s{r['seed']}.txt")
+    if not (os.path.exists(corpus) and os.path.getsize(corpus) == r["bytes"]):
+        os.makedirs(os.path.dirname(corpus), exist_ok=True)
+        corpora.gen_synthetic(corpus, r["bytes"], r["seed"], r["script"])
+    return case, corpus
+
+
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_full_size_matches_oracle_run(name, tmp_path):
+    """C2 (1 GB, vocab 8192) and C3 (10 GB, vocab 32000, min_pair_freq 2) at full size, bit-exact:
+    .model bytes, .vocab md5 and every merge / batch line against the oracle's full run committed
+    in tests/golden/fullsize/ (the oracle is pinned to the reference by every golden, including
+    the reference's own 31,744- and 63,744-merge runs)."""
+    import hashlib
+    case, corpus = _fullsize(name)
+    cfg = case["config"]
+    t = _trainer(vocab_size=cfg["vocab_size"], unk_id=cfg["unk_id"], character_coverage=cfg["character_coverage"],
+                 min_pair_freq=cfg["min_pair_freq"])
+    trace = str(tmp_path / "trace.txt")
+    t.set_option("trace", trace)
+    t.load_corpus(corpus)
+    n, model, vocab = _train_bytes(t, tmp_path, name)
+    st = t.stats()
+    t.destroy()
+    assert (st["num_words"], st["num_symbols"]) == (case["distinct_words"], case["symbols"])
+    assert n == case["merges"]
+    assert open(trace).read() == case["trace"]
+    assert model == case["model_bytes"]
+    assert hashlib.md5(vocab).hexdigest() == case["vocab_md5"]
 
 
 def test_full_size_c2_invariants(tmp_path):

@@ -11,7 +11,7 @@ from conftest import PKG, golden_cases
 pytestmark = pytest.mark.gpu
 
 
-def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None):
+def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None, index=1, spec_depth=None, speculate=None):
     from shredword.trainer import BPETrainer
 
     cfg = case["config"]
@@ -22,6 +22,11 @@ def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None):
     t.set_option("layout", layout)
     t.set_option("trace", trace)
     t.set_option("resident", resident)
+    t.set_option("index", index)
+    if spec_depth is not None:
+        t.set_option("spec_depth", spec_depth)
+    if speculate is not None:
+        t.set_option("speculate", speculate)
     t.load_corpus(corpus)
     merges = t.train()
     model, vocab = str(tmp_path / "g.model"), str(tmp_path / "g.vocab")
@@ -32,21 +37,59 @@ def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None):
     return merges, open(model, "rb").read(), open(vocab, "rb").read(), open(trace).read()
 
 
-API_CASES = [n for n in golden_cases() if not n.startswith("cli_")]
-
-
-@pytest.mark.parametrize("name", API_CASES)
-def test_types_layout_matches_reference(name, case_corpus, tmp_path):
-    """Default path: the LDS-resident merge loop (k_resident) wherever the table fits; the
-    adversarial corpora hold a word longer than one tile and take the launch path."""
-    case, corpus = case_corpus(name)
-    st = {}
-    merges, model, vocab, trace = _train(case, corpus, tmp_path, "types", stats=st)
+def _check(case, got):
+    merges, model, vocab, trace = got
     assert merges == case["merges"]
     assert trace == case["trace"]
     assert model == case["model_bytes"]
     assert vocab == case["vocab_bytes"]
-    if merges > 0 and not name.startswith("adv_"):
+
+
+API_CASES = [n for n in golden_cases() if not n.startswith("cli_")]
+# the deep reference runs (31,744 and 63,744 merges): every path runs them too
+DEEP = [n for n in API_CASES if "v32000" in n or "v64000" in n]
+
+
+@pytest.mark.parametrize("name", API_CASES)
+def test_types_layout_matches_reference(name, case_corpus, tmp_path):
+    """Default path: the indexed merge loop (k_word_loop: pair -> words index, one persistent
+    workgroup, speculation depth 1)."""
+    case, corpus = case_corpus(name)
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st))
+    if case["merges"] > 0:
+        assert st["index_merges"] >= case["merges"] and st["index_on"] == 1
+        assert st["resident_launches"] == 0
+
+
+@pytest.mark.parametrize("name", API_CASES)
+def test_index_loop_no_speculation_matches_reference(name, case_corpus, tmp_path):
+    """The indexed loop one merge at a time (no guesses, so no undo)."""
+    case, corpus = case_corpus(name)
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, speculate=0))
+    assert st["index_undos"] == 0
+
+
+@pytest.mark.parametrize("name", API_CASES)
+def test_index_loop_deep_speculation_matches_reference(name, case_corpus, tmp_path):
+    """The indexed loop with three guesses in flight behind the current merge (undone exactly
+    when the replay picks otherwise)."""
+    case, corpus = case_corpus(name)
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, spec_depth=3))
+    if case["merges"] > 200:
+        assert st["index_undos"] > 0 and st["spec_hits"] > 0
+
+
+@pytest.mark.parametrize("name", API_CASES)
+def test_types_layout_resident_matches_reference(name, case_corpus, tmp_path):
+    """The LDS-resident tile loop (k_resident) wherever the table fits; the adversarial corpora
+    hold a word longer than one tile and take the launch path."""
+    case, corpus = case_corpus(name)
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, index=0))
+    if case["merges"] > 0 and not name.startswith("adv_"):
         assert st["resident_launches"] > 0
 
 
@@ -56,12 +99,8 @@ def test_types_layout_resident_hbm_matches_reference(name, case_corpus, tmp_path
     monkeypatch.setenv("SHREDWORD_RESIDENT_HBM", "1")
     case, corpus = case_corpus(name)
     st = {}
-    merges, model, vocab, trace = _train(case, corpus, tmp_path, "types", stats=st)
-    assert merges == case["merges"]
-    assert trace == case["trace"]
-    assert model == case["model_bytes"]
-    assert vocab == case["vocab_bytes"]
-    if merges > 0:
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, index=0))
+    if case["merges"] > 0:
         assert st["resident_launches"] > 0
 
 
@@ -70,24 +109,15 @@ def test_types_layout_resident_deep_speculation_matches_reference(name, case_cor
     """k_resident with three guessed merges in flight behind the current one."""
     monkeypatch.setenv("SHREDWORD_SPEC_DEPTH", "3")
     case, corpus = case_corpus(name)
-    st = {}
-    merges, model, vocab, trace = _train(case, corpus, tmp_path, "types", stats=st)
-    assert merges == case["merges"]
-    assert trace == case["trace"]
-    assert model == case["model_bytes"]
-    assert vocab == case["vocab_bytes"]
+    _check(case, _train(case, corpus, tmp_path, "types", index=0))
 
 
 @pytest.mark.parametrize("name", API_CASES)
 def test_types_layout_launch_path_matches_reference(name, case_corpus, tmp_path):
-    """The per-merge launch path (k_merge + speculation + k_unmerge), resident loop off."""
+    """The per-merge launch path (k_merge + speculation + k_unmerge), both loops off."""
     case, corpus = case_corpus(name)
     st = {}
-    merges, model, vocab, trace = _train(case, corpus, tmp_path, "types", resident=0, stats=st)
-    assert merges == case["merges"]
-    assert trace == case["trace"]
-    assert model == case["model_bytes"]
-    assert vocab == case["vocab_bytes"]
+    _check(case, _train(case, corpus, tmp_path, "types", resident=0, stats=st, index=0))
     assert st["resident_launches"] == 0
 
 
@@ -95,11 +125,7 @@ def test_types_layout_launch_path_matches_reference(name, case_corpus, tmp_path)
                                   "ascii1m_unk7_cov09", "small_v300"])
 def test_stream_layout_matches_reference(name, case_corpus, tmp_path):
     case, corpus = case_corpus(name)
-    merges, model, vocab, trace = _train(case, corpus, tmp_path, "stream")
-    assert merges == case["merges"]
-    assert trace == case["trace"]
-    assert model == case["model_bytes"]
-    assert vocab == case["vocab_bytes"]
+    _check(case, _train(case, corpus, tmp_path, "stream"))
 
 
 @pytest.mark.parametrize("name", [n for n in golden_cases() if n.startswith("cli_")])

@@ -5,6 +5,7 @@ The goldens were produced by the reference's own sources (zero-initialised build
 .model byte, .vocab byte, [MERGE] line and per-batch heap size, so it may serve as the parity
 checker for the HIP path and as the CPU baseline.
 """
+import concurrent.futures
 import os
 import subprocess
 
@@ -13,14 +14,33 @@ import pytest
 from conftest import golden_cases
 
 
+@pytest.fixture(scope="session")
+def oracle_runs(case_corpus, oracle_bin, tmp_path_factory):
+    """Every golden's oracle run, started together on a pool of host cores (the deep cases,
+    31,744 and 63,744 merges of a reference-cost O(S) loop, take minutes each)."""
+    out = tmp_path_factory.mktemp("oracle_runs")
+    pool = concurrent.futures.ThreadPoolExecutor(max_workers=max(2, (os.cpu_count() or 4) - 1))
+
+    def run(name, case, corpus):
+        cfg = case["config"]
+        model, vocab, trace = (str(out / f"{name}.{n}") for n in ("model", "vocab", "trace"))
+        subprocess.run([oracle_bin, corpus, str(cfg["vocab_size"]), str(cfg["unk_id"]),
+                        repr(cfg["character_coverage"]), str(cfg["min_pair_freq"]), model, vocab,
+                        "--trace", trace], check=True, stderr=subprocess.DEVNULL)
+        return model, vocab, trace
+
+    cases = {n: case_corpus(n) for n in golden_cases()}
+    # longest first: the deep runs set the wall time
+    order = sorted(cases, key=lambda n: -cases[n][0]["merges"])
+    futs = {n: pool.submit(run, n, *cases[n]) for n in order}
+    yield lambda n: futs[n].result()
+    pool.shutdown(wait=True)
+
+
 @pytest.mark.parametrize("name", golden_cases())
-def test_oracle_matches_reference_golden(name, case_corpus, oracle_bin, tmp_path):
-    case, corpus = case_corpus(name)
-    cfg = case["config"]
-    model, vocab, trace = (str(tmp_path / n) for n in ("o.model", "o.vocab", "o.trace"))
-    subprocess.run([oracle_bin, corpus, str(cfg["vocab_size"]), str(cfg["unk_id"]),
-                    repr(cfg["character_coverage"]), str(cfg["min_pair_freq"]), model, vocab,
-                    "--trace", trace], check=True, stderr=subprocess.DEVNULL)
+def test_oracle_matches_reference_golden(name, case_corpus, oracle_runs):
+    case, _ = case_corpus(name)
+    model, vocab, trace = oracle_runs(name)
     assert open(model, "rb").read() == case["model_bytes"]
     assert open(vocab, "rb").read() == case["vocab_bytes"]
     assert open(trace).read() == case["trace"]
