@@ -909,7 +909,9 @@ void WordLoop::ensure_slots(uint32_t cap) {
 }
 
 void WordLoop::reserve(int32_t max_id) {
-  const uint32_t need = (uint32_t)std::max<int32_t>(max_id, 0) + 2;
+  // + kSlots: the guesses posted past the last merge of a batch (rolled back at its end) use ids
+  // up to max_id + kSlots - 1, and the tables can grow only while nothing is in flight
+  const uint32_t need = (uint32_t)std::max<int32_t>(max_id, 0) + 2 + kSlots;
   if (need <= cap_ && dsum_) return;
   if (!posted_.empty()) fatal("WordLoop::reserve with a merge in flight");
   stop();
