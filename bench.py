@@ -475,8 +475,11 @@ def main():
         k1_ms = st["count_kernel_ms"] / max(1, st["count_launches"])
         k1_bytes = st["count_kernel_bytes"] / max(1, st["count_launches"])
         per_step_merges = merges / max(1, args.steps)
+        im = max(1, st["index_merges"])
         merge_loop = {
-            "kernel": ("k_resident (persistent merge loop, K2+K3: match, neighbour deltas, in-place compaction)"
+            "kernel": ("k_word_loop (indexed persistent merge loop, one workgroup: word lists, match, neighbour "
+                       "deltas, in-place compaction)" if st["index_merges"] else
+                       "k_resident (persistent merge loop, K2+K3: match, neighbour deltas, in-place compaction)"
                        if st["resident_launches"] else "k_merge (per-merge launches, K2+K3)"),
             "bound": "latency",
             "us_per_merge": 1e6 * elapsed / max(1, merges),
@@ -491,6 +494,24 @@ def main():
                      "not bandwidth; the HBM fraction is shown for completeness only"),
             "launches": merges,
         }
+        if st["index_merges"]:
+            merge_loop["index"] = {
+                "merges": st["index_merges"], "undos": st["index_undos"], "launches": st["index_launches"],
+                "words_listed_per_merge": st["index_candidates"] / im,
+                "words_scanned_per_merge": st["index_scanned"] / im,
+                "words_changed_per_merge": st["index_changed"] / im,
+                "occurrences_per_merge": st["index_occurrences"] / im,
+                "device_us_per_merge": st["index_dev_us"] / im,
+                "device_lookup_us_per_merge": st["index_dev_lookup_us"] / im,
+                "device_scan_us_per_merge": st["index_dev_scan_us"] / im,
+                "host_post_to_flag_us_per_merge": st["index_wait_us"] / im,
+                "device_build_us_per_merge": st["index_build_us"] / im,
+                "merges_without_pair_groups": st["index_no_sub"],
+                "group_entries_per_merge": st["index_staged"] / im,
+                "hybrid_switch_merge": st["index_switch_merge"],
+                "hybrid_switch_ms_total": st["index_switch_ms"],
+                "launch_ms_total": st["index_ms"],
+            }
         result = {
             "metric": "BPE merges/sec",
             "value": merges / elapsed,

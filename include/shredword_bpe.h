@@ -107,6 +107,14 @@ int shred_probe_rollback(Trainer* trainer, int32_t a, int32_t b);
  * tokens) into out[0 .. cap); returns the full length (call with cap 0 to size), -1 on error. */
 int64_t shred_debug_tokens(Trainer* trainer, int32_t* out, size_t cap);
 
+/* Diagnostic: the indexed loop's per-merge trace of the merges collected since timing was last
+ * switched on or the stats cleared (set_option timing / clear_stats): 12 uint32 per merge — X,
+ * listed words, scanned words, changed words, occurrences, device ns command -> flag, of which
+ * lookup ns and scan ns, then wave 0's stamps (ns after the command: pool entries loaded, first
+ * run loaded, first word merged, scan loop left).  Copies min(cap, n) values into out; returns n
+ * (-1 on error). */
+int64_t shred_index_trace(Trainer* trainer, uint32_t* out, size_t cap);
+
 typedef struct ShredStats {
   double load_seconds, init_seconds, train_seconds;
   double host_select_seconds, host_launch_seconds, host_wait_seconds, host_apply_seconds;
@@ -137,6 +145,14 @@ typedef struct ShredStats {
   double index_ms;             /* Σ k_word_loop launch durations (HIP events) */
   double index_dev_us;         /* Σ per-merge device time, command seen -> flag (device clock) */
   double index_wait_us;        /* Σ per-merge host time, post -> flag seen */
+  double index_dev_lookup_us;  /* of index_dev_us: command seen -> word list known */
+  double index_dev_scan_us;    /* of index_dev_us: word list known -> every listed word merged */
+  uint64_t index_scanned;      /* of index_candidates: words whose runs were read */
+  double index_build_us;       /* Σ device time building the merges' pair groups (after their flags) */
+  uint64_t index_no_sub;       /* merges whose pair groups were not built (words-of list + filter) */
+  uint64_t index_staged;       /* Σ pair-group entries written */
+  int64_t index_switch_merge;  /* hybrid: the first merge id of the indexed loop in the last train() (-1: none) */
+  double index_switch_ms;      /* hybrid: Σ host time of the resident -> indexed switches */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -2607,6 +2607,8 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
   if (const char* e = std::getenv("SHREDWORD_TILE_SKIP")) skip_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_RESIDENT")) resident_on_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_INDEX")) index_on_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SHREDWORD_HYBRID")) hybrid_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SHREDWORD_SWITCH_OCC")) switch_occ_ = std::strtoull(e, nullptr, 10);
   int nb = 0;  // resident workgroups of k_merge per CU
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_merge<true>), kThreads, 0));
   merge_blocks_per_cu_ = nb > 0 ? nb : 4;
@@ -2800,6 +2802,22 @@ void Device::index_sync() {
   }
 }
 
+// Hybrid: the resident loop ends (its tiles written back) and the indexed loop takes the merged
+// words from the tiles and indexes them, all on the device.
+void Device::hybrid_switch(int32_t X) {
+  const double t0 = now_seconds();
+  switch_pending_ = false;
+  park();
+  idx_phase_ = true;
+  if (!wl_ || !wl_->ready()) return;
+  wl_->reserve(std::max(X, reserved_max_id_));
+  wl_->load_tiles(tok_, tile_off_, tile_len_);
+  words_stale_ = false;
+  wl_pristine_index_ = false;
+  switch_x_ = X;
+  switch_ms_ += 1e3 * (now_seconds() - t0);
+}
+
 // A tile-path merge ran after the loop's last merge: the loop takes the tiles' words.
 void Device::index_refresh() {
   std::vector<int32_t> all(tok_elems_ + 4);
@@ -2832,11 +2850,18 @@ void Device::reset_tokens() {
   live_tokens_est_ = live_tokens0_;
   max_id_seen_ = max_id0_;
   index_.reset();
+  idx_phase_ = false;
+  switch_pending_ = false;
   if (wl_) {
-    wl_->reset();
-    if (!wl_pristine_index_) wl_->rebuild();
-    wl_pristine_index_ = true;
-    words_stale_ = false;
+    if (hybrid_resident_phase()) {  // the switch re-indexes the merged words
+      wl_->reset_words();
+      words_stale_ = true;
+    } else {
+      wl_->reset();
+      if (!wl_pristine_index_) wl_->rebuild();
+      wl_pristine_index_ = true;
+      words_stale_ = false;
+    }
   }
 }
 
@@ -3049,6 +3074,7 @@ void Device::flush_timing(bool block) {
 void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   HIP_OK(hipSetDevice(ordinal_));
   if (n < 1 || n > kChainMax) fatal("merge_chain: bad chain length");
+  if (switch_pending_ && n == 1 && run_count_ == 0 && res_posted_.empty()) hybrid_switch(X0);
   if (n == 1 && index_eligible() && run_count_ == 0 && res_posted_.empty()) {  // the indexed loop
     if (words_stale_) index_refresh();
     if (!wl_->in_flight()) wl_->reserve(X0);
@@ -3682,6 +3708,7 @@ void Device::set_resident(bool on) {
 // the table pointers, so they cannot grow under it).
 void Device::reserve_ids(int32_t max_id) {
   HIP_OK(hipSetDevice(ordinal_));
+  reserved_max_id_ = max_id;
   if (index_eligible() && !wl_->in_flight()) wl_->reserve(max_id);
   const uint32_t need = (uint32_t)std::max<int32_t>(max_id, 0) + 2;
   bool grow = false;
@@ -3865,6 +3892,7 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   }
   if (timing_) times_.merge_bytes += 4.0 * (double)live_tokens_est_;
   ++res_merges_;
+  if (hybrid_ && !idx_phase_ && index_on_ && wl_ && wl_->ready() && hs[0] < switch_occ_) switch_pending_ = true;
   live_tokens_est_ -= hs[0];
   records_total_ += n;
   records_max_ = std::max<uint64_t>(records_max_, n);

@@ -2,15 +2,16 @@
 //
 //   k_word_loop       the merge loop: one persistent workgroup (16 wave64s) that takes merge /
 //                     undo commands from a ring in pinned host memory.  Per merge (a, b) -> X:
-//                     directory lookup of (a, b) -> its word list; a lane per listed word scans
-//                     it greedily left to right (reference bpe.cpp:265-296), emits the four
-//                     neighbour deltas per occurrence into an LDS hash keyed (neighbour slot,
-//                     category) with Σ weight and min first touch (FreqChangeMap, bpe.cpp:9-50),
-//                     and compacts the word in place; the records go to host memory behind one
-//                     system release and a flag; then the new pairs (p, X) / (X, n) are grouped
-//                     in LDS and appended to the pool under new directory entries.
+//                     the word list of (a, b) (the words-of list of a or b, or the initial pair
+//                     directory); a lane per listed word loads the word's run with seven 16-B
+//                     loads into an LDS strip, scans it greedily left to right (reference
+//                     bpe.cpp:265-296), emits the four neighbour deltas per occurrence into an LDS
+//                     hash keyed (neighbour slot, category) with Σ weight and min first touch
+//                     (FreqChangeMap, bpe.cpp:9-50), compacts the word in place and appends it to
+//                     the words of X when it changed; the records go to host memory behind one
+//                     system release and a flag.
 //   k_wl_emit_pairs   initial index: every adjacent non-unk pair of every word -> (key, word)
-//   k_wl_mark / k_wl_scatter / k_wl_dir_init   sorted runs -> pool + directory
+//   k_wl_mark / k_wl_scatter / k_wl_counts / k_wl_dir_init   sorted runs -> pool + directory
 //   k_words_to_tiles  the word table back into the tile stream (headers + tokens)
 //
 // Integer and index work only: no MFMA.  Everything the loop touches per merge is a few KB of
@@ -45,19 +46,27 @@ namespace {
 
 typedef unsigned long long u64;
 
-constexpr int kWlThreads = 1024;
+constexpr int kWlThreads = 512;
 constexpr int kWlWaves = kWlThreads / 64;
 constexpr int kDh = 2048;               // LDS delta hash slots
-constexpr int kBh = 2048;               // LDS new-pair hash slots (build round)
+constexpr int kStripV = 6;              // 16-B loads per word run: [length][23 tokens]
+constexpr int kStrip = 4 * kStripV;     // ints per lane in the LDS strip
+constexpr uint32_t kStripTok = kStrip - 1;
+constexpr int kB = 2;                   // pool entries per lane per scan round (one load batch)
+constexpr int kBh = 2048;               // LDS slots of a build's key grouping and of its sub-table
+constexpr int kPend = 64;               // merges whose pair groups wait to be built
 constexpr uint32_t kRing = 64;          // command ring entries
-constexpr uint32_t kOpMerge = 1, kOpStop = 2, kOpTimeout = 3, kOpUnmerge = 4;
+constexpr uint32_t kOpNone = 0, kOpMerge = 1, kOpStop = 2, kOpTimeout = 3, kOpUnmerge = 4;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 constexpr u64 kEmpty64 = ~0ull;
-constexpr uint32_t kInvalidSeq = 0xFFFFFFFFu;
-// dstate words
-constexpr int kStSpill = 0, kStPoolTop = 1, kStKeys = 2, kStError = 3;
+constexpr uint32_t kNoList = 0xFFFFFFFFu;
+constexpr u64 kSubValid = 1ull << 40, kSubPending = 1ull << 41;
+constexpr uint32_t kSubFirst = 16;      // sub-table entries [0, 16): the empty table (X has no pairs)
+// dstate words: [0] unused, [1] pool top, [2] sub-table top, [3] error, [4..5] build ticks,
+// [6] merges without a sub-table, [7] staged entries (u32, wraps)
+constexpr int kStPoolTop = 1, kStSubTop = 2, kStError = 3, kStBuild = 4, kStNoSub = 6, kStStaged = 7;
 // error codes (dstate[kStError], reported by the host)
-constexpr uint32_t kErrPool = 1, kErrStage = 2, kErrDir = 3, kErrLookup = 4;
+constexpr uint32_t kErrPool = 1, kErrList = 2, kErrLookup = 4;
 
 struct WlCmd {
   u64 g[4];  // granules (seq | value << 32): op | slot << 8, a, b, X
@@ -65,29 +74,48 @@ struct WlCmd {
 
 struct WlSlotDev {
   DeltaRecord* recs;  // host-visible
-  uint32_t* hdr;      // host-visible: [0] records, [1] flag, [2] candidates, [3] changed words,
-                      //   [4..5] occurrences (u64), [6..7] device ticks command -> flag (u64)
+  uint32_t* hdr;      // host-visible: [0] records, [1] flag, [2] listed words, [3] changed words,
+                      //   [4..5] occurrences (u64), [6..7] device ticks command -> flag (u64),
+                      //   [8..9] ticks command -> list known, [10..11] ticks command -> words merged,
+                      //   [12] words whose runs were read, [13] 1: a filtered words-of list,
+                      //   [16..19] stamps (10 ns ticks after the command, thread 0): pool entries
+                      //   loaded, first run loaded, first word merged, ticks in builds this command
   uint32_t rec_cap;
+};
+
+// A pool entry: the word and a 64-bit signature of the ids it held when the entry was written
+// (bit sig_bit(id) per id; zero in the pair groups, which need no filter).  A words-of entry of id
+// M was written when M was created; every id older than M that the word holds now it held then
+// (only merge c creates c), so a word holding (c, d) now, max(c, d) <= M, has both bits.
+struct WEnt {
+  u64 e;    // run offset << 32 | word id
+  u64 sig;
+};
+
+// Pair groups of id X: a per-X open-addressing table (2^k entries) keyed by the delta key of the
+// new pair, slot(neighbour) * 4 + category (kNewLeft: (p, X), kNewRight: (X, n)).
+struct SubE {
+  uint32_t dk, off, cnt, pad;
 };
 
 struct WlParams {
   int32_t* wtok;
-  const uint32_t* woff;
-  uint32_t* wlen;
-  uint32_t* wmark;
   const u64* weight;
-  uint32_t nwords;
-  uint32_t* pool;
+  uint32_t* wmark;   // per word: the last command that scanned it (a group may list a word twice)
+  WEnt* pool;
   u64 pool_cap;
-  u64* dkey;
-  u64* dval;
-  uint32_t* dseq;
+  SubE* sub;
+  u64 sub_cap;
+  const u64* dkey;
+  const u64* dval;
   u64 dir_mask;
-  uint32_t* valid_seq;
+  u64* lst;          // per id: words-of list, pool offset | count << 32
+  uint32_t* lseq;    // per id: the command that made it (~0: none)
+  u64* xsub;         // per id: sub-table offset | log2 size << 32 | kSubValid, or kSubPending
+  u64* xgrp;         // per id: its groups' pool range, start | end << 32
   uint32_t id_cap;
-  u64* sk[2];
-  uint32_t* sw[2];
-  uint32_t* sslot;
+  uint32_t* stg_dk;  // staged new pairs of the merges whose groups wait: delta key, pool entry
+  u64* stg_e;
   u64 stage_cap;
   u64* dsum;
   u64* dft;
@@ -114,30 +142,45 @@ __device__ __forceinline__ u64 pair_key(int32_t a, int32_t b) { return ((u64)(ui
 __device__ __forceinline__ uint32_t slot_of(int32_t id, uint32_t cap) {
   return (uint32_t)id < cap ? (uint32_t)id + 1u : 0u;
 }
-__device__ __forceinline__ u64 ld_agent(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ u64 sig_bit(int32_t id) { return 1ull << (((uint32_t)id * 0x9E3779B1u) >> 26); }
+__device__ __forceinline__ uint32_t sub_hash(uint32_t dk, uint32_t lg) { return (dk * 0x9E3779B1u) >> (32 - lg); }
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct DeltaH {
   uint32_t key[kDh];
-  u64 sum[kDh];
-  u64 ft[kDh];
+  u64 sum[kDh];  // Σ weight
+  u64 ft[kDh];   // min first touch
 };
-struct BuildH {
-  u64 key[kBh];
-  uint32_t cnt[kBh];
-  uint32_t fill[kBh];
-  uint32_t off[kBh];
+struct BuildL {
+  uint32_t hk[kBh], hc[kBh], ho[kBh];  // grouping: delta key, entries, group offset
+  uint32_t sk[kBh], so[kBh], sc[kBh];  // the sub-table being assembled (sc: fill counts first)
 };
 union LdsU {
-  DeltaH d;
-  BuildH b;
+  int32_t strip[kStrip * kWlThreads];  // [position][lane]: conflict-free per wave (scan)
+  BuildL b;                             // a pending merge's pair groups (build)
+};
+static_assert(sizeof(BuildL) <= sizeof(int32_t) * kStrip * kWlThreads, "build tables share the strip");
+
+struct PendE {
+  int32_t X;
+  uint32_t seq, off, n;  // creating command, staged entries
+};
+
+// The merge's shared state in LDS.
+struct MergeCtx {
+  uint32_t* n_stage;  // staged new pairs of this merge
+  uint32_t* bfail;    // 1: a staged entry did not fit (this merge gets no sub-table)
+  uint32_t* nspill;   // delta keys spilled past the LDS hash
+  uint32_t stage_base, stage_room;
+  uint32_t* st;  // diagnostic stamps of thread 0 (shader clocks)
 };
 
 // One neighbour delta (reference freq_change_add, bpe.cpp:274-290): Σ weight and min first touch
 // per key = slot * 4 + category, in the LDS hash; keys past it go to the global spill tables.
-__device__ __forceinline__ void delta_add(DeltaH& h, const WlParams& p, uint32_t key, u64 w, u64 ft) {
+__device__ __forceinline__ void delta_add(DeltaH& h, const WlParams& p, const MergeCtx& c, uint32_t key, u64 w,
+                                          u64 ft) {
   uint32_t s = (key * 2654435761u) >> (32 - 11);
 #pragma unroll 1
   for (int probe = 0; probe < 32; ++probe) {
@@ -151,52 +194,58 @@ __device__ __forceinline__ void delta_add(DeltaH& h, const WlParams& p, uint32_t
   }
   const u64 old = atomicAdd(&p.dsum[key], w);
   atomicMin(&p.dft[key], ft);
-  if (old == 0) p.dlist[atomicAdd(&p.dstate[kStSpill], 1u)] = key;  // weights are >= 1
+  if (old == 0) p.dlist[atomicAdd(c.nspill, 1u)] = key;  // weights are >= 1
 }
 
-// A new pair of merge X listed for word w (superset entries are harmless: the word is rescanned).
-__device__ __forceinline__ void stage_pair(const WlParams& p, uint32_t* n_stage, int32_t c, int32_t d, uint32_t w) {
-  if (c == p.unk || d == p.unk) return;  // pairs holding unk are never merged (bpe.cpp:251-258)
-  const uint32_t i = atomicAdd(n_stage, 1u);
-  if (i < p.stage_cap) {
-    p.sk[0][i] = pair_key(c, d);
-    p.sw[0][i] = w;
+// A new pair (neighbour next to X) of word entry e, delta key dk: one entry of its group.
+__device__ __forceinline__ void stage_new(const WlParams& p, const MergeCtx& c, uint32_t dk, u64 e) {
+  const uint32_t i = atomicAdd(c.n_stage, 1u);
+  if (i < c.stage_room) {
+    p.stg_dk[c.stage_base + i] = dk;
+    p.stg_e[c.stage_base + i] = e;
   } else {
-    atomicMax(&p.dstate[kStError], kErrStage);
+    *c.bfail = 1u;
   }
 }
 
-// Merge (a, b) -> X in word w, greedy left to right as the reference's chain walk; returns the
-// occurrences merged.  First touch = (rank << 32) | (input position << 2) | category.
-__device__ __forceinline__ uint32_t merge_word(const WlParams& p, DeltaH& h, uint32_t* n_stage, uint32_t w, int32_t a,
-                                               int32_t b, int32_t X, uint32_t seq) {
-  const uint32_t old = atomicExch(&p.wmark[w], seq);  // a list may name a word twice
-  const uint32_t o = p.woff[w];
-  const uint32_t L = p.wlen[w];
-  if (old == seq || L < 2) return 0;
-  const u64 wc = p.weight[w];
-  const u64 rank = (u64)w << 32;
-  int32_t* t = p.wtok + o;
+// The four deltas of one occurrence and its new pairs' group entries.  prev: the left neighbour
+// after merging (X when just produced), has_l false at the word's start; n: the original token
+// after the pair, has_n false at the word's end.
+__device__ __forceinline__ void occurrence(const WlParams& p, DeltaH& h, const MergeCtx& c, bool has_l, int32_t prev,
+                                           bool has_n, int32_t n, u64 wc, u64 ft, u64 e) {
+  if (has_l) {
+    const uint32_t sl = slot_of(prev, p.cap) * 4u;
+    delta_add(h, p, c, sl + 0u, wc, ft | 0u);
+    delta_add(h, p, c, sl + 1u, wc, ft | 1u);
+    if (prev != p.unk) stage_new(p, c, sl + 1u, e);
+  }
+  if (has_n) {
+    const uint32_t sn = slot_of(n, p.cap) * 4u;
+    delta_add(h, p, c, sn + 2u, wc, ft | 2u);
+    delta_add(h, p, c, sn + 3u, wc, ft | 3u);
+    if (n != p.unk) stage_new(p, c, sn + 3u, e);
+  }
+}
+
+// Merge (a, b) -> X in one word of L tokens read from HBM (t: its tokens), greedy left to right
+// as the reference's chain walk (the path of words longer than the strip); returns the
+// occurrences merged, the new length in *len and the id signature in *sig.  First touch =
+// (rank << 32) | (input position << 2) | category.
+__device__ __forceinline__ uint32_t merge_run(const WlParams& p, DeltaH& h, const MergeCtx& c, int32_t* t, uint32_t L,
+                                              u64 e, u64 wc, int32_t a, int32_t b, int32_t X, uint32_t* len,
+                                              u64* sig) {
+  const u64 rank = (e & 0xFFFFFFFFull) << 32;
   uint32_t j = 0, k = 0, occ = 0;
+  u64 sg = sig_bit(X);
   int32_t prev = 0;
-  int32_t c0 = t[0], c1 = t[1];
+  int32_t c0 = t[0], c1 = L > 1 ? t[1] : 0;
 #pragma unroll 1
   while (j < L) {
     if (j + 1 < L && c0 == a && c1 == b) {
       const bool has_n = j + 2 < L;
       const int32_t n = has_n ? t[j + 2] : 0;  // the original next token (bpe.cpp:283-289)
       const int32_t n2 = j + 3 < L ? t[j + 3] : 0;
-      const u64 ft = rank | ((u64)j << 2);
-      if (k > 0) {  // left neighbour: X when it was just produced (bpe.cpp:276-279)
-        delta_add(h, p, slot_of(prev, p.cap) * 4u + 0u, wc, ft | 0u);
-        delta_add(h, p, slot_of(prev, p.cap) * 4u + 1u, wc, ft | 1u);
-        stage_pair(p, n_stage, prev, X, w);
-      }
-      if (has_n) {
-        delta_add(h, p, slot_of(n, p.cap) * 4u + 2u, wc, ft | 2u);
-        delta_add(h, p, slot_of(n, p.cap) * 4u + 3u, wc, ft | 3u);
-        stage_pair(p, n_stage, X, n, w);
-      }
+      occurrence(p, h, c, k > 0, prev, has_n, n, wc, rank | ((u64)j << 2), e);
       t[k] = X;
       prev = X;
       ++k;
@@ -206,6 +255,7 @@ __device__ __forceinline__ uint32_t merge_word(const WlParams& p, DeltaH& h, uin
       c1 = n2;
     } else {
       if (occ) t[k] = c0;  // positions before the first occurrence are unchanged
+      sg |= sig_bit(c0);
       prev = c0;
       ++k;
       ++j;
@@ -213,21 +263,96 @@ __device__ __forceinline__ uint32_t merge_word(const WlParams& p, DeltaH& h, uin
       c1 = j + 1 < L ? t[j + 1] : 0;
     }
   }
-  if (occ) p.wlen[w] = k;
+  *len = k;
+  *sig = sg;
   return occ;
 }
 
-// Undo of merge X in word w: every X back into (a, b), right to left in place.
-__device__ __forceinline__ void unmerge_word(const WlParams& p, uint32_t w, int32_t a, int32_t b, int32_t X,
-                                             uint32_t seq) {
-  const uint32_t old = atomicExch(&p.wmark[w], seq);
-  const uint32_t o = p.woff[w];
-  const uint32_t L = p.wlen[w];
-  if (old == seq || L == 0) return;
-  int32_t* t = p.wtok + o;
+// A word's run: kStripV 16-B loads (one round trip), the length and up to kStripTok tokens.
+struct Run {
+  int4 v[kStripV];
+};
+__device__ __forceinline__ Run load_run(const int32_t* r) {
+  Run x;
+  const int4* r4 = reinterpret_cast<const int4*>(r);
+#pragma unroll
+  for (int q = 0; q < kStripV; ++q) x.v[q] = r4[q];
+  return x;
+}
+__device__ __forceinline__ int32_t run_at(const Run& x, int i) {
+  const int4 q = x.v[i >> 2];
+  return (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w;
+}
+
+// Merge (a, b) -> X in a word of L <= kStripTok tokens held in registers, in two passes so that
+// a wave's lanes emit their deltas in lock step: (1) the greedy left-to-right walk, unrolled over
+// the registers (position j is taken by the pair (j, j + 1) unless the previous position was),
+// writes the output to this lane's LDS strip and marks the output positions holding X; (2) per
+// occurrence, lowest output position first, the four neighbour deltas — left neighbour
+// out[k - 1] (X when just produced), right neighbour the original token after the pair
+// (out[k + 1], or a where that is the next occurrence's X); input position of occurrence o at
+// output k: k + o.  The changed run is written back with 16-B stores.  Same results as merge_run.
+__device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, const MergeCtx& c, int32_t* s,
+                                               int32_t* r, const Run& x, uint32_t L, u64 e, u64 wc, int32_t a,
+                                               int32_t b, int32_t X, uint32_t* len, u64* sig) {
+  uint32_t k = 0, occ = 0, xm = 0;
+  bool skip = false;
+  u64 sg = sig_bit(X);
+#pragma unroll
+  for (int j = 0; j < (int)kStripTok; ++j) {
+    const int32_t t0 = run_at(x, 1 + j);
+    const int32_t t1 = j + 1 < (int)kStripTok ? run_at(x, 2 + j) : 0;
+    const bool in = (uint32_t)j < L;
+    const bool emit = in && !skip;
+    const bool m = emit && (uint32_t)(j + 1) < L && t0 == a && t1 == b;
+    if (emit) s[(1 + k) * kWlThreads] = m ? X : t0;
+    xm |= (m ? 1u : 0u) << k;
+    if (emit && !m) sg |= sig_bit(t0);
+    k += emit ? 1u : 0u;
+    occ += m ? 1u : 0u;
+    skip = m;
+  }
+  *len = k;
+  *sig = sg;
+  if (threadIdx.x == 0) c.st[5] = (uint32_t)__builtin_amdgcn_s_memtime();
+  if (!occ) return 0;
+  const u64 rank = (e & 0xFFFFFFFFull) << 32;
+  uint32_t m = xm, o = 0;
+  while (__ballot(m != 0u)) {
+    if (m) {
+      const uint32_t ko = (uint32_t)__ffs(m) - 1u;
+      m &= m - 1u;
+      const uint32_t jo = ko + o;
+      ++o;
+      const int32_t prev = ko > 0 ? s[ko * kWlThreads] : 0;  // out[ko - 1]
+      const bool has_n = jo + 2 < L;
+      const int32_t nx = has_n ? s[(2 + ko) * kWlThreads] : 0;  // out[ko + 1]
+      occurrence(p, h, c, ko > 0, prev, has_n, nx == X ? a : nx, wc, rank | ((u64)jo << 2), e);
+    }
+  }
+  if (threadIdx.x == 0) c.st[6] = (uint32_t)__builtin_amdgcn_s_memtime();
+  // the run [length][k tokens] from the first 16-B group that changed
+  s[0] = (int32_t)k;
+  int4* r4 = reinterpret_cast<int4*>(r);
+  const uint32_t q0 = (uint32_t)__ffs(xm) >> 2;  // (1 + first X position) / 4
+  for (uint32_t q = 0; q <= (k >> 2); ++q) {
+    if (q != 0 && q < q0) continue;
+    int4 v;
+    v.x = s[(4 * q + 0) * kWlThreads];
+    v.y = s[(4 * q + 1) * kWlThreads];
+    v.z = s[(4 * q + 2) * kWlThreads];
+    v.w = s[(4 * q + 3) * kWlThreads];
+    r4[q] = v;
+  }
+  return occ;
+}
+
+// Undo of merge X in one word (tokens t, L of them): every X back into (a, b), right to left in
+// place; returns the new length.
+__device__ __forceinline__ uint32_t unmerge_run(int32_t* t, uint32_t L, int32_t a, int32_t b, int32_t X) {
   uint32_t nx = 0;
   for (uint32_t j = 0; j < L; ++j) nx += t[j] == X;
-  if (!nx) return;
+  if (!nx) return L;
   uint32_t q = L + nx;
   for (uint32_t j = L; j-- > 0;) {
     const int32_t v = t[j];
@@ -238,7 +363,7 @@ __device__ __forceinline__ void unmerge_word(const WlParams& p, uint32_t w, int3
       t[--q] = v;
     }
   }
-  p.wlen[w] = L + nx;
+  return L + nx;
 }
 
 __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
@@ -251,23 +376,134 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
   return x;
 }
 
-// Directory insert of a key of merge `seq` (one thread per key; keys of one round are distinct).
-__device__ __forceinline__ void dir_insert(const WlParams& p, u64 key, uint32_t off, uint32_t cnt, uint32_t seq) {
-  u64 h = mix64(key) & p.dir_mask;
-  for (u64 probe = 0; probe <= p.dir_mask; ++probe) {
-    const u64 prev = atomicCAS(&p.dkey[h], kEmpty64, key);
-    if (prev == kEmpty64 || prev == key) {
-      p.dval[h] = (u64)off | ((u64)cnt << 32);
-      p.dseq[h] = seq;
-      if (prev == kEmpty64) {
-        const uint32_t n = atomicAdd(&p.dstate[kStKeys], 1u);
-        if ((u64)n * 4 > (p.dir_mask + 1) * 3) atomicMax(&p.dstate[kStError], kErrDir);
-      }
-      return;
-    }
-    h = (h + 1) & p.dir_mask;
+// The loop's state in LDS.
+struct LoopS {
+  uint32_t cmd[8];
+  uint32_t nout, nchg, pool_top, sub_top, err, scan, nstage, bfail, filter, nspill, need;
+  uint32_t stage_top, pend_head, pend_n, build_ok, nkeys, total;
+  uint32_t wsum[kWlWaves], wkeys[kWlWaves];
+  uint32_t st[8];
+  u64 lk[2];  // word list: pool offset, count
+  u64 occ, t[2];
+  PendE pend[kPend];
+};
+
+// Builds the pair groups of the oldest pending merge (every thread of the workgroup calls it):
+// its staged (delta key, word) entries grouped by key in LDS, placed in the pool by group, and
+// a sub-table of 2^k >= 2 x keys entries assembled in LDS and copied out.  A merge undone before
+// its build is skipped.  Too many keys or no room: the merge keeps its words-of list instead.
+__device__ void build_front(const WlParams& p, BuildL& B, LoopS& S, uint32_t* nosub, uint32_t* staged) {
+  const uint32_t tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const PendE pe = S.pend[S.pend_head];
+  const bool live = pe.X >= 0 && (uint32_t)pe.X < p.id_cap && p.lseq[pe.X] == pe.seq;
+  for (int i = tid; i < kBh; i += kWlThreads) {
+    B.hk[i] = kEmpty32;
+    B.hc[i] = 0;
+    B.sc[i] = 0;
   }
-  atomicMax(&p.dstate[kStError], kErrDir);
+  if (tid == 0) S.build_ok = live ? 1u : 0u;
+  __syncthreads();
+  if (live)
+    for (uint32_t i = tid; i < pe.n; i += kWlThreads) {
+      const uint32_t dk = p.stg_dk[pe.off + i];
+      uint32_t s = sub_hash(dk, 11);
+      bool ok = false;
+      for (int probe = 0; probe < 64; ++probe) {
+        const uint32_t prev = atomicCAS(&B.hk[s], kEmpty32, dk);
+        if (prev == kEmpty32 || prev == dk) {
+          atomicAdd(&B.hc[s], 1u);
+          ok = true;
+          break;
+        }
+        s = (s + 1) & (kBh - 1);
+      }
+      if (!ok) S.build_ok = 0;
+    }
+  __syncthreads();
+  // exclusive offsets of the groups and the number of keys
+  constexpr int kPer = kBh / kWlThreads;
+  uint32_t c[kPer], sum = 0, nk = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    c[q] = B.hc[kPer * tid + q];
+    sum += c[q];
+    nk += c[q] != 0u;
+  }
+  const uint32_t incl = wave_incl_add(sum), kin = wave_incl_add(nk);
+  if (lane == 63) {
+    S.wsum[wid] = incl;
+    S.wkeys[wid] = kin;
+  }
+  __syncthreads();
+  uint32_t before = 0, total = 0, nkeys = 0;
+  for (int q = 0; q < kWlWaves; ++q) {
+    before += q < wid ? S.wsum[q] : 0u;
+    total += S.wsum[q];
+    nkeys += S.wkeys[q];
+  }
+  uint32_t ex = before + incl - sum;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    B.ho[kPer * tid + q] = ex;
+    ex += c[q];
+  }
+  uint32_t lg = 4;
+  while ((1u << lg) < 2u * nkeys) ++lg;
+  const uint32_t P = 1u << lg;
+  const uint32_t gbase = S.pool_top, sbase = S.sub_top;
+  const bool ok = S.build_ok != 0u && total == pe.n && P <= (uint32_t)kBh && (u64)gbase + total <= p.pool_cap &&
+                  (u64)sbase + P <= p.sub_cap;
+  __syncthreads();
+  if (ok) {
+    for (uint32_t i = tid; i < P; i += kWlThreads) B.sk[i] = kEmpty32;
+    for (uint32_t i = tid; i < pe.n; i += kWlThreads) {  // place the entries by group
+      const uint32_t dk = p.stg_dk[pe.off + i];
+      uint32_t s = sub_hash(dk, 11);
+      while (B.hk[s] != dk) s = (s + 1) & (kBh - 1);
+      const uint32_t pos = gbase + B.ho[s] + atomicAdd(&B.sc[s], 1u);
+      WEnt ne;
+      ne.e = p.stg_e[pe.off + i];
+      ne.sig = 0;
+      p.pool[pos] = ne;
+    }
+    __syncthreads();
+    for (int i = tid; i < kBh; i += kWlThreads) B.sc[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < kBh; i += kWlThreads) {  // the sub-table
+      const uint32_t cnt = B.hc[i];
+      if (!cnt) continue;
+      const uint32_t dk = B.hk[i];
+      uint32_t hs = sub_hash(dk, lg);
+      while (atomicCAS(&B.sk[hs], kEmpty32, dk) != kEmpty32) hs = (hs + 1) & (P - 1);
+      B.so[hs] = gbase + B.ho[i];
+      B.sc[hs] = cnt;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < P; i += kWlThreads) {
+      SubE se;
+      se.dk = B.sk[i];
+      se.off = B.so[i];
+      se.cnt = B.sc[i];
+      se.pad = 0;
+      p.sub[sbase + i] = se;
+    }
+  }
+  if (tid == 0) {
+    if (ok) {
+      p.xsub[pe.X] = (u64)sbase | ((u64)lg << 32) | kSubValid;
+      p.xgrp[pe.X] = (u64)gbase | ((u64)(gbase + total) << 32);
+      S.pool_top = gbase + total;
+      S.sub_top = sbase + P;
+      *staged += total;
+    } else if (live) {
+      p.xsub[pe.X] = 0;  // its words-of list serves
+      ++*nosub;
+    }
+    S.pend_head = (S.pend_head + 1) % kPend;
+    if (--S.pend_n == 0) S.stage_top = 0;
+  }
+  __syncthreads();
 }
 
 }  // namespace
@@ -275,22 +511,30 @@ __device__ __forceinline__ void dir_insert(const WlParams& p, u64 key, uint32_t 
 // The merge loop (see the file comment).  One workgroup; command numbers start at p.seq0.
 __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   __shared__ LdsU u;
-  __shared__ uint32_t s_cmd[8];
-  __shared__ uint32_t s_nout, s_nstage, s_ndefer, s_pool_top, s_base, s_total;
-  __shared__ u64 s_lk[2];  // lookup: pool offset, count
-  __shared__ u64 s_occ, s_changed;
-  __shared__ uint32_t s_wsum[kWlWaves];
+  __shared__ DeltaH s_h;
+  __shared__ LoopS S;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t tid = threadIdx.x;
-  if (tid == 0) s_pool_top = ld_agent(&p.dstate[kStPoolTop]);
+  int32_t* const mys = u.strip + tid;
+  if (tid == 0) {
+    S.pool_top = ld_agent(&p.dstate[kStPoolTop]);
+    S.sub_top = ld_agent(&p.dstate[kStSubTop]);
+    S.stage_top = 0;
+    S.pend_head = 0;
+    S.pend_n = 0;
+  }
   uint32_t expect = p.seq0;
   uint32_t exit_op = kOpStop;
+  u64 build_ticks = 0;
+  uint32_t nosub = 0, staged = 0;
   __syncthreads();
   for (;;) {
-    // ---- wave 0 waits for the next command (one round trip reads all four granules)
+    // ---- the next command: wave 0 reads the four granules in one round trip; while none is
+    // posted, the oldest pending pair groups are built, else wave 0 waits
     if (wid == 0) {
-      uint32_t op = 0, a = 0, b = 0, X = 0, idle = 0;
       const u64* g = p.ring[expect % kRing].g;
+      const bool block = S.pend_n == 0;
+      uint32_t op = kOpNone, a = 0, b = 0, X = 0, idle = 0;
       for (;;) {
         const u64 v = lane < 4 ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
         const bool tagged = lane >= 4 || (uint32_t)v == expect;
@@ -302,6 +546,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           X = __shfl(val, 3, 64);
           break;
         }
+        if (!block) break;
         if (++idle >= p.idle_polls) {
           op = kOpTimeout;
           break;
@@ -309,126 +554,311 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         __builtin_amdgcn_s_sleep(1);
       }
       if (lane == 0) {
-        s_cmd[0] = op & 0xFFu;
-        s_cmd[1] = a;
-        s_cmd[2] = b;
-        s_cmd[3] = X;
-        s_cmd[4] = (op >> 8) & 0xFFu;  // slot
-        s_cmd[5] = expect;
+        S.cmd[0] = op & 0xFFu;
+        S.cmd[1] = a;
+        S.cmd[2] = b;
+        S.cmd[3] = X;
+        S.cmd[4] = (op >> 8) & 0xFFu;  // slot
+        S.cmd[5] = expect;
       }
     }
     __syncthreads();
-    const uint32_t op = s_cmd[0];
-    const int32_t a = (int32_t)s_cmd[1], b = (int32_t)s_cmd[2], X = (int32_t)s_cmd[3];
-    const uint32_t slot = s_cmd[4], seq = s_cmd[5];
+    const uint32_t op = S.cmd[0];
+    if (op == kOpNone) {  // idle: one pending build
+      const u64 tb = __builtin_amdgcn_s_memrealtime();
+      build_front(p, u.b, S, &nosub, &staged);
+      build_ticks += __builtin_amdgcn_s_memrealtime() - tb;
+      continue;
+    }
+    const int32_t a = (int32_t)S.cmd[1], b = (int32_t)S.cmd[2], X = (int32_t)S.cmd[3];
+    const uint32_t slot = S.cmd[4], seq = S.cmd[5];
     ++expect;
     if (op != kOpMerge && op != kOpUnmerge) {
       exit_op = op;
       break;
     }
-    // ---- the word list of (a, b): wave 0 probes 16 directory slots per round trip
-    u64 t_cmd = 0;
-    if (wid == 0) {
-      if (lane == 0) t_cmd = __builtin_amdgcn_s_memrealtime();
-      const u64 key = pair_key(a, b);
-      const int32_t M = a > b ? a : b;
-      u64 h = mix64(key) & p.dir_mask;
-      u64 off = 0, cnt = 0;
-      bool err = false;
-      for (uint32_t base = 0;; base += 16) {
-        const u64 idx = (h + base + (u64)lane) & p.dir_mask;
-        u64 k = kEmpty64, v = 0;
-        uint32_t sq = 0, vs = 0;
-        if (lane < 16) {
-          k = ld_agent(p.dkey + idx);
-          v = p.dval[idx];
-          sq = p.dseq[idx];
+    // ---- the word list.  Merge (a, b), M = max(a, b): when the loop created M, the group of
+    // the pair in M's sub-table (every word that held the pair when M was created; built first
+    // if it waits), or, when M has no sub-table, M's words-of list filtered by signature; else
+    // the initial directory entry of (a, b) (every word that held the pair when the index was
+    // built).  Undo: the words of X, exactly.  Wave 0: one round trip for the id tables and 16
+    // directory slots, one more for the sub-table.
+    const u64 t_cmd = __builtin_amdgcn_s_memrealtime();
+    u64 t_built = 0;
+    for (;;) {
+      if (wid == 0) {
+        const bool undo = op == kOpUnmerge;
+        const int32_t M = undo ? X : (a > b ? a : b);
+        u64 lv64 = 0;
+        bool lv = false;
+        if (lane >= 16 && lane < 19 && M >= 0 && (uint32_t)M < p.id_cap) {
+          if (lane == 16) lv = p.lseq[M] != kNoList;
+          if (lane == 17) lv64 = p.lst[M];
+          if (lane == 18) lv64 = p.xsub[M];
         }
-        if (lane == 16) vs = M >= kBaseVocab && (uint32_t)M < p.id_cap ? p.valid_seq[M] : 0u;
-        vs = __shfl(vs, 16, 64);
-        const u64 hit = __ballot(lane < 16 && k == key);
-        const u64 emp = __ballot(lane < 16 && k == kEmpty64);
-        const u64 any = hit | emp;
-        if (any) {
-          const int f = __ffsll((long long)any) - 1;
-          if ((hit >> f) & 1ull) {
-            const u64 vf = __shfl(v, f, 64);
-            const uint32_t sf = __shfl(sq, f, 64);
-            if (sf == vs) {
-              off = (uint32_t)vf;
-              cnt = vf >> 32;
-            } else {
-              err = op == kOpMerge;
+        const u64 key = pair_key(a, b);
+        const u64 h = mix64(key) & p.dir_mask;
+        u64 dk = kEmpty64, dv = 0;
+        if (!undo && lane < 16) {
+          dk = p.dkey[(h + (u64)lane) & p.dir_mask];
+          dv = p.dval[(h + (u64)lane) & p.dir_mask];
+        }
+        const bool has_list = (__ballot(lv) >> 16) & 1ull;
+        const u64 wl = __shfl(lv64, 17, 64), xs = __shfl(lv64, 18, 64);
+        u64 off = 0, cnt = 0;
+        bool err = false, filter = false, need = false;
+        if (has_list && !undo && (xs & kSubPending) && S.pend_n) {
+          need = true;
+        } else if (has_list && (undo || !(xs & kSubValid))) {  // (pending with an empty queue: cannot happen)
+          off = (uint32_t)wl;
+          cnt = wl >> 32;
+          filter = !undo;
+        } else if (has_list) {
+          // the pair's delta key in M's table: (c, M) is a new-left pair of neighbour c, (M, d) a
+          // new-right pair of neighbour d, (M, M) new-left (the right neighbour was never M)
+          const uint32_t nk = a == b ? slot_of(M, p.cap) * 4u + 1u
+                                     : b == M ? slot_of(a, p.cap) * 4u + 1u : slot_of(b, p.cap) * 4u + 3u;
+          const uint32_t lg = (uint32_t)(xs >> 32) & 31u, mask = (1u << lg) - 1u;
+          const SubE* tb = p.sub + (uint32_t)xs;
+          const uint32_t h0 = sub_hash(nk, lg);
+          for (uint32_t base = 0;; base += 16) {
+            uint32_t kk = kEmpty32, ko = 0, kc = 0;
+            if (lane < 16) {
+              const SubE se = tb[(h0 + base + (uint32_t)lane) & mask];
+              kk = se.dk;
+              ko = se.off;
+              kc = se.cnt;
             }
-          } else {
-            err = op == kOpMerge;  // a selected pair always has a list
+            const u64 hit = __ballot(lane < 16 && kk == nk);
+            const u64 emp = __ballot(lane < 16 && kk == kEmpty32);
+            const u64 any = hit | emp;
+            if (any) {
+              const int f = __ffsll((long long)any) - 1;
+              if ((hit >> f) & 1ull) {
+                off = __shfl(ko, f, 64);
+                cnt = __shfl(kc, f, 64);
+              } else {
+                err = true;  // a selected pair always has a group
+              }
+              break;
+            }
+            if (base > mask) {
+              err = true;
+              break;
+            }
           }
-          break;
+        } else if (undo) {
+          err = true;  // every merged id has its words-of list
+        } else {
+          for (u64 base = 0;; base += 16) {
+            if (base) {
+              dk = kEmpty64;
+              if (lane < 16) {
+                dk = p.dkey[(h + base + (u64)lane) & p.dir_mask];
+                dv = p.dval[(h + base + (u64)lane) & p.dir_mask];
+              }
+            }
+            const u64 hit = __ballot(lane < 16 && dk == key);
+            const u64 emp = __ballot(lane < 16 && dk == kEmpty64);
+            const u64 any = hit | emp;
+            if (any) {
+              const int f = __ffsll((long long)any) - 1;
+              const u64 vf = __shfl(dv, f, 64);
+              if ((hit >> f) & 1ull) {
+                off = (uint32_t)vf;
+                cnt = vf >> 32;
+              } else {
+                err = true;  // a selected pair always has a list
+              }
+              break;
+            }
+            if (base > p.dir_mask) {
+              err = true;
+              break;
+            }
+          }
         }
-        if (base > p.dir_mask) {
-          err = op == kOpMerge;
-          break;
+        if (lane == 0) {
+          S.need = need ? 1u : 0u;
+          S.lk[0] = off;
+          S.lk[1] = err ? 0 : cnt;
+          S.nout = 0;
+          S.nchg = 0;
+          S.scan = 0;
+          S.nstage = 0;
+          S.bfail = 0;
+          S.nspill = 0;
+          S.filter = filter ? 1u : 0u;
+          S.occ = 0;
+          S.err = 0;
+          S.st[0] = S.st[1] = S.st[2] = 0;
+          if (err) atomicMax(&p.dstate[kStError], undo ? kErrList : kErrLookup);
+          if (!undo && (u64)S.pool_top + cnt > p.pool_cap) {
+            S.err = 1;
+            atomicMax(&p.dstate[kStError], kErrPool);
+          }
+          S.t[0] = __builtin_amdgcn_s_memrealtime() - t_cmd;
         }
       }
-      if (lane == 0) {
-        s_lk[0] = off;
-        s_lk[1] = cnt;
-        s_nout = 0;
-        s_nstage = 0;
-        s_occ = 0;
-        s_changed = 0;
-        if (err) atomicMax(&p.dstate[kStError], kErrLookup);
+      __syncthreads();
+      if (!S.need) break;
+      // M's pair groups wait: build the pending merges up to M's
+      const u64 tb = __builtin_amdgcn_s_memrealtime();
+      const int32_t M = a > b ? a : b;
+      bool more = true;
+      while (more && S.pend_n) {
+        more = S.pend[S.pend_head].X != M;
+        build_front(p, u.b, S, &nosub, &staged);
       }
+      const u64 dt = __builtin_amdgcn_s_memrealtime() - tb;
+      build_ticks += dt;
+      t_built += dt;
     }
     if (op == kOpMerge)
       for (int i = tid; i < kDh; i += kWlThreads) {
-        u.d.key[i] = kEmpty32;
-        u.d.sum[i] = 0;
-        u.d.ft[i] = kEmpty64;
+        s_h.key[i] = kEmpty32;
+        s_h.sum[i] = 0;
+        s_h.ft[i] = kEmpty64;
       }
     __syncthreads();
-    const u64 off = s_lk[0], cnt = s_lk[1];
+    const u64 off = S.lk[0], cnt = S.lk[1];
+    const uint32_t top = S.pool_top;
     if (op == kOpUnmerge) {
-      for (u64 i = tid; i < cnt; i += kWlThreads) unmerge_word(p, p.pool[off + i], a, b, X, seq);
+      for (u64 i = tid; i < cnt; i += kWlThreads) {
+        const u64 e = p.pool[off + i].e;
+        int32_t* r = p.wtok + (uint32_t)(e >> 32);
+        const uint32_t L = (uint32_t)r[0];
+        const uint32_t nl = unmerge_run(r + 1, L, a, b, X);
+        if (nl != L) r[0] = (int32_t)nl;
+      }
       __syncthreads();
-      if (tid == 0 && X >= kBaseVocab && (uint32_t)X < p.id_cap) p.valid_seq[X] = kInvalidSeq;
+      if (tid == 0 && X >= 0 && (uint32_t)X < p.id_cap) {
+        // release the guess's groups, sub-table and list when they are the last ones
+        const u64 xs = p.xsub[X];
+        if (xs & kSubValid) {
+          const u64 xg = p.xgrp[X];
+          if ((uint32_t)(xg >> 32) == S.pool_top) S.pool_top = (uint32_t)xg;
+          const uint32_t so = (uint32_t)xs;
+          if (so >= kSubFirst && so + (1u << ((xs >> 32) & 31u)) == S.sub_top) S.sub_top = so;
+        }
+        if (off + cnt == (u64)S.pool_top) S.pool_top = (uint32_t)off;
+        p.lseq[X] = kNoList;
+        p.xsub[X] = 0;
+      }
       __syncthreads();
       continue;
     }
-    // ---- the merge over the listed words, a lane per word
-    uint32_t my_occ = 0, my_changed = 0;
-    for (u64 i = tid; i < cnt; i += kWlThreads) {
-      const uint32_t m = merge_word(p, u.d, &s_nstage, p.pool[off + i], a, b, X, seq);
-      my_occ += m;
-      my_changed += m ? 1u : 0u;
-    }
-    {
-      const uint32_t wo = wave_incl_add(my_occ), wc = wave_incl_add(my_changed);
-      if (lane == 63 && (wo || wc)) {
-        atomicAdd(&s_occ, (u64)wo);
-        atomicAdd(&s_changed, (u64)wc);
+    // ---- the merge over the listed words; changed words become the words of X.  Each round a
+    // lane loads kB pool entries (coalesced), then merges them one at a time (a words-of list
+    // only where the signature holds a and b): the run in one round trip, the walk in
+    // registers.  A group may name a word twice: the word mark lets one lane take it.
+    const bool append = S.err == 0;
+    const bool filt = S.filter != 0;
+    const u64 need = sig_bit(a) | sig_bit(b);
+    const uint32_t stage_base = S.stage_top;
+    const MergeCtx mc{&S.nstage, &S.bfail, &S.nspill, stage_base,
+                      (uint32_t)std::min<u64>(p.stage_cap - stage_base, 0xFFFFFFFFull), S.st};
+    uint32_t my_occ = 0, my_scan = 0;
+    for (u64 base = 0; base < cnt; base += (u64)kWlThreads * kB) {
+      u64 ex[kB], sx[kB];
+#pragma unroll
+      for (int q = 0; q < kB; ++q) {
+        const u64 i = base + (u64)q * kWlThreads + tid;
+        ex[q] = kEmpty64;
+        sx[q] = 0;
+        if (i < cnt) {
+          const WEnt v = p.pool[off + i];
+          ex[q] = v.e;
+          sx[q] = v.sig;
+        }
+      }
+      if (base == 0 && tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        S.st[0] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
+      }
+#pragma unroll 1
+      for (int q = 0; q < kB; ++q) {
+        u64 e = ex[0], sg = sx[0];
+#pragma unroll
+        for (int z = 1; z < kB; ++z)
+          if (q == z) {
+            e = ex[z];
+            sg = sx[z];
+          }
+        uint32_t occ = 0;
+        u64 nsig = 0;
+        if (e != kEmpty64 && (!filt || (sg & need) == need)) {
+          const uint32_t w = (uint32_t)e;
+          int32_t* r = p.wtok + (uint32_t)(e >> 32);
+          const uint32_t old = atomicExch(&p.wmark[w], seq);
+          const Run x = load_run(r);
+          const u64 wc = p.weight[w];
+          // every load of the word lands here, once: a first use of wc later would wait (vmcnt
+          // counts stores too) for the stores issued by then
+          asm volatile("s_waitcnt vmcnt(0)" ::"v"(old), "v"(wc), "v"(x.v[0].x) : "memory");
+          const uint32_t L = (uint32_t)x.v[0].x;
+          uint32_t nl = L;
+          if (base == 0 && q == 0 && tid == 0) {
+            S.st[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
+            S.st[4] = (uint32_t)__builtin_amdgcn_s_memtime();
+            S.st[5] = S.st[6] = S.st[4];
+          }
+          if (old != seq) {
+            ++my_scan;
+            if (L >= 2) {
+              if (L <= kStripTok) {
+                occ = merge_regs(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig);
+              } else {
+                occ = merge_run(p, s_h, mc, r + 1, L, e, wc, a, b, X, &nl, &nsig);
+                if (occ) r[0] = (int32_t)nl;
+              }
+            }
+            my_occ += occ;
+          }
+          if (base == 0 && q == 0 && tid == 0) {
+            S.st[2] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
+            S.st[7] = (uint32_t)__builtin_amdgcn_s_memtime();
+          }
+        }
+        const u64 chg = __ballot(occ != 0);
+        if (chg) {
+          const int lead = __ffsll((long long)chg) - 1;
+          uint32_t nb = 0;
+          if (lane == lead) nb = atomicAdd(&S.nchg, (uint32_t)__popcll(chg));
+          nb = __shfl(nb, lead, 64);
+          if (occ && append) {
+            const uint32_t rk = (uint32_t)__popcll(chg & ((1ull << lane) - 1ull));
+            WEnt ne;
+            ne.e = e;
+            ne.sig = nsig;
+            p.pool[(u64)top + nb + rk] = ne;
+          }
+        }
       }
     }
+    if (my_occ) atomicAdd(&S.occ, (u64)my_occ);
+    if (my_scan) atomicAdd(&S.scan, my_scan);
     __syncthreads();
+    if (tid == 0) S.t[1] = __builtin_amdgcn_s_memrealtime() - t_cmd;
     // ---- the records to host memory (LDS hash, then the spilled keys), then the flag
     const WlSlotDev& sd = p.sl[slot & (WordLoop::kSlots - 1)];
+    const uint32_t nchg = append ? S.nchg : 0u;
     for (int i = tid; i < kDh; i += kWlThreads) {
-      const uint32_t key = u.d.key[i];
+      const uint32_t key = s_h.key[i];
       if (key == kEmpty32) continue;
-      const uint32_t r = atomicAdd(&s_nout, 1u);
+      const uint32_t r = atomicAdd(&S.nout, 1u);
       u64* dst = reinterpret_cast<u64*>(sd.recs + r);
       dst[0] = (u64)key;
-      dst[1] = u.d.sum[i];
-      dst[2] = u.d.ft[i];
+      dst[1] = s_h.sum[i];
+      dst[2] = s_h.ft[i];
     }
-    __syncthreads();
     {
-      const uint32_t nsp = ld_agent(&p.dstate[kStSpill]);
+      const uint32_t nsp = S.nspill;  // complete: every delta was added before the barrier above
       for (uint32_t i = tid; i < nsp; i += kWlThreads) {
         const uint32_t key = p.dlist[i];
         const u64 sum = atomicExch(&p.dsum[key], 0ull);
         const u64 ft = atomicExch(&p.dft[key], kEmpty64);
-        const uint32_t r = atomicAdd(&s_nout, 1u);
+        const uint32_t r = atomicAdd(&S.nout, 1u);
         u64* dst = reinterpret_cast<u64*>(sd.recs + r);
         dst[0] = (u64)key;
         dst[1] = sum;
@@ -438,100 +868,63 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      p.dstate[kStSpill] = 0;
-      sd.hdr[0] = s_nout;
+      sd.hdr[0] = S.nout;
       sd.hdr[2] = (uint32_t)cnt;
-      sd.hdr[3] = (uint32_t)s_changed;
-      reinterpret_cast<u64*>(sd.hdr)[2] = s_occ;
-      reinterpret_cast<u64*>(sd.hdr)[3] = (u64)__builtin_amdgcn_s_memrealtime() - t_cmd;
+      sd.hdr[3] = S.nchg;
+      u64* h64 = reinterpret_cast<u64*>(sd.hdr);
+      h64[2] = S.occ;
+      h64[3] = (u64)__builtin_amdgcn_s_memrealtime() - t_cmd;
+      h64[4] = S.t[0];
+      h64[5] = S.t[1];
+      sd.hdr[12] = S.scan;
+      sd.hdr[13] = S.filter;
+      sd.hdr[16] = S.st[0];
+      sd.hdr[17] = S.st[1];
+      sd.hdr[18] = S.st[2];
+      sd.hdr[19] = (uint32_t)t_built;
+      sd.hdr[20] = S.st[5] - S.st[4];  // shader clocks: pass 1
+      sd.hdr[21] = S.st[6] - S.st[5];  //   pass 2
+      sd.hdr[22] = S.st[7] - S.st[6];  //   run stores
       __threadfence_system();
       __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    // ---- the index entries of merge X's new pairs (after the flag: off the host's path)
-    uint32_t n = s_nstage < p.stage_cap ? s_nstage : (uint32_t)p.stage_cap;
-    int src = 0;
-    while (n > 0) {
-      for (int i = tid; i < kBh; i += kWlThreads) {
-        u.b.key[i] = kEmpty64;
-        u.b.cnt[i] = 0;
-        u.b.fill[i] = 0;
-      }
-      if (tid == 0) s_ndefer = 0;
-      __syncthreads();
-      for (uint32_t e = tid; e < n; e += kWlThreads) {
-        const u64 key = p.sk[src][e];
-        uint32_t s = (uint32_t)(mix64(key) >> 53) & (kBh - 1);
-        uint32_t got = kEmpty32;
-        for (int probe = 0; probe < 64; ++probe) {
-          const u64 prev = atomicCAS(&u.b.key[s], kEmpty64, key);
-          if (prev == kEmpty64 || prev == key) {
-            got = s;
-            break;
-          }
-          s = (s + 1) & (kBh - 1);
-        }
-        if (got != kEmpty32) {
-          atomicAdd(&u.b.cnt[got], 1u);
-        } else {  // this round's table is full: the entry waits for the next round
-          const uint32_t d = atomicAdd(&s_ndefer, 1u);
-          p.sk[src ^ 1][d] = key;
-          p.sw[src ^ 1][d] = p.sw[src][e];
-        }
-        p.sslot[e] = got;
-      }
-      __syncthreads();
-      {  // exclusive offsets of the slots (2 per thread), the round's total
-        const uint32_t c0 = u.b.cnt[2 * tid], c1 = u.b.cnt[2 * tid + 1];
-        const uint32_t incl = wave_incl_add(c0 + c1);
-        if (lane == 63) s_wsum[wid] = incl;
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-        for (int q = 0; q < kWlWaves; ++q) {
-          before += q < wid ? s_wsum[q] : 0u;
-          total += s_wsum[q];
-        }
-        const uint32_t ex = before + incl - (c0 + c1);
-        u.b.off[2 * tid] = ex;
-        u.b.off[2 * tid + 1] = ex + c0;
-        if (tid == 0) {
-          s_base = s_pool_top;
-          s_total = total;
-          if ((u64)s_pool_top + total > p.pool_cap) atomicMax(&p.dstate[kStError], kErrPool);
-          else s_pool_top += total;
-        }
-      }
-      __syncthreads();
-      const uint32_t base = s_base;
-      const bool fits = (u64)base + s_total <= p.pool_cap;
-      if (fits) {
-        for (uint32_t e = tid; e < n; e += kWlThreads) {
-          const uint32_t s = p.sslot[e];
-          if (s == kEmpty32) continue;
-          const uint32_t pos = base + u.b.off[s] + atomicAdd(&u.b.fill[s], 1u);
-          p.pool[pos] = p.sw[src][e];
-        }
-        for (int s = tid; s < kBh; s += kWlThreads) {
-          const u64 key = u.b.key[s];
-          if (key != kEmpty64) dir_insert(p, key, base + u.b.off[s], u.b.cnt[s], seq);
-        }
-      }
-      __syncthreads();
-      n = s_ndefer;
-      src ^= 1;
-      if (n) {  // deferred entries live in the other buffer pair now; keep buffer 0 the source
-        for (uint32_t e = tid; e < n; e += kWlThreads) {
-          p.sk[0][e] = p.sk[1][e];
-          p.sw[0][e] = p.sw[1][e];
-        }
-        src = 0;
-        __syncthreads();
+    // ---- after the flag (off the host's path): the words of X, and its pair groups queued for
+    // a build (when idle, when a lookup needs them, or when the queue is full)
+    if (tid == 0 && X >= 0 && (uint32_t)X < p.id_cap) {
+      p.lst[X] = (u64)top | ((u64)nchg << 32);
+      p.lseq[X] = seq;
+      S.pool_top = top + nchg;
+      const uint32_t n = S.nstage;
+      if (!append || S.bfail) {
+        p.xsub[X] = 0;  // its words-of list serves
+        ++nosub;
+      } else if (n == 0) {
+        p.xsub[X] = (u64)0 | ((u64)4 << 32) | kSubValid;  // the empty table: X has no pairs
+        p.xgrp[X] = (u64)S.pool_top | ((u64)S.pool_top << 32);
+      } else {
+        p.xsub[X] = kSubPending;
+        const uint32_t q = (S.pend_head + S.pend_n) % kPend;
+        S.pend[q] = PendE{X, seq, stage_base, n};
+        ++S.pend_n;
+        S.stage_top = stage_base + n;
       }
     }
-    if (tid == 0 && X >= kBaseVocab && (uint32_t)X < p.id_cap) p.valid_seq[X] = seq;
     __syncthreads();
+    if (S.pend_n == kPend || (u64)S.stage_top * 2 > p.stage_cap) {
+      const u64 tb = __builtin_amdgcn_s_memrealtime();
+      while (S.pend_n) build_front(p, u.b, S, &nosub, &staged);
+      build_ticks += __builtin_amdgcn_s_memrealtime() - tb;
+    }
   }
+  // the pending groups before the launch ends (the next launch starts with an empty queue)
+  while (S.pend_n) build_front(p, u.b, S, &nosub, &staged);
   if (tid == 0) {
-    p.dstate[kStPoolTop] = s_pool_top;
+    p.dstate[kStPoolTop] = S.pool_top;
+    p.dstate[kStSubTop] = S.sub_top;
+    u64* b64 = reinterpret_cast<u64*>(p.dstate + kStBuild);
+    *b64 += build_ticks;
+    p.dstate[kStNoSub] += nosub;
+    p.dstate[kStStaged] += staged;
     __threadfence_system();
     __hip_atomic_store(&p.status[0], exit_op, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -539,21 +932,22 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
 
 namespace {
 
-// Initial index: pair j of word w goes to entry (woff[w] - w) + j (a word of capacity c owns
-// c - 1 entries); pairs holding unk and capacity past the live length emit EMPTY.
-__global__ void k_wl_emit_pairs(const int32_t* wtok, const uint32_t* woff, const uint32_t* wlen, uint32_t W,
-                                int32_t unk, u64* key, uint32_t* val) {
+// Initial index: entry woff[w] + j holds pair j of word w (tokens j, j + 1); pairs holding unk,
+// pairs past the live length and the run's length/padding slots emit EMPTY.
+__global__ void k_wl_emit_pairs(const int32_t* wtok, const uint32_t* woff, uint32_t W, int32_t unk, u64* key,
+                                uint32_t* val) {
   for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < W; w += gridDim.x * blockDim.x) {
-    const uint32_t o = woff[w], capw = woff[w + 1] - o, L = wlen[w];
-    const uint64_t base = (uint64_t)o - w;
-    for (uint32_t j = 0; j + 1 < capw; ++j) {
+    const uint32_t o = woff[w], span = woff[w + 1] - o;
+    const uint32_t L = (uint32_t)wtok[o];
+    const int32_t* t = wtok + o + 1;
+    for (uint32_t j = 0; j < span; ++j) {
       u64 k = kEmpty64;
       if (j + 1 < L) {
-        const int32_t x = wtok[o + j], y = wtok[o + j + 1];
+        const int32_t x = t[j], y = t[j + 1];
         if (x != unk && y != unk) k = pair_key(x, y);
       }
-      key[base + j] = k;
-      val[base + j] = w;
+      key[o + j] = k;
+      val[o + j] = w;
     }
   }
 }
@@ -570,11 +964,26 @@ __global__ void k_wl_mark(const u64* key, const uint32_t* val, uint64_t n, uint3
   }
 }
 
+// The signature of every word (the ids it holds now).
+__global__ void k_wl_word_sig(const int32_t* wtok, const uint32_t* woff, uint32_t W, u64* wsig) {
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < W; w += gridDim.x * blockDim.x) {
+    const uint32_t o = woff[w], L = (uint32_t)wtok[o];
+    u64 sg = 0;
+    for (uint32_t j = 0; j < L; ++j) sg |= sig_bit(wtok[o + 1 + j]);
+    wsig[w] = sg;
+  }
+}
+
 __global__ void k_wl_scatter(const u64* key, const uint32_t* val, uint64_t n, const uint32_t* keep,
-                             const uint32_t* pos, const uint32_t* head, const uint32_t* kidx, uint32_t* pool,
-                             u64* ikey, u64* ival) {
+                             const uint32_t* pos, const uint32_t* head, const uint32_t* kidx, const uint32_t* woff,
+                             const u64* wsig, WEnt* pool, u64* ikey, u64* ival) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    if (keep[i]) pool[pos[i]] = val[i];
+    if (keep[i]) {
+      WEnt ent;
+      ent.e = ((u64)woff[val[i]] << 32) | val[i];
+      ent.sig = wsig[val[i]];
+      pool[pos[i]] = ent;
+    }
     if (head[i]) {
       ikey[kidx[i]] = key[i];
       ival[kidx[i]] = pos[i];  // offset; the count is filled in by k_wl_counts
@@ -591,8 +1000,7 @@ __global__ void k_wl_counts(u64* ival, uint64_t nk, uint64_t total) {
 }
 
 // The initial directory (after a memset of the keys to EMPTY): no key repeats.
-__global__ void k_wl_dir_init(const u64* ikey, const u64* ival, uint64_t nk, u64* dkey, u64* dval, uint32_t* dseq,
-                              u64 mask) {
+__global__ void k_wl_dir_init(const u64* ikey, const u64* ival, uint64_t nk, u64* dkey, u64* dval, u64 mask) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nk; i += (uint64_t)gridDim.x * blockDim.x) {
     const u64 key = ikey[i];
     u64 h = mix64(key) & mask;
@@ -600,7 +1008,6 @@ __global__ void k_wl_dir_init(const u64* ikey, const u64* ival, uint64_t nk, u64
       const u64 prev = atomicCAS(&dkey[h], kEmpty64, key);
       if (prev == kEmpty64) {
         dval[h] = ival[i];
-        dseq[h] = 0;
         break;
       }
       h = (h + 1) & mask;
@@ -610,9 +1017,9 @@ __global__ void k_wl_dir_init(const u64* ikey, const u64* ival, uint64_t nk, u64
 
 // Words -> tiles: a wave per tile writes [header][tokens] for its words in rank order and the
 // tile's live length; the old tail up to the previous length becomes padding.
-__global__ void k_words_to_tiles(const int32_t* wtok, const uint32_t* woff, const uint32_t* wlen,
-                                 const uint32_t* tile_first, const uint32_t* tile_nw, uint32_t ntiles, int32_t* tok,
-                                 const uint64_t* tile_off, uint32_t* tile_len) {
+__global__ void k_words_to_tiles(const int32_t* wtok, const uint32_t* woff, const uint32_t* tile_first,
+                                 const uint32_t* tile_nw, uint32_t ntiles, int32_t* tok, const uint64_t* tile_off,
+                                 uint32_t* tile_len) {
   const int lane = threadIdx.x & 63;
   const uint32_t waves = gridDim.x * (blockDim.x / 64);
   for (uint32_t t = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); t < ntiles; t += waves) {
@@ -622,20 +1029,44 @@ __global__ void k_words_to_tiles(const int32_t* wtok, const uint32_t* woff, cons
     for (uint32_t q = 0; q < nw; q += 64) {
       const uint32_t w = f + q + (uint32_t)lane;
       const bool on = q + (uint32_t)lane < nw;
-      const uint32_t len = on ? wlen[w] : 0u;
+      const int32_t* s = on ? wtok + woff[w] : wtok;
+      const uint32_t len = on ? (uint32_t)s[0] : 0u;
       const uint32_t need = on ? len + 1u : 0u;
       const uint32_t incl = wave_incl_add(need);
       if (on) {
         int32_t* d = dst + base + incl - need;
         d[0] = (int32_t)((uint32_t)kHeaderBase + w);
-        const int32_t* s = wtok + woff[w];
-        for (uint32_t j = 0; j < len; ++j) d[1 + j] = s[j];
+        for (uint32_t j = 0; j < len; ++j) d[1 + j] = s[1 + j];
       }
       base += __shfl(incl, 63, 64);
     }
     const uint32_t old = tile_len[t];
     for (uint32_t i = base + (uint32_t)lane; i < old; i += 64) dst[i] = INT32_MIN;
     if (lane == 0) tile_len[t] = base;
+  }
+}
+
+// Tiles -> words (inverse of k_words_to_tiles): a thread per tile walks its entries; each word's
+// tokens go to its run after the live length.
+__global__ void k_tiles_to_words(const int32_t* tok, const uint64_t* tile_off, const uint32_t* tile_len,
+                                 uint32_t ntiles, const uint32_t* woff, int32_t* wtok) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
+    const int32_t* src = tok + tile_off[t];
+    const uint32_t n = tile_len[t];
+    int32_t* run = nullptr;
+    uint32_t len = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      const int32_t v = src[i];
+      if (v < kHeaderLimit) {
+        if (run) run[0] = (int32_t)len;
+        const uint32_t w = (uint32_t)(v - kHeaderBase);
+        run = wtok + woff[w];
+        len = 0;
+      } else if (run) {
+        run[1 + len++] = v;
+      }
+    }
+    if (run) run[0] = (int32_t)len;
   }
 }
 
@@ -648,6 +1079,8 @@ T* wl_alloc(size_t n, size_t* acc) {
 }
 
 inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+
+constexpr uint32_t kRunPad = 4 * kStripV + 4;  // ints past the last run (its 16-B loads may overrun)
 
 }  // namespace
 
@@ -684,18 +1117,16 @@ WordLoop::~WordLoop() {
 }
 
 void WordLoop::free_all() {
-  void* ptrs[] = {wtok_, wtok0_, woff_, wlen_, wlen0_, wmark_, tile_first_, tile_nw_, pool_, dkey_, dval_, dseq_,
-                  init_key_, init_val_, valid_seq_, stage_key_[0], stage_key_[1], stage_w_[0], stage_w_[1],
-                  stage_slot_, dsum_, dft_, dlist_, dstate_};
+  void* ptrs[] = {wtok_, wtok0_, woff_, tile_first_, tile_nw_, pool_, dkey_, dval_, init_key_, init_val_,
+                  lst_, lseq_, xsub_, xgrp_, wmark_, sub_, stg_e_, stg_dk_, dsum_, dft_, dlist_, dstate_};
   for (void* p : ptrs)
     if (p) WL_OK(hipFree(p));
   wtok_ = wtok0_ = nullptr;
-  woff_ = wlen_ = wlen0_ = wmark_ = tile_first_ = tile_nw_ = pool_ = dseq_ = valid_seq_ = stage_slot_ = dlist_ =
-      dstate_ = nullptr;
-  dkey_ = dval_ = init_key_ = init_val_ = dsum_ = dft_ = nullptr;
-  stage_key_[0] = stage_key_[1] = nullptr;
-  stage_w_[0] = stage_w_[1] = nullptr;
+  woff_ = tile_first_ = tile_nw_ = lseq_ = wmark_ = stg_dk_ = dlist_ = dstate_ = nullptr;
+  pool_ = dkey_ = dval_ = init_key_ = init_val_ = lst_ = xsub_ = xgrp_ = stg_e_ = dsum_ = dft_ = nullptr;
+  sub_ = nullptr;
   cap_ = id_cap_ = 0;
+  dir_cap_ = 0;
   bytes_ = 0;
   ready_ = false;
 }
@@ -704,14 +1135,16 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
   WL_OK(hipSetDevice(ordinal_));
   if (running_) stop();
   free_all();
-  // the words of the tile stream in rank order (types layout: one entry per distinct word)
+  // the words of the tile stream in rank order (types layout: one entry per distinct word), each
+  // as a 16-B aligned run [length][tokens]
   std::vector<uint32_t> woff, tfirst, tnw;
   std::vector<int32_t> wtok;
   woff.reserve(ts.entries + 1);
-  wtok.reserve(ts.live);
+  wtok.reserve(ts.live + 4 * ts.entries + 8);
   tfirst.reserve(ts.num_tiles());
   tnw.reserve(ts.num_tiles());
   uint32_t expect_rank = 0;
+  uint64_t ntok = 0;
   for (size_t t = 0; t < ts.num_tiles(); ++t) {
     const int32_t* p = ts.tok.data() + ts.off[t];
     tfirst.push_back((uint32_t)woff.size());
@@ -721,64 +1154,64 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
         const uint32_t r = (uint32_t)(p[i] - kHeaderBase);
         if (r != expect_rank) return false;  // not the whole table in rank order: not for this loop
         ++expect_rank;
-        if (wtok.size() >= 0xFFFFFFF0ull) return false;
+        while (wtok.size() & 3) wtok.push_back(0);
+        if (wtok.size() >= 0xFFFFFF00ull) return false;  // offsets are 32-bit
         woff.push_back((uint32_t)wtok.size());
+        wtok.push_back(0);  // the live length
         ++nw;
       } else {
         if (woff.empty()) return false;
         wtok.push_back(p[i]);
+        ++wtok[woff.back()];
+        ++ntok;
       }
     }
     tnw.push_back(nw);
   }
+  while (wtok.size() & 3) wtok.push_back(0);
+  if (wtok.size() >= 0xFFFFFF00ull) return false;
   woff.push_back((uint32_t)wtok.size());
   nwords_ = (uint32_t)(woff.size() - 1);
-  nsym_ = wtok.size();
+  nint_ = wtok.size();
+  ntok_ = ntok;
   ntiles_ = (uint32_t)ts.num_tiles();
-  if (nwords_ == 0 || nsym_ - nwords_ >= (1ull << 31)) return false;  // hipcub sizes are int
-  std::vector<uint32_t> wlen(nwords_);
-  for (uint32_t w = 0; w < nwords_; ++w) {
-    wlen[w] = woff[w + 1] - woff[w];
-    if (wlen[w] == 0) return false;  // words are never empty (strtok)
-  }
+  if (nwords_ == 0 || nint_ >= (1ull << 31)) return false;  // hipcub sizes are int
+  for (uint32_t w = 0; w < nwords_; ++w)
+    if (wtok[woff[w]] == 0) return false;  // words are never empty (strtok)
+  wtok.resize(nint_ + kRunPad, 0);
   weight_ = reinterpret_cast<const unsigned long long*>(d_weight);
   woff_h_ = woff;
-  wtok_ = wl_alloc<int32_t>(nsym_ + 4, &bytes_);
-  wtok0_ = wl_alloc<int32_t>(nsym_ + 4, &bytes_);
+  wtok_ = wl_alloc<int32_t>(nint_ + kRunPad, &bytes_);
+  wtok0_ = wl_alloc<int32_t>(nint_ + kRunPad, &bytes_);
   woff_ = wl_alloc<uint32_t>(nwords_ + 1, &bytes_);
-  wlen_ = wl_alloc<uint32_t>(nwords_, &bytes_);
-  wlen0_ = wl_alloc<uint32_t>(nwords_, &bytes_);
-  wmark_ = wl_alloc<uint32_t>(nwords_, &bytes_);
   tile_first_ = wl_alloc<uint32_t>(ntiles_, &bytes_);
   tile_nw_ = wl_alloc<uint32_t>(ntiles_, &bytes_);
   hipStream_t s = S(stream_);
-  WL_OK(hipMemcpyAsync(wtok0_, wtok.data(), nsym_ * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  WL_OK(hipMemcpyAsync(wtok0_, wtok.data(), (nint_ + kRunPad) * sizeof(int32_t), hipMemcpyHostToDevice, s));
   WL_OK(hipMemcpyAsync(woff_, woff.data(), woff.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-  WL_OK(hipMemcpyAsync(wlen0_, wlen.data(), nwords_ * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   WL_OK(hipMemcpyAsync(tile_first_, tfirst.data(), ntiles_ * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   WL_OK(hipMemcpyAsync(tile_nw_, tnw.data(), ntiles_ * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-  WL_OK(hipMemcpyAsync(wtok_, wtok0_, nsym_ * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-  WL_OK(hipMemcpyAsync(wlen_, wlen0_, nwords_ * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-  WL_OK(hipMemsetAsync(wmark_, 0, nwords_ * sizeof(uint32_t), s));
-  // index capacity: the initial entries (< S), plus <= 2 per occurrence merged (Σ <= S) for
-  // the run and its undone guesses; directory at most 3/4 full
-  const uint64_t npairs = nsym_ - nwords_;
-  pool_cap_ = npairs + 4 * nsym_ + 4096;
-  pool_ = wl_alloc<uint32_t>(pool_cap_, &bytes_);
-  uint64_t want = 2 * (std::min<uint64_t>(npairs, 1ull << 24) + 2 * nsym_) + 4096;
-  dir_cap_ = 1ull << 16;
-  while (dir_cap_ < want && dir_cap_ < (1ull << 28)) dir_cap_ <<= 1;
-  dkey_ = wl_alloc<u64>(dir_cap_, &bytes_);
-  dval_ = wl_alloc<u64>(dir_cap_, &bytes_);
-  dseq_ = wl_alloc<uint32_t>(dir_cap_, &bytes_);
-  stage_cap_ = nsym_ + 4096;  // a merge stages <= 2 pairs per occurrence, <= 1 per token of a word
-  for (int k = 0; k < 2; ++k) {
-    stage_key_[k] = wl_alloc<u64>(stage_cap_, &bytes_);
-    stage_w_[k] = wl_alloc<uint32_t>(stage_cap_, &bytes_);
-  }
-  stage_slot_ = wl_alloc<uint32_t>(stage_cap_, &bytes_);
+  WL_OK(hipMemcpyAsync(wtok_, wtok0_, (nint_ + kRunPad) * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  // pool: the initial index (<= one entry per adjacent pair) and the words-of lists of the run:
+  // a merge lists only the words it shortened, so Σ over a run <= Σ (length - 1); the lists of
+  // undone guesses are released (each is the last one when its undo runs)
+  // pool: the initial index (<= one entry per adjacent pair), the words-of lists (a merge lists
+  // the words it shortened: Σ over a run <= Σ (length - 1)) and the pair groups (<= 2 entries
+  // per occurrence merged: Σ <= 2 Σ (length - 1)); undone guesses release theirs (each is the
+  // last when its undo runs)
+  pool_cap_ = 4 * ntok_ + 4096;
+  pool_ = wl_alloc<u64>(2 * pool_cap_, &bytes_);  // WEnt: entry + signature
+  sub_cap_ = 4 * ntok_ + 16 * 65536;               // Σ 2^k <= 4 x keys, >= 16 per merge
+  sub_ = wl_alloc<uint32_t>(4 * sub_cap_, &bytes_);
+  WL_OK(hipMemsetAsync(sub_, 0xFF, kSubFirst * sizeof(SubE), s));  // the empty table
+  stage_cap_ = 2 * ntok_ + 4096;
+  stg_e_ = wl_alloc<u64>(stage_cap_, &bytes_);
+  stg_dk_ = wl_alloc<uint32_t>(stage_cap_, &bytes_);
+  wmark_ = wl_alloc<uint32_t>(nwords_, &bytes_);
+  WL_OK(hipMemsetAsync(wmark_, 0, (size_t)nwords_ * sizeof(uint32_t), s));
   dstate_ = wl_alloc<uint32_t>(8, &bytes_);
   WL_OK(hipMemsetAsync(dstate_, 0, 8 * sizeof(uint32_t), s));
+  WL_OK(hipStreamSynchronize(s));
   reserve(kBaseVocab + 1);
   build_index();
   ready_ = true;
@@ -789,7 +1222,7 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
 // The index of the current words: every (pair, word) once, grouped by pair.
 void WordLoop::build_index() {
   hipStream_t s = S(stream_);
-  const uint64_t n = nsym_ - nwords_;
+  const uint64_t n = nint_;
   size_t acc = 0;
   u64* kin = wl_alloc<u64>(n, &acc);
   u64* kout = wl_alloc<u64>(n, &acc);
@@ -799,8 +1232,11 @@ void WordLoop::build_index() {
   uint32_t* head = wl_alloc<uint32_t>(n + 1, &acc);
   uint32_t* pos = wl_alloc<uint32_t>(n + 1, &acc);
   uint32_t* kidx = wl_alloc<uint32_t>(n + 1, &acc);
+  u64* wsig = wl_alloc<u64>(nwords_, &acc);
   const int grid = 2048;
-  k_wl_emit_pairs<<<grid, 256, 0, s>>>(wtok_, woff_, wlen_, nwords_, unk_, kin, vin);
+  k_wl_word_sig<<<grid, 256, 0, s>>>(wtok_, woff_, nwords_, wsig);
+  WL_OK(hipGetLastError());
+  k_wl_emit_pairs<<<grid, 256, 0, s>>>(wtok_, woff_, nwords_, unk_, kin, vin);
   WL_OK(hipGetLastError());
   size_t tmp_bytes = 0, tb2 = 0;
   WL_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 64, s));
@@ -820,31 +1256,44 @@ void WordLoop::build_index() {
   WL_OK(hipStreamSynchronize(s));
   init_pool_n_ = tot[0];
   init_keys_n_ = tot[1];
+  if (init_pool_n_ > pool_cap_) fatal("WordLoop: the initial index exceeds the pool");
   if (init_key_) WL_OK(hipFree(init_key_));
   if (init_val_) WL_OK(hipFree(init_val_));
   init_key_ = wl_alloc<u64>(init_keys_n_, &bytes_);
   init_val_ = wl_alloc<u64>(init_keys_n_, &bytes_);
-  k_wl_scatter<<<grid, 256, 0, s>>>(kout, vout, n, keep, pos, head, kidx, pool_, init_key_, init_val_);
+  k_wl_scatter<<<grid, 256, 0, s>>>(kout, vout, n, keep, pos, head, kidx, woff_, wsig, reinterpret_cast<WEnt*>(pool_),
+                                    init_key_, init_val_);
   WL_OK(hipGetLastError());
   k_wl_counts<<<256, 256, 0, s>>>(init_val_, init_keys_n_, init_pool_n_);
   WL_OK(hipGetLastError());
   WL_OK(hipStreamSynchronize(s));
   for (void* p : {(void*)kin, (void*)kout, (void*)vin, (void*)vout, (void*)keep, (void*)head, (void*)pos, (void*)kidx,
-                  tmp})
+                  (void*)wsig, tmp})
     WL_OK(hipFree(p));
+  // the directory: at most half full
+  uint64_t want = 1024;
+  while (want < 2 * init_keys_n_) want <<= 1;
+  if (want != dir_cap_) {
+    if (dkey_) WL_OK(hipFree(dkey_));
+    if (dval_) WL_OK(hipFree(dval_));
+    dir_cap_ = want;
+    dkey_ = wl_alloc<u64>(dir_cap_, &bytes_);
+    dval_ = wl_alloc<u64>(dir_cap_, &bytes_);
+  }
   restore_index();
 }
 
-// The directory and counters as right after build_index().
+// The directory, the words-of lists and the counters as right after build_index().
 void WordLoop::restore_index() {
   hipStream_t s = S(stream_);
   WL_OK(hipMemsetAsync(dkey_, 0xFF, dir_cap_ * sizeof(u64), s));
   if (init_keys_n_) {
-    k_wl_dir_init<<<1024, 256, 0, s>>>(init_key_, init_val_, init_keys_n_, dkey_, dval_, dseq_, dir_cap_ - 1);
+    k_wl_dir_init<<<1024, 256, 0, s>>>(init_key_, init_val_, init_keys_n_, dkey_, dval_, dir_cap_ - 1);
     WL_OK(hipGetLastError());
   }
-  if (valid_seq_) WL_OK(hipMemsetAsync(valid_seq_, 0, id_cap_ * sizeof(uint32_t), s));
-  const uint32_t st[4] = {0, (uint32_t)init_pool_n_, (uint32_t)init_keys_n_, 0};
+  if (lseq_) WL_OK(hipMemsetAsync(lseq_, 0xFF, id_cap_ * sizeof(uint32_t), s));
+  if (xsub_) WL_OK(hipMemsetAsync(xsub_, 0, id_cap_ * sizeof(u64), s));
+  const uint32_t st[8] = {0, (uint32_t)init_pool_n_, kSubFirst, 0, 0, 0, 0, 0};
   WL_OK(hipMemcpyAsync(dstate_, st, sizeof(st), hipMemcpyHostToDevice, s));
   WL_OK(hipStreamSynchronize(s));
 }
@@ -853,8 +1302,7 @@ bool WordLoop::load_current(const TiledStream& ts) {
   WL_OK(hipSetDevice(ordinal_));
   if (!ready_ || !posted_.empty()) return false;
   stop();
-  std::vector<int32_t> wtok(nsym_, 0);
-  std::vector<uint32_t> wlen(nwords_, 0);
+  std::vector<int32_t> wtok(nint_ + kRunPad, 0);
   uint32_t w = 0;
   bool open = false;
   for (size_t t = 0; t < ts.num_tiles(); ++t) {
@@ -865,19 +1313,42 @@ bool WordLoop::load_current(const TiledStream& ts) {
         if ((uint32_t)(p[i] - kHeaderBase) != w || w >= nwords_) return false;
         open = true;
       } else {
-        if (!open || wlen[w] >= woff_h_[w + 1] - woff_h_[w]) return false;
-        wtok[woff_h_[w] + wlen[w]++] = p[i];
+        if (!open) return false;
+        int32_t& len = wtok[woff_h_[w]];
+        if (1u + (uint32_t)len >= woff_h_[w + 1] - woff_h_[w]) return false;  // past the run
+        wtok[woff_h_[w] + 1 + (uint32_t)len] = p[i];
+        ++len;
       }
     }
   }
   if (!open || w + 1 != nwords_) return false;
   hipStream_t s = S(stream_);
-  WL_OK(hipMemcpyAsync(wtok_, wtok.data(), nsym_ * sizeof(int32_t), hipMemcpyHostToDevice, s));
-  WL_OK(hipMemcpyAsync(wlen_, wlen.data(), nwords_ * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  WL_OK(hipMemcpyAsync(wtok_, wtok.data(), wtok.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
   WL_OK(hipStreamSynchronize(s));
   build_index();
   dirty_ = false;
   return true;
+}
+
+void WordLoop::load_tiles(const int32_t* tok, const uint64_t* tile_off, const uint32_t* tile_len) {
+  WL_OK(hipSetDevice(ordinal_));
+  if (!ready_) return;
+  if (!posted_.empty()) fatal("WordLoop::load_tiles with a merge in flight");
+  stop();
+  const int grid = (int)std::min<uint32_t>((ntiles_ + 255) / 256, 4096);
+  k_tiles_to_words<<<std::max(grid, 1), 256, 0, S(stream_)>>>(tok, tile_off, tile_len, ntiles_, woff_, wtok_);
+  WL_OK(hipGetLastError());
+  build_index();
+  dirty_ = false;
+}
+
+void WordLoop::reset_words() {
+  WL_OK(hipSetDevice(ordinal_));
+  if (!ready_) return;
+  if (!posted_.empty()) fatal("WordLoop::reset_words with a merge in flight");
+  stop();
+  WL_OK(hipMemcpyAsync(wtok_, wtok0_, (nint_ + kRunPad) * sizeof(int32_t), hipMemcpyDeviceToDevice, S(stream_)));
+  dirty_ = false;
 }
 
 void WordLoop::reset() {
@@ -886,8 +1357,7 @@ void WordLoop::reset() {
   if (!posted_.empty()) fatal("WordLoop::reset with a merge in flight");
   stop();
   hipStream_t s = S(stream_);
-  WL_OK(hipMemcpyAsync(wtok_, wtok0_, nsym_ * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-  WL_OK(hipMemcpyAsync(wlen_, wlen0_, nwords_ * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  WL_OK(hipMemcpyAsync(wtok_, wtok0_, (nint_ + kRunPad) * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
   restore_index();
   dirty_ = false;
 }
@@ -900,8 +1370,8 @@ void WordLoop::ensure_slots(uint32_t cap) {
     WL_OK(hipHostMalloc((void**)&sl.host_recs, (size_t)rec_cap * sizeof(DeltaRecord), pin));
     WL_OK(hipHostGetDevicePointer(&sl.dev_recs, sl.host_recs, 0));
     if (!sl.host_hdr) {
-      WL_OK(hipHostMalloc((void**)&sl.host_hdr, 64, pin));
-      std::memset(sl.host_hdr, 0, 64);
+      WL_OK(hipHostMalloc((void**)&sl.host_hdr, 128, pin));
+      std::memset(sl.host_hdr, 0, 128);
       WL_OK(hipHostGetDevicePointer(&sl.dev_hdr, sl.host_hdr, 0));
     }
     sl.rec_cap = rec_cap;
@@ -926,14 +1396,25 @@ void WordLoop::reserve(int32_t max_id) {
   dlist_ = wl_alloc<uint32_t>(keys, &bytes_);
   WL_OK(hipMemsetAsync(dsum_, 0, keys * sizeof(u64), s));
   WL_OK(hipMemsetAsync(dft_, 0xFF, keys * sizeof(u64), s));
-  uint32_t* vs = wl_alloc<uint32_t>(cap, &bytes_);
-  WL_OK(hipMemsetAsync(vs, 0, (size_t)cap * sizeof(uint32_t), s));
-  if (valid_seq_) {
-    WL_OK(hipMemcpyAsync(vs, valid_seq_, (size_t)id_cap_ * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  // the words-of lists (ids past the old capacity have none)
+  u64* nl = wl_alloc<u64>(cap, &bytes_);
+  uint32_t* ns = wl_alloc<uint32_t>(cap, &bytes_);
+  u64* nx = wl_alloc<u64>(cap, &bytes_);
+  u64* ne = wl_alloc<u64>(cap, &bytes_);
+  WL_OK(hipMemsetAsync(ns, 0xFF, (size_t)cap * sizeof(uint32_t), s));
+  WL_OK(hipMemsetAsync(nx, 0, (size_t)cap * sizeof(u64), s));
+  if (lseq_) {
+    WL_OK(hipMemcpyAsync(nl, lst_, (size_t)id_cap_ * sizeof(u64), hipMemcpyDeviceToDevice, s));
+    WL_OK(hipMemcpyAsync(ns, lseq_, (size_t)id_cap_ * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    WL_OK(hipMemcpyAsync(nx, xsub_, (size_t)id_cap_ * sizeof(u64), hipMemcpyDeviceToDevice, s));
+    WL_OK(hipMemcpyAsync(ne, xgrp_, (size_t)id_cap_ * sizeof(u64), hipMemcpyDeviceToDevice, s));
     WL_OK(hipStreamSynchronize(s));
-    WL_OK(hipFree(valid_seq_));
+    for (void* q : {(void*)lst_, (void*)lseq_, (void*)xsub_, (void*)xgrp_}) WL_OK(hipFree(q));
   }
-  valid_seq_ = vs;
+  lst_ = nl;
+  lseq_ = ns;
+  xsub_ = nx;
+  xgrp_ = ne;
   id_cap_ = cap;
   cap_ = cap;
   ensure_slots(cap);
@@ -943,25 +1424,23 @@ void WordLoop::reserve(int32_t max_id) {
 void WordLoop::launch() {
   WlParams p{};
   p.wtok = wtok_;
-  p.woff = woff_;
-  p.wlen = wlen_;
-  p.wmark = wmark_;
   p.weight = weight_;
-  p.nwords = nwords_;
-  p.pool = pool_;
+  p.pool = reinterpret_cast<WEnt*>(pool_);
   p.pool_cap = pool_cap_;
   p.dkey = dkey_;
   p.dval = dval_;
-  p.dseq = dseq_;
   p.dir_mask = dir_cap_ - 1;
-  p.valid_seq = valid_seq_;
-  p.id_cap = id_cap_;
-  p.sk[0] = stage_key_[0];
-  p.sk[1] = stage_key_[1];
-  p.sw[0] = stage_w_[0];
-  p.sw[1] = stage_w_[1];
-  p.sslot = stage_slot_;
+  p.lst = lst_;
+  p.lseq = lseq_;
+  p.xsub = xsub_;
+  p.xgrp = xgrp_;
+  p.wmark = wmark_;
+  p.sub = static_cast<SubE*>(sub_);
+  p.sub_cap = sub_cap_;
+  p.stg_e = stg_e_;
+  p.stg_dk = stg_dk_;
   p.stage_cap = stage_cap_;
+  p.id_cap = id_cap_;
   p.dsum = dsum_;
   p.dft = dft_;
   p.dlist = dlist_;
@@ -1009,8 +1488,6 @@ void WordLoop::post_merge(int32_t a, int32_t b, int32_t X) {
   if (!ready_) fatal("WordLoop::post_merge before upload");
   if (posted_.size() >= (size_t)kSlots) fatal("WordLoop: every merge slot is in flight");
   if (X < 0 || (uint32_t)X + 2 > cap_) fatal("WordLoop: merge id beyond the reserved ids");
-  Slot& sl = slot_[(uint32_t)X & (kSlots - 1)];
-  (void)sl;
   const uint32_t seq = post(kOpMerge, a, b, X);
   posted_.push_back({X, a, b, seq, now_seconds()});
   dirty_ = true;
@@ -1040,12 +1517,22 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   wait_flag(sl, pp.seq);
   st_.wait_us += 1e6 * (now_seconds() - pp.t_post);
   const uint32_t* h = sl.host_hdr;
+  const uint64_t* h64 = reinterpret_cast<const uint64_t*>(h);
   const size_t n = h[0];
   st_.merges += 1;
   st_.candidates += h[2];
+  st_.scanned += h[12];
   st_.changed += h[3];
-  st_.occurrences += reinterpret_cast<const uint64_t*>(h)[2];
-  st_.dev_us += 1e-2 * (double)reinterpret_cast<const uint64_t*>(h)[3];  // s_memrealtime: 100 MHz
+  st_.occurrences += h64[2];
+  st_.dev_us += 1e-2 * (double)h64[3];  // s_memrealtime: 100 MHz
+  st_.dev_lookup_us += 1e-2 * (double)h64[4];
+  st_.dev_scan_us += 1e-2 * (double)(h64[5] - h64[4]);
+  if (timing_) {
+    const uint32_t rec[kTraceFields] = {(uint32_t)X, h[2], h[12], h[3], (uint32_t)h64[2], (uint32_t)(10 * h64[3]),
+                                        (uint32_t)(10 * h64[4]), (uint32_t)(10 * (h64[5] - h64[4])),
+                                        h[20], h[21], h[22], 10 * h[19]};
+    trace_.insert(trace_.end(), rec, rec + kTraceFields);
+  }
   if (n > sl.rec_cap) fatal("k_word_loop: record overflow");
   *recs = sl.host_recs;
   return n;
@@ -1071,11 +1558,16 @@ void WordLoop::stop() {
   float ms = 0;
   WL_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]));
   st_.kernel_ms += ms;
-  uint32_t ds[4];
+  uint32_t ds[8];
   WL_OK(hipMemcpy(ds, dstate_, sizeof(ds), hipMemcpyDeviceToHost));
+  st_.build_us += 1e-2 * (double)(ds[kStBuild] | ((uint64_t)ds[kStBuild + 1] << 32));
+  st_.no_sub += ds[kStNoSub];
+  st_.staged += ds[kStStaged];
+  const uint32_t zero[4] = {0, 0, 0, 0};
+  WL_OK(hipMemcpy(dstate_ + kStBuild, zero, sizeof(zero), hipMemcpyHostToDevice));
   if (ds[kStError]) {
-    static const char* what[] = {"", "index pool exhausted", "new-pair staging overflow", "index directory full",
-                                 "a merged pair had no word list"};
+    static const char* what[] = {"", "index pool exhausted", "an undone merge had no word list",
+                                 "sub-table overflow", "a merged pair had no word list"};
     std::fprintf(stderr, "[ERROR]\t k_word_loop: %s (code %u)\n", ds[kStError] < 5 ? what[ds[kStError]] : "?",
                  ds[kStError]);
     fatal("k_word_loop failed");
@@ -1092,7 +1584,7 @@ void WordLoop::sync_tiles(int32_t* tok, const uint64_t* tile_off, uint32_t* tile
   if (!dirty_ || !ready_) return;
   if (running_) stop();
   const int grid = (int)std::min<uint32_t>((ntiles_ + 3) / 4, 4096);
-  k_words_to_tiles<<<std::max(grid, 1), 256, 0, S(stream_)>>>(wtok_, woff_, wlen_, tile_first_, tile_nw_, ntiles_, tok,
+  k_words_to_tiles<<<std::max(grid, 1), 256, 0, S(stream_)>>>(wtok_, woff_, tile_first_, tile_nw_, ntiles_, tok,
                                                            tile_off, tile_len);
   WL_OK(hipGetLastError());
   dirty_ = false;

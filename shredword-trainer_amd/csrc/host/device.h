@@ -86,6 +86,7 @@ class Device : public Backend {
     return speculate_ && !resident_eligible() && !index_eligible() ? kChainMax : 1;
   }
   bool can_overlap() const override {
+    if (switch_pending_) return false;  // drain the resident loop: the indexed loop takes over
     if (index_eligible()) return speculate_;
     return speculate_ && (!resident_eligible() || (uint32_t)max_id_seen_ + 3 < min_slot_cap());
   }
@@ -114,7 +115,22 @@ class Device : public Backend {
   // The indexed merge loop (word_loop.h): the default for the types layout on one GPU.
   void set_index(bool on);
   bool index_on() const { return index_on_; }
-  bool index_eligible() const { return index_on_ && wl_ && wl_->ready() && !exchange_; }
+  // Hybrid: the first merges (each changes many words) run on k_resident, which spreads a merge
+  // over every CU; once a merge changes fewer than switch_occ_ occurrences the indexed loop (one
+  // workgroup, a few round trips per merge) takes over for the rest of train().
+  bool hybrid_resident_phase() const {
+    return hybrid_ && !idx_phase_ && resident_on_ && resident_ok_ && !exchange_ && ntiles_ > 0;
+  }
+  bool index_eligible() const {
+    return index_on_ && wl_ && wl_->ready() && !exchange_ && !hybrid_resident_phase();
+  }
+  void set_hybrid(bool on) {
+    park();
+    hybrid_ = on;
+  }
+  void set_switch_occurrences(uint64_t n) { switch_occ_ = n; }
+  int64_t switch_merge() const { return switch_x_; }
+  double switch_ms() const { return switch_ms_; }
   const WordLoop* word_loop() const { return wl_; }
   uint64_t resident_launches() const { return res_launches_; }
   bool resident_tokens_in_lds() const { return res_lds_tok_; }
@@ -131,7 +147,10 @@ class Device : public Backend {
   // Copies the live token stream back (tests): per entry, header then tokens.
   void download_tokens(std::vector<int32_t>* out);
 
-  void set_timing(bool on) { timing_ = on; }
+  void set_timing(bool on) {
+    timing_ = on;
+    if (wl_) wl_->set_timing(on);
+  }
   const KernelTimes& times() {
     flush_timing(true);
     return times_;
@@ -300,6 +319,14 @@ class Device : public Backend {
   bool index_on_ = true;           // option (SHREDWORD_INDEX / set_option index)
   bool words_stale_ = false;       // a tile-path merge changed the tiles after the words
   bool wl_pristine_index_ = true;  // the loop's initial index is the uploaded table's
+  bool hybrid_ = true;             // option (SHREDWORD_HYBRID / set_option hybrid)
+  bool idx_phase_ = false;         // hybrid: the indexed loop has taken over this train()
+  bool switch_pending_ = false;    // hybrid: a resident merge changed < switch_occ_ occurrences
+  uint64_t switch_occ_ = 2048;     // option (SHREDWORD_SWITCH_OCC / set_option switch_occ)
+  int64_t switch_x_ = -1;          // the first merge id the indexed loop ran (stats)
+  double switch_ms_ = 0;           // Σ host time of the switches (tiles -> words + index build)
+  int32_t reserved_max_id_ = 0;    // the last reserve_ids()
+  void hybrid_switch(int32_t X);
   uint64_t wl_ms_seen_ = 0;        // merges already folded into times_
   double wl_kms_seen_ = 0;         // launch time already folded into times_
 

@@ -41,6 +41,8 @@ struct Trainer {
   uint32_t exchange_bucket = 0;  // records per rank and exchange bucket (0: default)
   int resident = -1;             // LDS-resident merge loop: -1 default (on), 0 off, 1 on
   int index = -1;                // indexed merge loop: -1 default (on), 0 off, 1 on
+  int hybrid = -1;               // resident first, indexed after: -1 default (on), 0 off, 1 on
+  int64_t switch_occ = -1;       // hybrid switch: occurrences of a resident merge below which (-1 default)
   int spec_depth = 0;            // resident guesses in flight (0: env SHREDWORD_SPEC_DEPTH or default)
   bool gpu_load = true;          // count the corpus words on the device (types layout)
   double load_s = 0;
@@ -98,6 +100,14 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
   } else if (key == "index") {
     t->index = std::atoi(val.c_str()) != 0 ? 1 : 0;
     if (t->dev) t->dev->set_index(t->index != 0);
+  } else if (key == "hybrid") {
+    t->hybrid = std::atoi(val.c_str()) != 0 ? 1 : 0;
+    if (t->dev) t->dev->set_hybrid(t->hybrid != 0);
+  } else if (key == "switch_occ") {
+    const long long n = std::atoll(val.c_str());
+    if (n < 0) return -1;
+    t->switch_occ = n;
+    if (t->dev) t->dev->set_switch_occurrences((uint64_t)n);
   } else if (key == "spec_depth") {
     const int d = std::atoi(val.c_str());
     if (d < 1 || d > Device::kResSlots - 1) return -1;
@@ -131,6 +141,8 @@ bool ensure_device(Trainer* t, const char* caller) {
     t->dev->set_unk(t->config.unk_id);
     if (t->resident >= 0) t->dev->set_resident(t->resident != 0);
     if (t->index >= 0) t->dev->set_index(t->index != 0);
+    if (t->hybrid >= 0) t->dev->set_hybrid(t->hybrid != 0);
+    if (t->switch_occ >= 0) t->dev->set_switch_occurrences((uint64_t)t->switch_occ);
     t->dev->set_spec_depth(t->spec_depth ? t->spec_depth : env_int("SHREDWORD_SPEC_DEPTH", 1));
     if (dist_active() || t->local_exchange) {
       Device::Exchange x;
@@ -326,6 +338,15 @@ int64_t shred_debug_tokens(Trainer* t, int32_t* out, size_t cap) {
   return (int64_t)v.size();
 }
 
+int64_t shred_index_trace(Trainer* t, uint32_t* out, size_t cap) {
+  if (!t || !t->dev) return -1;
+  const WordLoop* wl = t->dev->word_loop();
+  if (!wl) return 0;
+  const std::vector<uint32_t>& v = wl->trace();
+  if (out) std::memcpy(out, v.data(), std::min(cap, v.size()) * sizeof(uint32_t));
+  return (int64_t)v.size();
+}
+
 int shred_get_stats(const Trainer* tc, ShredStats* s) {
   if (!tc || !s) return -1;
   Trainer* t = const_cast<Trainer*>(tc);
@@ -367,6 +388,14 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
       s->index_ms = w.kernel_ms;
       s->index_dev_us = w.dev_us;
       s->index_wait_us = w.wait_us;
+      s->index_dev_lookup_us = w.dev_lookup_us;
+      s->index_dev_scan_us = w.dev_scan_us;
+      s->index_scanned = w.scanned;
+      s->index_build_us = w.build_us;
+      s->index_no_sub = w.no_sub;
+      s->index_staged = w.staged;
+      s->index_switch_merge = t->dev->switch_merge();
+      s->index_switch_ms = t->dev->switch_ms();
     }
   }
   {

@@ -1,30 +1,35 @@
 // The indexed merge loop (types layout, one GPU): K2+K3 of SURVEY.md §7.1 driven by an exact
-// pair -> words occurrence index instead of a scan of the whole token table (§8 f3 "tile
-// skipping ... or an occurrence index").
+// word index instead of a scan of the whole token table (§8 f3 "tile skipping ... or an
+// occurrence index").
 //
 // Why an index.  A merge of (a, b) only changes the words that hold (a, b).  The reference finds
 // them by walking every symbol of every word twice per merge (recompute_freq bpe.cpp:52-65 and
-// the merge scan bpe.cpp:265-296); on C3 that is 15 M symbols per merge for ~280 words that
-// actually change.  Two facts make an exact index cheap to keep:
-//  * a merge creates adjacencies only next to its new id X: (p, X) and (X, n) (bpe.cpp:274-290),
-//    so the words holding a pair (c, d) are all listed either by the initial index (every pair of
-//    the table when the index was built) or by the one merge that created max(c, d);
-//  * lists may over-approximate (a listed word that no longer holds the pair is scanned and left
-//    alone), so nothing is ever removed from them.
-// The device therefore holds, in HBM: the table as one int32 run per word (rank order, capacity =
-// initial length, live length beside it), a pool of word ids, and an open-addressing directory
-// pair -> (pool offset, count, creating command).  Merge X scans only the words its pair lists,
-// emits the reference's four neighbour deltas per occurrence (reduced per (neighbour, category)
-// with the minimum first touch, exactly as k_resident/k_merge do), compacts each word in place,
-// hands the records to the host, and then appends the words of every new pair (p, X) / (X, n) to
-// the pool under a directory entry of its own.
+// the merge scan bpe.cpp:265-296); on C3 that is 15 M symbols per merge for ~300 words that
+// actually change.  Two facts give an index that costs nothing to extend:
+//  * only merge X creates the id X (bpe.cpp:274-290), so every word that ever holds X is one of
+//    the words merge X changed: that list ("words of X") is a superset of the holders of X for
+//    the rest of the run;
+//  * a merge never makes two older ids adjacent (it only puts X next to its neighbours), so a
+//    pair of ids that predate the index occurs only where it occurred when the index was built.
+// Hence the words of pair (c, d): the shorter words-of list of c and d when either was created by
+// the loop, else the initial pair index (every adjacent pair of the table at build time, grouped
+// by pair).  Lists may over-approximate (a listed word that no longer holds the pair is scanned
+// and left alone), so nothing is ever removed from them.
+//
+// Device layout, in HBM: one run per word in rank order, 16-B aligned, [live length][tokens ...]
+// (capacity = the initial length); a pool of u64 word entries (run offset << 32 | word id); the
+// initial pair index as an open-addressing directory pair -> (pool offset, count); per id X the
+// words-of list (pool offset, count) and the command that made it.  Merge X scans the words its
+// pair lists, emits the reference's four neighbour deltas per occurrence (reduced per
+// (neighbour, category) with the minimum first touch, as k_resident/k_merge do), compacts each
+// word in place, appends the words it changed to the pool as the words of X, and hands the
+// records to the host.  A wrong guess is undone exactly: UNMERGE expands X back into (a, b) in
+// the words of X and releases its list.
 //
 // Execution: one persistent workgroup of 1024 threads (k_word_loop) polls a command ring in
 // pinned host memory, so a merge costs a handful of dependent memory round trips instead of a
 // fan-out to 256 workgroups and a fan-in.  One workgroup is always co-resident, so the launch
-// cannot deadlock on partial residency whatever else holds the GPU.  Speculative guesses are
-// undone exactly (UNMERGE expands X back into (a, b) in the words of (a, b)'s list; the guess's
-// directory entries are invalidated by its command number).
+// cannot deadlock on partial residency whatever else holds the GPU.
 #pragma once
 
 #include <cstddef>
@@ -39,14 +44,19 @@ namespace shred {
 struct WordLoopStats {
   uint64_t merges = 0;        // merges collected
   uint64_t undos = 0;         // guesses undone
-  uint64_t candidates = 0;    // Σ listed words scanned by collected merges
+  uint64_t candidates = 0;    // Σ listed words of collected merges
+  uint64_t scanned = 0;       //   of which: words whose runs were read (signature hits)
   uint64_t changed = 0;       // Σ words a collected merge changed
   uint64_t occurrences = 0;   // Σ occurrences merged
   uint64_t launches = 0;      // persistent launches
   double kernel_ms = 0;       // Σ launch durations (HIP events)
   double dev_us = 0;          // Σ device time command seen -> flag raised (s_memrealtime)
+  double dev_lookup_us = 0;   //   of which: command seen -> word list known
+  double dev_scan_us = 0;     //   of which: word list known -> every listed word merged
   double wait_us = 0;         // Σ host time post -> flag seen
-  uint64_t build_rounds = 0;  // index build rounds (> merges when a merge had > 2048 new pairs)
+  double build_us = 0;        // Σ device time building pair groups (after the flags)
+  uint64_t no_sub = 0;        // merges whose pair groups were not built (their words-of list serves)
+  uint64_t staged = 0;        // Σ pair-group entries written
 };
 
 class WordLoop {
@@ -70,6 +80,11 @@ class WordLoop {
   bool load_current(const TiledStream& ts);
   // Re-indexes the current words (the initial index then describes them).
   void rebuild() { build_index(); }
+  // The current words from the device tile stream of the same table (tok, tile_off, tile_len in
+  // device memory; the tile path merged them), then re-indexed: all on the device.
+  void load_tiles(const int32_t* tok, const uint64_t* tile_off, const uint32_t* tile_len);
+  // Back to the uploaded words without restoring the initial index (a load_tiles follows).
+  void reset_words();
   // Delta slots and id tables for ids <= max_id (stops the launch if they must grow).
   void reserve(int32_t max_id);
 
@@ -91,7 +106,16 @@ class WordLoop {
   void mark_tiles_current() { dirty_ = false; }
 
   const WordLoopStats& stats() const { return st_; }
-  void clear_stats() { st_ = WordLoopStats(); }
+  void clear_stats() {
+    st_ = WordLoopStats();
+    trace_.clear();
+  }
+  // Per collected merge while timing is on, kTraceFields u32 each: X, listed words, scanned
+  // words, changed words, occurrences, device ns command -> flag, of which lookup ns, scan ns;
+  // then thread 0's stamps (ns after the command): pool entries loaded, first run loaded, first
+  // word merged; and ns spent building pair groups this merge needed first.
+  static constexpr int kTraceFields = 12;
+  const std::vector<uint32_t>& trace() const { return trace_; }
   void set_timing(bool on) { timing_ = on; }
   size_t device_bytes() const { return bytes_; }
   uint32_t words() const { return nwords_; }
@@ -125,39 +149,41 @@ class WordLoop {
   bool ready_ = false, running_ = false, dirty_ = false, timing_ = false;
 
   uint32_t nwords_ = 0;
-  uint64_t nsym_ = 0;          // Σ word capacities
+  uint64_t nint_ = 0;          // int32 elements of the word runs (lengths + tokens + padding)
+  uint64_t ntok_ = 0;          // Σ initial word lengths
   uint32_t ntiles_ = 0;
-  int32_t* wtok_ = nullptr;    // tokens, word w at [woff[w], woff[w] + wcap)
+  int32_t* wtok_ = nullptr;    // word w: run at woff[w] (16-B aligned) = [live length][tokens]
   int32_t* wtok0_ = nullptr;   // pristine copy
   uint32_t* woff_ = nullptr;   // W + 1
   std::vector<uint32_t> woff_h_;
-  uint32_t* wlen_ = nullptr;   // live length
-  uint32_t* wlen0_ = nullptr;
-  uint32_t* wmark_ = nullptr;  // last command that claimed the word (duplicate list entries)
   const unsigned long long* weight_ = nullptr;
   uint32_t* tile_first_ = nullptr;  // per tile: first word, count (sync_tiles)
   uint32_t* tile_nw_ = nullptr;
   // index
-  uint32_t* pool_ = nullptr;
+  unsigned long long* pool_ = nullptr;   // word entries {run offset << 32 | word id, id signature}
   uint64_t pool_cap_ = 0;
-  unsigned long long* dkey_ = nullptr;   // directory: pair key (EMPTY = ~0)
-  unsigned long long* dval_ = nullptr;   //            pool offset | count << 32
-  uint32_t* dseq_ = nullptr;   //            creating command (0 = initial index)
+  unsigned long long* dkey_ = nullptr;   // initial pair directory: pair key (EMPTY = ~0)
+  unsigned long long* dval_ = nullptr;   //   pool offset | count << 32
   uint64_t dir_cap_ = 0;
   unsigned long long* init_key_ = nullptr;   // the initial index as sorted runs (restore on reset)
   unsigned long long* init_val_ = nullptr;
   uint64_t init_keys_n_ = 0;
   uint64_t init_pool_n_ = 0;
-  uint32_t* valid_seq_ = nullptr;  // per id: the command whose directory entries are valid
-  uint32_t id_cap_ = 0;
-  unsigned long long* stage_key_[2] = {};    // per merge: new pairs (key, word), and the deferred round
-  uint32_t* stage_w_[2] = {};
-  uint32_t* stage_slot_ = nullptr;
+  unsigned long long* lst_ = nullptr;    // per id: words-of list, pool offset | count << 32
+  uint32_t* lseq_ = nullptr;             // per id: the command that made the list (~0: none)
+  unsigned long long* xsub_ = nullptr;   // per id: pair-group sub-table (offset | log2 size << 32 | valid)
+  unsigned long long* xgrp_ = nullptr;   // per id: its pair groups' pool range (start | end << 32)
+  uint32_t* wmark_ = nullptr;            // per word: the last command that scanned it
+  void* sub_ = nullptr;                  // sub-tables (16-B entries)
+  uint64_t sub_cap_ = 0;
+  unsigned long long* stg_e_ = nullptr;  // staged group entries of the merges whose groups wait
+  uint32_t* stg_dk_ = nullptr;
   uint64_t stage_cap_ = 0;
-  unsigned long long* dsum_ = nullptr;       // delta spill tables (keys past the LDS hash), 4 x (cap + 1)
+  uint32_t id_cap_ = 0;
+  unsigned long long* dsum_ = nullptr;   // delta spill tables (keys past the LDS hash), 4 x (cap + 1)
   unsigned long long* dft_ = nullptr;
   uint32_t* dlist_ = nullptr;
-  uint32_t* dstate_ = nullptr;     // [0] spill count, [1] pool top, [2] directory keys, [3] error
+  uint32_t* dstate_ = nullptr;     // [0] spill count, [1] pool top, [2] sub top, [3] error, [4..7] stats
   uint32_t cap_ = 0;               // delta slots: ids < cap_ have slot id + 1
 
   Slot slot_[kSlots];
@@ -169,6 +195,7 @@ class WordLoop {
   std::vector<Post> posted_;
   void* ev_[2] = {};
   WordLoopStats st_;
+  std::vector<uint32_t> trace_;
   size_t bytes_ = 0;
 };
 

@@ -10,7 +10,7 @@ import ctypes
 import os
 import sysconfig
 from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_int, c_int32, c_int64,
-                    c_size_t, c_uint64, c_void_p)
+                    c_size_t, c_uint32, c_uint64, c_void_p)
 
 
 def _get_lib_path():
@@ -84,7 +84,10 @@ class ShredStats(Structure):
                 ("index_on", c_uint64), ("index_merges", c_uint64), ("index_undos", c_uint64),
                 ("index_launches", c_uint64), ("index_candidates", c_uint64), ("index_changed", c_uint64),
                 ("index_occurrences", c_uint64), ("index_ms", c_double), ("index_dev_us", c_double),
-                ("index_wait_us", c_double)]
+                ("index_wait_us", c_double),
+                ("index_dev_lookup_us", c_double), ("index_dev_scan_us", c_double),
+                ("index_scanned", c_uint64), ("index_build_us", c_double), ("index_no_sub", c_uint64),
+                ("index_staged", c_uint64), ("index_switch_merge", c_int64), ("index_switch_ms", c_double)]
 
 
 Trainer = c_void_p
@@ -119,6 +122,7 @@ lib.shred_probe_merge.argtypes, lib.shred_probe_merge.restype = [Trainer, c_int3
 if hasattr(lib, "shred_probe_rollback"):  # diagnostics (absent from older builds)
     lib.shred_probe_rollback.argtypes, lib.shred_probe_rollback.restype = [Trainer, c_int32, c_int32], c_int
     lib.shred_debug_tokens.argtypes, lib.shred_debug_tokens.restype = [Trainer, POINTER(c_int32), c_size_t], c_int64
+    lib.shred_index_trace.argtypes, lib.shred_index_trace.restype = [Trainer, POINTER(c_uint32), c_size_t], c_int64
 lib.shred_get_stats.argtypes, lib.shred_get_stats.restype = [Trainer, POINTER(ShredStats)], c_int
 lib.shred_device_count.argtypes, lib.shred_device_count.restype = [], c_int
 lib.shred_hbm_probe.argtypes = [c_int, c_size_t, c_int, POINTER(c_double), POINTER(c_double)]

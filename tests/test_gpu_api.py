@@ -284,6 +284,39 @@ def test_index_lockstep(depth, medium_corpus, tmp_path):
     assert paths[0] == paths[1]
 
 
+@pytest.mark.parametrize("switch_occ", [300, 1 << 40])
+def test_hybrid_lockstep(switch_occ, medium_corpus):
+    """The hybrid path (k_resident, then the indexed loop from the first merge that changes fewer
+    than switch_occ occurrences) against the launch path in bpe_merge_batch chunks: the same
+    merges and device token stream after every chunk (the switch happens inside a chunk)."""
+    from shredword.cbase import lib
+    ts = []
+    for hybrid in (0, 1):
+        t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+        if hybrid:
+            t.set_option("switch_occ", switch_occ)
+        else:
+            t.set_option("resident", 0)
+            t.set_option("index", 0)
+        t.load_corpus(medium_corpus)
+        lib.bpe_init(t.trainer)
+        ts.append(t)
+    done = 0
+    for chunk in [1, 300, 7, 1000, 64] * 20:
+        na = lib.bpe_merge_batch(ts[0].trainer, chunk)
+        nb = lib.bpe_merge_batch(ts[1].trainer, chunk)
+        assert na == nb
+        xa, xb = ts[0].tokens(), ts[1].tokens()
+        assert xa.shape == xb.shape and (xa == xb).all(), f"streams differ after {done + na} merges"
+        done += na
+        if na < chunk:
+            break
+    st = ts[1].stats()
+    assert st["resident_launches"] > 0 and st["index_merges"] > 0 and st["index_switch_merge"] >= 256
+    for t in ts:
+        t.destroy()
+
+
 def test_index_after_tile_path_merges(medium_corpus, tmp_path):
     """Merges on the tile path (index off) followed by indexed merges (index on) on the same
     trainer: the loop re-reads the merged tiles and re-indexes them; then reset() returns to the

@@ -11,7 +11,8 @@ from conftest import PKG, golden_cases
 pytestmark = pytest.mark.gpu
 
 
-def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None, index=1, spec_depth=None, speculate=None):
+def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None, index=1, spec_depth=None, speculate=None,
+           hybrid=None, switch_occ=None):
     from shredword.trainer import BPETrainer
 
     cfg = case["config"]
@@ -23,6 +24,10 @@ def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None, index
     t.set_option("trace", trace)
     t.set_option("resident", resident)
     t.set_option("index", index)
+    if hybrid is not None:
+        t.set_option("hybrid", hybrid)
+    if switch_occ is not None:
+        t.set_option("switch_occ", switch_occ)
     if spec_depth is not None:
         t.set_option("spec_depth", spec_depth)
     if speculate is not None:
@@ -52,14 +57,40 @@ DEEP = [n for n in API_CASES if "v32000" in n or "v64000" in n]
 
 @pytest.mark.parametrize("name", API_CASES)
 def test_types_layout_matches_reference(name, case_corpus, tmp_path):
-    """Default path: the indexed merge loop (k_word_loop: pair -> words index, one persistent
-    workgroup, speculation depth 1)."""
+    """Default path: hybrid — k_resident while a merge changes many words, then the indexed merge
+    loop (k_word_loop: word lists, one persistent workgroup, speculation depth 1)."""
     case, corpus = case_corpus(name)
     st = {}
     _check(case, _train(case, corpus, tmp_path, "types", stats=st))
     if case["merges"] > 0:
+        assert st["index_on"] == 1
+        if not name.startswith("adv_"):  # (a word longer than a tile: the launch path, then the loop)
+            assert st["resident_launches"] > 0 or st["index_merges"] >= case["merges"]
+
+
+@pytest.mark.parametrize("name", API_CASES)
+def test_index_loop_matches_reference(name, case_corpus, tmp_path):
+    """The indexed merge loop from the first merge (hybrid off)."""
+    case, corpus = case_corpus(name)
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, hybrid=0))
+    if case["merges"] > 0:
         assert st["index_merges"] >= case["merges"] and st["index_on"] == 1
         assert st["resident_launches"] == 0
+
+
+@pytest.mark.parametrize("switch_occ", [1 << 40, 300, 0])
+@pytest.mark.parametrize("name", [n for n in API_CASES if not n.startswith("adv_") and "v64000" not in n])
+def test_hybrid_switch_points(name, switch_occ, case_corpus, tmp_path):
+    """The resident -> indexed switch after the first resident merge, at a mid-run merge, and
+    never: the same bytes."""
+    case, corpus = case_corpus(name)
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, switch_occ=switch_occ))
+    if case["merges"] > 2 and switch_occ == 1 << 40:
+        assert st["resident_launches"] > 0 and st["index_switch_merge"] >= 256 and st["index_merges"] > 0
+    if switch_occ == 0 and case["merges"] > 0:
+        assert st["index_merges"] == 0 and st["index_switch_merge"] == -1
 
 
 @pytest.mark.parametrize("name", API_CASES)
@@ -67,7 +98,7 @@ def test_index_loop_no_speculation_matches_reference(name, case_corpus, tmp_path
     """The indexed loop one merge at a time (no guesses, so no undo)."""
     case, corpus = case_corpus(name)
     st = {}
-    _check(case, _train(case, corpus, tmp_path, "types", stats=st, speculate=0))
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, speculate=0, hybrid=0))
     assert st["index_undos"] == 0
 
 
@@ -77,7 +108,7 @@ def test_index_loop_deep_speculation_matches_reference(name, case_corpus, tmp_pa
     when the replay picks otherwise)."""
     case, corpus = case_corpus(name)
     st = {}
-    _check(case, _train(case, corpus, tmp_path, "types", stats=st, spec_depth=3))
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, spec_depth=3, hybrid=0))
     if case["merges"] > 200:
         assert st["index_undos"] > 0 and st["spec_hits"] > 0
 
