@@ -2852,6 +2852,7 @@ void Device::reset_tokens() {
   index_.reset();
   idx_phase_ = false;
   switch_pending_ = false;
+  sw_n_ = 0;
   if (wl_) {
     if (hybrid_resident_phase()) {  // the switch re-indexes the merged words
       wl_->reset_words();
@@ -3892,7 +3893,14 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   }
   if (timing_) times_.merge_bytes += 4.0 * (double)live_tokens_est_;
   ++res_merges_;
-  if (hybrid_ && !idx_phase_ && index_on_ && wl_ && wl_->ready() && hs[0] < switch_occ_) switch_pending_ = true;
+  if (hybrid_ && !idx_phase_ && index_on_ && wl_ && wl_->ready()) {
+    // entries merged per merge is far from monotone (a frequent pair of a few common words sits
+    // between pairs spread over many words): switch once a whole window of merges stayed small
+    sw_win_[sw_n_++ % kSwitchWindow] = hs[0];
+    uint64_t mx = 0;
+    for (uint64_t v : sw_win_) mx = std::max(mx, v);
+    if (sw_n_ >= kSwitchWindow && mx < switch_occ_) switch_pending_ = true;
+  }
   live_tokens_est_ -= hs[0];
   records_total_ += n;
   records_max_ = std::max<uint64_t>(records_max_, n);

@@ -47,24 +47,19 @@ namespace {
 typedef unsigned long long u64;
 
 constexpr int kWlThreads = 512;
-constexpr int kWlWaves = kWlThreads / 64;
 constexpr int kDh = 2048;               // LDS delta hash slots
 constexpr int kStripV = 6;              // 16-B loads per word run: [length][23 tokens]
 constexpr int kStrip = 4 * kStripV;     // ints per lane in the LDS strip
 constexpr uint32_t kStripTok = kStrip - 1;
-constexpr int kB = 2;                   // pool entries per lane per scan round (one load batch)
-constexpr int kBh = 2048;               // LDS slots of a build's key grouping and of its sub-table
-constexpr int kPend = 64;               // merges whose pair groups wait to be built
+constexpr int kB = 8;                   // pool entries per lane per scan round (one load batch)
+constexpr int kQ = kWlThreads * kB + kWlThreads;  // LDS queue of filtered entries (a round + a remainder)
 constexpr uint32_t kRing = 64;          // command ring entries
-constexpr uint32_t kOpNone = 0, kOpMerge = 1, kOpStop = 2, kOpTimeout = 3, kOpUnmerge = 4;
+constexpr uint32_t kOpMerge = 1, kOpStop = 2, kOpTimeout = 3, kOpUnmerge = 4;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
 constexpr u64 kEmpty64 = ~0ull;
 constexpr uint32_t kNoList = 0xFFFFFFFFu;
-constexpr u64 kSubValid = 1ull << 40, kSubPending = 1ull << 41;
-constexpr uint32_t kSubFirst = 16;      // sub-table entries [0, 16): the empty table (X has no pairs)
-// dstate words: [0] unused, [1] pool top, [2] sub-table top, [3] error, [4..5] build ticks,
-// [6] merges without a sub-table, [7] staged entries (u32, wraps)
-constexpr int kStPoolTop = 1, kStSubTop = 2, kStError = 3, kStBuild = 4, kStNoSub = 6, kStStaged = 7;
+// dstate words: [1] pool top, [3] error
+constexpr int kStPoolTop = 1, kStError = 3;
 // error codes (dstate[kStError], reported by the host)
 constexpr uint32_t kErrPool = 1, kErrList = 2, kErrLookup = 4;
 
@@ -78,45 +73,33 @@ struct WlSlotDev {
                       //   [4..5] occurrences (u64), [6..7] device ticks command -> flag (u64),
                       //   [8..9] ticks command -> list known, [10..11] ticks command -> words merged,
                       //   [12] words whose runs were read, [13] 1: a filtered words-of list,
-                      //   [16..19] stamps (10 ns ticks after the command, thread 0): pool entries
-                      //   loaded, first run loaded, first word merged, ticks in builds this command
+                      //   [16..18] stamps (10 ns ticks after the command, thread 0): pool entries
+                      //   loaded, first run loaded, first word merged
   uint32_t rec_cap;
 };
 
-// A pool entry: the word and a 64-bit signature of the ids it held when the entry was written
-// (bit sig_bit(id) per id; zero in the pair groups, which need no filter).  A words-of entry of id
-// M was written when M was created; every id older than M that the word holds now it held then
-// (only merge c creates c), so a word holding (c, d) now, max(c, d) <= M, has both bits.
+// A pool entry: the word and a 64-bit filter.  In the words-of list of id M (the words merge M
+// changed) the filter holds a bit per (neighbour, side) of M in the word right after merge M:
+// nbit(p, 0) for each left neighbour p (X when just produced), nbit(n, 1) for each original
+// token n after the pair.  A merge never makes two older ids adjacent, so every adjacency
+// (c, M) / (M, d) the word holds later it held right after merge M: a word holding the pair
+// now has its bit.  Initial-index entries (exact lists) hold all ones.
 struct WEnt {
   u64 e;    // run offset << 32 | word id
   u64 sig;
 };
 
-// Pair groups of id X: a per-X open-addressing table (2^k entries) keyed by the delta key of the
-// new pair, slot(neighbour) * 4 + category (kNewLeft: (p, X), kNewRight: (X, n)).
-struct SubE {
-  uint32_t dk, off, cnt, pad;
-};
-
 struct WlParams {
   int32_t* wtok;
   const u64* weight;
-  uint32_t* wmark;   // per word: the last command that scanned it (a group may list a word twice)
   WEnt* pool;
   u64 pool_cap;
-  SubE* sub;
-  u64 sub_cap;
   const u64* dkey;
   const u64* dval;
   u64 dir_mask;
   u64* lst;          // per id: words-of list, pool offset | count << 32
   uint32_t* lseq;    // per id: the command that made it (~0: none)
-  u64* xsub;         // per id: sub-table offset | log2 size << 32 | kSubValid, or kSubPending
-  u64* xgrp;         // per id: its groups' pool range, start | end << 32
   uint32_t id_cap;
-  uint32_t* stg_dk;  // staged new pairs of the merges whose groups wait: delta key, pool entry
-  u64* stg_e;
-  u64 stage_cap;
   u64* dsum;
   u64* dft;
   uint32_t* dlist;
@@ -142,8 +125,11 @@ __device__ __forceinline__ u64 pair_key(int32_t a, int32_t b) { return ((u64)(ui
 __device__ __forceinline__ uint32_t slot_of(int32_t id, uint32_t cap) {
   return (uint32_t)id < cap ? (uint32_t)id + 1u : 0u;
 }
-__device__ __forceinline__ u64 sig_bit(int32_t id) { return 1ull << (((uint32_t)id * 0x9E3779B1u) >> 26); }
-__device__ __forceinline__ uint32_t sub_hash(uint32_t dk, uint32_t lg) { return (dk * 0x9E3779B1u) >> (32 - lg); }
+// filter bit of neighbour id on side s (0: left of M, 1: right of M)
+__device__ __forceinline__ u64 nbit(int32_t id, uint32_t s) {
+  const uint32_t v = (uint32_t)id * 2u + s;
+  return 1ull << ((v ^ (v >> 6) ^ (v >> 12) ^ (v >> 18)) & 63u);
+}
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -153,28 +139,10 @@ struct DeltaH {
   u64 sum[kDh];  // Σ weight
   u64 ft[kDh];   // min first touch
 };
-struct BuildL {
-  uint32_t hk[kBh], hc[kBh], ho[kBh];  // grouping: delta key, entries, group offset
-  uint32_t sk[kBh], so[kBh], sc[kBh];  // the sub-table being assembled (sc: fill counts first)
-};
-union LdsU {
-  int32_t strip[kStrip * kWlThreads];  // [position][lane]: conflict-free per wave (scan)
-  BuildL b;                             // a pending merge's pair groups (build)
-};
-static_assert(sizeof(BuildL) <= sizeof(int32_t) * kStrip * kWlThreads, "build tables share the strip");
-
-struct PendE {
-  int32_t X;
-  uint32_t seq, off, n;  // creating command, staged entries
-};
 
 // The merge's shared state in LDS.
 struct MergeCtx {
-  uint32_t* n_stage;  // staged new pairs of this merge
-  uint32_t* bfail;    // 1: a staged entry did not fit (this merge gets no sub-table)
-  uint32_t* nspill;   // delta keys spilled past the LDS hash
-  uint32_t stage_base, stage_room;
-  uint32_t* st;  // diagnostic stamps of thread 0 (shader clocks)
+  uint32_t* nspill;  // delta keys spilled past the LDS hash
 };
 
 // One neighbour delta (reference freq_change_add, bpe.cpp:274-290): Σ weight and min first touch
@@ -197,46 +165,37 @@ __device__ __forceinline__ void delta_add(DeltaH& h, const WlParams& p, const Me
   if (old == 0) p.dlist[atomicAdd(c.nspill, 1u)] = key;  // weights are >= 1
 }
 
-// A new pair (neighbour next to X) of word entry e, delta key dk: one entry of its group.
-__device__ __forceinline__ void stage_new(const WlParams& p, const MergeCtx& c, uint32_t dk, u64 e) {
-  const uint32_t i = atomicAdd(c.n_stage, 1u);
-  if (i < c.stage_room) {
-    p.stg_dk[c.stage_base + i] = dk;
-    p.stg_e[c.stage_base + i] = e;
-  } else {
-    *c.bfail = 1u;
-  }
-}
-
-// The four deltas of one occurrence and its new pairs' group entries.  prev: the left neighbour
-// after merging (X when just produced), has_l false at the word's start; n: the original token
-// after the pair, has_n false at the word's end.
-__device__ __forceinline__ void occurrence(const WlParams& p, DeltaH& h, const MergeCtx& c, bool has_l, int32_t prev,
-                                           bool has_n, int32_t n, u64 wc, u64 ft, u64 e) {
+// The four deltas of one occurrence (prev: the left neighbour after merging, X when just
+// produced, has_l false at the word's start; n: the original token after the pair, has_n false
+// at the word's end); returns its filter bits.
+__device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const MergeCtx& c, bool has_l, int32_t prev,
+                                          bool has_n, int32_t n, u64 wc, u64 ft) {
+  u64 f = 0;
   if (has_l) {
     const uint32_t sl = slot_of(prev, p.cap) * 4u;
     delta_add(h, p, c, sl + 0u, wc, ft | 0u);
     delta_add(h, p, c, sl + 1u, wc, ft | 1u);
-    if (prev != p.unk) stage_new(p, c, sl + 1u, e);
+    f |= nbit(prev, 0);
   }
   if (has_n) {
     const uint32_t sn = slot_of(n, p.cap) * 4u;
     delta_add(h, p, c, sn + 2u, wc, ft | 2u);
     delta_add(h, p, c, sn + 3u, wc, ft | 3u);
-    if (n != p.unk) stage_new(p, c, sn + 3u, e);
+    f |= nbit(n, 1);
   }
+  return f;
 }
 
 // Merge (a, b) -> X in one word of L tokens read from HBM (t: its tokens), greedy left to right
 // as the reference's chain walk (the path of words longer than the strip); returns the
-// occurrences merged, the new length in *len and the id signature in *sig.  First touch =
+// occurrences merged, the new length in *len and the filter bits in *sig.  First touch =
 // (rank << 32) | (input position << 2) | category.
 __device__ __forceinline__ uint32_t merge_run(const WlParams& p, DeltaH& h, const MergeCtx& c, int32_t* t, uint32_t L,
                                               u64 e, u64 wc, int32_t a, int32_t b, int32_t X, uint32_t* len,
                                               u64* sig) {
   const u64 rank = (e & 0xFFFFFFFFull) << 32;
   uint32_t j = 0, k = 0, occ = 0;
-  u64 sg = sig_bit(X);
+  u64 f = 0;
   int32_t prev = 0;
   int32_t c0 = t[0], c1 = L > 1 ? t[1] : 0;
 #pragma unroll 1
@@ -245,7 +204,7 @@ __device__ __forceinline__ uint32_t merge_run(const WlParams& p, DeltaH& h, cons
       const bool has_n = j + 2 < L;
       const int32_t n = has_n ? t[j + 2] : 0;  // the original next token (bpe.cpp:283-289)
       const int32_t n2 = j + 3 < L ? t[j + 3] : 0;
-      occurrence(p, h, c, k > 0, prev, has_n, n, wc, rank | ((u64)j << 2), e);
+      f |= occurrence(p, h, c, k > 0, prev, has_n, n, wc, rank | ((u64)j << 2));
       t[k] = X;
       prev = X;
       ++k;
@@ -255,7 +214,6 @@ __device__ __forceinline__ uint32_t merge_run(const WlParams& p, DeltaH& h, cons
       c1 = n2;
     } else {
       if (occ) t[k] = c0;  // positions before the first occurrence are unchanged
-      sg |= sig_bit(c0);
       prev = c0;
       ++k;
       ++j;
@@ -264,7 +222,7 @@ __device__ __forceinline__ uint32_t merge_run(const WlParams& p, DeltaH& h, cons
     }
   }
   *len = k;
-  *sig = sg;
+  *sig = f;
   return occ;
 }
 
@@ -285,9 +243,10 @@ __device__ __forceinline__ int32_t run_at(const Run& x, int i) {
 }
 
 // Merge (a, b) -> X in a word of L <= kStripTok tokens held in registers, in two passes so that
-// a wave's lanes emit their deltas in lock step: (1) the greedy left-to-right walk, unrolled over
-// the registers (position j is taken by the pair (j, j + 1) unless the previous position was),
-// writes the output to this lane's LDS strip and marks the output positions holding X; (2) per
+// a wave's lanes emit their deltas in lock step: (1) the greedy left-to-right walk, unrolled and
+// branch-free over the registers (position j is taken by the pair (j, j + 1) unless the
+// previous position was), writes the output to this lane's LDS strip (skipped positions write
+// the length slot, rewritten last) and marks the output positions holding X; (2) per
 // occurrence, lowest output position first, the four neighbour deltas — left neighbour
 // out[k - 1] (X when just produced), right neighbour the original token after the pair
 // (out[k + 1], or a where that is the next occurrence's X); input position of occurrence o at
@@ -295,29 +254,26 @@ __device__ __forceinline__ int32_t run_at(const Run& x, int i) {
 __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, const MergeCtx& c, int32_t* s,
                                                int32_t* r, const Run& x, uint32_t L, u64 e, u64 wc, int32_t a,
                                                int32_t b, int32_t X, uint32_t* len, u64* sig) {
-  uint32_t k = 0, occ = 0, xm = 0;
+  uint32_t k = 0, xm = 0;
   bool skip = false;
-  u64 sg = sig_bit(X);
 #pragma unroll
   for (int j = 0; j < (int)kStripTok; ++j) {
     const int32_t t0 = run_at(x, 1 + j);
     const int32_t t1 = j + 1 < (int)kStripTok ? run_at(x, 2 + j) : 0;
-    const bool in = (uint32_t)j < L;
-    const bool emit = in && !skip;
+    const bool emit = (uint32_t)j < L && !skip;
     const bool m = emit && (uint32_t)(j + 1) < L && t0 == a && t1 == b;
-    if (emit) s[(1 + k) * kWlThreads] = m ? X : t0;
+    s[(emit ? 1u + k : 0u) * kWlThreads] = m ? X : t0;
     xm |= (m ? 1u : 0u) << k;
-    if (emit && !m) sg |= sig_bit(t0);
     k += emit ? 1u : 0u;
-    occ += m ? 1u : 0u;
     skip = m;
   }
   *len = k;
-  *sig = sg;
-  if (threadIdx.x == 0) c.st[5] = (uint32_t)__builtin_amdgcn_s_memtime();
-  if (!occ) return 0;
+  *sig = 0;
+  if (!xm) return 0;
+  const uint32_t occ = (uint32_t)__popc(xm);
   const u64 rank = (e & 0xFFFFFFFFull) << 32;
   uint32_t m = xm, o = 0;
+  u64 f = 0;
   while (__ballot(m != 0u)) {
     if (m) {
       const uint32_t ko = (uint32_t)__ffs(m) - 1u;
@@ -327,10 +283,10 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
       const int32_t prev = ko > 0 ? s[ko * kWlThreads] : 0;  // out[ko - 1]
       const bool has_n = jo + 2 < L;
       const int32_t nx = has_n ? s[(2 + ko) * kWlThreads] : 0;  // out[ko + 1]
-      occurrence(p, h, c, ko > 0, prev, has_n, nx == X ? a : nx, wc, rank | ((u64)jo << 2), e);
+      f |= occurrence(p, h, c, ko > 0, prev, has_n, nx == X ? a : nx, wc, rank | ((u64)jo << 2));
     }
   }
-  if (threadIdx.x == 0) c.st[6] = (uint32_t)__builtin_amdgcn_s_memtime();
+  *sig = f;
   // the run [length][k tokens] from the first 16-B group that changed
   s[0] = (int32_t)k;
   int4* r4 = reinterpret_cast<int4*>(r);
@@ -379,162 +335,34 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
 // The loop's state in LDS.
 struct LoopS {
   uint32_t cmd[8];
-  uint32_t nout, nchg, pool_top, sub_top, err, scan, nstage, bfail, filter, nspill, need;
-  uint32_t stage_top, pend_head, pend_n, build_ok, nkeys, total;
-  uint32_t wsum[kWlWaves], wkeys[kWlWaves];
-  uint32_t st[8];
+  uint32_t nout, nchg, pool_top, err, scan, filter, nspill, qn;
+  uint32_t st[4];
   u64 lk[2];  // word list: pool offset, count
+  u64 need;   // filter bits the listed words must hold
   u64 occ, t[2];
-  PendE pend[kPend];
 };
-
-// Builds the pair groups of the oldest pending merge (every thread of the workgroup calls it):
-// its staged (delta key, word) entries grouped by key in LDS, placed in the pool by group, and
-// a sub-table of 2^k >= 2 x keys entries assembled in LDS and copied out.  A merge undone before
-// its build is skipped.  Too many keys or no room: the merge keeps its words-of list instead.
-__device__ void build_front(const WlParams& p, BuildL& B, LoopS& S, uint32_t* nosub, uint32_t* staged) {
-  const uint32_t tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
-  const PendE pe = S.pend[S.pend_head];
-  const bool live = pe.X >= 0 && (uint32_t)pe.X < p.id_cap && p.lseq[pe.X] == pe.seq;
-  for (int i = tid; i < kBh; i += kWlThreads) {
-    B.hk[i] = kEmpty32;
-    B.hc[i] = 0;
-    B.sc[i] = 0;
-  }
-  if (tid == 0) S.build_ok = live ? 1u : 0u;
-  __syncthreads();
-  if (live)
-    for (uint32_t i = tid; i < pe.n; i += kWlThreads) {
-      const uint32_t dk = p.stg_dk[pe.off + i];
-      uint32_t s = sub_hash(dk, 11);
-      bool ok = false;
-      for (int probe = 0; probe < 64; ++probe) {
-        const uint32_t prev = atomicCAS(&B.hk[s], kEmpty32, dk);
-        if (prev == kEmpty32 || prev == dk) {
-          atomicAdd(&B.hc[s], 1u);
-          ok = true;
-          break;
-        }
-        s = (s + 1) & (kBh - 1);
-      }
-      if (!ok) S.build_ok = 0;
-    }
-  __syncthreads();
-  // exclusive offsets of the groups and the number of keys
-  constexpr int kPer = kBh / kWlThreads;
-  uint32_t c[kPer], sum = 0, nk = 0;
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    c[q] = B.hc[kPer * tid + q];
-    sum += c[q];
-    nk += c[q] != 0u;
-  }
-  const uint32_t incl = wave_incl_add(sum), kin = wave_incl_add(nk);
-  if (lane == 63) {
-    S.wsum[wid] = incl;
-    S.wkeys[wid] = kin;
-  }
-  __syncthreads();
-  uint32_t before = 0, total = 0, nkeys = 0;
-  for (int q = 0; q < kWlWaves; ++q) {
-    before += q < wid ? S.wsum[q] : 0u;
-    total += S.wsum[q];
-    nkeys += S.wkeys[q];
-  }
-  uint32_t ex = before + incl - sum;
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    B.ho[kPer * tid + q] = ex;
-    ex += c[q];
-  }
-  uint32_t lg = 4;
-  while ((1u << lg) < 2u * nkeys) ++lg;
-  const uint32_t P = 1u << lg;
-  const uint32_t gbase = S.pool_top, sbase = S.sub_top;
-  const bool ok = S.build_ok != 0u && total == pe.n && P <= (uint32_t)kBh && (u64)gbase + total <= p.pool_cap &&
-                  (u64)sbase + P <= p.sub_cap;
-  __syncthreads();
-  if (ok) {
-    for (uint32_t i = tid; i < P; i += kWlThreads) B.sk[i] = kEmpty32;
-    for (uint32_t i = tid; i < pe.n; i += kWlThreads) {  // place the entries by group
-      const uint32_t dk = p.stg_dk[pe.off + i];
-      uint32_t s = sub_hash(dk, 11);
-      while (B.hk[s] != dk) s = (s + 1) & (kBh - 1);
-      const uint32_t pos = gbase + B.ho[s] + atomicAdd(&B.sc[s], 1u);
-      WEnt ne;
-      ne.e = p.stg_e[pe.off + i];
-      ne.sig = 0;
-      p.pool[pos] = ne;
-    }
-    __syncthreads();
-    for (int i = tid; i < kBh; i += kWlThreads) B.sc[i] = 0;
-    __syncthreads();
-    for (int i = tid; i < kBh; i += kWlThreads) {  // the sub-table
-      const uint32_t cnt = B.hc[i];
-      if (!cnt) continue;
-      const uint32_t dk = B.hk[i];
-      uint32_t hs = sub_hash(dk, lg);
-      while (atomicCAS(&B.sk[hs], kEmpty32, dk) != kEmpty32) hs = (hs + 1) & (P - 1);
-      B.so[hs] = gbase + B.ho[i];
-      B.sc[hs] = cnt;
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < P; i += kWlThreads) {
-      SubE se;
-      se.dk = B.sk[i];
-      se.off = B.so[i];
-      se.cnt = B.sc[i];
-      se.pad = 0;
-      p.sub[sbase + i] = se;
-    }
-  }
-  if (tid == 0) {
-    if (ok) {
-      p.xsub[pe.X] = (u64)sbase | ((u64)lg << 32) | kSubValid;
-      p.xgrp[pe.X] = (u64)gbase | ((u64)(gbase + total) << 32);
-      S.pool_top = gbase + total;
-      S.sub_top = sbase + P;
-      *staged += total;
-    } else if (live) {
-      p.xsub[pe.X] = 0;  // its words-of list serves
-      ++*nosub;
-    }
-    S.pend_head = (S.pend_head + 1) % kPend;
-    if (--S.pend_n == 0) S.stage_top = 0;
-  }
-  __syncthreads();
-}
 
 }  // namespace
 
 // The merge loop (see the file comment).  One workgroup; command numbers start at p.seq0.
 __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
-  __shared__ LdsU u;
+  __shared__ int32_t s_strip[kStrip * kWlThreads];  // [position][lane]: conflict-free per wave
   __shared__ DeltaH s_h;
   __shared__ LoopS S;
+  __shared__ u64 s_q[kQ];  // the listed entries that pass the filter, merged densely
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t tid = threadIdx.x;
-  int32_t* const mys = u.strip + tid;
-  if (tid == 0) {
-    S.pool_top = ld_agent(&p.dstate[kStPoolTop]);
-    S.sub_top = ld_agent(&p.dstate[kStSubTop]);
-    S.stage_top = 0;
-    S.pend_head = 0;
-    S.pend_n = 0;
-  }
+  int32_t* const mys = s_strip + tid;
+  if (tid == 0) S.pool_top = ld_agent(&p.dstate[kStPoolTop]);
   uint32_t expect = p.seq0;
   uint32_t exit_op = kOpStop;
-  u64 build_ticks = 0;
-  uint32_t nosub = 0, staged = 0;
+  const MergeCtx mc{&S.nspill};
   __syncthreads();
   for (;;) {
-    // ---- the next command: wave 0 reads the four granules in one round trip; while none is
-    // posted, the oldest pending pair groups are built, else wave 0 waits
+    // ---- wave 0 waits for the next command (one round trip reads all four granules)
     if (wid == 0) {
       const u64* g = p.ring[expect % kRing].g;
-      const bool block = S.pend_n == 0;
-      uint32_t op = kOpNone, a = 0, b = 0, X = 0, idle = 0;
+      uint32_t op = 0, a = 0, b = 0, X = 0, idle = 0;
       for (;;) {
         const u64 v = lane < 4 ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
         const bool tagged = lane >= 4 || (uint32_t)v == expect;
@@ -546,7 +374,6 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           X = __shfl(val, 3, 64);
           break;
         }
-        if (!block) break;
         if (++idle >= p.idle_polls) {
           op = kOpTimeout;
           break;
@@ -564,12 +391,6 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     }
     __syncthreads();
     const uint32_t op = S.cmd[0];
-    if (op == kOpNone) {  // idle: one pending build
-      const u64 tb = __builtin_amdgcn_s_memrealtime();
-      build_front(p, u.b, S, &nosub, &staged);
-      build_ticks += __builtin_amdgcn_s_memrealtime() - tb;
-      continue;
-    }
     const int32_t a = (int32_t)S.cmd[1], b = (int32_t)S.cmd[2], X = (int32_t)S.cmd[3];
     const uint32_t slot = S.cmd[4], seq = S.cmd[5];
     ++expect;
@@ -577,142 +398,86 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       exit_op = op;
       break;
     }
-    // ---- the word list.  Merge (a, b), M = max(a, b): when the loop created M, the group of
-    // the pair in M's sub-table (every word that held the pair when M was created; built first
-    // if it waits), or, when M has no sub-table, M's words-of list filtered by signature; else
-    // the initial directory entry of (a, b) (every word that held the pair when the index was
-    // built).  Undo: the words of X, exactly.  Wave 0: one round trip for the id tables and 16
-    // directory slots, one more for the sub-table.
+    // ---- the word list.  Merge (a, b), M = max(a, b): when the loop created M, M's words-of
+    // list with the filter bit of the pair's other id on its side ((c, M): c on the left, (M, d):
+    // d on the right, (M, M): M on the left); else the initial directory entry of (a, b) (every
+    // word that held the pair when the index was built, exact).  Undo: the words of X, exactly.
+    // Wave 0 reads the id tables and 16 directory slots in one round trip.
     const u64 t_cmd = __builtin_amdgcn_s_memrealtime();
-    u64 t_built = 0;
-    for (;;) {
-      if (wid == 0) {
-        const bool undo = op == kOpUnmerge;
-        const int32_t M = undo ? X : (a > b ? a : b);
-        u64 lv64 = 0;
-        bool lv = false;
-        if (lane >= 16 && lane < 19 && M >= 0 && (uint32_t)M < p.id_cap) {
-          if (lane == 16) lv = p.lseq[M] != kNoList;
-          if (lane == 17) lv64 = p.lst[M];
-          if (lane == 18) lv64 = p.xsub[M];
-        }
-        const u64 key = pair_key(a, b);
-        const u64 h = mix64(key) & p.dir_mask;
-        u64 dk = kEmpty64, dv = 0;
-        if (!undo && lane < 16) {
-          dk = p.dkey[(h + (u64)lane) & p.dir_mask];
-          dv = p.dval[(h + (u64)lane) & p.dir_mask];
-        }
-        const bool has_list = (__ballot(lv) >> 16) & 1ull;
-        const u64 wl = __shfl(lv64, 17, 64), xs = __shfl(lv64, 18, 64);
-        u64 off = 0, cnt = 0;
-        bool err = false, filter = false, need = false;
-        if (has_list && !undo && (xs & kSubPending) && S.pend_n) {
-          need = true;
-        } else if (has_list && (undo || !(xs & kSubValid))) {  // (pending with an empty queue: cannot happen)
-          off = (uint32_t)wl;
-          cnt = wl >> 32;
-          filter = !undo;
-        } else if (has_list) {
-          // the pair's delta key in M's table: (c, M) is a new-left pair of neighbour c, (M, d) a
-          // new-right pair of neighbour d, (M, M) new-left (the right neighbour was never M)
-          const uint32_t nk = a == b ? slot_of(M, p.cap) * 4u + 1u
-                                     : b == M ? slot_of(a, p.cap) * 4u + 1u : slot_of(b, p.cap) * 4u + 3u;
-          const uint32_t lg = (uint32_t)(xs >> 32) & 31u, mask = (1u << lg) - 1u;
-          const SubE* tb = p.sub + (uint32_t)xs;
-          const uint32_t h0 = sub_hash(nk, lg);
-          for (uint32_t base = 0;; base += 16) {
-            uint32_t kk = kEmpty32, ko = 0, kc = 0;
+    if (wid == 0) {
+      const bool undo = op == kOpUnmerge;
+      const int32_t M = undo ? X : (a > b ? a : b);
+      u64 lv64 = 0;
+      bool lv = false;
+      if ((lane == 16 || lane == 17) && M >= 0 && (uint32_t)M < p.id_cap) {
+        if (lane == 16) lv = p.lseq[M] != kNoList;
+        if (lane == 17) lv64 = p.lst[M];
+      }
+      const u64 key = pair_key(a, b);
+      const u64 h = mix64(key) & p.dir_mask;
+      u64 dk = kEmpty64, dv = 0;
+      if (!undo && lane < 16) {
+        dk = p.dkey[(h + (u64)lane) & p.dir_mask];
+        dv = p.dval[(h + (u64)lane) & p.dir_mask];
+      }
+      const bool has_list = (__ballot(lv) >> 16) & 1ull;
+      const u64 wl = __shfl(lv64, 17, 64);
+      u64 off = 0, cnt = 0, need = 0;
+      bool err = false;
+      if (has_list) {
+        off = (uint32_t)wl;
+        cnt = wl >> 32;
+        if (!undo) need = a == b ? nbit(M, 0) : b == M ? nbit(a, 0) : nbit(b, 1);
+      } else if (undo) {
+        err = true;  // every merged id has its words-of list
+      } else {
+        for (u64 base = 0;; base += 16) {
+          if (base) {
+            dk = kEmpty64;
             if (lane < 16) {
-              const SubE se = tb[(h0 + base + (uint32_t)lane) & mask];
-              kk = se.dk;
-              ko = se.off;
-              kc = se.cnt;
-            }
-            const u64 hit = __ballot(lane < 16 && kk == nk);
-            const u64 emp = __ballot(lane < 16 && kk == kEmpty32);
-            const u64 any = hit | emp;
-            if (any) {
-              const int f = __ffsll((long long)any) - 1;
-              if ((hit >> f) & 1ull) {
-                off = __shfl(ko, f, 64);
-                cnt = __shfl(kc, f, 64);
-              } else {
-                err = true;  // a selected pair always has a group
-              }
-              break;
-            }
-            if (base > mask) {
-              err = true;
-              break;
+              dk = p.dkey[(h + base + (u64)lane) & p.dir_mask];
+              dv = p.dval[(h + base + (u64)lane) & p.dir_mask];
             }
           }
-        } else if (undo) {
-          err = true;  // every merged id has its words-of list
-        } else {
-          for (u64 base = 0;; base += 16) {
-            if (base) {
-              dk = kEmpty64;
-              if (lane < 16) {
-                dk = p.dkey[(h + base + (u64)lane) & p.dir_mask];
-                dv = p.dval[(h + base + (u64)lane) & p.dir_mask];
-              }
+          const u64 hit = __ballot(lane < 16 && dk == key);
+          const u64 emp = __ballot(lane < 16 && dk == kEmpty64);
+          const u64 any = hit | emp;
+          if (any) {
+            const int f = __ffsll((long long)any) - 1;
+            const u64 vf = __shfl(dv, f, 64);
+            if ((hit >> f) & 1ull) {
+              off = (uint32_t)vf;
+              cnt = vf >> 32;
+            } else {
+              err = true;  // a selected pair always has a list
             }
-            const u64 hit = __ballot(lane < 16 && dk == key);
-            const u64 emp = __ballot(lane < 16 && dk == kEmpty64);
-            const u64 any = hit | emp;
-            if (any) {
-              const int f = __ffsll((long long)any) - 1;
-              const u64 vf = __shfl(dv, f, 64);
-              if ((hit >> f) & 1ull) {
-                off = (uint32_t)vf;
-                cnt = vf >> 32;
-              } else {
-                err = true;  // a selected pair always has a list
-              }
-              break;
-            }
-            if (base > p.dir_mask) {
-              err = true;
-              break;
-            }
+            break;
+          }
+          if (base > p.dir_mask) {
+            err = true;
+            break;
           }
         }
-        if (lane == 0) {
-          S.need = need ? 1u : 0u;
-          S.lk[0] = off;
-          S.lk[1] = err ? 0 : cnt;
-          S.nout = 0;
-          S.nchg = 0;
-          S.scan = 0;
-          S.nstage = 0;
-          S.bfail = 0;
-          S.nspill = 0;
-          S.filter = filter ? 1u : 0u;
-          S.occ = 0;
-          S.err = 0;
-          S.st[0] = S.st[1] = S.st[2] = 0;
-          if (err) atomicMax(&p.dstate[kStError], undo ? kErrList : kErrLookup);
-          if (!undo && (u64)S.pool_top + cnt > p.pool_cap) {
-            S.err = 1;
-            atomicMax(&p.dstate[kStError], kErrPool);
-          }
-          S.t[0] = __builtin_amdgcn_s_memrealtime() - t_cmd;
+      }
+      if (lane == 0) {
+        S.lk[0] = off;
+        S.lk[1] = err ? 0 : cnt;
+        S.need = need;
+        S.nout = 0;
+        S.nchg = 0;
+        S.scan = 0;
+        S.nspill = 0;
+        S.filter = need != 0;
+        S.occ = 0;
+        S.err = 0;
+        S.st[0] = S.st[1] = S.st[2] = 0;
+        if (err) atomicMax(&p.dstate[kStError], undo ? kErrList : kErrLookup);
+        if (!undo && (u64)S.pool_top + cnt > p.pool_cap) {
+          S.err = 1;
+          atomicMax(&p.dstate[kStError], kErrPool);
         }
+        S.t[0] = __builtin_amdgcn_s_memrealtime() - t_cmd;
       }
-      __syncthreads();
-      if (!S.need) break;
-      // M's pair groups wait: build the pending merges up to M's
-      const u64 tb = __builtin_amdgcn_s_memrealtime();
-      const int32_t M = a > b ? a : b;
-      bool more = true;
-      while (more && S.pend_n) {
-        more = S.pend[S.pend_head].X != M;
-        build_front(p, u.b, S, &nosub, &staged);
-      }
-      const u64 dt = __builtin_amdgcn_s_memrealtime() - tb;
-      build_ticks += dt;
-      t_built += dt;
     }
     if (op == kOpMerge)
       for (int i = tid; i < kDh; i += kWlThreads) {
@@ -733,32 +498,20 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       }
       __syncthreads();
       if (tid == 0 && X >= 0 && (uint32_t)X < p.id_cap) {
-        // release the guess's groups, sub-table and list when they are the last ones
-        const u64 xs = p.xsub[X];
-        if (xs & kSubValid) {
-          const u64 xg = p.xgrp[X];
-          if ((uint32_t)(xg >> 32) == S.pool_top) S.pool_top = (uint32_t)xg;
-          const uint32_t so = (uint32_t)xs;
-          if (so >= kSubFirst && so + (1u << ((xs >> 32) & 31u)) == S.sub_top) S.sub_top = so;
-        }
-        if (off + cnt == (u64)S.pool_top) S.pool_top = (uint32_t)off;
+        if (off + cnt == (u64)S.pool_top) S.pool_top = (uint32_t)off;  // the guess's list was the last one
         p.lseq[X] = kNoList;
-        p.xsub[X] = 0;
       }
       __syncthreads();
       continue;
     }
     // ---- the merge over the listed words; changed words become the words of X.  Each round a
-    // lane loads kB pool entries (coalesced), then merges them one at a time (a words-of list
-    // only where the signature holds a and b): the run in one round trip, the walk in
-    // registers.  A group may name a word twice: the word mark lets one lane take it.
+    // lane loads kB pool entries (coalesced) and queues in LDS those whose filter holds the
+    // pair's bit; once a workgroup's worth is queued (and at the end) the queue is merged
+    // densely, a lane per word: the run in one round trip, the walk in registers.
     const bool append = S.err == 0;
-    const bool filt = S.filter != 0;
-    const u64 need = sig_bit(a) | sig_bit(b);
-    const uint32_t stage_base = S.stage_top;
-    const MergeCtx mc{&S.nstage, &S.bfail, &S.nspill, stage_base,
-                      (uint32_t)std::min<u64>(p.stage_cap - stage_base, 0xFFFFFFFFull), S.st};
+    const u64 need = S.need;
     uint32_t my_occ = 0, my_scan = 0;
+    if (tid == 0) S.qn = 0;
     for (u64 base = 0; base < cnt; base += (u64)kWlThreads * kB) {
       u64 ex[kB], sx[kB];
 #pragma unroll
@@ -776,49 +529,49 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         S.st[0] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
       }
-#pragma unroll 1
-      for (int q = 0; q < kB; ++q) {
-        u64 e = ex[0], sg = sx[0];
 #pragma unroll
-        for (int z = 1; z < kB; ++z)
-          if (q == z) {
-            e = ex[z];
-            sg = sx[z];
-          }
+      for (int q = 0; q < kB; ++q) {
+        const bool pass = ex[q] != kEmpty64 && (sx[q] & need) == need;
+        const u64 bl = __ballot(pass);
+        if (bl) {
+          const int lead = __ffsll((long long)bl) - 1;
+          uint32_t qb = 0;
+          if (lane == lead) qb = atomicAdd(&S.qn, (uint32_t)__popcll(bl));
+          qb = __shfl(qb, lead, 64);
+          if (pass) s_q[qb + (uint32_t)__popcll(bl & ((1ull << lane) - 1ull))] = ex[q];
+        }
+      }
+      __syncthreads();
+      const uint32_t qn = S.qn;
+      __syncthreads();  // every thread has read qn before the next round queues more
+      const bool last = base + (u64)kWlThreads * kB >= cnt;
+      if (qn < (uint32_t)kWlThreads && !last) continue;
+      for (uint32_t qi = tid; qi < ((qn + kWlThreads - 1) / kWlThreads) * kWlThreads; qi += kWlThreads) {
         uint32_t occ = 0;
-        u64 nsig = 0;
-        if (e != kEmpty64 && (!filt || (sg & need) == need)) {
+        u64 nsig = 0, e = kEmpty64;
+        if (qi < qn) {
+          e = s_q[qi];
           const uint32_t w = (uint32_t)e;
           int32_t* r = p.wtok + (uint32_t)(e >> 32);
-          const uint32_t old = atomicExch(&p.wmark[w], seq);
           const Run x = load_run(r);
           const u64 wc = p.weight[w];
           // every load of the word lands here, once: a first use of wc later would wait (vmcnt
           // counts stores too) for the stores issued by then
-          asm volatile("s_waitcnt vmcnt(0)" ::"v"(old), "v"(wc), "v"(x.v[0].x) : "memory");
+          asm volatile("s_waitcnt vmcnt(0)" ::"v"(wc), "v"(x.v[0].x) : "memory");
           const uint32_t L = (uint32_t)x.v[0].x;
           uint32_t nl = L;
-          if (base == 0 && q == 0 && tid == 0) {
-            S.st[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
-            S.st[4] = (uint32_t)__builtin_amdgcn_s_memtime();
-            S.st[5] = S.st[6] = S.st[4];
-          }
-          if (old != seq) {
-            ++my_scan;
-            if (L >= 2) {
-              if (L <= kStripTok) {
-                occ = merge_regs(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig);
-              } else {
-                occ = merge_run(p, s_h, mc, r + 1, L, e, wc, a, b, X, &nl, &nsig);
-                if (occ) r[0] = (int32_t)nl;
-              }
+          if (qi == 0 && base == 0) S.st[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
+          ++my_scan;
+          if (L >= 2) {
+            if (L <= kStripTok) {
+              occ = merge_regs(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig);
+            } else {
+              occ = merge_run(p, s_h, mc, r + 1, L, e, wc, a, b, X, &nl, &nsig);
+              if (occ) r[0] = (int32_t)nl;
             }
-            my_occ += occ;
           }
-          if (base == 0 && q == 0 && tid == 0) {
-            S.st[2] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
-            S.st[7] = (uint32_t)__builtin_amdgcn_s_memtime();
-          }
+          my_occ += occ;
+          if (qi == 0 && base == 0) S.st[2] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
         }
         const u64 chg = __ballot(occ != 0);
         if (chg) {
@@ -835,14 +588,24 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           }
         }
       }
+      __syncthreads();
+      if (tid == 0) S.qn = 0;
+      __syncthreads();
     }
     if (my_occ) atomicAdd(&S.occ, (u64)my_occ);
     if (my_scan) atomicAdd(&S.scan, my_scan);
     __syncthreads();
-    if (tid == 0) S.t[1] = __builtin_amdgcn_s_memrealtime() - t_cmd;
     // ---- the records to host memory (LDS hash, then the spilled keys), then the flag
     const WlSlotDev& sd = p.sl[slot & (WordLoop::kSlots - 1)];
     const uint32_t nchg = append ? S.nchg : 0u;
+    if (tid == 0) {
+      S.t[1] = __builtin_amdgcn_s_memrealtime() - t_cmd;
+      if (X >= 0 && (uint32_t)X < p.id_cap) {
+        p.lst[X] = (u64)top | ((u64)nchg << 32);
+        p.lseq[X] = seq;
+        S.pool_top = top + nchg;
+      }
+    }
     for (int i = tid; i < kDh; i += kWlThreads) {
       const uint32_t key = s_h.key[i];
       if (key == kEmpty32) continue;
@@ -881,50 +644,13 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       sd.hdr[16] = S.st[0];
       sd.hdr[17] = S.st[1];
       sd.hdr[18] = S.st[2];
-      sd.hdr[19] = (uint32_t)t_built;
-      sd.hdr[20] = S.st[5] - S.st[4];  // shader clocks: pass 1
-      sd.hdr[21] = S.st[6] - S.st[5];  //   pass 2
-      sd.hdr[22] = S.st[7] - S.st[6];  //   run stores
       __threadfence_system();
       __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    // ---- after the flag (off the host's path): the words of X, and its pair groups queued for
-    // a build (when idle, when a lookup needs them, or when the queue is full)
-    if (tid == 0 && X >= 0 && (uint32_t)X < p.id_cap) {
-      p.lst[X] = (u64)top | ((u64)nchg << 32);
-      p.lseq[X] = seq;
-      S.pool_top = top + nchg;
-      const uint32_t n = S.nstage;
-      if (!append || S.bfail) {
-        p.xsub[X] = 0;  // its words-of list serves
-        ++nosub;
-      } else if (n == 0) {
-        p.xsub[X] = (u64)0 | ((u64)4 << 32) | kSubValid;  // the empty table: X has no pairs
-        p.xgrp[X] = (u64)S.pool_top | ((u64)S.pool_top << 32);
-      } else {
-        p.xsub[X] = kSubPending;
-        const uint32_t q = (S.pend_head + S.pend_n) % kPend;
-        S.pend[q] = PendE{X, seq, stage_base, n};
-        ++S.pend_n;
-        S.stage_top = stage_base + n;
-      }
-    }
     __syncthreads();
-    if (S.pend_n == kPend || (u64)S.stage_top * 2 > p.stage_cap) {
-      const u64 tb = __builtin_amdgcn_s_memrealtime();
-      while (S.pend_n) build_front(p, u.b, S, &nosub, &staged);
-      build_ticks += __builtin_amdgcn_s_memrealtime() - tb;
-    }
   }
-  // the pending groups before the launch ends (the next launch starts with an empty queue)
-  while (S.pend_n) build_front(p, u.b, S, &nosub, &staged);
   if (tid == 0) {
     p.dstate[kStPoolTop] = S.pool_top;
-    p.dstate[kStSubTop] = S.sub_top;
-    u64* b64 = reinterpret_cast<u64*>(p.dstate + kStBuild);
-    *b64 += build_ticks;
-    p.dstate[kStNoSub] += nosub;
-    p.dstate[kStStaged] += staged;
     __threadfence_system();
     __hip_atomic_store(&p.status[0], exit_op, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -964,24 +690,14 @@ __global__ void k_wl_mark(const u64* key, const uint32_t* val, uint64_t n, uint3
   }
 }
 
-// The signature of every word (the ids it holds now).
-__global__ void k_wl_word_sig(const int32_t* wtok, const uint32_t* woff, uint32_t W, u64* wsig) {
-  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < W; w += gridDim.x * blockDim.x) {
-    const uint32_t o = woff[w], L = (uint32_t)wtok[o];
-    u64 sg = 0;
-    for (uint32_t j = 0; j < L; ++j) sg |= sig_bit(wtok[o + 1 + j]);
-    wsig[w] = sg;
-  }
-}
-
 __global__ void k_wl_scatter(const u64* key, const uint32_t* val, uint64_t n, const uint32_t* keep,
                              const uint32_t* pos, const uint32_t* head, const uint32_t* kidx, const uint32_t* woff,
-                             const u64* wsig, WEnt* pool, u64* ikey, u64* ival) {
+                             WEnt* pool, u64* ikey, u64* ival) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     if (keep[i]) {
       WEnt ent;
       ent.e = ((u64)woff[val[i]] << 32) | val[i];
-      ent.sig = wsig[val[i]];
+      ent.sig = ~0ull;  // an exact list: no filter
       pool[pos[i]] = ent;
     }
     if (head[i]) {
@@ -1118,13 +834,12 @@ WordLoop::~WordLoop() {
 
 void WordLoop::free_all() {
   void* ptrs[] = {wtok_, wtok0_, woff_, tile_first_, tile_nw_, pool_, dkey_, dval_, init_key_, init_val_,
-                  lst_, lseq_, xsub_, xgrp_, wmark_, sub_, stg_e_, stg_dk_, dsum_, dft_, dlist_, dstate_};
+                  lst_, lseq_, dsum_, dft_, dlist_, dstate_};
   for (void* p : ptrs)
     if (p) WL_OK(hipFree(p));
   wtok_ = wtok0_ = nullptr;
-  woff_ = tile_first_ = tile_nw_ = lseq_ = wmark_ = stg_dk_ = dlist_ = dstate_ = nullptr;
-  pool_ = dkey_ = dval_ = init_key_ = init_val_ = lst_ = xsub_ = xgrp_ = stg_e_ = dsum_ = dft_ = nullptr;
-  sub_ = nullptr;
+  woff_ = tile_first_ = tile_nw_ = lseq_ = dlist_ = dstate_ = nullptr;
+  pool_ = dkey_ = dval_ = init_key_ = init_val_ = lst_ = dsum_ = dft_ = nullptr;
   cap_ = id_cap_ = 0;
   dir_cap_ = 0;
   bytes_ = 0;
@@ -1199,16 +914,8 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
   // the words it shortened: Σ over a run <= Σ (length - 1)) and the pair groups (<= 2 entries
   // per occurrence merged: Σ <= 2 Σ (length - 1)); undone guesses release theirs (each is the
   // last when its undo runs)
-  pool_cap_ = 4 * ntok_ + 4096;
+  pool_cap_ = 3 * ntok_ + 4096;
   pool_ = wl_alloc<u64>(2 * pool_cap_, &bytes_);  // WEnt: entry + signature
-  sub_cap_ = 4 * ntok_ + 16 * 65536;               // Σ 2^k <= 4 x keys, >= 16 per merge
-  sub_ = wl_alloc<uint32_t>(4 * sub_cap_, &bytes_);
-  WL_OK(hipMemsetAsync(sub_, 0xFF, kSubFirst * sizeof(SubE), s));  // the empty table
-  stage_cap_ = 2 * ntok_ + 4096;
-  stg_e_ = wl_alloc<u64>(stage_cap_, &bytes_);
-  stg_dk_ = wl_alloc<uint32_t>(stage_cap_, &bytes_);
-  wmark_ = wl_alloc<uint32_t>(nwords_, &bytes_);
-  WL_OK(hipMemsetAsync(wmark_, 0, (size_t)nwords_ * sizeof(uint32_t), s));
   dstate_ = wl_alloc<uint32_t>(8, &bytes_);
   WL_OK(hipMemsetAsync(dstate_, 0, 8 * sizeof(uint32_t), s));
   WL_OK(hipStreamSynchronize(s));
@@ -1232,10 +939,7 @@ void WordLoop::build_index() {
   uint32_t* head = wl_alloc<uint32_t>(n + 1, &acc);
   uint32_t* pos = wl_alloc<uint32_t>(n + 1, &acc);
   uint32_t* kidx = wl_alloc<uint32_t>(n + 1, &acc);
-  u64* wsig = wl_alloc<u64>(nwords_, &acc);
   const int grid = 2048;
-  k_wl_word_sig<<<grid, 256, 0, s>>>(wtok_, woff_, nwords_, wsig);
-  WL_OK(hipGetLastError());
   k_wl_emit_pairs<<<grid, 256, 0, s>>>(wtok_, woff_, nwords_, unk_, kin, vin);
   WL_OK(hipGetLastError());
   size_t tmp_bytes = 0, tb2 = 0;
@@ -1261,14 +965,14 @@ void WordLoop::build_index() {
   if (init_val_) WL_OK(hipFree(init_val_));
   init_key_ = wl_alloc<u64>(init_keys_n_, &bytes_);
   init_val_ = wl_alloc<u64>(init_keys_n_, &bytes_);
-  k_wl_scatter<<<grid, 256, 0, s>>>(kout, vout, n, keep, pos, head, kidx, woff_, wsig, reinterpret_cast<WEnt*>(pool_),
+  k_wl_scatter<<<grid, 256, 0, s>>>(kout, vout, n, keep, pos, head, kidx, woff_, reinterpret_cast<WEnt*>(pool_),
                                     init_key_, init_val_);
   WL_OK(hipGetLastError());
   k_wl_counts<<<256, 256, 0, s>>>(init_val_, init_keys_n_, init_pool_n_);
   WL_OK(hipGetLastError());
   WL_OK(hipStreamSynchronize(s));
   for (void* p : {(void*)kin, (void*)kout, (void*)vin, (void*)vout, (void*)keep, (void*)head, (void*)pos, (void*)kidx,
-                  (void*)wsig, tmp})
+                  tmp})
     WL_OK(hipFree(p));
   // the directory: at most half full
   uint64_t want = 1024;
@@ -1292,8 +996,7 @@ void WordLoop::restore_index() {
     WL_OK(hipGetLastError());
   }
   if (lseq_) WL_OK(hipMemsetAsync(lseq_, 0xFF, id_cap_ * sizeof(uint32_t), s));
-  if (xsub_) WL_OK(hipMemsetAsync(xsub_, 0, id_cap_ * sizeof(u64), s));
-  const uint32_t st[8] = {0, (uint32_t)init_pool_n_, kSubFirst, 0, 0, 0, 0, 0};
+  const uint32_t st[8] = {0, (uint32_t)init_pool_n_, 0, 0, 0, 0, 0, 0};
   WL_OK(hipMemcpyAsync(dstate_, st, sizeof(st), hipMemcpyHostToDevice, s));
   WL_OK(hipStreamSynchronize(s));
 }
@@ -1399,22 +1102,19 @@ void WordLoop::reserve(int32_t max_id) {
   // the words-of lists (ids past the old capacity have none)
   u64* nl = wl_alloc<u64>(cap, &bytes_);
   uint32_t* ns = wl_alloc<uint32_t>(cap, &bytes_);
-  u64* nx = wl_alloc<u64>(cap, &bytes_);
-  u64* ne = wl_alloc<u64>(cap, &bytes_);
+
   WL_OK(hipMemsetAsync(ns, 0xFF, (size_t)cap * sizeof(uint32_t), s));
-  WL_OK(hipMemsetAsync(nx, 0, (size_t)cap * sizeof(u64), s));
+
   if (lseq_) {
     WL_OK(hipMemcpyAsync(nl, lst_, (size_t)id_cap_ * sizeof(u64), hipMemcpyDeviceToDevice, s));
     WL_OK(hipMemcpyAsync(ns, lseq_, (size_t)id_cap_ * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-    WL_OK(hipMemcpyAsync(nx, xsub_, (size_t)id_cap_ * sizeof(u64), hipMemcpyDeviceToDevice, s));
-    WL_OK(hipMemcpyAsync(ne, xgrp_, (size_t)id_cap_ * sizeof(u64), hipMemcpyDeviceToDevice, s));
+
     WL_OK(hipStreamSynchronize(s));
-    for (void* q : {(void*)lst_, (void*)lseq_, (void*)xsub_, (void*)xgrp_}) WL_OK(hipFree(q));
+    for (void* q : {(void*)lst_, (void*)lseq_}) WL_OK(hipFree(q));
   }
   lst_ = nl;
   lseq_ = ns;
-  xsub_ = nx;
-  xgrp_ = ne;
+
   id_cap_ = cap;
   cap_ = cap;
   ensure_slots(cap);
@@ -1432,14 +1132,7 @@ void WordLoop::launch() {
   p.dir_mask = dir_cap_ - 1;
   p.lst = lst_;
   p.lseq = lseq_;
-  p.xsub = xsub_;
-  p.xgrp = xgrp_;
-  p.wmark = wmark_;
-  p.sub = static_cast<SubE*>(sub_);
-  p.sub_cap = sub_cap_;
-  p.stg_e = stg_e_;
-  p.stg_dk = stg_dk_;
-  p.stage_cap = stage_cap_;
+
   p.id_cap = id_cap_;
   p.dsum = dsum_;
   p.dft = dft_;
@@ -1530,7 +1223,7 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   if (timing_) {
     const uint32_t rec[kTraceFields] = {(uint32_t)X, h[2], h[12], h[3], (uint32_t)h64[2], (uint32_t)(10 * h64[3]),
                                         (uint32_t)(10 * h64[4]), (uint32_t)(10 * (h64[5] - h64[4])),
-                                        h[20], h[21], h[22], 10 * h[19]};
+                                        10 * h[16], 10 * h[17], 10 * h[18], 0u};
     trace_.insert(trace_.end(), rec, rec + kTraceFields);
   }
   if (n > sl.rec_cap) fatal("k_word_loop: record overflow");
@@ -1560,14 +1253,10 @@ void WordLoop::stop() {
   st_.kernel_ms += ms;
   uint32_t ds[8];
   WL_OK(hipMemcpy(ds, dstate_, sizeof(ds), hipMemcpyDeviceToHost));
-  st_.build_us += 1e-2 * (double)(ds[kStBuild] | ((uint64_t)ds[kStBuild + 1] << 32));
-  st_.no_sub += ds[kStNoSub];
-  st_.staged += ds[kStStaged];
-  const uint32_t zero[4] = {0, 0, 0, 0};
-  WL_OK(hipMemcpy(dstate_ + kStBuild, zero, sizeof(zero), hipMemcpyHostToDevice));
+
   if (ds[kStError]) {
-    static const char* what[] = {"", "index pool exhausted", "an undone merge had no word list",
-                                 "sub-table overflow", "a merged pair had no word list"};
+    static const char* what[] = {"", "index pool exhausted", "an undone merge had no word list", "",
+                                 "a merged pair had no word list"};
     std::fprintf(stderr, "[ERROR]\t k_word_loop: %s (code %u)\n", ds[kStError] < 5 ? what[ds[kStError]] : "?",
                  ds[kStError]);
     fatal("k_word_loop failed");

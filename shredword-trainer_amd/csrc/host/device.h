@@ -116,8 +116,9 @@ class Device : public Backend {
   void set_index(bool on);
   bool index_on() const { return index_on_; }
   // Hybrid: the first merges (each changes many words) run on k_resident, which spreads a merge
-  // over every CU; once a merge changes fewer than switch_occ_ occurrences the indexed loop (one
-  // workgroup, a few round trips per merge) takes over for the rest of train().
+  // over every CU; once kSwitchWindow merges in a row changed fewer than switch_occ_ table
+  // entries each, the indexed loop (one workgroup, a few round trips per merge) takes over for
+  // the rest of train().
   bool hybrid_resident_phase() const {
     return hybrid_ && !idx_phase_ && resident_on_ && resident_ok_ && !exchange_ && ntiles_ > 0;
   }
@@ -322,7 +323,10 @@ class Device : public Backend {
   bool hybrid_ = true;             // option (SHREDWORD_HYBRID / set_option hybrid)
   bool idx_phase_ = false;         // hybrid: the indexed loop has taken over this train()
   bool switch_pending_ = false;    // hybrid: a resident merge changed < switch_occ_ occurrences
-  uint64_t switch_occ_ = 2048;     // option (SHREDWORD_SWITCH_OCC / set_option switch_occ)
+  uint64_t switch_occ_ = 400;      // option (SHREDWORD_SWITCH_OCC / set_option switch_occ)
+  static constexpr int kSwitchWindow = 64;
+  uint64_t sw_win_[kSwitchWindow] = {};  // entries merged by the last resident merges
+  uint64_t sw_n_ = 0;
   int64_t switch_x_ = -1;          // the first merge id the indexed loop ran (stats)
   double switch_ms_ = 0;           // Σ host time of the switches (tiles -> words + index build)
   int32_t reserved_max_id_ = 0;    // the last reserve_ids()

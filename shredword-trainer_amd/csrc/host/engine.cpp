@@ -108,6 +108,13 @@ bool Engine::merge_one(Backend& be, int remaining) {
   sel_.apply(a, b, X, recs, n);
   times_.launch_s += t2 - t1;
   times_.wait_s += t3 - t2;
+  if (launched) {
+    times_.wait_hit_s += t3 - t2;
+    ++times_.n_hit;
+  } else {
+    times_.wait_miss_s += t3 - t2;
+    ++times_.n_miss;
+  }
   times_.apply_s += now_seconds() - t3;
   return true;
 }
@@ -167,6 +174,12 @@ int Engine::train(Backend& be) {
   if (trace_) std::fflush(trace_);
   times_.train_s += now_seconds() - t0;
   if (log_ >= 1) std::printf("[INFO]\t Training completed. Performed %d merges\n", total);
+  if (std::getenv("SHREDWORD_ENGINE_REPORT"))
+    std::fprintf(stderr, "[ENGINE] merges %d: select %.2f us, apply %.2f us per merge; wait %.2f us per guessed merge (%llu), "
+                 "%.2f us per posted merge (%llu)\n", total, 1e6 * times_.select_s / std::max(1, total),
+                 1e6 * times_.apply_s / std::max(1, total), 1e6 * times_.wait_hit_s / std::max<uint64_t>(1, times_.n_hit),
+                 (unsigned long long)times_.n_hit, 1e6 * times_.wait_miss_s / std::max<uint64_t>(1, times_.n_miss),
+                 (unsigned long long)times_.n_miss);
   return total;
 }
 

@@ -47,6 +47,8 @@ class Backend {
 struct EngineTimes {
   double init_s = 0, train_s = 0;
   double select_s = 0, launch_s = 0, wait_s = 0, apply_s = 0;
+  double wait_hit_s = 0, wait_miss_s = 0;  // wait_s of merges whose guess ran / had to be posted
+  uint64_t n_hit = 0, n_miss = 0;
 };
 
 class Engine {

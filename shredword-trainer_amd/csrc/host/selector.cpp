@@ -30,7 +30,7 @@ void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
 }
 
 void Selector::grow() {
-  std::vector<Info> old(table_.size() * 4, Info{kEmptyKey, 0, 0, 0});
+  HugeVec<Info> old(table_.size() * 4, Info{kEmptyKey, 0, 0, 0});
   old.swap(table_);
   mask_ = table_.size() - 1;
   for (const Info& in : old) {

@@ -17,11 +17,53 @@
 //                   in reverse order of first touch, clamped at 0, net-zero entries included.
 #pragma once
 
+#include <sys/mman.h>
+
 #include <cstddef>
 #include <cstdint>
+#include <new>
 #include <vector>
 
 namespace shred {
+
+// Allocator for the selector's big random-access arrays (pair table, heap): 2 MiB-aligned
+// anonymous mappings marked MADV_HUGEPAGE, so a lookup or a heap level costs a cache miss and
+// not also a page walk (at C3 the pair table is ~400 MB and the heap ~70 MB).  Small requests
+// use operator new.
+template <class T>
+struct HugeAlloc {
+  using value_type = T;
+  static constexpr size_t kHuge = size_t(1) << 21;
+  HugeAlloc() = default;
+  template <class U>
+  HugeAlloc(const HugeAlloc<U>&) {}
+  T* allocate(size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes < kHuge) return static_cast<T*>(::operator new(bytes));
+    const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
+    char* p = static_cast<char*>(mmap(nullptr, len + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0));
+    if (p == MAP_FAILED) throw std::bad_alloc();
+    char* a = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
+    if (a > p) munmap(p, a - p);
+    if (a + len < p + len + kHuge) munmap(a + len, (p + len + kHuge) - (a + len));
+    madvise(a, len, MADV_HUGEPAGE);
+    return reinterpret_cast<T*>(a);
+  }
+  void deallocate(T* ptr, size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes < kHuge) {
+      ::operator delete(ptr);
+      return;
+    }
+    munmap(ptr, (bytes + kHuge - 1) & ~(kHuge - 1));
+  }
+  template <class U>
+  bool operator==(const HugeAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const HugeAlloc<U>&) const { return false; }
+};
+template <class T>
+using HugeVec = std::vector<T, HugeAlloc<T>>;
 
 // One device delta record: key = slot * 4 + category (see DeltaCategory); the neighbour id is
 // slot - 1, slot 0 standing for unk_id when unk_id lies outside [0, slot capacity).
@@ -102,13 +144,13 @@ class Selector {
 
   int32_t unk_ = 0;
   uint64_t min_freq_ = 2000;
-  std::vector<Info> table_;
+  HugeVec<Info> table_;
   size_t count_ = 0;
   uint64_t mask_ = 0;
   // The reference's binary heap (heap.cpp), struct-of-arrays: the sifts compare frequencies only,
   // so they walk a dense u64 array (8 children per cache line pair) and move the payload beside.
-  std::vector<uint64_t> hf_;
-  std::vector<HeapPay> hp_;
+  HugeVec<uint64_t> hf_;
+  HugeVec<HeapPay> hp_;
   std::vector<Change> changes_;
   std::vector<uint32_t> change_index_;
   std::vector<Change> staged_;  // apply: the first counting pass

@@ -171,14 +171,6 @@ class WordLoop {
   uint64_t init_pool_n_ = 0;
   unsigned long long* lst_ = nullptr;    // per id: words-of list, pool offset | count << 32
   uint32_t* lseq_ = nullptr;             // per id: the command that made the list (~0: none)
-  unsigned long long* xsub_ = nullptr;   // per id: pair-group sub-table (offset | log2 size << 32 | valid)
-  unsigned long long* xgrp_ = nullptr;   // per id: its pair groups' pool range (start | end << 32)
-  uint32_t* wmark_ = nullptr;            // per word: the last command that scanned it
-  void* sub_ = nullptr;                  // sub-tables (16-B entries)
-  uint64_t sub_cap_ = 0;
-  unsigned long long* stg_e_ = nullptr;  // staged group entries of the merges whose groups wait
-  uint32_t* stg_dk_ = nullptr;
-  uint64_t stage_cap_ = 0;
   uint32_t id_cap_ = 0;
   unsigned long long* dsum_ = nullptr;   // delta spill tables (keys past the LDS hash), 4 x (cap + 1)
   unsigned long long* dft_ = nullptr;
