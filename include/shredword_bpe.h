@@ -153,6 +153,7 @@ typedef struct ShredStats {
   uint64_t index_staged;       /* Σ pair-group entries written */
   int64_t index_switch_merge;  /* hybrid: the first merge id of the indexed loop in the last train() (-1: none) */
   double index_switch_ms;      /* hybrid: Σ host time of the resident -> indexed switches */
+  uint64_t resident_aborts;    /* k_resident launches that found their grid not co-resident (then off) */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 
@@ -163,6 +164,12 @@ int shred_device_count(void);
  * streaming copy of `bytes`, `reps` timed launches each; GB/s of bytes moved (copy counts read +
  * write).  Returns 0, or -1 without a device / on allocation failure. */
 int shred_hbm_probe(int device, size_t bytes, int reps, double* read_gbps, double* copy_gbps);
+
+/* Diagnostic (tests of the resident loop's co-residency check): fills every wave slot of all CUs
+ * but `free_cus` with a spinning kernel on its own stream, until shred_release() or
+ * `max_seconds`; returns once it runs (NULL on bad arguments).  */
+void* shred_occupy(int device, int free_cus, double max_seconds);
+void shred_release(void* handle);
 
 /* Multi-GPU (one process per GPU, RCCL over xGMI): rank 0 calls shred_dist_unique_id, the
  * bytes are broadcast out of band (torch.distributed), then every rank calls shred_dist_init

@@ -15,6 +15,7 @@
 // with 64-bit atomics (sum) and atomicMin (first touch), so the reduction is order-free and the
 // result bit-identical run to run.
 #include <hip/hip_runtime.h>
+#include <thread>
 
 #ifndef SHRED_MAX_GROUPS
 #define SHRED_MAX_GROUPS 256
@@ -986,6 +987,9 @@ constexpr uint32_t kResGatherWg = 1, kResFirstWorker = 2;
 constexpr int kResGatherBatch = 16;  // records per gatherer thread per round trip
 static_assert(kResDeltaW < (1 << 12) && kResMaxTiles * kWaveTok < (1u << 22), "region header fields (k_resident)");
 constexpr uint32_t kOpUnmerge = 4;
+// k_resident: not every workgroup became resident within the leader's bound (another kernel or
+// process holds CUs); every workgroup leaves without touching the table, the host falls back
+constexpr uint32_t kOpAbort = 5;
 
 // One host command (pinned host memory, written by the host; only the leader reads it).
 // Every field is an 8-byte granule {seq, value} written by one aligned 8-byte store, so the
@@ -1030,7 +1034,10 @@ struct ResParams {
   const ResMbox* mbox;
   uint32_t* cmd;             // device command ring: kResRing x 8 words [a, b, X, nparts, slot, op, stamp lo, hi]
   u64* q;                    // per-workgroup queues: kResRing entries each (zeroed before the launch)
-  uint32_t* status;          // host-visible: [0] kOpTimeout once the leader gave up waiting
+  uint32_t* status;          // host-visible: [0] kOpTimeout / kOpAbort when the launch ended itself,
+                             //   [2] 1 once every workgroup was seen resident
+  uint32_t* arrive;          // workgroups that started (zeroed before the launch)
+  uint32_t arrive_polls;     // the leader's bound on waiting for them
   uint32_t seq0;             // first command number of this launch
   uint32_t leader_polls;     // idle leader iterations before the launch ends itself
   uint32_t keys_per_merge, slot_cap;
@@ -1387,6 +1394,9 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   const uint32_t t0 = p.wg_tiles[me], nt = p.wg_tiles[me + 1] - t0;
   const uint32_t r0 = p.wg_rank[me], nr = p.wg_rank[me + 1] - r0;
   int32_t* st = s_tok[wid];
+  // ---- co-residency: every workgroup counts itself in; the leader dispatches nothing until all
+  // have (below), so a launch that is only partly resident aborts instead of hanging
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(p.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   // ---- residency: tiles, weights and signatures into LDS
   for (uint32_t i = threadIdx.x; i < nt; i += kThreads) {
@@ -1428,6 +1438,32 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   uint32_t consumed = 0;     // thread 0: entries taken from this workgroup's queue
   uint32_t exit_op = kOpStop;
   const u64* myq = p.q + (size_t)me * kResRing * 2;
+  if (me == 0 && wid == 0) {  // the leader waits (bounded) until every workgroup is resident
+    bool all = false;
+    for (uint32_t k = 0; k < p.arrive_polls && !all; ++k) {
+      all = __hip_atomic_load(p.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= G;
+      if (!all) __builtin_amdgcn_s_sleep(8);
+    }
+    if (lane == 0) {
+      if (all) {
+        __hip_atomic_store(p.status + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {  // an abort as the first entry of every queue (the missing workgroups read it when
+                // they start, after the host has moved on to another stream)
+        for (uint32_t wg = 0; wg < G; ++wg) {
+          u64 h0, h1;
+          q_pack(1, 0, kOpAbort, 0, G, 0, 0, 0, &h0, &h1);
+          u64* e = p.q + (size_t)wg * kResRing * 2;
+          __hip_atomic_store(e, h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(e + 1, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __threadfence_system();
+        __hip_atomic_store(p.status, kOpAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      s_cmd[7] = all ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  if (me == 0 && s_cmd[7] == 0) return;  // aborted: the table was not touched
   for (;;) {
     // ---- the leader hands out the next host command, if one is posted (one poll per pass)
     if (me == 0 && wid == 0) {
@@ -1512,6 +1548,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
     __syncthreads();
     const uint32_t op = s_cmd[0];
     if (op == 0) continue;  // the leader's workgroup: nothing queued for it yet
+    if (op == kOpAbort) return;  // the launch aborted before any merge: nothing to write back
     if (op != kOpMerge && op != kOpUnmerge) {
       exit_op = op;
       break;
@@ -2509,6 +2546,71 @@ T* dalloc(size_t n, size_t* acc) {
 }  // namespace
 
 // ==========================================================================================
+// Diagnostic (tests of k_resident's co-residency check): workgroups of 1024 threads that fill
+// every wave slot of all CUs but `free_cus`, spinning on their own stream until the host raises a
+// flag or `max_seconds` pass (every wave reaches one of the two exits).  Each workgroup marks
+// itself started.
+__global__ __launch_bounds__(1024) void k_occupy(const uint32_t* release, uint32_t* started, uint64_t max_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) __hip_atomic_store(started + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    if (__hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
+    __builtin_amdgcn_s_sleep(64);
+  }
+}
+
+struct Occupier {
+  int ordinal;
+  hipStream_t stream;
+  uint32_t* host;  // pinned: [0] release flag, [1..] started marks
+  void* dev;
+  uint32_t groups;
+};
+
+void* Device::occupy(int ordinal, int free_cus, double max_seconds) {
+  if (max_seconds <= 0 || hipSetDevice(ordinal) != hipSuccess) return nullptr;
+  hipDeviceProp_t pr;
+  HIP_OK(hipGetDeviceProperties(&pr, ordinal));
+  const int per_cu = std::max(1, pr.maxThreadsPerMultiProcessor / 1024);
+  const int groups = per_cu * (pr.multiProcessorCount - free_cus);
+  const size_t lds = 0;
+  if (groups < 1) return nullptr;
+  Occupier* o = new Occupier{ordinal, nullptr, nullptr, nullptr, (uint32_t)groups};
+  HIP_OK(hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking));
+  const unsigned pin = hipHostMallocMapped | hipHostMallocCoherent;
+  HIP_OK(hipHostMalloc((void**)&o->host, (size_t)(groups + 1) * sizeof(uint32_t), pin));
+  std::memset(o->host, 0, (size_t)(groups + 1) * sizeof(uint32_t));
+  HIP_OK(hipHostGetDevicePointer(&o->dev, o->host, 0));
+  uint32_t* d = static_cast<uint32_t*>(o->dev);
+  k_occupy<<<groups, 1024, lds, o->stream>>>(d, d + 1, (uint64_t)(max_seconds * 1e8));
+  HIP_OK(hipGetLastError());
+  const double t0 = now_seconds();  // until every workgroup runs (or 10 s)
+  for (;;) {
+    uint32_t n = 0;
+    for (int g = 0; g < groups; ++g) n += __atomic_load_n(&o->host[1 + g], __ATOMIC_ACQUIRE);
+    if (n == (uint32_t)groups || now_seconds() - t0 > 10.0) {
+      if (std::getenv("SHREDWORD_RESIDENT_REPORT"))
+ std::fprintf(stderr, "[OCCUPY] %u of %d workgroups (1024 threads, %d per CU) running after %.1f ms\n", n, groups, per_cu,
+                     1e3 * (now_seconds() - t0));
+      break;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+  return o;
+}
+
+void Device::release(void* handle) {
+  Occupier* o = static_cast<Occupier*>(handle);
+  if (!o) return;
+  (void)hipSetDevice(o->ordinal);
+  __atomic_store_n(&o->host[0], 1u, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(o->stream);
+  (void)hipStreamDestroy(o->stream);
+  (void)hipHostFree(o->host);
+  delete o;
+}
+
 int Device::hbm_probe(int ordinal, size_t bytes, int reps, double* read_gbps, double* copy_gbps) {
   std::string why;
   if (!available(&why) || bytes < (1u << 20) || reps < 1) return -1;
@@ -2608,6 +2710,7 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
   if (const char* e = std::getenv("SHREDWORD_RESIDENT")) resident_on_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_INDEX")) index_on_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_HYBRID")) hybrid_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SHREDWORD_RESIDENT_ARRIVE_POLLS")) res_arrive_polls_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_SWITCH_OCC")) switch_occ_ = std::strtoull(e, nullptr, 10);
   int nb = 0;  // resident workgroups of k_merge per CU
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_merge<true>), kThreads, 0));
@@ -2679,6 +2782,11 @@ Device::~Device() {
   delete wl_;  // ends its launch first
   wl_ = nullptr;
   (void)hipStreamSynchronize(S(stream_));
+  for (void* s : retired_streams_) {  // aborted resident launches: their late workgroups leave first
+    (void)hipStreamSynchronize(S(s));
+    (void)hipStreamDestroy(S(s));
+  }
+  retired_streams_.clear();
   free_resident();
   if (res_mbox_) (void)hipHostFree(res_mbox_);
   if (res_status_) (void)hipHostFree(res_status_);
@@ -2818,18 +2926,36 @@ void Device::hybrid_switch(int32_t X) {
   switch_ms_ += 1e3 * (now_seconds() - t0);
 }
 
+// The resident launch aborted before dispatching anything (some workgroups never became
+// resident: another kernel or process holds CUs).  Resident is off for this device from here on;
+// the merges posted to it run again, in order, on the indexed loop (or the launch path).  The
+// launch's missing workgroups may start only once those CUs free up, and they hold its stream
+// until then, so all further work moves to a fresh stream.
+void Device::resident_abort_fallback() {
+  std::vector<ResPost> inflight;
+  inflight.swap(res_posted_);
+  res_running_ = false;
+  resident_ok_ = false;
+  ++res_aborts_;
+  for (int32_t& x : res_abandoned_) x = -1;
+  retired_streams_.push_back(stream_);
+  hipStream_t s;
+  HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  stream_ = s;
+  if (wl_) wl_->set_stream(stream_);
+  if (std::getenv("SHREDWORD_RESIDENT_REPORT"))
+    std::fprintf(stderr, "[RESIDENT] launch aborted (not every workgroup resident): %zu merges move to the %s\n",
+                 inflight.size(), wl_ && wl_->ready() ? "indexed loop" : "launch path");
+  for (const ResPost& rp : inflight) {
+    const int32_t ab[2] = {rp.a, rp.b};
+    merge_chain(ab, 1, rp.X);
+  }
+}
+
 // A tile-path merge ran after the loop's last merge: the loop takes the tiles' words.
 void Device::index_refresh() {
-  std::vector<int32_t> all(tok_elems_ + 4);
-  TiledStream ts;
-  ts.off.resize(ntiles_);
-  ts.len.resize(ntiles_);
-  HIP_OK(hipMemcpyAsync(all.data(), tok_, all.size() * sizeof(int32_t), hipMemcpyDeviceToHost, S(stream_)));
-  HIP_OK(hipMemcpyAsync(ts.off.data(), tile_off_, ntiles_ * sizeof(uint64_t), hipMemcpyDeviceToHost, S(stream_)));
-  HIP_OK(hipMemcpyAsync(ts.len.data(), tile_len_, ntiles_ * sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
-  HIP_OK(hipStreamSynchronize(S(stream_)));
-  ts.tok = std::move(all);
-  if (!wl_->load_current(ts)) fatal("index_refresh: the tile stream no longer matches the word table");
+  park();
+  wl_->load_tiles(tok_, tile_off_, tile_len_);
   words_stale_ = false;
   wl_pristine_index_ = false;
 }
@@ -3090,7 +3216,13 @@ void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   }
   if (n == 1 && run_count_ == 0 && ntiles_ && resident_eligible() && X0 < (1 << 20)) {  // k_resident (ids: 20 bits)
     if (res_posted_.size() >= (size_t)kResSlots) fatal("merge_chain: every resident slot has a merge in flight");
-    const int slot = pick_resident_slot();
+    const int slot = res_running_ && __atomic_load_n(&res_status_[0], __ATOMIC_ACQUIRE) == kOpAbort ? -1
+                                                                                                    : pick_resident_slot();
+    if (slot < 0) {  // the launch aborted (not co-resident): this merge and those in flight go elsewhere
+      resident_abort_fallback();
+      merge_chain(ab, n, X0);
+      return;
+    }
     bool grow = false;
     for (const MergeSlot& s2 : slot_) grow |= !s2.dsum || (uint32_t)X0 + 2 > s2.cap;
     if (grow) {  // the delta tables grow: only between launches
@@ -3571,9 +3703,9 @@ void Device::download_tokens(std::vector<int32_t>* out) {
 // roll back, park.  See the kernel's comment for the protocol.
 void Device::free_resident() {
   for (void* p : {(void*)res_wg_tiles_, (void*)res_wg_rank_, (void*)res_tile_lofs_, (void*)res_cmd_, (void*)res_q_,
-                  (void*)res_dbg_, (void*)res_stamps_})
+                  (void*)res_dbg_, (void*)res_stamps_, (void*)res_arrive_})
     if (p) HIP_OK(hipFree(p));
-  res_wg_tiles_ = res_wg_rank_ = res_tile_lofs_ = res_cmd_ = nullptr;
+  res_wg_tiles_ = res_wg_rank_ = res_tile_lofs_ = res_cmd_ = res_arrive_ = nullptr;
   res_q_ = nullptr;
   res_dbg_ = nullptr;
   res_stamps_ = nullptr;
@@ -3664,6 +3796,7 @@ void Device::plan_resident(const TiledStream& ts) {
   res_tile_lofs_ = dalloc<uint32_t>(T, &bytes_alloc_);
   res_cmd_ = dalloc<uint32_t>(kResRing * 8, &bytes_alloc_);
   res_q_ = dalloc<uint64_t>((size_t)G * kResRing * 2, &bytes_alloc_);
+  res_arrive_ = dalloc<uint32_t>(16, &bytes_alloc_);
   HIP_OK(hipMemcpy(res_wg_tiles_, wg_tiles.data(), (G + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(res_wg_rank_, wg_rank.data(), (G + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_OK(hipMemcpy(res_tile_lofs_, lofs.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -3698,6 +3831,8 @@ void Device::plan_resident(const TiledStream& ts) {
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kThreads, shm));
   if (per_cu < 1 || (long)per_cu * cu_count_ < (long)G) return;
   resident_ok_ = true;
+  if (std::getenv("SHREDWORD_RESIDENT_REPORT"))
+    std::fprintf(stderr, "[RESIDENT] plan: grid %u, %zu B of LDS per workgroup, %d per CU\n", G, (size_t)shm, per_cu);
 }
 
 void Device::set_resident(bool on) {
@@ -3739,6 +3874,8 @@ void Device::start_resident() {
   rp.cmd = res_cmd_;
   rp.q = reinterpret_cast<u64*>(res_q_);
   rp.status = (uint32_t*)res_status_dev_;
+  rp.arrive = res_arrive_;
+  rp.arrive_polls = res_arrive_polls_;
   rp.seq0 = seq_ + 1;
   rp.leader_polls = 1u << 23;  // ~10 s without a command: the launch ends itself (the host relaunches)
   rp.keys_per_merge = keys_per_merge_;
@@ -3765,7 +3902,9 @@ void Device::start_resident() {
   rp.dbg = res_dbg_;
   rp.stamps = U(res_stamps_);
   res_status_[0] = 0;
+  res_status_[2] = 0;
   HIP_OK(hipMemsetAsync(res_q_, 0, (size_t)res_grid_ * kResRing * 2 * sizeof(uint64_t), S(stream_)));
+  HIP_OK(hipMemsetAsync(res_arrive_, 0, sizeof(uint32_t), S(stream_)));
   HIP_OK(hipEventRecord((hipEvent_t)res_ev_[0], S(stream_)));
   // a plain launch: one workgroup per CU by its LDS footprint, checked against the occupancy
   // query at plan time (plan_resident), so every workgroup is resident together
@@ -3840,17 +3979,18 @@ int Device::pick_resident_slot() {
       return s;
     }
     if (wait_slot < 0) fatal("k_resident: no free merge slot");
-    wait_resident(slot_[wait_slot], res_abandoned_[wait_slot]);
+    if (!wait_resident(slot_[wait_slot], res_abandoned_[wait_slot])) return -1;  // the launch aborted
   }
 }
 
-void Device::wait_resident(const MergeSlot& sl, int32_t X) {
+bool Device::wait_resident(const MergeSlot& sl, int32_t X) {
   volatile uint32_t* flag = sl.host_count + 1;
   const double t0 = now_seconds();
   unsigned spins = 0;
   while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != (uint32_t)X) {
     __builtin_ia32_pause();
     if (++spins % 4096 != 0) continue;
+    if (__atomic_load_n(&res_status_[0], __ATOMIC_ACQUIRE) == kOpAbort) return false;
     if (__atomic_load_n(&res_status_[0], __ATOMIC_ACQUIRE) == kOpTimeout)
       fatal("k_resident ended on its time-out before a posted merge completed");
     if (res_dbg_ && now_seconds() - t0 > 3.0) resident_dump("no flag after 3 s");
@@ -3860,10 +4000,15 @@ void Device::wait_resident(const MergeSlot& sl, int32_t X) {
       if (now_seconds() - t0 > 600.0) fatal("k_resident did not signal completion within 600 s");
     }
   }
+  return true;
 }
 
 size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   if (res_posted_.empty() || res_posted_.front().X != X) fatal("collect: merge X is not the oldest posted merge");
+  if (!wait_resident(slot_[res_posted_.front().slot], X)) {  // not co-resident: nothing ran
+    resident_abort_fallback();
+    return collect(X, recs);
+  }
   const ResPost rp = res_posted_.front();
   res_posted_.erase(res_posted_.begin());
   MergeSlot& sl = slot_[rp.slot];

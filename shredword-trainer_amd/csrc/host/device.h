@@ -47,6 +47,11 @@ class Device : public Backend {
   // Achievable HBM bandwidth on `ordinal` (streaming read and copy of `bytes`, `reps` timed
   // launches each, HIP events); GB/s of bytes moved.  0, or -1 without a device.
   static int hbm_probe(int ordinal, size_t bytes, int reps, double* read_gbps, double* copy_gbps);
+  // Diagnostic: fills every wave slot of all CUs but `free_cus` with a spinning kernel on its own
+  // stream (returns once it runs) until release() or max_seconds; tests the resident loop's
+  // co-residency check.
+  static void* occupy(int ordinal, int free_cus, double max_seconds);
+  static void release(void* handle);
 
   explicit Device(int device_ordinal);
   ~Device();
@@ -134,6 +139,7 @@ class Device : public Backend {
   double switch_ms() const { return switch_ms_; }
   const WordLoop* word_loop() const { return wl_; }
   uint64_t resident_launches() const { return res_launches_; }
+  uint64_t resident_aborts() const { return res_aborts_; }
   bool resident_tokens_in_lds() const { return res_lds_tok_; }
   double resident_ms() const { return res_ms_; }
   // mean dispatch -> host flag time of a resident merge (device clock), us
@@ -331,6 +337,11 @@ class Device : public Backend {
   double switch_ms_ = 0;           // Σ host time of the switches (tiles -> words + index build)
   int32_t reserved_max_id_ = 0;    // the last reserve_ids()
   void hybrid_switch(int32_t X);
+  void resident_abort_fallback();
+  std::vector<void*> retired_streams_;  // streams of aborted resident launches
+  uint64_t res_aborts_ = 0;
+  uint32_t* res_arrive_ = nullptr;      // k_resident: workgroups that started
+  uint32_t res_arrive_polls_ = 20000;   // the leader's co-residency bound (~20 ms; env SHREDWORD_RESIDENT_ARRIVE_POLLS)
   uint64_t wl_ms_seen_ = 0;        // merges already folded into times_
   double wl_kms_seen_ = 0;         // launch time already folded into times_
 
@@ -346,7 +357,7 @@ class Device : public Backend {
   void free_resident();
   void start_resident();
   uint32_t post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int slot);
-  void wait_resident(const MergeSlot& sl, int32_t X);
+  bool wait_resident(const MergeSlot& sl, int32_t X);  // false: the launch aborted
   int pick_resident_slot();
   size_t collect_resident(int32_t X, const DeltaRecord** recs);
   [[noreturn]] void resident_dump(const char* why);

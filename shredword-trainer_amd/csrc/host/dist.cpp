@@ -1,11 +1,13 @@
 // Multi-GPU plumbing over RCCL: see dist.h.
 #include "dist.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <unordered_map>
 
 #include "common.h"
@@ -13,9 +15,47 @@
 namespace shred {
 
 namespace {
+// RCCL is opened on first use, not linked: a one-GPU process never maps it, and a process that
+// already holds one (PyTorch-ROCm's, loaded by torch.distributed) shares that copy.  Two RCCLs
+// in one process with torch abort at exit (double free), measured.
+struct Rccl {
+  decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;
+  decltype(&ncclAllReduce) AllReduce = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+};
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = nullptr;
+    for (const char* n : {"librccl.so", "librccl.so.1"})  // a copy already in the process
+      if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+    for (const char* n : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1"})
+      if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+    if (!h) fatal("RCCL (librccl.so.1) could not be loaded: the multi-GPU exchange needs it");
+    auto sym = [&](const char* name) {
+      void* f = dlsym(h, name);
+      if (!f) fatal("RCCL lacks a symbol the exchange uses");
+      return f;
+    };
+    r.GetUniqueId = reinterpret_cast<decltype(r.GetUniqueId)>(sym("ncclGetUniqueId"));
+    r.CommInitRank = reinterpret_cast<decltype(r.CommInitRank)>(sym("ncclCommInitRank"));
+    r.CommInitAll = reinterpret_cast<decltype(r.CommInitAll)>(sym("ncclCommInitAll"));
+    r.CommDestroy = reinterpret_cast<decltype(r.CommDestroy)>(sym("ncclCommDestroy"));
+    r.AllGather = reinterpret_cast<decltype(r.AllGather)>(sym("ncclAllGather"));
+    r.AllReduce = reinterpret_cast<decltype(r.AllReduce)>(sym("ncclAllReduce"));
+    r.GetErrorString = reinterpret_cast<decltype(r.GetErrorString)>(sym("ncclGetErrorString"));
+  });
+  return r;
+}
+
 void nccl_ok(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) {
-    std::fprintf(stderr, "[ERROR]\t RCCL %s failed: %s\n", what, ncclGetErrorString(r));
+    std::fprintf(stderr, "[ERROR]\t RCCL %s failed: %s\n", what, rccl().GetErrorString(r));
     std::fflush(stderr);
     std::abort();
   }
@@ -37,7 +77,7 @@ DistState& dist_state() {
 int dist_unique_id(void* out, size_t cap) {
   if (cap < sizeof(ncclUniqueId)) return -1;
   ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  if (rccl().GetUniqueId(&id) != ncclSuccess) return -1;
   std::memcpy(out, &id, sizeof(id));
   return (int)sizeof(id);
 }
@@ -54,7 +94,7 @@ int dist_init(int rank, int world, const void* id, size_t len, int device) {
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   ncclComm_t comm;
-  if (ncclCommInitRank(&comm, world, uid, rank) != ncclSuccess) return -1;
+  if (rccl().CommInitRank(&comm, world, uid, rank) != ncclSuccess) return -1;
   s.rank = rank;
   s.world = world;
   s.device = device;
@@ -64,13 +104,13 @@ int dist_init(int rank, int world, const void* id, size_t len, int device) {
 
 int dist_finalize() {
   DistState& s = dist_state();
-  if (s.comm) ncclCommDestroy((ncclComm_t)s.comm);
+  if (s.comm) rccl().CommDestroy((ncclComm_t)s.comm);
   s = DistState();
   return 0;
 }
 
 void dist_allgather_device(void* comm, const void* send, void* recv, size_t bytes, void* stream) {
-  nccl_ok(ncclAllGather(send, recv, bytes, ncclUint8, (ncclComm_t)comm, (hipStream_t)stream), "ncclAllGather");
+  nccl_ok(rccl().AllGather(send, recv, bytes, ncclUint8, (ncclComm_t)comm, (hipStream_t)stream), "ncclAllGather");
 }
 
 void* dist_local_comm(int device) {
@@ -80,14 +120,14 @@ void* dist_local_comm(int device) {
   hip_ok(hipSetDevice(device), "hipSetDevice");
   ncclComm_t comm;
   int dev = device;
-  nccl_ok(ncclCommInitAll(&comm, 1, &dev), "ncclCommInitAll");
+  nccl_ok(rccl().CommInitAll(&comm, 1, &dev), "ncclCommInitAll");
   comms.emplace(device, comm);
   return comm;
 }
 
 void dist_allreduce_device(uint64_t* buf, size_t n, bool min_op, void* stream) {
   if (!dist_active() || n == 0) return;
-  nccl_ok(ncclAllReduce(buf, buf, n, ncclUint64, min_op ? ncclMin : ncclSum, (ncclComm_t)dist_state().comm,
+  nccl_ok(rccl().AllReduce(buf, buf, n, ncclUint64, min_op ? ncclMin : ncclSum, (ncclComm_t)dist_state().comm,
                         (hipStream_t)stream),
           "ncclAllReduce");
 }
@@ -128,7 +168,7 @@ void dist_merge_pairs(std::vector<PairCount>* pairs) {
   hip_ok(hipMalloc(&dsend, bytes), "hipMalloc");
   hip_ok(hipMalloc(&drecv, bytes * s.world), "hipMalloc");
   hip_ok(hipMemcpy(dsend, send.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy");
-  nccl_ok(ncclAllGather(dsend, drecv, bytes, ncclUint8, (ncclComm_t)s.comm, nullptr), "ncclAllGather");
+  nccl_ok(rccl().AllGather(dsend, drecv, bytes, ncclUint8, (ncclComm_t)s.comm, nullptr), "ncclAllGather");
   hip_ok(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
   std::vector<uint8_t> recv(bytes * s.world);
   hip_ok(hipMemcpy(recv.data(), drecv, recv.size(), hipMemcpyDeviceToHost), "hipMemcpy");

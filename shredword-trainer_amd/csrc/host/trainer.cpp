@@ -376,6 +376,7 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
     s->resident_launches = t->dev->resident_launches();
     s->resident_ms = t->dev->resident_ms();
     s->resident_latency_us = t->dev->resident_latency_us();
+    s->resident_aborts = t->dev->resident_aborts();
     if (const WordLoop* wl = t->dev->word_loop()) {
       const WordLoopStats& w = wl->stats();
       s->index_on = t->dev->index_eligible() ? 1 : 0;
@@ -432,6 +433,9 @@ int shred_device_count(void) {
 int shred_hbm_probe(int device, size_t bytes, int reps, double* read_gbps, double* copy_gbps) {
   return Device::hbm_probe(device, bytes, reps, read_gbps, copy_gbps);
 }
+
+void* shred_occupy(int device, int free_cus, double max_seconds) { return Device::occupy(device, free_cus, max_seconds); }
+void shred_release(void* handle) { Device::release(handle); }
 
 int shred_dist_unique_id(void* out, size_t cap) { return dist_unique_id(out, cap); }
 int shred_dist_init(int rank, int world, const void* id, size_t len, int device) {

@@ -98,6 +98,11 @@ class WordLoop {
   // Ends the persistent launch (nothing may be in flight).
   void stop();
   bool running() const { return running_; }
+  // Later work goes to this stream (nothing may be in flight).
+  void set_stream(void* s) {
+    if (running_) stop();
+    stream_ = s;
+  }
 
   // Writes the current words back into the tile stream (headers + tokens, tile_len), so the tile
   // kernels (K1, K6, downloads) see the merged table.  No-op when nothing changed since.

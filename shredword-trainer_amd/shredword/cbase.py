@@ -35,20 +35,6 @@ def _get_lib_path():
     raise FileNotFoundError(f"Could not find trainer library in {search}. Available files: {available}")
 
 
-def _share_hip_runtime():
-    """One HIP stack per process.  PyTorch-ROCm ships its own HIP/HSA/rocprofiler-register
-    libraries and asks for them by unversioned names; a process whose first HIP call came from
-    libtrainer.so (/opt/rocm's stack) and that imports torch later holds two copies and aborts at
-    exit (measured: even hipGetDeviceCount before `import torch` does it).  Importing torch first,
-    when it is installed, makes libtrainer.so bind to torch's already-loaded runtime (same SONAME),
-    as in bench.py.  torch is plumbing only; nothing here uses it."""
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
-
-
-_share_hip_runtime()
 _lib_path = _get_lib_path()
 lib = ctypes.CDLL(_lib_path, mode=getattr(ctypes, "RTLD_GLOBAL", 0))
 
@@ -87,7 +73,8 @@ class ShredStats(Structure):
                 ("index_wait_us", c_double),
                 ("index_dev_lookup_us", c_double), ("index_dev_scan_us", c_double),
                 ("index_scanned", c_uint64), ("index_build_us", c_double), ("index_no_sub", c_uint64),
-                ("index_staged", c_uint64), ("index_switch_merge", c_int64), ("index_switch_ms", c_double)]
+                ("index_staged", c_uint64), ("index_switch_merge", c_int64), ("index_switch_ms", c_double),
+                ("resident_aborts", c_uint64)]
 
 
 Trainer = c_void_p
@@ -127,6 +114,8 @@ lib.shred_get_stats.argtypes, lib.shred_get_stats.restype = [Trainer, POINTER(Sh
 lib.shred_device_count.argtypes, lib.shred_device_count.restype = [], c_int
 lib.shred_hbm_probe.argtypes = [c_int, c_size_t, c_int, POINTER(c_double), POINTER(c_double)]
 lib.shred_hbm_probe.restype = c_int
+lib.shred_occupy.argtypes, lib.shred_occupy.restype = [c_int, c_int, c_double], c_void_p
+lib.shred_release.argtypes, lib.shred_release.restype = [c_void_p], None
 lib.shred_dist_unique_id.argtypes, lib.shred_dist_unique_id.restype = [c_void_p, c_size_t], c_int
 lib.shred_dist_init.argtypes, lib.shred_dist_init.restype = [c_int, c_int, c_void_p, c_size_t, c_int], c_int
 lib.shred_dist_finalize.argtypes, lib.shred_dist_finalize.restype = [], c_int

@@ -138,7 +138,10 @@ def medium_oracle(medium_corpus, tmp_path_factory):
 @pytest.mark.parametrize("layout,bucket", [("types", 0), ("types", 8), ("stream", 64)])
 def test_exchange_path_matches_oracle(layout, bucket, medium_corpus, medium_oracle, tmp_path):
     """The multi-GPU path on one GPU: every merge's records go through the RCCL all-gather (a
-    single-rank communicator) and k_xout, small buckets force the overflow round."""
+    single-rank communicator) and k_xout, small buckets force the overflow round.  torch is
+    imported first, as in a real multi-GPU process (torch.distributed): the library then shares
+    torch's RCCL instead of opening its own (two RCCLs in one process abort at exit)."""
+    import torch  # noqa: F401
     t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
     t.set_option("layout", layout)
     t.set_option("exchange", "local")
@@ -472,3 +475,93 @@ def test_gpu_word_count_matches_host(kind, medium_corpus, tmp_path, monkeypatch)
         outs.append((n, model, vocab, st["num_words"], st["num_symbols"], st["num_occurrences"]))
     assert outs[0] == outs[1]
 
+
+
+def test_resident_abort_falls_back(medium_corpus, medium_oracle, tmp_path, monkeypatch):
+    """k_resident's co-residency check: with a zero bound the leader never sees every workgroup
+    (an abort on every launch); the merges it was given run again on the indexed loop, and the
+    files are still the oracle's."""
+    monkeypatch.setenv("SHREDWORD_RESIDENT_ARRIVE_POLLS", "0")
+    t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+    t.load_corpus(medium_corpus)
+    n, model, vocab = _train_bytes(t, tmp_path, "ab")
+    st = t.stats()
+    t.destroy()
+    assert (model, vocab) == medium_oracle
+    assert n > 1000
+    assert st["resident_aborts"] >= 1 and st["index_merges"] > 0
+
+
+def test_resident_partial_residency(medium_corpus, medium_oracle, tmp_path):
+    """Another process fills every wave slot of all CUs but 16 while train() runs: k_resident's grid
+    cannot be co-resident, its leader aborts within its bound instead of hanging, and the run
+    completes bit-exact through the fallback (reported in stats).  (A second process: kernels of
+    one process may share a hardware queue and then never run side by side.)"""
+    import sys
+    holder = subprocess.Popen(
+        [sys.executable, "-c",
+         "import sys; sys.path.insert(0, %r)\n"
+         "from shredword.cbase import lib\n"
+         "h = lib.shred_occupy(0, 16, 60.0)\n"
+         "print('ready' if h else 'failed', flush=True)\n"
+         "sys.stdin.read()\n"
+         "lib.shred_release(h)\n" % os.path.join(os.path.dirname(ORACLE), "shredword-trainer_amd")],
+        stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    try:
+        assert holder.stdout.readline().strip() == "ready"
+        t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+        t.load_corpus(medium_corpus)
+        n, model, vocab = _train_bytes(t, tmp_path, "pr")
+        st = t.stats()
+    finally:
+        holder.stdin.close()
+        holder.wait(timeout=120)
+    t.destroy()
+    assert (model, vocab) == medium_oracle
+    assert n > 1000
+    assert st["resident_aborts"] >= 1
+
+
+_PLAIN_CTYPES = r'''
+import ctypes, os, sys, tempfile
+from ctypes import c_size_t, c_int32, c_float, c_uint64, c_char_p, c_int, c_void_p, Structure, POINTER
+lib = ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_GLOBAL)   # as the reference's cbase.py:28-30
+class BPEConfig(Structure):
+    _fields_ = [("target_vocab_size", c_size_t), ("unk_id", c_int32), ("character_coverage", c_float),
+                ("min_pair_freq", c_uint64)]
+lib.create_trainer.argtypes, lib.create_trainer.restype = [POINTER(BPEConfig)], c_void_p
+lib.bpe_load_corpus.argtypes, lib.bpe_load_corpus.restype = [c_void_p, c_char_p], c_int
+lib.bpe_train.argtypes, lib.bpe_train.restype = [c_void_p], c_int
+lib.bpe_save.argtypes, lib.bpe_save.restype = [c_void_p, c_char_p, c_char_p], None
+lib.bpe_trainer_destroy.argtypes, lib.bpe_trainer_destroy.restype = [c_void_p], None
+d = tempfile.mkdtemp()
+p = os.path.join(d, "c.txt")
+open(p, "w").write("ab abc aab bca the then them other " * 3000)
+cfg = BPEConfig(300, 0, 0.995, 2)
+t = lib.create_trainer(ctypes.byref(cfg))
+assert lib.bpe_load_corpus(t, p.encode()) == 0
+n = lib.bpe_train(t)
+lib.bpe_save(t, os.path.join(d, "m").encode(), os.path.join(d, "v").encode())
+lib.bpe_trainer_destroy(t)
+assert n > 0
+if sys.argv[2] == "torch":
+    import torch
+    x = torch.arange(1000, device="cuda").sum().item()
+    assert x == 499500
+print("ok", n, flush=True)
+'''
+
+
+@pytest.mark.parametrize("then", ["torch", "none"])
+def test_plain_ctypes_then_torch_exits_cleanly(then, tmp_path):
+    """The reference's binding (plain ctypes.CDLL of the library, no torch imported first), a
+    train, then `import torch` and a CUDA op in the same process: one HIP runtime, exit code 0."""
+    import sys
+    from conftest import PKG
+    script = tmp_path / "plain.py"
+    script.write_text(_PLAIN_CTYPES)
+    lib_path = os.path.join(PKG, "shredword", "libtrainer.so")
+    proc = subprocess.run([sys.executable, str(script), lib_path, then], capture_output=True, text=True, timeout=240,
+                          env=dict(os.environ, SHREDWORD_LOG="0"))
+    assert proc.returncode == 0, (proc.returncode, proc.stderr[-2000:])
+    assert proc.stdout.strip().startswith("ok")

@@ -62,10 +62,8 @@ def test_types_layout_matches_reference(name, case_corpus, tmp_path):
     case, corpus = case_corpus(name)
     st = {}
     _check(case, _train(case, corpus, tmp_path, "types", stats=st))
-    if case["merges"] > 0:
-        assert st["index_on"] == 1
-        if not name.startswith("adv_"):  # (a word longer than a tile: the launch path, then the loop)
-            assert st["resident_launches"] > 0 or st["index_merges"] >= case["merges"]
+    if case["merges"] > 0 and not name.startswith("adv_"):  # (adv_: a word longer than a tile)
+        assert st["resident_launches"] > 0 or st["index_merges"] >= case["merges"], st
 
 
 @pytest.mark.parametrize("name", API_CASES)
