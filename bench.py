@@ -139,7 +139,8 @@ def cpu_baseline_finish(h, cfg_name, target_merges, gpu_merges, timeout=600):
     h["err"].close()
     if h["proc"].returncode != 0 or "TIMING" not in err:
         raise RuntimeError(f"bpe_oracle failed (rc {h['proc'].returncode}): {err[-300:]}")
-    fields = dict(kv.split("=") for kv in err.split("TIMING", 1)[1].split())
+    line = err.split("TIMING", 1)[1].splitlines()[0]
+    fields = dict(kv.split("=", 1) for kv in line.split() if "=" in kv)
     merges, train_s, load_s = int(fields["merges"]), float(fields["train"]), float(fields["load"])
     res = {
         "value": merges / train_s if train_s > 0 else None, "unit": "merges/s", "cores": 1, "kind": "port",
