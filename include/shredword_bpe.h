@@ -92,6 +92,11 @@ int loadVocab(void* trainer, const char* path);
  *                               types layout, files without NUL bytes; same table either way)
  *   exchange_bucket = <n>       multi-GPU: records per rank in the fixed all-gather bucket
  *                               (default 1024; larger record sets take a second round)
+ *   verify_argmax = <n>         debug (K5 check): every n merges (0 = off, the default; env
+ *                               SHREDWORD_VERIFY_ARGMAX) the device recounts the corpus's pairs
+ *                               and reduces them (k_pair_max): the host heap's selected frequency
+ *                               must be the largest pair count and the pair's own count
+ *                               (stats: verify_checks, verify_failures; results are unchanged)
  * Returns 0, or -1 for an unknown key/value. */
 int shred_set_option(Trainer* trainer, const char* key, const char* value);
 /* Restores the loaded corpus to its unmerged state and forgets merges (benchmark repeats). */
@@ -154,6 +159,8 @@ typedef struct ShredStats {
   int64_t index_switch_merge;  /* hybrid: the first merge id of the indexed loop in the last train() (-1: none) */
   double index_switch_ms;      /* hybrid: Σ host time of the resident -> indexed switches */
   uint64_t resident_aborts;    /* k_resident launches that found their grid not co-resident (then off) */
+  uint64_t verify_checks;      /* verify_argmax: selections checked against a device recount */
+  uint64_t verify_failures;    /* of verify_checks: frequency != device max or != the pair's count */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -2306,6 +2306,21 @@ __global__ __launch_bounds__(kThreads) void k_pair_dense_collect(const u64* cnt,
   }
 }
 
+// K5 check (debug): the largest count of a collected pair list, and (a, b)'s count.
+__global__ __launch_bounds__(kThreads) void k_pair_max(const PairCount* pc, uint32_t n, int32_t a, int32_t b, u64* r) {
+  u64 mx = 0;
+  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+    const PairCount p = pc[i];
+    mx = p.count > mx ? p.count : mx;
+    if (p.a == a && p.b == b) r[1] = p.count;  // one entry per pair: a single writer
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const u64 v = (u64)__shfl_xor((unsigned long long)mx, o);
+    mx = v > mx ? v : mx;
+  }
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(reinterpret_cast<unsigned long long*>(r), (unsigned long long)mx);
+}
+
 // ------------------------------------------------------------------------------------------
 // K1 bulk (stream layout, every id a byte): pair counts only, over the tiles past the ft tiles
 // (the first occurrence of every type is packed into tiles [0, ft_tiles), where k_pair_dense
@@ -3093,9 +3108,13 @@ void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
   HIP_OK(hipMemcpyAsync(hflags, flags, sizeof(hflags), hipMemcpyDeviceToHost, S(stream_)));
   HIP_OK(hipStreamSynchronize(S(stream_)));
   if (hflags[0]) fatal("pair table overflow in k_pair_count / k_pair_collect");
-  out->resize(hflags[1]);
-  if (hflags[1])
-    HIP_OK(hipMemcpy(out->data(), dout, hflags[1] * sizeof(PairCount), hipMemcpyDeviceToHost));
+  if (pmq_) {
+    reduce_pair_max(dout, hflags[1]);
+  } else {
+    out->resize(hflags[1]);
+    if (hflags[1])
+      HIP_OK(hipMemcpy(out->data(), dout, hflags[1] * sizeof(PairCount), hipMemcpyDeviceToHost));
+  }
   if (timing_) {
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[2], (hipEvent_t)ev_[3]));
@@ -3151,8 +3170,12 @@ void Device::count_pairs_dense(int32_t unk_id, uint64_t live, std::vector<PairCo
   uint32_t hn = 0;
   HIP_OK(hipMemcpyAsync(&hn, n, sizeof(uint32_t), hipMemcpyDeviceToHost, S(stream_)));
   HIP_OK(hipStreamSynchronize(S(stream_)));
-  out->resize(hn);
-  if (hn) HIP_OK(hipMemcpy(out->data(), dout, hn * sizeof(PairCount), hipMemcpyDeviceToHost));
+  if (pmq_) {
+    reduce_pair_max(dout, hn);
+  } else {
+    out->resize(hn);
+    if (hn) HIP_OK(hipMemcpy(out->data(), dout, hn * sizeof(PairCount), hipMemcpyDeviceToHost));
+  }
   if (timing_) {
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[2], (hipEvent_t)ev_[3]));
@@ -3170,6 +3193,37 @@ void Device::count_pairs_dense(int32_t unk_id, uint64_t live, std::vector<PairCo
     }
   }
   for (void* q : {(void*)cnt, (void*)ft, (void*)n, (void*)dout}) HIP_OK(hipFree(q));
+}
+
+void Device::reduce_pair_max(const PairCount* dout, uint32_t n) {
+  size_t acc = 0;
+  u64* r = dalloc<u64>(2, &acc);
+  HIP_OK(hipMemsetAsync(r, 0, 2 * sizeof(u64), S(stream_)));
+  if (n) k_pair_max<<<(int)std::min<uint32_t>((n + kThreads - 1) / kThreads, 1024), kThreads, 0, S(stream_)>>>(
+      dout, n, pmq_->a, pmq_->b, r);
+  HIP_OK(hipGetLastError());
+  u64 h[2];
+  HIP_OK(hipMemcpyAsync(h, r, sizeof(h), hipMemcpyDeviceToHost, S(stream_)));
+  HIP_OK(hipStreamSynchronize(S(stream_)));
+  HIP_OK(hipFree(r));
+  pmq_->max_freq = h[0];
+  pmq_->ab_freq = h[1];
+}
+
+// K5 check: one rank reduces its fresh K1 histogram on the device; under RCCL the ranks' lists
+// are merged first (a pair's count is a sum over ranks), then reduced on the host.
+void Device::pair_max(int32_t unk_id, int32_t a, int32_t b, uint64_t* max_freq, uint64_t* ab_freq) {
+  if (xchg_.world > 1) {
+    Backend::pair_max(unk_id, a, b, max_freq, ab_freq);
+    return;
+  }
+  PairMaxQuery q{a, b, 0, 0};
+  pmq_ = &q;
+  std::vector<PairCount> none;
+  count_pairs(unk_id, &none);
+  pmq_ = nullptr;
+  *max_freq = q.max_freq;
+  *ab_freq = q.ab_freq;
 }
 
 // Folds completed sampled k_merge launches into times_ (block: wait for all of them).

@@ -198,21 +198,30 @@ __global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __rest
 }
 
 // ---- word cache: every distinct word is encoded once -------------------------------------
-// A corpus repeats its words (C2: 121 M occurrences of 380 K distinct words), so the default path
-// encodes each distinct word once and copies its ids to every occurrence:
+// A corpus repeats its words (C3: 1.13 G occurrences of 1.25 M distinct words), so the default
+// path encodes each distinct word once and copies its ids to every occurrence:
 //   k_cache_insert  per occurrence: 64-bit hash of (bytes, length) into an open-addressing table
-//                   (key, min first offset); a full probe window flags an overflow;
-//   k_cache_encode  per used slot: the lowest-rank loop on the word's first occurrence, ids kept
-//                   at store[first ..);
-//   k_cache_words   per occurrence: find the slot, compare the bytes with the first occurrence
-//                   (a 64-bit collision is flagged, never trusted), copy the ids into the thread's
-//                   packed run — the same per-thread / per-block counts k_encode_emit consumes.
-// An overflow or a collision reruns the call on the direct path (k_encode_words): exact always.
+//                   of 16-byte slots (key, payload = the inserting occurrence's offset): a read
+//                   that hits L2 for a hot word, a CAS only for an empty slot; a full probe
+//                   window flags an overflow (the table then grows 4x);
+//   k_cache_encode  per used slot: the lowest-rank loop on that occurrence; the ids, then the
+//                   word's bytes, go to a dense arena (one entry per distinct word), and the
+//                   payload becomes (arena offset, length, id count);
+//   k_cache_words   per occurrence: the slot (key and payload in one 16-byte load), a byte compare
+//                   with the arena copy (a 64-bit collision is flagged, never trusted); then the
+//                   block's ids are written as one contiguous run from its first word start
+//                   (per-block count + start);
+//   k_block_emit    one workgroup per block copies its run to the output, coalesced.
+// An arena overflow or a collision reruns the call on the direct path (k_encode_words): exact
+// always.  HBM traffic per text byte: 2 B of text reads (insert, words) + 4 B x ids / byte x 3
+// (run write, emit read, emit write); the slot table and arena stay in L2/MALL for a corpus of
+// repeated words.
 constexpr int kCacheProbes = 128;
+constexpr int kSpanWords = kSpan / 2 + 1;  // words starting in one span, at most
 
-// The workgroup's chunk of text staged in LDS (coalesced 4-byte loads), with a few bytes before
-// it and kOverhang after: word scans, hashes and compares read LDS, and global memory only for
-// bytes outside the staged window.
+// The chunk's text staged in LDS (coalesced 4-byte loads), with a few bytes before it and
+// kOverhang after: word scans, hashes and compares read LDS, and global memory only for bytes
+// outside the staged window.
 constexpr int kOverhang = 256;
 constexpr int kStageBytes = 4 + kChunk + kOverhang;
 
@@ -223,8 +232,8 @@ struct TextView {
   __device__ __forceinline__ uint32_t operator[](u64 i) const { return (i >= lo && i < hi) ? l[i - lo] : g[i]; }
 };
 
-__device__ __forceinline__ TextView stage_chunk(const uint8_t* __restrict__ text, u64 n, uint32_t* lds) {
-  const u64 cbase = (u64)blockIdx.x * kChunk;
+__device__ __forceinline__ TextView stage_chunk(const uint8_t* __restrict__ text, u64 n, u64 chunk, uint32_t* lds) {
+  const u64 cbase = chunk * kChunk;
   const u64 lo = cbase >= 4 ? cbase - 4 : 0;
   u64 hi = lo + kStageBytes;
   if (hi > n) hi = n;
@@ -251,7 +260,7 @@ __device__ __forceinline__ u64 word_hash(const T& t, u64 s, uint32_t L) {
   return h | 1ull;  // 0 marks an empty slot
 }
 
-// Calls f(s, L) for every word starting in this thread's span (L may exceed kEncMaxWord).
+// Calls f(s, L, j) for every word starting in the span at `base` (L may exceed kEncMaxWord).
 template <typename T, typename F>
 __device__ __forceinline__ void for_each_word(const T& text, u64 n, u64 base, F f) {
   if (base >= n) return;
@@ -277,118 +286,171 @@ __device__ __forceinline__ void for_each_word(const T& text, u64 n, u64 base, F 
   }
 }
 
+__device__ __forceinline__ void flag(u64* misc, u64 bit) {
+  atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), (unsigned long long)bit);
+}
+
 __global__ __launch_bounds__(kThreads) void k_cache_insert(const uint8_t* __restrict__ text, u64 n,
-                                                           u64* __restrict__ key, u64* __restrict__ first,
-                                                           u64 cmask, u64* __restrict__ misc) {
+                                                           u64* __restrict__ slot, u64 cmask, u64* __restrict__ misc) {
   __shared__ uint32_t s_text[kStageBytes / 4];
-  const TextView tv = stage_chunk(text, n, s_text);
+  const TextView tv = stage_chunk(text, n, blockIdx.x, s_text);
   const u64 base = (u64)blockIdx.x * kChunk + (u64)threadIdx.x * kSpan;
   for_each_word(tv, n, base, [&](u64 s, u64 L, int) {
     if (L > (u64)kEncMaxWord) {
-      atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), 1ull);
+      flag(misc, 1);
       return;
     }
     const u64 h = word_hash(tv, s, (uint32_t)L);
     u64 i = (h >> 17) & cmask;
     for (int p = 0; p < kCacheProbes; ++p, i = (i + 1) & cmask) {
-      u64 k = key[i];
+      u64 k = slot[2 * i];  // hot words: a read that hits L2, no atomic
       if (k == 0) {
-        k = atomicCAS(reinterpret_cast<unsigned long long*>(key + i), 0ull, (unsigned long long)h);
-        if (k == 0) k = h;
+        k = atomicCAS(reinterpret_cast<unsigned long long*>(slot + 2 * i), 0ull, (unsigned long long)h);
+        if (k == 0) {
+          slot[2 * i + 1] = s;  // any occurrence spells the word (k_cache_words checks them all)
+          return;
+        }
       }
-      if (k == h) {
-        // hot words hit one slot from every wave: only an earlier occurrence needs the atomic
-        if (s < __hip_atomic_load(first + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-          atomicMin(reinterpret_cast<unsigned long long*>(first + i), (unsigned long long)s);
-        return;
-      }
+      if (k == h) return;
     }
-    atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), 2ull);  // window full
+    flag(misc, 2);  // window full
   });
 }
+
+// Payload of an encoded slot: arena offset (int32 units) | length << 32 | id count << 48.  The arena
+// entry at that offset: a header (id count | length << 16), the ids, the word's bytes.
+__device__ __forceinline__ u64 pack_payload(u64 off, u64 L, u64 m) { return off | L << 32 | m << 48; }
 
 template <bool kPacked>
 __global__ __launch_bounds__(kThreads) void k_cache_encode(const uint8_t* __restrict__ text, u64 n,
                                                            const int32_t* __restrict__ byte_map,
                                                            const u64* __restrict__ tab, u64 mask,
-                                                           const u64* __restrict__ key, const u64* __restrict__ first,
-                                                           uint32_t* __restrict__ nids, u64 cap,
-                                                           int32_t* __restrict__ store, int32_t* __restrict__ rank) {
+                                                           u64* __restrict__ slot, u64 cap,
+                                                           int32_t* __restrict__ arena, u64 arena_cap,
+                                                           int32_t* __restrict__ rank, u64* __restrict__ misc) {
   __shared__ int s_map[256];
   __shared__ int s_strip[(kPacked ? 1 : 2) * kStrip * kThreads];
   const int tid = threadIdx.x;
   for (int i = tid; i < 256; i += kThreads) s_map[i] = byte_map[i];
   __syncthreads();
   const u64 i = (u64)blockIdx.x * kThreads + tid;
-  if (i >= cap || key[i] == 0) return;
-  const u64 s = first[i];
+  if (i >= cap || slot[2 * i] == 0) return;
+  const u64 s = slot[2 * i + 1];
   u64 e = s;
   while (e < n && !is_delim(text[e])) ++e;  // <= kEncMaxWord (insert checked)
   const int L = (int)(e - s);
+  const u64 need = 1 + (u64)L + (u64)(L + 3) / 4;  // header (m | L << 16), ids (<= L), then the bytes
+  const u64 off = atomicAdd(reinterpret_cast<unsigned long long*>(misc + 2), (unsigned long long)need);
+  if (off + need > arena_cap) {
+    flag(misc, 8);  // arena full
+    return;
+  }
+  int32_t* ids = arena + off + 1;
   int m;
   if (L <= kStrip) {
     if (kPacked) {
       uint32_t* q = reinterpret_cast<uint32_t*>(s_strip) + tid;
       for (int k = 0; k < L; ++k) q[k * kThreads] = (uint32_t)s_map[text[s + k]] << 16;
       m = merge_word_packed(q, L, tab, mask);
-      for (int k = 0; k < m; ++k) store[s + k] = (int)(q[k * kThreads] >> 16);
+      for (int k = 0; k < m; ++k) ids[k] = (int)(q[k * kThreads] >> 16);
     } else {
       LdsRef tok{s_strip + tid}, rk{s_strip + kStrip * kThreads + tid};
       for (int k = 0; k < L; ++k) tok(k) = s_map[text[s + k]];
       m = merge_word(tok, rk, L, tab, mask);
-      for (int k = 0; k < m; ++k) store[s + k] = tok(k);
+      for (int k = 0; k < m; ++k) ids[k] = tok(k);
     }
-  } else {
-    GlobalRef gt{store + s}, gr{rank + s};
+  } else {  // tokens in the arena entry, ranks in scratch at the word's own text offset
+    GlobalRef gt{ids}, gr{rank + s};
     for (int k = 0; k < L; ++k) gt(k) = s_map[text[s + k]];
     m = merge_word(gt, gr, L, tab, mask);
   }
-  nids[i] = (uint32_t)m;
+  uint32_t* bytes = reinterpret_cast<uint32_t*>(ids + m);
+  for (int k = 0; k < L; k += 4) {
+    uint32_t w = 0;
+    for (int b = 0; b < 4 && k + b < L; ++b) w |= (uint32_t)text[s + k + b] << (8 * b);
+    bytes[k / 4] = w;
+  }
+  arena[off] = m | L << 16;
+  slot[2 * i + 1] = pack_payload(off, (u64)L, (u64)m);
 }
 
 __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restrict__ text, u64 n,
-                                                          const u64* __restrict__ key, const u64* __restrict__ first,
-                                                          const uint32_t* __restrict__ nids, u64 cmask,
-                                                          const int32_t* __restrict__ store, int32_t* __restrict__ pad,
-                                                          uint32_t* __restrict__ tcnt, u64* __restrict__ bcnt,
+                                                          const u64* __restrict__ slot, u64 cmask,
+                                                          const int32_t* __restrict__ arena, int32_t* __restrict__ pad,
+                                                          uint32_t* __restrict__ bstart, u64* __restrict__ bcnt,
                                                           u64* __restrict__ misc) {
-  __shared__ uint32_t s_sum;
   __shared__ uint32_t s_text[kStageBytes / 4];
+  __shared__ uint32_t s_list[kSpanWords * kThreads];  // this chunk's words: arena offsets, column per thread
+  __shared__ uint32_t s_inc[kThreads];
+  __shared__ uint32_t s_start;
   const int tid = threadIdx.x;
-  if (tid == 0) s_sum = 0;
-  const TextView tv = stage_chunk(text, n, s_text);  // synchronises
-  const u64 base = (u64)blockIdx.x * kChunk + (u64)tid * kSpan;
-  uint32_t cnt = 0, j0 = 0xFFFFFFFFu;
-  u64 wpos = 0;
-  for_each_word(tv, n, base, [&](u64 s, u64 L, int j) {
-    if (j0 == 0xFFFFFFFFu) { j0 = (uint32_t)j; wpos = s; }
+  const u64 chunk = blockIdx.x;
+  if (tid == 0) s_start = 0xFFFFFFFFu;
+  const TextView tv = stage_chunk(text, n, chunk, s_text);  // synchronises
+  const u64 cbase = chunk * kChunk;
+  const u64 base = cbase + (u64)tid * kSpan;
+  uint32_t cnt = 0, nw = 0, first = 0xFFFFFFFFu;
+  for_each_word(tv, n, base, [&](u64 s, u64 L, int) {
+    if (first == 0xFFFFFFFFu) first = (uint32_t)(s - cbase);
     if (L > (u64)kEncMaxWord) return;  // flagged by k_cache_insert
     const u64 h = word_hash(tv, s, (uint32_t)L);
-    u64 i = (h >> 17) & cmask;
-    int p = 0;
-    for (; p < kCacheProbes && key[i] != h; ++p) i = (i + 1) & cmask;
-    if (p == kCacheProbes) return;  // flagged by k_cache_insert (overflow)
-    const u64 f = first[i];
-    bool same = f + L <= n && (f + L == n || is_delim(text[f + L]));
-    if (same && f != s) {  // branch-free compare: the loads are independent and pipeline
-      uint32_t diff = 0;
-      for (u64 k = 0; k < L; ++k) diff |= text[f + k] ^ tv[s + k];
-      same = diff == 0;
+    u64 pay = 0, i = (h >> 17) & cmask;
+    for (int p = 0; p < kCacheProbes; ++p, i = (i + 1) & cmask) {
+      const ulonglong2 sl = *reinterpret_cast<const ulonglong2*>(slot + 2 * i);  // key and payload: one load
+      if (sl.x == h) {
+        pay = sl.y;
+        break;
+      }
+      if (sl.x == 0) break;
     }
-    if (!same) {
-      atomicOr(reinterpret_cast<unsigned long long*>(misc + 1), 4ull);  // 64-bit collision
+    if (!pay) return;  // not inserted: an overflow, flagged by k_cache_insert / k_cache_encode
+    const uint32_t m = (uint32_t)(pay >> 48), pl = (uint32_t)(pay >> 32) & 0xFFFFu;
+    const uint8_t* ab = reinterpret_cast<const uint8_t*>(arena + (uint32_t)pay + 1 + m);
+    uint32_t diff = pl != (uint32_t)L;
+    for (uint32_t k = 0; k < pl && !diff; ++k) diff |= ab[k] ^ tv[s + k];
+    if (diff) {
+      flag(misc, 4);  // 64-bit collision
       return;
     }
-    const uint32_t m = nids[i];
-    for (uint32_t k = 0; k < m; ++k) pad[wpos + k] = store[f + k];
-    wpos += m;
+    s_list[nw * kThreads + tid] = (uint32_t)pay;
+    ++nw;
     cnt += m;
   });
-  if (j0 == 0xFFFFFFFFu) j0 = 0;
-  tcnt[(u64)blockIdx.x * kThreads + tid] = cnt << 5 | j0;
-  if (cnt) atomicAdd(&s_sum, cnt);
+  if (first != 0xFFFFFFFFu) atomicMin(&s_start, first);
+  // block-inclusive scan of the per-thread id counts
+  s_inc[tid] = cnt;
   __syncthreads();
-  if (tid == 0) bcnt[blockIdx.x] = s_sum;
+  for (int d = 1; d < kThreads; d <<= 1) {
+    const uint32_t v = tid >= d ? s_inc[tid - d] : 0;
+    __syncthreads();
+    s_inc[tid] += v;
+    __syncthreads();
+  }
+  const uint32_t start = s_start == 0xFFFFFFFFu ? 0u : s_start;
+  int32_t* dst = pad + cbase + start + (s_inc[tid] - cnt);
+  for (uint32_t w = 0; w < nw; ++w) {
+    const int32_t* src = arena + s_list[w * kThreads + tid];
+    const uint32_t m = (uint32_t)src[0] & 0xFFFFu;
+    ++src;
+    for (uint32_t k = 0; k < m; ++k) dst[k] = src[k];
+    dst += m;
+  }
+  if (tid == 0) {
+    bcnt[chunk] = s_inc[kThreads - 1];
+    bstart[chunk] = start;
+  }
+}
+
+// Block b's run pad[b * kChunk + bstart[b], + count) -> out at its exclusive block sum.
+__global__ __launch_bounds__(kThreads) void k_block_emit(const int32_t* __restrict__ pad,
+                                                         const uint32_t* __restrict__ bstart,
+                                                         const u64* __restrict__ bcnt, const u64* __restrict__ binc,
+                                                         int32_t* __restrict__ out) {
+  const u64 b = blockIdx.x;
+  const u64 total = bcnt[b];
+  const int32_t* src = pad + b * kChunk + bstart[b];
+  int32_t* dst = out + (binc[b] - total);
+  for (u64 i = threadIdx.x; i < total; i += kThreads) dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(kThreads) void k_encode_emit(const int32_t* __restrict__ pad, const uint32_t* __restrict__ tcnt,
@@ -450,17 +512,19 @@ EncodeDevice* EncodeDevice::create(int device, const std::vector<uint64_t>& tabl
   EncodeDevice* d = new EncodeDevice();
   d->device_ = device;
   d->mask_ = table.size() - 1;
-  // 16-bit packing needs every id (bytes' symbols and 256 + rank) below 0xFFFF
-  size_t merges = 0;
-  for (uint64_t e : table) merges += e != kEncEmpty;
-  d->packed_ = 256 + merges < 0xFFFFu;
+  // 16-bit packing needs every id (bytes' symbols and 256 + rank) below 0xFFFF: decided from the
+  // largest rank in the table (a merge list with repeated pairs has ranks past its distinct pairs)
+  uint64_t max_rank = 0;
+  for (uint64_t e : table)
+    if (e != kEncEmpty) max_rank = std::max<uint64_t>(max_rank, e & 0xFFFFFu);
+  d->packed_ = 256 + max_rank < 0xFFFFu;
   for (int b = 0; b < 256; ++b) d->packed_ = d->packed_ && byte_map[b] >= 0 && byte_map[b] < 0xFFFF;
   hipStream_t st = nullptr;
   bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
   d->stream_ = st;
   ok = ok && hipMalloc(&d->table_, table.size() * 8) == hipSuccess;
   ok = ok && hipMalloc(&d->byte_map_, 256 * 4) == hipSuccess;
-  ok = ok && hipMalloc(&d->misc_, 16) == hipSuccess;
+  ok = ok && hipMalloc(&d->misc_, 32) == hipSuccess;
   ok = ok && hipHostMalloc(&d->host_misc_, 16, hipHostMallocDefault) == hipSuccess;
   ok = ok && hipMemcpy(d->table_, table.data(), table.size() * 8, hipMemcpyHostToDevice) == hipSuccess;
   ok = ok && hipMemcpy(d->byte_map_, byte_map, 256 * 4, hipMemcpyHostToDevice) == hipSuccess;
@@ -481,7 +545,7 @@ EncodeDevice::~EncodeDevice() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize((hipStream_t)stream_);
   for (void* p : {(void*)table_, (void*)byte_map_, (void*)misc_, (void*)pad_, (void*)rank_, (void*)tcnt_,
-                  (void*)bcnt_, (void*)dtext_, (void*)dout_, (void*)ckey_, (void*)cfirst_, (void*)cnids_, scan_tmp_})
+                  (void*)bcnt_, (void*)dtext_, (void*)dout_, (void*)cslot_, scan_tmp_})
     if (p) (void)hipFree(p);
   if (host_misc_) (void)hipHostFree(host_misc_);
   for (void* e : ev_)
@@ -491,21 +555,23 @@ EncodeDevice::~EncodeDevice() {
 
 bool EncodeDevice::reserve(size_t n, std::string* why) {
   if (n <= cap_bytes_) return true;
-  for (void* p : {(void*)pad_, (void*)rank_, (void*)tcnt_, (void*)bcnt_, (void*)ckey_, (void*)cfirst_, (void*)cnids_,
-                  scan_tmp_})
+  for (void* p : {(void*)pad_, (void*)rank_, (void*)tcnt_, (void*)bcnt_, (void*)cslot_, scan_tmp_})
     if (p) (void)hipFree(p);
   scan_tmp_ = nullptr;
   pad_ = rank_ = nullptr;
-  ckey_ = cfirst_ = nullptr;
-  cnids_ = nullptr;
+  cslot_ = nullptr;
   tcnt_ = nullptr;
   bcnt_ = nullptr;
   cap_bytes_ = 0;
   const size_t nb = (n + kChunk - 1) / kChunk, cap = nb * kChunk;  // every later n <= cap fits
-  ccap_ = 1 << 20;  // word-cache slots: >= 1 M and >= one per 256 text bytes (overflow -> direct path)
+  // word-cache slots: the table is allocated for one slot per 256 text bytes; a call starts with
+  // one per 4096 (a small table keeps the probed lines cache-resident) and grows it 4x while a
+  // probe window overflows, then takes the direct path
+  ccap_ = 1 << 20;
   while (ccap_ < cap / 256) ccap_ <<= 1;
-  if (hipMalloc(&ckey_, ccap_ * 8) != hipSuccess || hipMalloc(&cfirst_, ccap_ * 8) != hipSuccess ||
-      hipMalloc(&cnids_, ccap_ * 4) != hipSuccess) {
+  ccap_min_ = 1 << 20;
+  while (ccap_min_ < cap / 4096) ccap_min_ <<= 1;
+  if (hipMalloc(&cslot_, ccap_ * 16) != hipSuccess) {
     *why = "word-cache allocation failed";
     return false;
   }
@@ -520,10 +586,24 @@ bool EncodeDevice::reserve(size_t n, std::string* why) {
   return true;
 }
 
+namespace {
+// Restores the caller's current device when an encoder call returns.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+}  // namespace
+
 int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t cap, void* stream, double* kernel_ms) {
   if (kernel_ms) *kernel_ms = 0;
   if (n == 0) return 0;
   if (!text || !out) return -1;
+  DeviceGuard guard;
   ENC_OK(hipSetDevice(device_));
   std::string why;
   if (!reserve(n, &why)) {
@@ -536,19 +616,19 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
   const char* env = std::getenv("SHREDWORD_ENCODE_CACHE");
   bool cached = !(env && env[0] == '0');
   ENC_OK(hipEventRecord(ev[0], st));
+  size_t cc = ccap_min_;
   for (;;) {
-    ENC_OK(hipMemsetAsync(misc_, 0, 16, st));
+    ENC_OK(hipMemsetAsync(misc_, 0, 32, st));
     if (cached) {
-      ENC_OK(hipMemsetAsync(ckey_, 0, ccap_ * 8, st));
-      ENC_OK(hipMemsetAsync(cfirst_, 0xFF, ccap_ * 8, st));
-      k_cache_insert<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, ckey_, cfirst_, ccap_ - 1, misc_);
+      ENC_OK(hipMemsetAsync(cslot_, 0, cc * 16, st));
+      k_cache_insert<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, cslot_, cc - 1, misc_);
       ENC_OK(hipGetLastError());
       auto enck = packed_ ? k_cache_encode<true> : k_cache_encode<false>;
-      enck<<<dim3((unsigned)(ccap_ / kThreads)), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, ckey_,
-                                                                          cfirst_, cnids_, ccap_, rank_, pad_);
+      enck<<<dim3((unsigned)(cc / kThreads)), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, cslot_, cc,
+                                                                       rank_, cap_bytes_, pad_, misc_);
       ENC_OK(hipGetLastError());
-      k_cache_words<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, ckey_, cfirst_, cnids_, ccap_ - 1, rank_,
-                                                                   pad_, tcnt_, bcnt_, misc_);
+      k_cache_words<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, cslot_, cc - 1, rank_, pad_, tcnt_, bcnt_,
+                                                                   misc_);
     } else {
       const bool aligned = (reinterpret_cast<uintptr_t>(text) & 15) == 0;
       auto kern = aligned ? (packed_ ? k_encode_words<true, true> : k_encode_words<true, false>)
@@ -562,19 +642,27 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
     ENC_OK(hipMemcpyAsync(misc_, bcnt_ + 2 * nb - 1, 8, hipMemcpyDeviceToDevice, st));
     ENC_OK(hipMemcpyAsync(host_misc_, misc_, 16, hipMemcpyDeviceToHost, st));
     ENC_OK(hipStreamSynchronize(st));
-    if (host_misc_[1] & 1) return -3;
-    if (!(host_misc_[1] & 6)) break;
-    cached = false;  // cache overflow or a 64-bit word-hash collision: redo on the direct path
+    const uint64_t fl = host_misc_[1];
+    if (fl & 1) return -3;
+    if (!(fl & 14)) break;
+    if (fl == 2 && cc < ccap_) {  // only a probe window overflowed: a bigger table
+      cc = std::min(ccap_, cc * 4);
+      continue;
+    }
+    cached = false;  // cache / arena overflow or a 64-bit word-hash collision: redo on the direct path
     if (std::getenv("SHREDWORD_ENCODE_DEBUG"))
       std::fprintf(stderr, "[DEBUG]\t encoder: word cache %s (%zu slots); direct path\n",
-                   host_misc_[1] & 4 ? "hash collision" : "overflow", ccap_);
+                   fl & 4 ? "hash collision" : fl & 8 ? "arena overflow" : "overflow", cc);
     ++fallbacks_;
   }
   ENC_OK(hipEventRecord(ev[1], st));
   const u64 total = host_misc_[0];
   if (total > cap) return -2;
   ENC_OK(hipEventRecord(ev[2], st));
-  if (total) k_encode_emit<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(pad_, tcnt_, bcnt_ + nb, out);
+  if (total && cached)
+    k_block_emit<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(pad_, tcnt_, bcnt_, bcnt_ + nb, out);
+  else if (total)
+    k_encode_emit<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(pad_, tcnt_, bcnt_ + nb, out);
   ENC_OK(hipGetLastError());
   ENC_OK(hipEventRecord(ev[3], st));
   ENC_OK(hipStreamSynchronize(st));
@@ -599,22 +687,48 @@ bool EncodeDevice::reserve_host(size_t n) {
   return true;
 }
 
+// Host text in pieces of at most kHostPiece bytes, each cut just after a delimiter (words never
+// straddle two pieces, so the ids are those of one call): device memory stays at ~14 B per piece
+// byte (5 B staging + the scratch reserve() sizes) whatever the text length.
 int64_t EncodeDevice::encode_host(const uint8_t* text, size_t n, int32_t* out, size_t cap) {
   if (n == 0) return 0;
   if (!text || !out) return -1;
+  DeviceGuard guard;
   ENC_OK(hipSetDevice(device_));
-  if (!reserve_host(n)) {
-    std::fprintf(stderr, "[ERROR]\t encoder: staging allocation failed (%zu bytes)\n", n);
+  size_t piece = kHostPiece;
+  if (const char* e = std::getenv("SHREDWORD_ENCODE_PIECE"))  // tests: small pieces
+    piece = std::max<size_t>((size_t)std::strtoull(e, nullptr, 10), (size_t)kEncMaxWord + 2);
+  piece = std::min(n, piece);
+  if (!reserve_host(piece)) {
+    std::fprintf(stderr, "[ERROR]\t encoder: staging allocation failed (%zu bytes)\n", piece);
     return -1;
   }
   hipStream_t st = (hipStream_t)stream_;
-  ENC_OK(hipMemcpyAsync(dtext_, text, n, hipMemcpyHostToDevice, st));
-  const int64_t r = encode(dtext_, n, dout_, cap, nullptr, nullptr);
-  if (r > 0) {
-    ENC_OK(hipMemcpyAsync(out, dout_, (size_t)r * 4, hipMemcpyDeviceToHost, st));
-    ENC_OK(hipStreamSynchronize(st));
+  size_t pos = 0, done = 0;
+  while (pos < n) {
+    size_t len = std::min(piece, n - pos);
+    if (pos + len < n) {  // end the piece after its last delimiter
+      size_t k = len;
+      const size_t lo = len > (size_t)kEncMaxWord + 1 ? len - (size_t)kEncMaxWord - 1 : 0;
+      while (k > lo) {
+        const uint8_t c = text[pos + k - 1];
+        if (c == 9 || c == 10 || c == 13 || c == 32) break;
+        --k;
+      }
+      if (k == lo) return -3;  // no delimiter in the last kEncMaxWord + 1 bytes: a word past the limit
+      len = k;
+    }
+    ENC_OK(hipMemcpyAsync(dtext_, text + pos, len, hipMemcpyHostToDevice, st));
+    const int64_t r = encode(dtext_, len, dout_, cap - done, nullptr, nullptr);
+    if (r < 0) return r;
+    if (r > 0) {
+      ENC_OK(hipMemcpyAsync(out + done, dout_, (size_t)r * 4, hipMemcpyDeviceToHost, st));
+      ENC_OK(hipStreamSynchronize(st));
+    }
+    done += (size_t)r;
+    pos += len;
   }
-  return r;
+  return (int64_t)done;
 }
 
 }  // namespace shred

@@ -2,14 +2,15 @@
 // counting of reference bpe.cpp:110-153 / hash.cpp:29-72 on the device).
 //
 // The file's bytes are uploaded once; then, on gfx950:
-//   k_word_count   one thread per 64-byte chunk takes the words that START in its chunk (maximal
-//                  runs of bytes outside "\t\r\n "), hashes each (64-bit FNV-1a + length mix)
-//                  with its djb2 & 4095 (the reference StrMap bucket), and counts it in a
+//   k_word_count   per 16 KB tile staged in LDS (coalesced 16-B loads: the text is read from HBM
+//                  once), one thread per 64-byte chunk takes the words that START in its chunk
+//                  (maximal runs of bytes outside "\t\r\n "), hashes each (64-bit FNV-1a + length
+//                  mix) with its djb2 & 4095 (the reference StrMap bucket), and counts it in a
 //                  per-workgroup LDS table (count, min first offset) that spills to, and is
-//                  flushed into, one open-addressing HBM table with 64-bit atomics;
-//   k_word_verify  every occurrence is compared byte for byte with its entry's first occurrence,
-//                  so a 64-bit key collision is detected (the count is then repeated with another
-//                  seed) and the table is exact;
+//                  flushed into, one open-addressing HBM table with 64-bit atomics.  Every
+//                  occurrence is compared byte for byte with an earlier occurrence of its key
+//                  (the one atomicMin hands back), so a 64-bit key collision is detected (the
+//                  count is then repeated with another seed) and the table is exact;
 //   k_word_compact entries -> (bucket << 52 | first offset) keys, radix-sorted (hipCUB): the
 //                  reference word order, since first offsets are distinct;
 //   k_word_gather  rank -> {first, count, length} records for the host.
@@ -45,59 +46,76 @@ typedef unsigned long long u64;
 
 constexpr int kChunkBytes = 64;      // bytes whose word starts one thread owns
 constexpr int kLoadThreads = 256;
-constexpr int kLdsSlots = 2048;      // per-workgroup staging table (57 KB: two workgroups per CU)
+constexpr int kTileBytes = kChunkBytes * kLoadThreads;  // 16 KB of text per workgroup step
+constexpr int kTileStride = kChunkBytes + 4;  // LDS bytes per chunk: the lanes' chunks start in distinct banks
+constexpr int kLdsSlots = 1536;      // per-workgroup table: 36 B a slot (54 KB) + 17 KB tile: two workgroups per CU
 constexpr int kLdsProbes = 8;
-constexpr size_t kPadBytes = 256;    // ' ' past the corpus: every word scan ends inside the buffer
+constexpr int kSpell = 16;           // leading bytes of a word an LDS slot keeps
+constexpr size_t kPadBytes = kTileBytes + 256;  // ' ' past the corpus: every tile load and word scan stays inside
 
 __device__ __forceinline__ bool delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }
 
+// One 32-byte HBM slot per distinct word (a probe and its atomics touch one cache line).
+struct Slot {
+  u64 key;     // 0 = empty; else mix(hash, len, seed) | 1
+  u64 cnt;
+  u64 nfirst;  // ~(min first offset): 0 = none yet, so the table clears with one memset
+  uint32_t len;
+  uint32_t bkt;  // djb2 & 4095
+};
+static_assert(sizeof(Slot) == 32, "slot layout");
+
 struct Table {
-  u64* key;       // 0 = empty; else mix(hash, len, seed) | 1
-  u64* cnt;
-  u64* first;     // min first offset
-  uint32_t* len;
-  uint32_t* bkt;  // djb2 & 4095
-  u64 mask;       // capacity - 1
+  Slot* slot;
+  u64 mask;         // capacity - 1
   uint32_t* nkeys;
   uint32_t* flags;  // [0] table too full, [1] key collision
 };
 
-__device__ __forceinline__ u64 word_key(u64 h, uint32_t len, u64 seed) {
+// kmask keeps all 64 bits (tests narrow it, SHREDWORD_LOAD_KEY_BITS, to force key collisions).
+__device__ __forceinline__ u64 word_key(u64 h, uint32_t len, u64 seed, u64 kmask) {
   h ^= (u64)len * 0x9E3779B97F4A7C15ull ^ seed;
   h ^= h >> 31;
   h *= 0xD6E8FEB86659FD93ull;
   h ^= h >> 32;
-  return h | 1ull;
+  return (h & kmask) | 1ull;
 }
 
-// The word starting at d[pos]: its key, djb2 bucket and length.
-__device__ __forceinline__ void scan_word(const uint8_t* d, u64 pos, u64 seed, u64* key, uint32_t* bkt, uint32_t* len) {
-  u64 h = 0xCBF29CE484222325ull ^ seed;
-  uint32_t dj = 5381u;  // djb2 in 32 bits: its & 4095 equals the reference's 64-bit value's
-  uint32_t l = 0;
-  for (;; ++l) {
-    const uint32_t c = d[pos + l];
-    if (delim(c)) break;
-    h = (h ^ c) * 0x100000001B3ull;
-    dj = dj * 33u + c;
-  }
-  *key = word_key(h, l, seed);
-  *bkt = dj & 4095u;
-  *len = l;
+// Byte p of the workgroup's tile (p may run past the tile: then from HBM).
+__device__ __forceinline__ uint32_t tile_byte(const uint8_t* s, const uint8_t* d, u64 base, uint32_t p) {
+  return p < (uint32_t)kTileBytes ? s[(p / kChunkBytes) * kTileStride + (p % kChunkBytes)] : d[base + p];
 }
 
-__device__ __forceinline__ void table_add(const Table& t, u64 key, uint32_t bkt, uint32_t len, u64 cnt, u64 first) {
+// True when the words at d[a] and d[b] (a's length len) spell the same bytes.
+__device__ __forceinline__ bool same_global(const uint8_t* d, u64 a, u64 b, uint32_t len) {
+  uint32_t diff = delim(d[b + len]) ? 0u : 1u;
+  for (uint32_t k = 0; k < len; ++k) diff |= d[a + k] ^ d[b + k];
+  return diff == 0;
+}
+
+// Adds (cnt, first) to key's slot.  Exactness: every add but the slot's very first compares its
+// occurrence with the offset the atomic hands back — an occurrence some earlier add stored — so
+// all the occurrences behind one key are linked by byte-equal pairs, or flags[1] is raised (a
+// 64-bit key collision: the count is repeated with another seed).
+__device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 key, uint32_t bkt, uint32_t len,
+                                          u64 cnt, u64 first) {
   u64 s = key & t.mask;
   for (u64 probe = 0; probe <= t.mask; ++probe) {
-    const u64 prev = atomicCAS(&t.key[s], 0ull, key);
+    Slot& e = t.slot[s];
+    u64 prev = e.key;
     if (prev == 0ull) {
-      t.len[s] = len;
-      t.bkt[s] = bkt;
-      if (atomicAdd(t.nkeys, 1u) > (uint32_t)((t.mask + 1) / 4 * 3)) atomicOr(&t.flags[0], 1u);
+      prev = atomicCAS(&e.key, 0ull, key);
+      if (prev == 0ull) {
+        e.len = len;
+        e.bkt = bkt;
+        if (atomicAdd(t.nkeys, 1u) > (uint32_t)((t.mask + 1) / 4 * 3)) atomicOr(&t.flags[0], 1u);
+        prev = key;
+      }
     }
-    if (prev == 0ull || prev == key) {
-      atomicAdd(&t.cnt[s], cnt);
-      atomicMin(&t.first[s], first);
+    if (prev == key) {
+      atomicAdd(&e.cnt, cnt);
+      const u64 old = ~atomicMax(&e.nfirst, ~first);
+      if (old != ~0ull && !same_global(d, first, old, len)) atomicOr(&t.flags[1], 1u);
       return;
     }
     s = (s + 1) & t.mask;
@@ -105,107 +123,145 @@ __device__ __forceinline__ void table_add(const Table& t, u64 key, uint32_t bkt,
   atomicOr(&t.flags[0], 1u);
 }
 
-__global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u64 n, Table t, u64 seed) {
+// One pass over the corpus.  Workgroup w owns a contiguous range of 16 KB tiles; each tile is
+// staged in LDS with coalesced 16-B loads (the text is read from HBM once), and each thread takes
+// the words that START in its 64-byte chunk (maximal runs of bytes outside "\t\r\n "), hashes each
+// (64-bit FNV-1a + length mix) and counts it in the workgroup's LDS table (count, min first
+// offset relative to the range, length, the first kSpell bytes of its creator's spelling), which
+// spills to, and at the end is flushed into, one open-addressing HBM table.
+// Exactness without a second pass: an LDS hit compares its bytes with the slot's kSpell-byte
+// spelling (LDS) and its length with the slot's; bytes past kSpell with the occurrence the
+// slot's atomicMin hands back (the same linking argument as table_add), and the flush and every
+// spill compare with the HBM slot's occurrence.  A slot is used once its length is published
+// (0 = being created: the occurrence then goes to HBM directly).  The reference StrMap bucket
+// (djb2 & 4095) is computed at the flush, from the slot's first occurrence.
+__global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u64 n, Table t, u64 seed, u64 kmask,
+                                                             u64 tiles_per_wg) {
   __shared__ u64 s_key[kLdsSlots];
-  __shared__ u64 s_first[kLdsSlots];
+  __shared__ uint32_t s_first[kLdsSlots];
   __shared__ uint32_t s_cnt[kLdsSlots];
   __shared__ uint32_t s_len[kLdsSlots];
-  __shared__ uint32_t s_bkt[kLdsSlots];
-  for (int i = threadIdx.x; i < kLdsSlots; i += kLoadThreads) {
+  __shared__ uint4 s_spell[kLdsSlots];
+  __shared__ uint32_t s_tile32[kLoadThreads * kTileStride / 4];
+  const uint8_t* s_tile = reinterpret_cast<const uint8_t*>(s_tile32);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kLdsSlots; i += kLoadThreads) {
     s_key[i] = 0;
-    s_first[i] = ~0ull;
+    s_first[i] = ~0u;
     s_cnt[i] = 0;
+    s_len[i] = 0;
   }
-  __syncthreads();
-  const u64 nchunks = (n + kChunkBytes - 1) / kChunkBytes;
-  for (u64 c = (u64)blockIdx.x * kLoadThreads + threadIdx.x; c < nchunks; c += (u64)gridDim.x * kLoadThreads) {
-    const u64 c0 = c * kChunkBytes;
-    const u64 c1 = c0 + kChunkBytes < n ? c0 + kChunkBytes : n;
-    uint32_t prev = c0 ? d[c0 - 1] : 32u;
-    for (u64 i = c0; i < c1; ++i) {
-      const uint32_t b = d[i];
-      if (!delim(b) && delim(prev)) {
-        u64 key;
-        uint32_t bkt, len;
-        scan_word(d, i, seed, &key, &bkt, &len);
-        uint32_t s = (uint32_t)(key >> 40) & (kLdsSlots - 1);
-        bool done = false;
-        for (int probe = 0; probe < kLdsProbes && !done; ++probe) {
-          const u64 old = atomicCAS(&s_key[s], 0ull, key);
-          if (old == 0ull || old == key) {
-            if (old == 0ull) {
-              s_len[s] = len;
-              s_bkt[s] = bkt;
-            }
+  const u64 ntiles = (n + kTileBytes - 1) / kTileBytes;
+  const u64 t0 = (u64)blockIdx.x * tiles_per_wg;
+  const u64 t1 = t0 + tiles_per_wg < ntiles ? t0 + tiles_per_wg : ntiles;
+  const u64 range = t0 * kTileBytes;  // LDS first offsets are relative to it (< 2^32: host-checked)
+  for (u64 tile = t0; tile < t1; ++tile) {
+    const u64 base = tile * kTileBytes;
+    __syncthreads();  // the previous tile's scans are done
+    const int4* g = reinterpret_cast<const int4*>(d + base);
+#pragma unroll
+    for (int j = 0; j < kTileBytes / 16 / kLoadThreads; ++j) {
+      const int q = j * kLoadThreads + tid;  // 16-B piece q of the tile
+      const int4 v = g[q];
+      uint32_t* dst = s_tile32 + (q / (kChunkBytes / 16)) * (kTileStride / 4) + (q % (kChunkBytes / 16)) * 4;
+      dst[0] = (uint32_t)v.x;
+      dst[1] = (uint32_t)v.y;
+      dst[2] = (uint32_t)v.z;
+      dst[3] = (uint32_t)v.w;
+    }
+    __syncthreads();
+    uint32_t p = (uint32_t)tid * kChunkBytes;
+    const uint32_t end = p + kChunkBytes;
+    const uint32_t prev = p ? tile_byte(s_tile, d, base, p - 1) : (base ? d[base - 1] : 32u);
+    if (!delim(prev))  // a word running in from the previous chunk belongs to that chunk
+      while (p < end && !delim(tile_byte(s_tile, d, base, p))) ++p;
+    for (;;) {
+      while (p < end && delim(tile_byte(s_tile, d, base, p))) ++p;
+      if (p >= end || base + p >= n) break;
+      u64 h = 0xCBF29CE484222325ull ^ seed;
+      uint32_t w[kSpell / 4] = {0, 0, 0, 0};  // the leading bytes, packed
+      uint32_t len = 0;
+      for (;; ++len) {
+        const uint32_t c = tile_byte(s_tile, d, base, p + len);
+        if (delim(c)) break;
+        h = (h ^ c) * 0x100000001B3ull;
+        if (len < (uint32_t)kSpell) w[len / 4] |= c << (8 * (len % 4));
+      }
+      const u64 key = word_key(h, len, seed, kmask), off = base + p;
+      const uint32_t rel = (uint32_t)(off - range);
+      uint32_t s = (uint32_t)(((key >> 32) * (u64)kLdsSlots) >> 32);
+      bool done = false;
+      for (int probe = 0; probe < kLdsProbes && !done; ++probe) {
+        u64 k = s_key[s];
+        bool mine = false;
+        if (k == 0ull) {
+          k = atomicCAS(&s_key[s], 0ull, key);
+          if (k == 0ull) {  // created: spelling and first offset, then the length publishes it
+            mine = true;
+            k = key;
+            s_spell[s] = make_uint4(w[0], w[1], w[2], w[3]);
+            atomicMin(&s_first[s], rel);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __hip_atomic_store(&s_len[s], len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             atomicAdd(&s_cnt[s], 1u);
-            atomicMin(&s_first[s], i);
             done = true;
-          } else {
-            s = (s + 1) & (kLdsSlots - 1);
           }
         }
-        if (!done) table_add(t, key, bkt, len, 1ull, i);
+        if (!mine && k == key) {
+          const uint32_t sl = __hip_atomic_load(&s_len[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (sl == 0u) break;  // being created: count this one in HBM
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          const uint4 sp = s_spell[s];
+          uint32_t diff = (sl != len) | (sp.x ^ w[0]) | (sp.y ^ w[1]) | (sp.z ^ w[2]) | (sp.w ^ w[3]);
+          uint32_t link = s_first[s];
+          if (rel < link) link = atomicMin(&s_first[s], rel);
+          if (len > (uint32_t)kSpell && link != ~0u && !diff) {
+            const u64 rep = range + link;
+            for (uint32_t q = kSpell; q < len; ++q) diff |= tile_byte(s_tile, d, base, p + q) ^ d[rep + q];
+          }
+          if (diff) atomicOr(&t.flags[1], 1u);
+          atomicAdd(&s_cnt[s], 1u);
+          done = true;
+        } else if (!done) {
+          s = s + 1 == (uint32_t)kLdsSlots ? 0u : s + 1;
+        }
       }
-      prev = b;
+      if (!done) {
+        uint32_t dj = 5381u;  // djb2 in 32 bits: its & 4095 equals the reference's 64-bit value's
+        for (uint32_t q = 0; q < len; ++q) dj = dj * 33u + tile_byte(s_tile, d, base, p + q);
+        table_add(d, t, key, dj & 4095u, len, 1ull, off);
+      }
+      p += len;
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kLdsSlots; i += kLoadThreads)
-    if (s_key[i]) table_add(t, s_key[i], s_bkt[i], s_len[i], s_cnt[i], s_first[i]);
-}
-
-// Every occurrence against its entry's first occurrence: a mismatch is a 64-bit key collision.
-__global__ __launch_bounds__(kLoadThreads) void k_word_verify(const uint8_t* d, u64 n, Table t, u64 seed) {
-  const u64 nchunks = (n + kChunkBytes - 1) / kChunkBytes;
-  for (u64 c = (u64)blockIdx.x * kLoadThreads + threadIdx.x; c < nchunks; c += (u64)gridDim.x * kLoadThreads) {
-    const u64 c0 = c * kChunkBytes;
-    const u64 c1 = c0 + kChunkBytes < n ? c0 + kChunkBytes : n;
-    uint32_t prev = c0 ? d[c0 - 1] : 32u;
-    for (u64 i = c0; i < c1; ++i) {
-      const uint32_t b = d[i];
-      if (!delim(b) && delim(prev)) {
-        u64 key;
-        uint32_t bkt, len;
-        scan_word(d, i, seed, &key, &bkt, &len);
-        u64 s = key & t.mask;
-        bool found = false;
-        for (u64 probe = 0; probe <= t.mask; ++probe) {
-          const u64 k = t.key[s];
-          if (k == key) {
-            found = true;
-            break;
-          }
-          if (k == 0ull) break;
-          s = (s + 1) & t.mask;
-        }
-        bool same = found && t.len[s] == len;
-        if (same) {
-          const u64 f = t.first[s];
-          for (uint32_t k = 0; k < len && same; ++k) same = d[f + k] == d[i + k];
-        }
-        if (!same) atomicOr(&t.flags[1], 1u);
-      }
-      prev = b;
-    }
+  for (int i = tid; i < kLdsSlots; i += kLoadThreads) {
+    if (!s_key[i]) continue;
+    const u64 first = range + s_first[i];
+    const uint32_t len = s_len[i];
+    uint32_t dj = 5381u;
+    for (uint32_t q = 0; q < len; ++q) dj = dj * 33u + d[first + q];
+    table_add(d, t, s_key[i], dj & 4095u, len, s_cnt[i], first);
   }
 }
 
 __global__ void k_word_compact(Table t, u64* okey, uint32_t* oslot, uint32_t* nout) {
   for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s <= t.mask; s += (u64)gridDim.x * blockDim.x) {
-    if (!t.key[s]) continue;
+    const Slot& e = t.slot[s];
+    if (!e.key) continue;
     const uint32_t i = atomicAdd(nout, 1u);
-    okey[i] = ((u64)t.bkt[s] << 52) | t.first[s];
+    okey[i] = ((u64)e.bkt << 52) | ~e.nfirst;
     oslot[i] = (uint32_t)s;
   }
 }
 
 __global__ void k_word_gather(Table t, const uint32_t* slot, uint32_t W, WordRec* out) {
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < W; r += gridDim.x * blockDim.x) {
-    const uint32_t s = slot[r];
+    const Slot& e = t.slot[slot[r]];
     WordRec w;
-    w.first = t.first[s];
-    w.count = t.cnt[s];
-    w.len = t.len[s];
+    w.first = ~e.nfirst;
+    w.count = e.cnt;
+    w.len = e.len;
     w.pad = 0;
     out[r] = w;
   }
@@ -263,37 +319,36 @@ bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec
   if (report) LOAD_OK(hipStreamSynchronize(st));
   const double t1 = wall();
 
-  // table capacity: a power of two >= n / 64 (grown while it overflows)
+  // table capacity: a power of two >= 1 M and >= n / 8192 (grown 4x while it is over 3/4 full):
+  // a small table keeps the slots the spills touch in L2 / MALL
   u64 cap = 1ull << 20;
-  while (cap < (u64)(n / 64) && cap < (1ull << 31)) cap <<= 1;
-  const u64 nchunks = (n + kChunkBytes - 1) / kChunkBytes;
-  const int grid = (int)std::min<u64>((nchunks + kLoadThreads - 1) / kLoadThreads, (u64)cus * 2);
+  while (cap < (u64)(n / 8192) && cap < (1ull << 29)) cap <<= 1;
+  u64 kmask = ~0ull;
+  if (const char* e = std::getenv("SHREDWORD_LOAD_KEY_BITS")) {
+    const int bits = std::atoi(e);
+    if (bits > 0 && bits < 64) kmask = (1ull << bits) - 1;
+  }
+  const u64 ntiles = (n + kTileBytes - 1) / kTileBytes;
+  u64 grid = std::min<u64>(ntiles, (u64)cus * 2);
+  u64 per = (ntiles + grid - 1) / grid;
+  while (per * (u64)kTileBytes >= (1ull << 32)) {  // LDS first offsets are 32-bit range-relative
+    grid *= 2;
+    per = (ntiles + grid - 1) / grid;
+  }
+  grid = (ntiles + per - 1) / per;
   for (int attempt = 0; attempt < 6; ++attempt) {
     const u64 seed = 0x51ED270B27A1F4A3ull * (u64)(attempt + 1);
-    DevBuf bkey, bcnt, bfirst, blen, bbkt, bmeta;
-    LOAD_OK(hipMalloc(&bkey.p, cap * 8));
-    LOAD_OK(hipMalloc(&bcnt.p, cap * 8));
-    LOAD_OK(hipMalloc(&bfirst.p, cap * 8));
-    LOAD_OK(hipMalloc(&blen.p, cap * 4));
-    LOAD_OK(hipMalloc(&bbkt.p, cap * 4));
+    DevBuf bslot, bmeta;
+    LOAD_OK(hipMalloc(&bslot.p, cap * sizeof(Slot)));
     LOAD_OK(hipMalloc(&bmeta.p, 64));
-    LOAD_OK(hipMemsetAsync(bkey.p, 0, cap * 8, st));
-    LOAD_OK(hipMemsetAsync(bcnt.p, 0, cap * 8, st));
-    LOAD_OK(hipMemsetAsync(bfirst.p, 0xFF, cap * 8, st));
+    LOAD_OK(hipMemsetAsync(bslot.p, 0, cap * sizeof(Slot), st));
     LOAD_OK(hipMemsetAsync(bmeta.p, 0, 64, st));
     Table t;
-    t.key = (u64*)bkey.p;
-    t.cnt = (u64*)bcnt.p;
-    t.first = (u64*)bfirst.p;
-    t.len = (uint32_t*)blen.p;
-    t.bkt = (uint32_t*)bbkt.p;
+    t.slot = (Slot*)bslot.p;
     t.mask = cap - 1;
     t.nkeys = (uint32_t*)bmeta.p;
     t.flags = (uint32_t*)bmeta.p + 4;
-    k_word_count<<<grid, kLoadThreads, 0, st>>>(db, n, t, seed);
-    LOAD_OK(hipGetLastError());
-    k_word_verify<<<(int)std::min<u64>((nchunks + kLoadThreads - 1) / kLoadThreads, (u64)cus * 8), kLoadThreads, 0,
-                    st>>>(db, n, t, seed);
+    k_word_count<<<(unsigned)grid, kLoadThreads, 0, st>>>(db, n, t, seed, kmask, per);
     LOAD_OK(hipGetLastError());
     uint32_t meta[16];
     LOAD_OK(hipMemcpyAsync(meta, bmeta.p, 64, hipMemcpyDeviceToHost, st));
@@ -301,7 +356,7 @@ bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec
     const double t2 = wall();
     const uint32_t W = meta[0];
     if (meta[4]) {  // too full: a bigger table
-      if (cap >= (1ull << 33)) break;
+      if (cap >= (1ull << 29)) break;
       cap <<= 2;
       continue;
     }
@@ -329,7 +384,7 @@ bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec
     if (W) LOAD_OK(hipMemcpyAsync(out->data(), brec.p, (size_t)W * sizeof(WordRec), hipMemcpyDeviceToHost, st));
     LOAD_OK(hipStreamSynchronize(st));
     if (report)
-      std::fprintf(stderr, "[LOAD] %zu bytes: upload %.1f ms, count+verify %.1f ms, order+gather %.1f ms, %u words\n", n,
+      std::fprintf(stderr, "[LOAD] %zu bytes: upload %.1f ms, count %.1f ms, order+gather %.1f ms, %u words\n", n,
                    1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (wall() - t2), W);
     return true;
   }

@@ -68,6 +68,9 @@ class Device : public Backend {
   // K1: weighted pair histogram with first touch, pairs holding unk skipped (bpe.cpp:187-206);
   // under RCCL the per-rank lists are merged (sum, min first touch).
   void count_pairs(int32_t unk_id, std::vector<PairCount>* out) override;
+  // K5 check (debug): K1 again, reduced on the device (k_pair_max) to the largest pair count and
+  // (a, b)'s count.
+  void pair_max(int32_t unk_id, int32_t a, int32_t b, uint64_t* max_freq, uint64_t* ab_freq) override;
 
   // K2+K3 for a chain of merges (ab[2i], ab[2i+1]) -> X0 + i: one k_merge launch applies them in
   // order per tile and reduces each merge's neighbour deltas separately.
@@ -245,6 +248,12 @@ class Device : public Backend {
   void exchange_launch(MergeSlot& sl);
   size_t exchange_finish(MergeSlot& sl, const DeltaRecord** recs);
   void count_pairs_dense(int32_t unk_id, uint64_t live, std::vector<PairCount>* out);
+  struct PairMaxQuery {
+    int32_t a, b;
+    uint64_t max_freq, ab_freq;
+  };
+  PairMaxQuery* pmq_ = nullptr;  // set by pair_max(): count_pairs reduces instead of collecting
+  void reduce_pair_max(const PairCount* dout, uint32_t n);
   void unmerge_run(ChainRun& run, int j0);
   void unmerge_launch(ChainRun& run, const uint32_t* tiles, size_t n_tiles, int j0 = 0);
   void flush_timing(bool block);

@@ -32,7 +32,9 @@ class EncodeDevice {
   // text / out on the device; stream = hipStream_t or nullptr.  Returns ids, -1 device error,
   // -2 cap too small, -3 word longer than kEncMaxWord.
   int64_t encode(const uint8_t* text, size_t n, int32_t* out, size_t cap, void* stream, double* kernel_ms);
-  // Host buffers: staged through cached device buffers.
+  // Host buffers: staged through cached device buffers in pieces of <= kHostPiece bytes cut at
+  // delimiters (device memory ~14 B per piece byte, whatever n is).
+  static constexpr size_t kHostPiece = size_t(256) << 20;
   int64_t encode_host(const uint8_t* text, size_t n, int32_t* out, size_t cap);
   // Calls that fell back from the word cache to the direct path (overflow or hash collision).
   uint64_t fallbacks() const { return fallbacks_; }
@@ -56,12 +58,12 @@ class EncodeDevice {
   uint64_t* bcnt_ = nullptr;    // [0, nb) block counts, [nb, 2 nb) inclusive sums
   void* scan_tmp_ = nullptr;     // hipCUB scan scratch
   size_t scan_tmp_bytes_ = 0;
-  uint64_t* misc_ = nullptr;    // [0] total ids, [1] flags: 1 long word, 2 cache overflow, 4 collision
-  // word cache (one slot per distinct word): 64-bit word hash, first occurrence, id count
-  size_t ccap_ = 0;
-  uint64_t* ckey_ = nullptr;
-  uint64_t* cfirst_ = nullptr;
-  uint32_t* cnids_ = nullptr;
+  uint64_t* misc_ = nullptr;    // [0] total ids, [1] flags: 1 long word, 2 probe window full, 4 collision,
+                                // 8 arena full; [2] word-cache arena top
+  // word cache (one 16-byte slot per distinct word): 64-bit word hash, payload (an occurrence's
+  // offset, then arena offset | length << 32 | id count << 48); the arena is rank_
+  size_t ccap_ = 0, ccap_min_ = 0;  // allocated slots; slots a call starts with
+  uint64_t* cslot_ = nullptr;
   uint64_t* host_misc_ = nullptr;  // pinned
   // host-path staging
   size_t host_cap_ = 0;

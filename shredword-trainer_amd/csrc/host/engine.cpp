@@ -38,6 +38,25 @@ void Engine::finish_speculation(Backend& be) {
   ++spec_misses_;
 }
 
+// K5 check: the guesses in flight are undone first (the device then holds exactly the corpus
+// after the confirmed merges), so the next launch starts from the selected merge again.
+void Engine::verify_selection(Backend& be, int32_t a, int32_t b, uint64_t freq) {
+  if (!pending_.empty()) {
+    be.rollback(pending_.front().X);
+    pending_.clear();
+  }
+  uint64_t mx = 0, fab = 0;
+  be.pair_max(unk_, a, b, &mx, &fab);
+  ++verify_checks_;
+  if (mx != freq || fab != freq) {
+    if (!verify_fail_)
+      std::fprintf(stderr, "[ERROR]\t argmax check at merge %zu: selected (%d,%d) freq=%llu, device recount: max=%llu, "
+                   "(%d,%d)=%llu\n", merge_a_.size(), a, b, (unsigned long long)freq, (unsigned long long)mx, a, b,
+                   (unsigned long long)fab);
+    ++verify_fail_;
+  }
+}
+
 // One merge (bpe.cpp:244-318): false when the heap holds no valid candidate.  `remaining` = how
 // many more merges the caller may still ask for (no guess runs past them).
 bool Engine::merge_one(Backend& be, int remaining) {
@@ -52,6 +71,7 @@ bool Engine::merge_one(Backend& be, int remaining) {
     return false;
   }
   const int32_t X = kBaseVocab + (int32_t)merge_a_.size();
+  if (verify_every_ && merge_a_.size() % (size_t)verify_every_ == 0) verify_selection(be, a, b, freq);
   if (log_ >= 2)
     std::printf("[MERGE]\t Merging (%d,%d) freq=%llu -> new_id=%d (merge %zu)\n", a, b, (unsigned long long)freq, X,
                 merge_a_.size() + 1);

@@ -42,6 +42,17 @@ class Backend {
   virtual void reserve_ids(int32_t max_id) {}
   // K6: final weighted token histogram over ids [0, T) (all ranks).
   virtual void token_freq(size_t T, std::vector<uint64_t>* freq) = 0;
+  // K5 check (debug): a fresh K1 over the current corpus reduced to the largest pair count
+  // (*max_freq) and the count of (a, b) (*ab_freq).  Default: reduced on the host.
+  virtual void pair_max(int32_t unk_id, int32_t a, int32_t b, uint64_t* max_freq, uint64_t* ab_freq) {
+    std::vector<PairCount> pc;
+    count_pairs(unk_id, &pc);
+    *max_freq = *ab_freq = 0;
+    for (const PairCount& p : pc) {
+      if (p.count > *max_freq) *max_freq = p.count;
+      if (p.a == a && p.b == b) *ab_freq = p.count;
+    }
+  }
 };
 
 struct EngineTimes {
@@ -82,6 +93,12 @@ class Engine {
     chain_window_ = window;
   }
   void set_speculation(bool on) { speculate_ = on; }
+  // K5 argmax verifier (debug): every `every` merges (0 = off), the selected pair's frequency is
+  // checked against a device recount of the corpus (Backend::pair_max): it must be the largest
+  // pair count and (a, b)'s own count.  Mismatches are counted and the first is printed.
+  void set_verify(int every) { verify_every_ = every < 0 ? 0 : every; }
+  uint64_t verify_checks() const { return verify_checks_; }
+  uint64_t verify_failures() const { return verify_fail_; }
   void finish_speculation(Backend& be);  // rolls back unconfirmed guesses (before any other access)
   uint64_t spec_hits() const { return spec_hits_; }
   uint64_t spec_misses() const { return spec_misses_; }
@@ -92,6 +109,7 @@ class Engine {
 
  private:
   bool merge_one(Backend& be, int remaining);
+  void verify_selection(Backend& be, int32_t a, int32_t b, uint64_t freq);
 
   size_t target_vocab_ = 0;
   int32_t unk_ = 0;
@@ -112,6 +130,8 @@ class Engine {
   std::vector<int32_t> used_;
   std::vector<int32_t> chain_ab_;
   uint64_t spec_hits_ = 0, spec_misses_ = 0, launches_ = 0;
+  int verify_every_ = 0;
+  uint64_t verify_checks_ = 0, verify_fail_ = 0;
   size_t probe_k_ = 0, probe_window_ = 256;
   std::vector<std::vector<int32_t>> chain_log_;
 };

@@ -115,6 +115,10 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
     if (t->dev) t->dev->set_spec_depth(d);
   } else if (key == "device") {
     t->device = std::atoi(val.c_str());
+  } else if (key == "verify_argmax") {
+    const int n = std::atoi(val.c_str());
+    if (n < 0) return -1;
+    t->engine.set_verify(n);
   } else {
     return -1;
   }
@@ -198,6 +202,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   if (const char* v = std::getenv("SHREDWORD_TRACE")) set_option(t, "trace", v);
   t->engine.set_speculation(env_int("SHREDWORD_SPECULATE", 1) != 0);
   if (const char* v = std::getenv("SHREDWORD_CHAIN")) set_option(t, "chain", v);
+  t->engine.set_verify(env_int("SHREDWORD_VERIFY_ARGMAX", 0));
   if (t->engine.log() >= 1) std::printf("[INFO]\t BPE trainer initialized. Heap initialized successfully.\n");
   return t;
 }
@@ -419,6 +424,8 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
   if (t->dev) s->exchange_overflows = t->dev->exchange_overflows();
   s->spec_hits = t->engine.spec_hits();
   s->spec_misses = t->engine.spec_misses();
+  s->verify_checks = t->engine.verify_checks();
+  s->verify_failures = t->engine.verify_failures();
   s->layout = (int32_t)t->layout;
   s->world_size = dist_active() ? dist_state().world : 1;
   return 0;

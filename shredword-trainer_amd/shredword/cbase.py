@@ -74,7 +74,7 @@ class ShredStats(Structure):
                 ("index_dev_lookup_us", c_double), ("index_dev_scan_us", c_double),
                 ("index_scanned", c_uint64), ("index_build_us", c_double), ("index_no_sub", c_uint64),
                 ("index_staged", c_uint64), ("index_switch_merge", c_int64), ("index_switch_ms", c_double),
-                ("resident_aborts", c_uint64)]
+                ("resident_aborts", c_uint64), ("verify_checks", c_uint64), ("verify_failures", c_uint64)]
 
 
 Trainer = c_void_p

@@ -34,6 +34,7 @@ class BPEEncoder:
         self.enc = lib.shred_encoder_load(model_path.encode("utf-8"),
                                           vocab_path.encode("utf-8") if vocab_path else None,
                                           int(unk_id), int(device))
+        self.device = int(device)
         if not self.enc:
             raise RuntimeError(f"Failed to create the encoder for {model_path} (see stderr; a GPU is required)")
         _LIVE.add(self)
@@ -49,6 +50,7 @@ class BPEEncoder:
         self.enc = lib.shred_encoder_create(m.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), m.shape[0],
                                             None if bm is None else bm.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                                             int(device))
+        self.device = int(device)
         if not self.enc:
             raise RuntimeError("Failed to create the encoder (invalid merges or no GPU; see stderr)")
         _LIVE.add(self)
@@ -90,9 +92,13 @@ class BPEEncoder:
         import torch
         if text.dtype != torch.uint8 or text.dim() != 1 or not text.is_cuda or not text.is_contiguous():
             raise ValueError("text must be a contiguous 1-D uint8 CUDA tensor")
+        if text.device.index != self.device:
+            raise ValueError(f"text is on {text.device}, the encoder on cuda:{self.device}")
         n = text.numel()
         if out is None:
             out = torch.empty(max(1, n), dtype=torch.int32, device=text.device)
+        elif out.dtype != torch.int32 or not out.is_cuda or not out.is_contiguous() or out.device != text.device:
+            raise ValueError("out must be a contiguous int32 tensor on the text's device")
         ms = ctypes.c_double()
         st = stream if stream is not None else torch.cuda.current_stream(text.device).cuda_stream
         r = self._check(lib.shred_encode_device(self.enc, text.data_ptr(), n, out.data_ptr(), out.numel(),

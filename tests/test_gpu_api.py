@@ -477,6 +477,24 @@ def test_gpu_word_count_matches_host(kind, medium_corpus, tmp_path, monkeypatch)
 
 
 
+def test_gpu_word_count_detects_key_collisions(medium_corpus, tmp_path, monkeypatch):
+    """Word keys narrowed to 12 bits (SHREDWORD_LOAD_KEY_BITS): thousands of distinct words share
+    keys, the byte compare inside k_word_count flags it on every seed, and the load falls back to
+    the host count -- the same word table as the 64-bit device count."""
+    monkeypatch.setenv("SHREDWORD_GPU_LOAD_MIN", "1")
+    outs = []
+    for bits in ("12", "64"):
+        monkeypatch.setenv("SHREDWORD_LOAD_KEY_BITS", bits)
+        t = _trainer(vocab_size=2000, unk_id=0, character_coverage=0.9995, min_pair_freq=2)
+        t.load_corpus(medium_corpus)
+        n, model, vocab = _train_bytes(t, tmp_path, f"k{bits}")
+        st = t.stats()
+        t.destroy()
+        assert st["load_on_gpu"] == (bits == "64")
+        outs.append((n, model, vocab, st["num_words"], st["num_occurrences"]))
+    assert outs[0] == outs[1]
+
+
 def test_resident_abort_falls_back(medium_corpus, medium_oracle, tmp_path, monkeypatch):
     """k_resident's co-residency check: with a zero bound the leader never sees every workgroup
     (an abort on every launch); the merges it was given run again on the indexed loop, and the

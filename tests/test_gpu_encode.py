@@ -190,3 +190,65 @@ def test_word_cache_overflow_falls_back_exactly():
     want = oracle_encode(merges, None, text)
     assert np.array_equal(enc.encode(text), want)
     enc.destroy()
+
+
+def test_repeated_pairs_past_16_bit_ids():
+    """A merge list with repeated pairs: 2 distinct pairs but ranks up to 65301 (ids past
+    0xFFFF), so the 16-bit LDS packing must be off (it is decided from the largest rank)."""
+    M = 65302
+    merges = np.empty((M, 3), dtype=np.int32)
+    merges[:, 0], merges[:, 1] = 97, 98
+    merges[:, 2] = 256 + np.arange(M)
+    merges[-1, :2] = (256, 99)  # rank 65301 -> id 65557
+    enc = _enc_from(merges)
+    for cache in ("1", "0"):
+        os.environ["SHREDWORD_ENCODE_CACHE"] = cache
+        try:
+            text = b"abc ab abcabc ca " * 1000
+            assert np.array_equal(enc.encode(text), oracle_encode(merges, None, text))
+            assert enc.encode(b"abc").tolist() == [65557]
+        finally:
+            del os.environ["SHREDWORD_ENCODE_CACHE"]
+    enc.destroy()
+
+
+def test_word_arena_overflow_falls_back_exactly():
+    """Distinct long words whose ids + bytes exceed the arena (one int per text byte): the
+    word-cache call reruns exactly on the direct path."""
+    rng = np.random.default_rng(4)
+    alpha = [97, 98, 99, 100]
+    merges = _random_merges(rng, alpha, 200)
+    text = b" ".join(bytes(rng.choice(alpha, size=1000).astype(np.uint8)) for _ in range(2000)) + b" "
+    enc = _enc_from(merges)
+    assert np.array_equal(enc.encode(text), oracle_encode(merges, None, text))
+    enc.destroy()
+
+
+def test_host_text_in_pieces(monkeypatch):
+    """encode() of host text in small pieces cut at delimiters gives the ids of one call, and a
+    word past the limit at a piece boundary is still rejected."""
+    rng = np.random.default_rng(8)
+    alpha = [97, 98, 99]
+    merges = _random_merges(rng, alpha, 400)
+    enc = _enc_from(merges)
+    text = b"".join(bytes(rng.choice(alpha, size=int(rng.integers(1, 60))).astype(np.uint8)) +
+                    bytes([int(rng.choice([9, 10, 13, 32]))]) for _ in range(40000))
+    want = enc.encode(text)
+    assert np.array_equal(want, oracle_encode(merges, None, text))
+    monkeypatch.setenv("SHREDWORD_ENCODE_PIECE", "5000")
+    assert np.array_equal(enc.encode(text), want)
+    with pytest.raises(ValueError):
+        enc.encode(b"ab " * 3000 + b"a" * 1100 + b" ab")
+    enc.destroy()
+
+
+def test_device_mismatch_is_refused():
+    import torch
+    enc = _enc_from(np.array([[97, 98, 256]], np.int32))
+    with pytest.raises(ValueError):
+        enc.encode_device(torch.zeros(4, dtype=torch.uint8))  # host tensor
+    t = torch.tensor(list(b"ab ab"), dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(ValueError):
+        enc.encode_device(t, out=torch.empty(8, dtype=torch.int64, device="cuda:0"))
+    assert enc.encode_device(t)[0].cpu().tolist() == [256, 256]
+    enc.destroy()

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None, index=1, spec_depth=None, speculate=None,
-           hybrid=None, switch_occ=None):
+           hybrid=None, switch_occ=None, verify=None):
     from shredword.trainer import BPETrainer
 
     cfg = case["config"]
@@ -32,6 +32,8 @@ def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None, index
         t.set_option("spec_depth", spec_depth)
     if speculate is not None:
         t.set_option("speculate", speculate)
+    if verify is not None:
+        t.set_option("verify_argmax", verify)
     t.load_corpus(corpus)
     merges = t.train()
     model, vocab = str(tmp_path / "g.model"), str(tmp_path / "g.vocab")
@@ -75,6 +77,24 @@ def test_index_loop_matches_reference(name, case_corpus, tmp_path):
     if case["merges"] > 0:
         assert st["index_merges"] >= case["merges"] and st["index_on"] == 1
         assert st["resident_launches"] == 0
+
+
+@pytest.mark.parametrize("path", ["hybrid", "index", "resident", "launch", "stream"])
+@pytest.mark.parametrize("name", API_CASES)
+def test_argmax_verifier(name, path, case_corpus, tmp_path):
+    """K5 check (verify_argmax): at every checked merge the device recounts the corpus's pairs and
+    reduces them (k_pair_max); the host heap's selected frequency is the largest count and the
+    pair's own count -- on every merge path, with the guesses in flight undone first, and the
+    files still the reference's.  Every merge is checked on the small goldens, every 97th on the
+    deep runs."""
+    case, corpus = case_corpus(name)
+    every = 97 if name in DEEP else 1
+    kw = {"hybrid": {}, "index": {"hybrid": 0}, "resident": {"index": 0}, "launch": {"index": 0, "resident": 0},
+          "stream": {}}[path]
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "stream" if path == "stream" else "types", stats=st, verify=every, **kw))
+    assert st["verify_failures"] == 0
+    assert st["verify_checks"] == (case["merges"] + every - 1) // every
 
 
 @pytest.mark.parametrize("switch_occ", [1 << 40, 300, 0])
