@@ -47,6 +47,9 @@ CONFIGS = {
                desc="C2: BPE vocab_size=8192 (min_pair_freq=2000) on 1 GB synthetic UTF-8 corpus"),
     "c3": dict(bytes=10_000_000_000, seed=3, script="utf8", vocab=32000, mpf=2, cov=0.995, unk=0,
                desc="C3: BPE vocab_size=32000 min_pair_freq=2 on 10 GB synthetic UTF-8 corpus"),
+    "c4": dict(bytes=80_000_000_000, seed=4, script="utf8", vocab=32000, mpf=2000, cov=0.995, unk=0, shards=8,
+               desc="C4: BPE vocab_size=32000 min_pair_freq=2000 on 80 GB synthetic UTF-8 corpus (8 x 10 GB "
+                    "shards of one logical corpus: the byte ranges the ranks of a sharded load count)"),
     "c5": dict(bytes=100_000_000_000, seed=5, script="mixed", vocab=64000, mpf=2000, cov=0.9995, unk=0,
                desc="C5: BPE vocab_size=64000 coverage=0.9995 on 100 GB mixed-script corpus"),
 }
@@ -530,7 +533,9 @@ def main():
                 "workload": cfg["desc"],
                 "corpus_bytes": cfg["bytes"], "seed": cfg["seed"], "script": cfg["script"],
                 "vocab_size": cfg["vocab"], "min_pair_freq": cfg["mpf"], "character_coverage": cfg["cov"],
-                "unk_id": cfg["unk"], "layout": args.layout, "parallelism": f"word-range shards x{world}",
+                "unk_id": cfg["unk"], "layout": args.layout,
+                "parallelism": (f"dp{world}: sharded load (byte ranges) + merge loop replicated on every rank"
+                                if world > 1 else "single GPU"),
                 "merges_per_step": per_step_merges, "distinct_words": st["num_words"],
                 "symbols": st["num_symbols"], "occurrences": st["num_occurrences"], "tiles": st["num_tiles"],
             },

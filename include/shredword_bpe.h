@@ -92,6 +92,14 @@ int loadVocab(void* trainer, const char* path);
  *                               types layout, files without NUL bytes; same table either way)
  *   exchange_bucket = <n>       multi-GPU: records per rank in the fixed all-gather bucket
  *                               (default 1024; larger record sets take a second round)
+ *   dist = auto | replicate | exchange
+ *                               multi-GPU mode (before load_corpus; default auto = exchange for
+ *                               the stream layout, replicate for types): replicate shards the
+ *                               load (each rank counts its byte range, word lists all-gathered and
+ *                               merged) and runs the merge loop on every rank over the full word
+ *                               table with no per-merge collective; exchange shards the word table
+ *                               and all-gathers each merge's neighbour records (RCCL over xGMI).
+ *                               Output bytes are identical in every mode and world size.
  *   verify_argmax = <n>         debug (K5 check): every n merges (0 = off, the default; env
  *                               SHREDWORD_VERIFY_ARGMAX) the device recounts the corpus's pairs
  *                               and reduces them (k_pair_max): the host heap's selected frequency

@@ -3070,13 +3070,13 @@ void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
   park();
   out->clear();
   if (!ntiles_) {
-    dist_merge_pairs(out);
+    if (xchg_.world > 1) dist_merge_pairs(out);
     return;
   }
   const uint64_t live = live_tokens();
   if (max_id_seen_ < kBaseVocab) {  // every id in the stream is a byte or unk (skipped)
     count_pairs_dense(unk_id, live, out);
-    dist_merge_pairs(out);
+    if (xchg_.world > 1) dist_merge_pairs(out);
     return;
   }
   // distinct pairs <= live tokens and <= (ids in play)^2
@@ -3126,7 +3126,7 @@ void Device::count_pairs(int32_t unk_id, std::vector<PairCount>* out) {
                           (layout_ == Layout::kTypes ? 8.0 * (double)nentries_ : 0.0);
   }
   for (void* p : {(void*)tkey, (void*)tcnt, (void*)tft, (void*)flags, (void*)dout}) HIP_OK(hipFree(p));
-  dist_merge_pairs(out);
+  if (xchg_.world > 1) dist_merge_pairs(out);
 }
 
 // K1 with every id a byte: dense tables, no hashing in HBM.
@@ -3719,7 +3719,7 @@ void Device::token_freq(size_t T, std::vector<uint64_t>* freq) {
   park();
   freq->assign(T, 0);
   if (!ntiles_ || !T) {
-    dist_allreduce_host(freq->data(), T, false);
+    if (xchg_.world > 1) dist_allreduce_host(freq->data(), T, false);
     return;
   }
   size_t acc = 0;
@@ -3734,7 +3734,7 @@ void Device::token_freq(size_t T, std::vector<uint64_t>* freq) {
   HIP_OK(hipMemcpyAsync(freq->data(), d, T * sizeof(u64), hipMemcpyDeviceToHost, S(stream_)));
   HIP_OK(hipStreamSynchronize(S(stream_)));
   HIP_OK(hipFree(d));
-  dist_allreduce_host(freq->data(), T, false);
+  if (xchg_.world > 1) dist_allreduce_host(freq->data(), T, false);
 }
 
 void Device::download_tokens(std::vector<int32_t>* out) {

@@ -225,11 +225,147 @@ void finish_table(const uint8_t* d, const std::vector<WordRec>& recs, const Load
   });
 }
 
+// Thread-local counting of the words of `pieces`, partitioned by hash, then merged per partition.
+std::vector<Counter> count_pieces(const uint8_t* d, const std::vector<Range>& pieces, int threads,
+                                  std::vector<uint64_t>* piece_words) {
+  std::vector<std::vector<Counter>> local(threads, std::vector<Counter>(kParts));
+  piece_words->assign(pieces.size(), 0);
+  parallel_for(threads, pieces.size(), [&](size_t p, int t) {
+    auto& parts = local[t];
+    uint64_t nw = 0;
+    scan_words(d, pieces[p], [&](uint64_t off, uint32_t len) {
+      uint64_t h = word_hash(d + off, len);
+      parts[h >> (64 - kPartBits)].add(d, h, off, len, 1, off);
+      ++nw;
+    });
+    (*piece_words)[p] = nw;
+  });
+  std::vector<Counter> merged(kParts);
+  parallel_for(threads, kParts, [&](size_t part, int) {
+    Counter& m = merged[part];
+    for (int t = 0; t < threads; ++t)
+      for (const Entry& e : local[t][part].ents) m.add(d, e.hash, e.first, e.len, e.count, e.first);
+  });
+  return merged;
+}
+
+struct OrderKey { uint64_t order; uint32_t part, idx; };
+
+// Reference word order (djb2 & 4095, first occurrence) over the merged counters, then the table.
+void order_and_finish(const uint8_t* d, const std::vector<Counter>& merged, const LoadOptions& opt, int threads,
+                      WordTable* out, std::vector<OrderKey>* keys_out) {
+  std::vector<size_t> part_base(kParts + 1, 0);
+  for (int p = 0; p < kParts; ++p) part_base[p + 1] = part_base[p] + merged[p].ents.size();
+  const size_t W = part_base[kParts];
+  if (W > (size_t)kMaxRank) fatal("corpus has more than 2^30 distinct words");
+  std::vector<OrderKey>& keys = *keys_out;
+  keys.resize(W);
+  parallel_for(threads, kParts, [&](size_t p, int) {
+    for (uint32_t i = 0; i < merged[p].ents.size(); ++i) {
+      const Entry& e = merged[p].ents[i];
+      uint64_t h = 5381;
+      for (uint32_t k = 0; k < e.len; ++k) h = h * 33 + d[e.first + k];
+      if (e.first >= (1ull << 52)) fatal("corpus larger than 2^52 bytes");
+      keys[part_base[p] + i] = {((h & 4095) << 52) | e.first, (uint32_t)p, i};
+    }
+  });
+  std::sort(keys.begin(), keys.end(), [](const OrderKey& a, const OrderKey& b) { return a.order < b.order; });
+  std::vector<WordRec> recs(W);
+  for (size_t r = 0; r < W; ++r) {
+    const Entry& e = merged[keys[r].part].ents[keys[r].idx];
+    recs[r] = WordRec{e.first, e.count, e.len, 0};
+  }
+  finish_table(d, recs, opt, threads, out);
+}
+
+// First position >= x after a delimiter (0 and n stay): the words starting before it end before it.
+uint64_t shard_cut(const uint8_t* d, uint64_t n, uint64_t x) {
+  if (x == 0 || x >= n) return std::min(x, n);
+  while (x < n && !is_delim(d[x - 1])) ++x;
+  return x;
+}
+
+// The distinct words starting in rank r's byte range (of W), with their hashes and global offsets.
+std::vector<Entry> shard_entries(const uint8_t* d, size_t n, const LoadOptions& opt, uint64_t r, uint64_t W,
+                                 int threads, bool* on_gpu) {
+  const uint64_t b = shard_cut(d, n, (uint64_t)((unsigned __int128)n * r / W));
+  const uint64_t e = shard_cut(d, n, (uint64_t)((unsigned __int128)n * (r + 1) / W));
+  std::vector<Entry> mine;
+  *on_gpu = false;
+  if (opt.gpu_device >= 0 && e > b && e - b >= opt.gpu_min_bytes) {
+    std::vector<WordRec> recs;
+    std::string why;
+    if (gpu_count_words(opt.gpu_device, d + b, e - b, &recs, &why)) {
+      *on_gpu = true;
+      mine.resize(recs.size());
+      parallel_for(threads, (recs.size() + 4095) / 4096, [&](size_t blk, int) {
+        const size_t i1 = std::min(recs.size(), (blk + 1) * 4096);
+        for (size_t i = blk * 4096; i < i1; ++i) {
+          const uint64_t f = b + recs[i].first;
+          mine[i] = Entry{word_hash(d + f, recs[i].len), f, recs[i].count, recs[i].len};
+        }
+      });
+      return mine;
+    }
+    std::fprintf(stderr, "[WARNING]\t GPU word count unavailable (%s): counting on the host\n", why.c_str());
+  }
+  if (e > b) {
+    const uint64_t target = std::max<uint64_t>(1 << 20, (e - b) / (uint64_t)(threads * 8) + 1);
+    std::vector<uint64_t> pw;
+    std::vector<Counter> c = count_pieces(d, split_pieces(d, {{b, e}}, target), threads, &pw);
+    for (const Counter& k : c) mine.insert(mine.end(), k.ents.begin(), k.ents.end());
+  }
+  return mine;
+}
+
+// Every rank's word list merged (counts summed, first occurrence min; equal hashes must spell
+// the same word: Counter::add compares the bytes), then the table in reference order.
+void merge_entries(const uint8_t* d, const Entry* all, size_t total, const LoadOptions& opt, int threads,
+                   WordTable* out) {
+  std::vector<std::vector<uint32_t>> by_part(kParts);
+  for (size_t i = 0; i < total; ++i) by_part[all[i].hash >> (64 - kPartBits)].push_back((uint32_t)i);
+  std::vector<Counter> merged(kParts);
+  parallel_for(threads, kParts, [&](size_t p, int) {
+    for (uint32_t i : by_part[p]) merged[p].add(d, all[i].hash, all[i].first, all[i].len, all[i].count, all[i].first);
+  });
+  std::vector<OrderKey> keys;
+  order_and_finish(d, merged, opt, threads, out, &keys);
+}
+
+// The sharded load (LoadOptions::shard_world > 1): this rank's words, then every rank's merged.
+// SHREDWORD_LOAD_SIM_SHARDS=k (tests, one process): the k ranges counted in turn, merged the same way.
+void load_sharded(const uint8_t* d, size_t n, const LoadOptions& opt, int threads, WordTable* out, int sim) {
+  bool on_gpu = false;
+  if (sim > 1) {
+    std::vector<Entry> all;
+    for (int r = 0; r < sim; ++r) {
+      bool g = false;
+      std::vector<Entry> m = shard_entries(d, n, opt, (uint64_t)r, (uint64_t)sim, threads, &g);
+      on_gpu = on_gpu || g;
+      all.insert(all.end(), m.begin(), m.end());
+    }
+    merge_entries(d, all.data(), all.size(), opt, threads, out);
+  } else {
+    std::vector<Entry> mine = shard_entries(d, n, opt, (uint64_t)opt.shard_rank, (uint64_t)opt.shard_world, threads,
+                                            &on_gpu);
+    size_t got = 0;
+    const Entry* all = (const Entry*)opt.gather(opt.gather_ctx, mine.data(), mine.size() * sizeof(Entry), &got);
+    merge_entries(d, all, got / sizeof(Entry), opt, threads, out);
+  }
+  out->counted_on_gpu = on_gpu;
+}
+
 }  // namespace
 
 void load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordTable* out) {
   int threads = opt.threads > 0 ? opt.threads : (int)std::thread::hardware_concurrency();
   threads = std::max(1, std::min(threads, 32));
+  const char* sim_env = std::getenv("SHREDWORD_LOAD_SIM_SHARDS");
+  const int sim = sim_env ? std::atoi(sim_env) : 0;
+  if (((opt.shard_world > 1 && opt.gather) || sim > 1) && !opt.want_stream && n > 0 && !std::memchr(d, 0, n)) {
+    load_sharded(d, n, opt, threads, out, sim);
+    return;
+  }
   // the device count (types layout, NUL-free files: every line is read whole, so the words are
   // the maximal runs of non-delimiters of the whole file)
   if (opt.gpu_device >= 0 && !opt.want_stream && n >= opt.gpu_min_bytes && !std::memchr(d, 0, n)) {
@@ -252,58 +388,14 @@ void load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordT
   for (auto& r : vis) vis_bytes += r.end - r.begin;
   uint64_t target = std::max<uint64_t>(1 << 20, vis_bytes / (uint64_t)(threads * 8) + 1);
   std::vector<Range> pieces = split_pieces(d, vis, target);
-
-  // Pass 1: thread-local counting, partitioned by hash.
-  std::vector<std::vector<Counter>> local(threads, std::vector<Counter>(kParts));
-  std::vector<uint64_t> piece_words(pieces.size(), 0);
-  parallel_for(threads, pieces.size(), [&](size_t p, int t) {
-    auto& parts = local[t];
-    uint64_t nw = 0;
-    scan_words(d, pieces[p], [&](uint64_t off, uint32_t len) {
-      uint64_t h = word_hash(d + off, len);
-      parts[h >> (64 - kPartBits)].add(d, h, off, len, 1, off);
-      ++nw;
-    });
-    piece_words[p] = nw;
-  });
-
-  // Merge per partition.
-  std::vector<Counter> merged(kParts);
-  parallel_for(threads, kParts, [&](size_t part, int) {
-    Counter& m = merged[part];
-    for (int t = 0; t < threads; ++t)
-      for (const Entry& e : local[t][part].ents) m.add(d, e.hash, e.first, e.len, e.count, e.first);
-  });
-  local.clear();
-  local.shrink_to_fit();
-
-  // Reference word order: (djb2 & 4095, first occurrence).
-  struct Key { uint64_t order; uint32_t part, idx; };
-  std::vector<size_t> part_base(kParts + 1, 0);
-  for (int p = 0; p < kParts; ++p) part_base[p + 1] = part_base[p] + merged[p].ents.size();
-  const size_t W = part_base[kParts];
-  if (W > (size_t)kMaxRank) fatal("corpus has more than 2^30 distinct words");
-  std::vector<Key> keys(W);
-  parallel_for(threads, kParts, [&](size_t p, int) {
-    for (uint32_t i = 0; i < merged[p].ents.size(); ++i) {
-      const Entry& e = merged[p].ents[i];
-      uint64_t h = 5381;
-      for (uint32_t k = 0; k < e.len; ++k) h = h * 33 + d[e.first + k];
-      if (e.first >= (1ull << 52)) fatal("corpus larger than 2^52 bytes");
-      keys[part_base[p] + i] = {((h & 4095) << 52) | e.first, (uint32_t)p, i};
-    }
-  });
-  std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) { return a.order < b.order; });
-
-  std::vector<WordRec> recs(W);
-  for (size_t r = 0; r < W; ++r) {
-    const Entry& e = merged[keys[r].part].ents[keys[r].idx];
-    recs[r] = WordRec{e.first, e.count, e.len, 0};
-  }
-  finish_table(d, recs, opt, threads, out);
+  std::vector<uint64_t> piece_words;
+  std::vector<Counter> merged = count_pieces(d, pieces, threads, &piece_words);
+  std::vector<OrderKey> keys;
+  order_and_finish(d, merged, opt, threads, out, &keys);
   WordTable& wt = *out;
 
   if (opt.want_stream) {
+    const size_t W = keys.size();
     // rank of every distinct word, addressable through the merged counters
     std::vector<std::vector<uint32_t>> rank_of(kParts);
     for (int p = 0; p < kParts; ++p) rank_of[p].resize(merged[p].ents.size());

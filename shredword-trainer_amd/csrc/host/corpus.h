@@ -37,6 +37,10 @@ struct WordTable {
   size_t num_symbols() const { return symbols.size(); }
 };
 
+// All-gather of a byte buffer across the ranks of a sharded load: returns every rank's buffer,
+// concatenated in rank order (*out_bytes = total), valid until the next call.
+typedef const void* (*LoadGather)(void* ctx, const void* send, size_t nbytes, size_t* out_bytes);
+
 struct LoadOptions {
   int32_t unk_id = 0;
   float coverage = 0.995f;
@@ -44,6 +48,13 @@ struct LoadOptions {
   int threads = 0;           // 0: hardware concurrency (capped at 32)
   int gpu_device = -1;       // >= 0: count words on this HIP device (types layout, NUL-free files)
   size_t gpu_min_bytes = 1 << 20;  // smaller files take the host path
+  // Sharded load (types layout, NUL-free files; SURVEY.md §8 f2 multi-GPU): rank r of `world`
+  // counts the words starting in its byte range only (on its GPU, or the host path); the ranks'
+  // distinct-word lists are all-gathered and merged (counts summed, first occurrence min,
+  // spellings compared byte for byte), so every rank builds the identical, full table.
+  int shard_rank = 0, shard_world = 1;
+  LoadGather gather = nullptr;
+  void* gather_ctx = nullptr;
 };
 
 // One distinct word found by the device count: its first offset in the file, its occurrence

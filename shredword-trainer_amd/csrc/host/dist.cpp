@@ -198,3 +198,44 @@ void dist_merge_pairs(std::vector<PairCount>* pairs) {
 }
 
 }  // namespace shred
+
+namespace shred {
+
+const void* dist_allgather_bytes(void*, const void* send, size_t nbytes, size_t* out_bytes) {
+  static std::vector<uint8_t> keep;
+  DistState& s = dist_state();
+  keep.clear();
+  if (!dist_active()) {
+    keep.assign((const uint8_t*)send, (const uint8_t*)send + nbytes);
+    *out_bytes = nbytes;
+    return keep.data();
+  }
+  uint64_t neg = ~(uint64_t)nbytes;  // max via min of the negation
+  dist_allreduce_host(&neg, 1, true);
+  const size_t top = (size_t)~neg;
+  const size_t slot = 8 + top;  // [u64 size][payload, padded to the largest]
+  std::vector<uint8_t> mine(slot, 0);
+  const uint64_t n64 = nbytes;
+  std::memcpy(mine.data(), &n64, 8);
+  if (nbytes) std::memcpy(mine.data() + 8, send, nbytes);
+  hip_ok(hipSetDevice(s.device), "hipSetDevice");
+  void *dsend = nullptr, *drecv = nullptr;
+  hip_ok(hipMalloc(&dsend, slot), "hipMalloc");
+  hip_ok(hipMalloc(&drecv, slot * s.world), "hipMalloc");
+  hip_ok(hipMemcpy(dsend, mine.data(), slot, hipMemcpyHostToDevice), "hipMemcpy");
+  nccl_ok(rccl().AllGather(dsend, drecv, slot, ncclUint8, (ncclComm_t)s.comm, nullptr), "ncclAllGather");
+  hip_ok(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+  std::vector<uint8_t> all(slot * s.world);
+  hip_ok(hipMemcpy(all.data(), drecv, all.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+  hip_ok(hipFree(dsend), "hipFree");
+  hip_ok(hipFree(drecv), "hipFree");
+  for (int r = 0; r < s.world; ++r) {
+    uint64_t n = 0;
+    std::memcpy(&n, all.data() + (size_t)r * slot, 8);
+    keep.insert(keep.end(), all.data() + (size_t)r * slot + 8, all.data() + (size_t)r * slot + 8 + n);
+  }
+  *out_bytes = keep.size();
+  return keep.data();
+}
+
+}  // namespace shred

@@ -1,6 +1,10 @@
 // Multi-GPU plumbing: one process per MI355X, RCCL over xGMI.
 //
-// The BPE path shards the word table by contiguous word ranges.  Per merge the
+// Two multi-GPU modes (trainer option dist):
+//  * replicate (default): the load is sharded -- each rank counts the words of its byte range and
+//    the word lists are all-gathered and merged (dist_allgather_bytes, corpus.h) -- and every rank
+//    then runs the whole merge loop on the full word table, with no per-merge collective;
+//  * exchange: the word table is sharded by contiguous word ranges.  Per merge the
 // only exchange is one all-gather of every rank's compacted neighbour-delta records (a fixed
 // bucket per rank; a second round only when a bucket overflows), so every rank receives the
 // identical record multiset, combines it (sum of weights, min of first touch: order-free) and
@@ -41,5 +45,8 @@ void dist_allreduce_device(uint64_t* dev_buf, size_t n, bool min_op, void* strea
 void dist_allreduce_host(uint64_t* host, size_t n, bool min_op);
 // Every rank's pair list, merged: counts summed, first touch min (synchronous).
 void dist_merge_pairs(std::vector<PairCount>* pairs);
+// All-gather of a host byte buffer of any size per rank (corpus.h LoadGather): every rank's
+// buffer concatenated in rank order, valid until the next call (synchronous).
+const void* dist_allgather_bytes(void* ctx, const void* send, size_t nbytes, size_t* out_bytes);
 
 }  // namespace shred

@@ -38,6 +38,9 @@ struct Trainer {
   bool timing = false;
   int device = -1;
   bool local_exchange = false;   // test: the multi-GPU exchange over a single-rank communicator
+  int dist_mode = -1;            // multi-GPU: 1 per-merge records exchange, 0 sharded load + replicated
+                                 // loop, -1 auto (exchange for the stream layout, replicate for types)
+  bool dist_exchange() const { return dist_mode == 1 || (dist_mode < 0 && layout == Layout::kStream); }
   uint32_t exchange_bucket = 0;  // records per rank and exchange bucket (0: default)
   int resident = -1;             // LDS-resident merge loop: -1 default (on), 0 off, 1 on
   int index = -1;                // indexed merge loop: -1 default (on), 0 off, 1 on
@@ -115,6 +118,12 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
     if (t->dev) t->dev->set_spec_depth(d);
   } else if (key == "device") {
     t->device = std::atoi(val.c_str());
+  } else if (key == "dist") {
+    if (val == "replicate") t->dist_mode = 0;
+    else if (val == "exchange") t->dist_mode = 1;
+    else if (val == "auto") t->dist_mode = -1;
+    else return -1;
+    t->device_stale = true;
   } else if (key == "verify_argmax") {
     const int n = std::atoi(val.c_str());
     if (n < 0) return -1;
@@ -148,7 +157,7 @@ bool ensure_device(Trainer* t, const char* caller) {
     if (t->hybrid >= 0) t->dev->set_hybrid(t->hybrid != 0);
     if (t->switch_occ >= 0) t->dev->set_switch_occurrences((uint64_t)t->switch_occ);
     t->dev->set_spec_depth(t->spec_depth ? t->spec_depth : env_int("SHREDWORD_SPEC_DEPTH", 1));
-    if (dist_active() || t->local_exchange) {
+    if ((dist_active() && t->dist_exchange()) || t->local_exchange) {
       Device::Exchange x;
       if (dist_active()) {
         x.rank = dist_state().rank;
@@ -169,7 +178,8 @@ bool ensure_device(Trainer* t, const char* caller) {
       return false;
     }
     size_t begin = 0, end = 0;
-    const int rank = dist_active() ? dist_state().rank : 0, world = dist_active() ? dist_state().world : 1;
+    const bool xshard = dist_active() && t->dist_exchange();  // replicate: every rank holds the whole table
+    const int rank = xshard ? dist_state().rank : 0, world = xshard ? dist_state().world : 1;
     shard_range(t->wt, t->layout, rank, world, &begin, &end);
     TiledStream ts;
     pack_tiles(t->wt, t->layout, begin, end, &ts);
@@ -203,6 +213,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   t->engine.set_speculation(env_int("SHREDWORD_SPECULATE", 1) != 0);
   if (const char* v = std::getenv("SHREDWORD_CHAIN")) set_option(t, "chain", v);
   t->engine.set_verify(env_int("SHREDWORD_VERIFY_ARGMAX", 0));
+  if (const char* v = std::getenv("SHREDWORD_DIST")) set_option(t, "dist", v);
   if (t->engine.log() >= 1) std::printf("[INFO]\t BPE trainer initialized. Heap initialized successfully.\n");
   return t;
 }
@@ -228,6 +239,11 @@ int bpe_load_corpus(Trainer* t, const char* path) {
     if (ord < 0) ord = dist_active() ? dist_state().device : env_int("LOCAL_RANK", 0);
     opt.gpu_device = ord % shred_device_count();
     opt.gpu_min_bytes = (size_t)env_int("SHREDWORD_GPU_LOAD_MIN", 1 << 20);
+  }
+  if (dist_active() && !t->dist_exchange() && !opt.want_stream) {  // sharded load, replicated merge loop
+    opt.shard_rank = dist_state().rank;
+    opt.shard_world = dist_state().world;
+    opt.gather = dist_allgather_bytes;
   }
   std::string err;
   WordTable wt;

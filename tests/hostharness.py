@@ -19,6 +19,9 @@ def load():
     lib.hh_open.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_uint64,
                             ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.hh_open.restype = ctypes.c_void_p
+    lib.hh_open_sharded.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_uint64,
+                                    ctypes.c_int, ctypes.c_int, GATHER_CB, ctypes.c_void_p]
+    lib.hh_open_sharded.restype = ctypes.c_void_p
     lib.hh_close.argtypes = [ctypes.c_void_p]
     lib.hh_set_exchange.argtypes = [ctypes.c_void_p, EXCHANGE_CB, GATHER_CB, ctypes.c_void_p]
     lib.hh_train.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
@@ -51,3 +54,16 @@ def open_case(lib, corpus, cfg, layout="types", rank=0, world=1):
     if not h:
         raise IOError(corpus)
     return h
+
+
+def table_fingerprint(lib, h):
+    """md5 over the word table in rank order: every spelling with its count (and the byte cut)."""
+    import hashlib
+    m = hashlib.md5()
+    buf = ctypes.create_string_buffer(1 << 16)
+    cnt = ctypes.c_uint64()
+    for i in range(lib.hh_num_words(h)):
+        n = lib.hh_word(h, i, buf, len(buf), ctypes.byref(cnt))
+        m.update(buf.raw[:n] + b"\0" + str(cnt.value).encode() + b"\n")
+    m.update(f"{lib.hh_num_symbols(h)} {lib.hh_distinct_bytes(h)} {lib.hh_kept_bytes(h)}".encode())
+    return m.hexdigest()

@@ -6,6 +6,11 @@ rank's list, concatenated in rank order — the records exchange the device path
 over xGMI); the initial pair table and the final token histogram are all-reduced (sum / min).
 Rank 0 writes .model/.vocab/trace.
 
+With SHARDED_LOAD=1 the load is sharded instead (corpus.h LoadOptions::shard_*: each rank counts
+its byte range, the word lists are merged over the same gloo all-gather) and the merge loop runs
+replicated over the full table, with no per-merge exchange; info_r<rank>.txt then also carries the
+table's fingerprint.
+
 usage: multirank_worker.py CORPUS VOCAB UNK COV MPF LAYOUT OUTDIR [SPECULATE [CHAIN]]
 """
 import ctypes
@@ -68,8 +73,14 @@ def main():
     cb = hostharness.EXCHANGE_CB(exchange)
     gcb = hostharness.GATHER_CB(gather)
     cfg = {"vocab_size": int(vocab), "unk_id": int(unk), "character_coverage": float(cov), "min_pair_freq": int(mpf)}
-    h = hostharness.open_case(lib, corpus, cfg, layout, rank, world)
-    lib.hh_set_exchange(h, cb, gcb, None)
+    sharded = os.environ.get("SHARDED_LOAD") == "1"
+    if sharded:
+        h = lib.hh_open_sharded(corpus.encode(), cfg["vocab_size"], cfg["unk_id"], cfg["character_coverage"],
+                                cfg["min_pair_freq"], rank, world, gcb, None)
+        assert h, corpus
+    else:
+        h = hostharness.open_case(lib, corpus, cfg, layout, rank, world)
+        lib.hh_set_exchange(h, cb, gcb, None)
     spec = (ctypes.c_uint64 * 2)()
     lib.hh_spec(h, speculate, spec)
     lib.hh_set_chain(h, chain)
@@ -80,7 +91,8 @@ def main():
                 1 if rank == 0 else 0)
     with open(os.path.join(outdir, f"info_r{rank}.txt"), "w") as f:
         lib.hh_spec(h, -1, spec)
-        f.write(f"{merges} {tiles} {spec[0]} {spec[1]}\n")
+        f.write(f"{merges} {tiles} {spec[0]} {spec[1]}" +
+                (f" {hostharness.table_fingerprint(lib, h)}" if sharded else "") + "\n")
     lib.hh_close(h)
     dist.barrier()
     dist.destroy_process_group()

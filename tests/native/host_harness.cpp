@@ -290,6 +290,34 @@ void* hh_open(const char* path, uint64_t vocab, int32_t unk, float cov, uint64_t
   return h;
 }
 
+// Sharded load (corpus.h LoadOptions::shard_*): this rank counts its byte range, the ranks'
+// word lists are merged through `gather`; the merge loop then runs replicated over the full table.
+void* hh_open_sharded(const char* path, uint64_t vocab, int32_t unk, float cov, uint64_t mpf, int rank, int world,
+                      GatherCb gather, void* ctx) {
+  Harness* h = new Harness();
+  if (cov <= 0.0f || cov >= 1.0f) cov = 0.995f;
+  if (mpf == 0) mpf = kDefaultMinPairFreq;
+  LoadOptions opt;
+  opt.unk_id = unk;
+  opt.coverage = cov;
+  opt.threads = 2;
+  opt.shard_rank = rank;
+  opt.shard_world = world;
+  opt.gather = gather;
+  opt.gather_ctx = ctx;
+  std::string err;
+  if (load_corpus(path, opt, &h->wt, &err) != 0) {
+    delete h;
+    return nullptr;
+  }
+  uint32_t cap = 1024;
+  while (cap < vocab + 1 || (unk >= 0 && cap < (uint64_t)unk + 1)) cap *= 2;
+  h->be.reset(new EmuBackend(h->wt, Layout::kTypes, 0, h->wt.num_words(), cap));
+  h->engine.configure(vocab, unk, mpf);
+  h->engine.set_log(0);
+  return h;
+}
+
 void hh_close(void* p) {
   Harness* h = (Harness*)p;
   if (h->trace) std::fclose(h->trace);

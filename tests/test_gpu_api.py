@@ -495,6 +495,25 @@ def test_gpu_word_count_detects_key_collisions(medium_corpus, tmp_path, monkeypa
     assert outs[0] == outs[1]
 
 
+@pytest.mark.parametrize("shards", [2, 5])
+def test_sharded_load_ranges_on_gpu(shards, medium_corpus, tmp_path, monkeypatch):
+    """The sharded load's per-rank step on the GPU (SHREDWORD_LOAD_SIM_SHARDS: the k byte ranges
+    counted by k_word_count in turn, in one process) merged into the table: the same bytes as the
+    whole-file device count."""
+    monkeypatch.setenv("SHREDWORD_GPU_LOAD_MIN", "1")
+    outs = []
+    for sim in ("0", str(shards)):
+        monkeypatch.setenv("SHREDWORD_LOAD_SIM_SHARDS", sim)
+        t = _trainer(vocab_size=3000, unk_id=0, character_coverage=0.9995, min_pair_freq=2)
+        t.load_corpus(medium_corpus)
+        n, model, vocab = _train_bytes(t, tmp_path, f"s{sim}")
+        st = t.stats()
+        t.destroy()
+        assert st["load_on_gpu"] == 1
+        outs.append((n, model, vocab, st["num_words"], st["num_symbols"], st["num_occurrences"]))
+    assert outs[0] == outs[1]
+
+
 def test_resident_abort_falls_back(medium_corpus, medium_oracle, tmp_path, monkeypatch):
     """k_resident's co-residency check: with a zero bound the leader never sees every workgroup
     (an abort on every launch); the merges it was given run again on the indexed loop, and the

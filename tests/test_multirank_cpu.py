@@ -69,3 +69,36 @@ def test_empty_shard_rank_joins_exchange(oracle_bin, tmp_path):
                     str(tmp_path / "o.vocab")], check=True, stderr=subprocess.DEVNULL)
     assert (tmp_path / "mr.model").read_bytes() == (tmp_path / "o.model").read_bytes()
     assert (tmp_path / "mr.vocab").read_bytes() == (tmp_path / "o.vocab").read_bytes()
+
+
+@pytest.mark.parametrize("name,world", [("small_v300", 2), ("adv_unk0", 3), ("ascii1m_unk7_cov09", 4),
+                                        ("utf8_2m_v2000_mpf50", 2), ("mixed2m_v4000", 4), ("adv_cov05", 2)])
+def test_sharded_load_replicated_loop(name, world, case_corpus, tmp_path):
+    """Sharded load (SURVEY.md §8 f2 multi-GPU half): every rank counts the words starting in its
+    byte range, the ranks' word lists are all-gathered and merged (sums, min first occurrence,
+    spellings compared), and every rank then holds the single-rank table -- same words, order,
+    counts and byte cut -- and runs the merge loop replicated, with the reference's files."""
+    import hostharness
+    case, corpus = case_corpus(name)
+    cfg = case["config"]
+    lib = hostharness.load()
+    h = hostharness.open_case(lib, corpus, cfg, "types")
+    want = hostharness.table_fingerprint(lib, h)
+    lib.hh_close(h)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
+               OMP_NUM_THREADS="1", SHARDED_LOAD="1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(TESTS, "multirank_worker.py"), corpus,
+                               str(cfg["vocab_size"]), str(cfg["unk_id"]), repr(cfg["character_coverage"]),
+                               str(cfg["min_pair_freq"]), "types", str(tmp_path)],
+                              env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(world)]
+    outs = [p.communicate(timeout=600)[0].decode(errors="replace") for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+    infos = [open(tmp_path / f"info_r{r}.txt").read().split() for r in range(world)]
+    assert all(i[4] == want for i in infos), (want, infos)
+    assert all(int(i[0]) == case["merges"] for i in infos)
+    for r in range(world):
+        assert open(tmp_path / f"trace_r{r}.txt").read() == case["trace"]
+    assert open(tmp_path / "mr.model", "rb").read() == case["model_bytes"]
+    assert open(tmp_path / "mr.vocab", "rb").read() == case["vocab_bytes"]
