@@ -25,8 +25,7 @@ void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
   table_.assign(1 << 20, Info{kEmptyKey, 0, 0, 0});  // 24 MB: no rehash below 512 k pairs
   mask_ = table_.size() - 1;
   count_ = 0;
-  hf_.clear();
-  hp_.clear();
+  heap_.assign(1, HeapNode{0, 0, 0});
 }
 
 void Selector::grow() {
@@ -78,48 +77,45 @@ bool Selector::lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) c
 
 void Selector::push(int32_t a, int32_t b, uint64_t freq, uint32_t version) {
   ++ctr_.pushes;
-  size_t i = hf_.size();
-  hf_.push_back(0);
-  hp_.push_back({});
+  if (freq >> 40 || version >> 24) fatal("heap node field overflow (pair count >= 2^40 or version >= 2^24)");
+  HeapNode* h = heap_.data();
+  heap_.push_back(HeapNode{0, 0, 0});
+  h = heap_.data();
+  size_t i = heap_.size() - 2;  // logical slot of the new node
   while (i > 0) {
     size_t p = (i - 1) >> 1;
-    if (hf_[p] >= freq) break;  // sift up only while parent < child (heap.cpp:76)
-    hf_[i] = hf_[p];
-    hp_[i] = hp_[p];
+    if (node_freq(h[p + 1]) >= freq) break;  // sift up only while parent < child (heap.cpp:76)
+    h[i + 1] = h[p + 1];
     i = p;
   }
-  hf_[i] = freq;
-  hp_[i] = {a, b, version};
+  h[i + 1] = HeapNode{freq << 24 | version, a, b};
 }
 
 Selector::HeapEnt Selector::pop() {
   ++ctr_.pops;
-  const HeapEnt top{hp_[0].a, hp_[0].b, hf_[0], hp_[0].version};
-  const uint64_t xf = hf_.back();
-  const HeapPay xp = hp_.back();
-  hf_.pop_back();
-  hp_.pop_back();
-  const size_t n = hf_.size();
+  HeapNode* h = heap_.data();
+  const HeapEnt top{h[1].a, h[1].b, node_freq(h[1]), node_version(h[1])};
+  const HeapNode x = heap_.back();
+  heap_.pop_back();
+  const size_t n = heap_.size() - 1;
   if (n == 0) return top;
+  const uint64_t xf = node_freq(x);
   size_t i = 0;
-  const uint64_t* f = hf_.data();
   for (;;) {  // left child if strictly greater, then right if strictly greater (heap.cpp:101-106)
     size_t l = 2 * i + 1, r = l + 1, best = i;
-    if (4 * i + 3 < n) __builtin_prefetch(f + 4 * i + 3);  // the grandchildren of both sides
-    if (8 * i + 7 < n) {                                  // and their children (one 64-B line)
-      __builtin_prefetch(f + 8 * i + 7);
-      __builtin_prefetch(f + 8 * i + 14);
+    if (4 * i + 3 < n) __builtin_prefetch(h + 4 * i + 4);  // the four grandchildren: one line
+    if (8 * i + 7 < n) {                                  // their eight children: two lines
+      __builtin_prefetch(h + 8 * i + 8);
+      __builtin_prefetch(h + 8 * i + 12);
     }
     uint64_t bf = xf;
-    if (l < n && f[l] > bf) { best = l; bf = f[l]; }
-    if (r < n && f[r] > bf) best = r;
+    if (l < n && node_freq(h[l + 1]) > bf) { best = l; bf = node_freq(h[l + 1]); }
+    if (r < n && node_freq(h[r + 1]) > bf) best = r;
     if (best == i) break;
-    hf_[i] = f[best];
-    hp_[i] = hp_[best];
+    h[i + 1] = h[best + 1];
     i = best;
   }
-  hf_[i] = xf;
-  hp_[i] = xp;
+  h[i + 1] = x;
   return top;
 }
 
@@ -158,7 +154,8 @@ bool Selector::predict_avoid(const int32_t* used, size_t n_used, size_t window, 
   // walk from the root that skips every subtree whose root is below the best found so far (the
   // heap property bounds the whole subtree), so it touches a handful of entries.  Ties: the
   // lowest heap slot, as a scan in slot order would pick.
-  const size_t n = std::min(window, hf_.size());
+  const size_t n = std::min(window, heap_size());
+  const HeapNode* h = heap_.data() + 1;  // logical slots
   uint64_t best_f = 0;
   size_t best = SIZE_MAX;
   size_t stack[64];
@@ -166,34 +163,35 @@ bool Selector::predict_avoid(const int32_t* used, size_t n_used, size_t window, 
   if (n) stack[sp++] = 0;
   while (sp) {
     const size_t i = stack[--sp];
-    const uint64_t f = hf_[i];
+    const uint64_t f = node_freq(h[i]);
     if (f < best_f || f < min_freq_ || (best != SIZE_MAX && f == best_f && i > best)) continue;
     const size_t l = 2 * i + 1;
     if (l + 1 < n && sp < 63) stack[sp++] = l + 1;
     if (l < n && sp < 63) stack[sp++] = l;
-    const HeapPay& e = hp_[i];
+    const HeapNode& e = h[i];
     if (e.a == unk_ || e.b == unk_) continue;
     bool clash = false;
     for (size_t k = 0; k < n_used; ++k) clash |= e.a == used[k] || e.b == used[k];
     if (clash) continue;
     const Info* in = find(pack_pair(e.a, e.b));
-    if (!in || in->version != e.version || in->freq != f) continue;
+    if (!in || in->version != node_version(e) || in->freq != f) continue;
     if (f > best_f || best == SIZE_MAX || i < best) {
       best_f = f;
       best = i;
     }
   }
   if (best == SIZE_MAX) return false;
-  *pa = hp_[best].a;
-  *pb = hp_[best].b;
+  *pa = h[best].a;
+  *pb = h[best].b;
   return true;
 }
 
 size_t Selector::predict_chain(int32_t a, int32_t b, size_t window, size_t k, int32_t* out) const {
-  const size_t n = std::min(window, hf_.size());
+  const size_t n = std::min(window, heap_size());
+  const HeapNode* h = heap_.data() + 1;
   std::vector<std::pair<uint64_t, size_t>> cand;  // (freq, heap slot) of the valid entries
   for (size_t i = 0; i < n; ++i) {
-    const HeapEnt e{hp_[i].a, hp_[i].b, hf_[i], hp_[i].version};
+    const HeapEnt e{h[i].a, h[i].b, node_freq(h[i]), node_version(h[i])};
     if (e.freq < min_freq_ || e.a == unk_ || e.b == unk_) continue;
     const Info* in = find(pack_pair(e.a, e.b));
     if (!in || in->version != e.version || in->freq != e.freq) continue;
@@ -204,7 +202,7 @@ size_t Selector::predict_chain(int32_t a, int32_t b, size_t window, size_t k, in
   size_t m = 0;
   for (const auto& c : cand) {
     if (m == k) break;
-    const HeapPay& e = hp_[c.second];
+    const HeapNode& e = h[c.second];
     bool clash = false;
     for (int32_t u : used) clash |= e.a == u || e.b == u;
     if (clash) continue;
@@ -218,10 +216,10 @@ size_t Selector::predict_chain(int32_t a, int32_t b, size_t window, size_t k, in
 }
 
 bool Selector::select(int32_t* a, int32_t* b, uint64_t* freq) {
-  while (!hf_.empty()) {
+  while (!heap_empty()) {
     HeapEnt top = pop();
-    if (!hf_.empty())  // the next top's pair info, fetched while this one is checked
-      __builtin_prefetch(&table_[mix64(pack_pair(hp_[0].a, hp_[0].b)) & mask_]);
+    if (!heap_empty())  // the next top's pair info, fetched while this one is checked
+      __builtin_prefetch(&table_[mix64(pack_pair(heap_[1].a, heap_[1].b)) & mask_]);
     Info& in = get(top.a, top.b);
     if (top.version != in.version) {  // stale entry
       ++ctr_.stale;

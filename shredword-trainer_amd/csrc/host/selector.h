@@ -114,9 +114,9 @@ class Selector {
   // share no token with (a, b) or with each other, by frequency.  out: k (a, b) pairs.
   size_t predict_chain(int32_t a, int32_t b, size_t window, size_t k, int32_t* out) const;
 
-  size_t heap_size() const { return hf_.size(); }
-  bool heap_empty() const { return hf_.empty(); }
-  uint64_t heap_top_freq() const { return hf_.empty() ? 0 : hf_[0]; }
+  size_t heap_size() const { return heap_.empty() ? 0 : heap_.size() - 1; }
+  bool heap_empty() const { return heap_.size() <= 1; }
+  uint64_t heap_top_freq() const { return heap_empty() ? 0 : node_freq(heap_[1]); }
   size_t num_pairs() const { return count_; }
   // freq/version of a pair (0/0 when absent); for tests.
   bool lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) const;
@@ -132,7 +132,10 @@ class Selector {
   // pair (INT32_MIN, INT32_MIN), which no token pair can be (ids are >= -2^30).
   struct Info { uint64_t key; uint64_t freq; uint32_t version; uint32_t seq; };
   struct HeapEnt { int32_t a, b; uint64_t freq; uint32_t version; };
-  struct HeapPay { int32_t a, b; uint32_t version; };
+  // A heap node in 16 bytes: frequency (40 bits) << 24 | version (24 bits), then the pair.
+  struct HeapNode { uint64_t fv; int32_t a, b; };
+  static uint64_t node_freq(const HeapNode& n) { return n.fv >> 24; }
+  static uint32_t node_version(const HeapNode& n) { return (uint32_t)(n.fv & 0xFFFFFFu); }
   struct Change { uint64_t hk; int64_t delta; uint64_t ft; };
   static constexpr uint64_t kEmptyKey = 0x8000000080000000ull;
 
@@ -147,10 +150,11 @@ class Selector {
   HugeVec<Info> table_;
   size_t count_ = 0;
   uint64_t mask_ = 0;
-  // The reference's binary heap (heap.cpp), struct-of-arrays: the sifts compare frequencies only,
-  // so they walk a dense u64 array (8 children per cache line pair) and move the payload beside.
-  HugeVec<uint64_t> hf_;
-  HugeVec<HeapPay> hp_;
+  // The reference's binary heap (heap.cpp), logical slot k stored at heap_[k + 1]: with 16-byte
+  // nodes on a 2 MiB-aligned array, the two children of a slot share one 32-byte half line and
+  // its four grandchildren one 64-byte line, so a sift level touches one cache line (frequency
+  // and payload together).  heap_[0] is padding.
+  HugeVec<HeapNode> heap_;
   std::vector<Change> changes_;
   std::vector<uint32_t> change_index_;
   std::vector<Change> staged_;  // apply: the first counting pass
