@@ -125,7 +125,28 @@ bool Engine::merge_one(Backend& be, int remaining) {
   const DeltaRecord* recs = nullptr;
   const size_t n = be.collect(X, &recs);
   const double t3 = now_seconds();
-  sel_.apply(a, b, X, recs, n);
+  sel_.apply_combine(a, b, X, recs, n);
+  // Late correction: with (a, b)'s changes known, a new pair holding X that is strictly more
+  // frequent than the guess in flight (made before them; its own count is unchanged by this
+  // merge) replaces it now, so the device undoes and redoes the guess while this merge is
+  // applied and the next one selected.  The exact selection still confirms or rolls back.
+  if (correct_ && speculate_ && chain == 1 && pending_.size() == 1 && pending_.front().X == X + 1 && remaining > 1 &&
+      be.can_overlap()) {
+    const Guess g = pending_.front();
+    int32_t pa, pb;
+    uint64_t pf = 0, gf = 0;
+    uint32_t gv = 0;
+    sel_.lookup(g.a, g.b, &gf, &gv);
+    if (sel_.predict_after(X, gf, &pa, &pb, &pf)) {
+      be.rollback(g.X);
+      pending_.clear();
+      pending_.push_back({pa, pb, X + 1});
+      ++launches_;
+      ++corrections_;
+      be.merge_scan(pa, pb, X + 1);
+    }
+  }
+  sel_.apply_finish(a, b, X);
   times_.launch_s += t2 - t1;
   times_.wait_s += t3 - t2;
   if (launched) {
@@ -135,7 +156,11 @@ bool Engine::merge_one(Backend& be, int remaining) {
     times_.wait_miss_s += t3 - t2;
     ++times_.n_miss;
   }
-  times_.apply_s += now_seconds() - t3;
+  const double t4 = now_seconds();
+  times_.apply_s += t4 - t3;
+  if (mtrace_on_)
+    mtrace_.push_back(MergeTime{(float)(1e6 * (t1 - t0)), (float)(1e6 * (t2 - t1)), (float)(1e6 * (t3 - t2)),
+                                (float)(1e6 * (t4 - t3)), (uint32_t)n, (uint8_t)(launched ? 1 : 0)});
   return true;
 }
 
@@ -161,6 +186,8 @@ int Engine::train(Backend& be) {
   const double t0 = now_seconds();
   if (log_ >= 1) std::printf("[INFO]\t Starting BPE training (target vocab size: %zu)\n", target_vocab_);
   sel_.reset(unk_, min_freq_);  // bpe_init (bpe.cpp:98-108)
+  mtrace_on_ = std::getenv("SHREDWORD_ENGINE_TRACE") != nullptr;
+  mtrace_.clear();
   count_bigrams(be);
   times_.init_s += now_seconds() - t0;
   int total = 0;
@@ -194,12 +221,22 @@ int Engine::train(Backend& be) {
   if (trace_) std::fflush(trace_);
   times_.train_s += now_seconds() - t0;
   if (log_ >= 1) std::printf("[INFO]\t Training completed. Performed %d merges\n", total);
+  if (const char* tp = std::getenv("SHREDWORD_ENGINE_TRACE")) {
+    if (FILE* f = std::fopen(tp, "w")) {
+      for (size_t i = 0; i < mtrace_.size(); ++i) {
+        const MergeTime& m = mtrace_[i];
+        std::fprintf(f, "%zu %u %.2f %.2f %.2f %.2f %u\n", i, m.hit, m.select_us, m.launch_us, m.wait_us, m.apply_us,
+                     m.records);
+      }
+      std::fclose(f);
+    }
+  }
   if (std::getenv("SHREDWORD_ENGINE_REPORT"))
     std::fprintf(stderr, "[ENGINE] merges %d: select %.2f us, apply %.2f us per merge; wait %.2f us per guessed merge (%llu), "
-                 "%.2f us per posted merge (%llu)\n", total, 1e6 * times_.select_s / std::max(1, total),
+                 "%.2f us per posted merge (%llu); corrections %llu\n", total, 1e6 * times_.select_s / std::max(1, total),
                  1e6 * times_.apply_s / std::max(1, total), 1e6 * times_.wait_hit_s / std::max<uint64_t>(1, times_.n_hit),
                  (unsigned long long)times_.n_hit, 1e6 * times_.wait_miss_s / std::max<uint64_t>(1, times_.n_miss),
-                 (unsigned long long)times_.n_miss);
+                 (unsigned long long)times_.n_miss, (unsigned long long)corrections_);
   return total;
 }
 

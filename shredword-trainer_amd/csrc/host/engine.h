@@ -93,6 +93,10 @@ class Engine {
     chain_window_ = window;
   }
   void set_speculation(bool on) { speculate_ = on; }
+  // Late correction of the guess in flight once the current merge's records are known (default
+  // on; SHREDWORD_CORRECT=0 turns it off).
+  void set_correction(bool on) { correct_ = on; }
+  uint64_t corrections() const { return corrections_; }
   // K5 argmax verifier (debug): every `every` merges (0 = off), the selected pair's frequency is
   // checked against a device recount of the corpus (Backend::pair_max): it must be the largest
   // pair count and (a, b)'s own count.  Mismatches are counted and the first is printed.
@@ -131,9 +135,16 @@ class Engine {
   std::vector<int32_t> chain_ab_;
   uint64_t spec_hits_ = 0, spec_misses_ = 0, launches_ = 0;
   int verify_every_ = 0;
+  bool correct_ = true;
+  uint64_t corrections_ = 0;
   uint64_t verify_checks_ = 0, verify_fail_ = 0;
   size_t probe_k_ = 0, probe_window_ = 256;
   std::vector<std::vector<int32_t>> chain_log_;
+  // SHREDWORD_ENGINE_TRACE=<path>: per merge (hit, select, launch, wait, apply µs, records),
+  // written at the end of train()
+  struct MergeTime { float select_us, launch_us, wait_us, apply_us; uint32_t records; uint8_t hit; };
+  std::vector<MergeTime> mtrace_;
+  bool mtrace_on_ = false;
 };
 
 }  // namespace shred

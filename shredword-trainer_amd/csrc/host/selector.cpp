@@ -22,23 +22,30 @@ void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
   unk_ = unk_id;
   min_freq_ = min_pair_freq;
   ctr_ = Counters();
-  table_.assign(1 << 20, Info{kEmptyKey, 0, 0, 0});  // 24 MB: no rehash below 512 k pairs
+  table_.assign(1 << 20, Info{kEmptyKey, 0});  // 16 MB: no rehash below 512 k pairs
+  seq_.assign(table_.size(), 0);
   mask_ = table_.size() - 1;
   count_ = 0;
   heap_.assign(1, HeapNode{0, 0, 0});
 }
 
 void Selector::grow() {
-  HugeVec<Info> old(table_.size() * 4, Info{kEmptyKey, 0, 0, 0});
+  HugeVec<Info> old(table_.size() * 4, Info{kEmptyKey, 0});
+  HugeVec<uint32_t> old_seq(old.size(), 0);
   old.swap(table_);
+  old_seq.swap(seq_);
   mask_ = table_.size() - 1;
-  for (const Info& in : old) {
+  for (size_t i = 0; i < old.size(); ++i) {
+    const Info& in = old[i];
     if (in.key == kEmptyKey) continue;
     uint64_t j = mix64(in.key) & mask_;
     while (table_[j].key != kEmptyKey) j = (j + 1) & mask_;
     table_[j] = in;
+    seq_[j] = old_seq[i];
   }
 }
+
+void Selector::info_overflow() { fatal("pair info field overflow (pair count >= 2^40 or version >= 2^24)"); }
 
 Selector::Info& Selector::get(int32_t a, int32_t b) {
   const uint64_t key = pack_pair(a, b);
@@ -54,7 +61,8 @@ Selector::Info& Selector::get(int32_t a, int32_t b) {
     j = mix64(key) & mask_;
     while (table_[j].key != kEmptyKey) j = (j + 1) & mask_;
   }
-  table_[j] = Info{key, 0, 0, (uint32_t)count_++};
+  table_[j] = Info{key, 0};
+  seq_[j] = (uint32_t)count_++;
   return table_[j];
 }
 
@@ -70,8 +78,8 @@ const Selector::Info* Selector::find(uint64_t key) const {
 
 bool Selector::lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) const {
   const Info* in = find(pack_pair(a, b));
-  *freq = in ? in->freq : 0;
-  *version = in ? in->version : 0;
+  *freq = in ? in->freq() : 0;
+  *version = in ? in->version() : 0;
   return in != nullptr;
 }
 
@@ -124,23 +132,23 @@ void Selector::add_counts(std::vector<PairCount> pairs) {
   std::sort(pairs.begin(), pairs.end(), [](const PairCount& x, const PairCount& y) { return x.ft < y.ft; });
   for (const PairCount& p : pairs) {
     Info& in = get(p.a, p.b);
-    if (in.freq == 0) in.version = 0;  // bpe.cpp:207-210
-    in.freq += p.count;
+    if (in.freq() == 0) in.set_version(0);  // bpe.cpp:207-210
+    in.set_freq(in.freq() + p.count);
   }
   // Heap build: bucket 0..4095, chain (creation) order, freq >= min (bpe.cpp:218-225).
   std::vector<std::pair<uint64_t, uint64_t>> order;  // ((bucket << 32) | seq, slot)
   order.reserve(count_);
   for (uint64_t i = 0; i < table_.size(); ++i) {
     const Info& in = table_[i];
-    if (in.key != kEmptyKey && in.freq >= min_freq_) {
+    if (in.key != kEmptyKey && in.freq() >= min_freq_) {
       uint32_t bk = pair_fnv(pair_first(in.key), pair_second(in.key)) & (kPairBuckets - 1);
-      order.push_back({((uint64_t)bk << 32) | in.seq, i});
+      order.push_back({((uint64_t)bk << 32) | seq_[i], i});
     }
   }
   std::sort(order.begin(), order.end());
   for (auto& o : order) {
     const Info& in = table_[o.second];
-    push(pair_first(in.key), pair_second(in.key), in.freq, in.version);
+    push(pair_first(in.key), pair_second(in.key), in.freq(), in.version());
   }
 }
 
@@ -174,7 +182,7 @@ bool Selector::predict_avoid(const int32_t* used, size_t n_used, size_t window, 
     for (size_t k = 0; k < n_used; ++k) clash |= e.a == used[k] || e.b == used[k];
     if (clash) continue;
     const Info* in = find(pack_pair(e.a, e.b));
-    if (!in || in->version != node_version(e) || in->freq != f) continue;
+    if (!in || in->version() != node_version(e) || in->freq() != f) continue;
     if (f > best_f || best == SIZE_MAX || i < best) {
       best_f = f;
       best = i;
@@ -194,7 +202,7 @@ size_t Selector::predict_chain(int32_t a, int32_t b, size_t window, size_t k, in
     const HeapEnt e{h[i].a, h[i].b, node_freq(h[i]), node_version(h[i])};
     if (e.freq < min_freq_ || e.a == unk_ || e.b == unk_) continue;
     const Info* in = find(pack_pair(e.a, e.b));
-    if (!in || in->version != e.version || in->freq != e.freq) continue;
+    if (!in || in->version() != e.version || in->freq() != e.freq) continue;
     cand.push_back({e.freq, i});
   }
   std::stable_sort(cand.begin(), cand.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
@@ -221,15 +229,15 @@ bool Selector::select(int32_t* a, int32_t* b, uint64_t* freq) {
     if (!heap_empty())  // the next top's pair info, fetched while this one is checked
       __builtin_prefetch(&table_[mix64(pack_pair(heap_[1].a, heap_[1].b)) & mask_]);
     Info& in = get(top.a, top.b);
-    if (top.version != in.version) {  // stale entry
+    if (top.version != in.version()) {  // stale entry
       ++ctr_.stale;
       continue;
     }
-    uint64_t actual = (top.a == unk_ || top.b == unk_) ? 0 : in.freq;
-    if (actual != in.freq) {
-      in.freq = actual;
-      in.version++;
-      if (actual >= min_freq_) push(top.a, top.b, actual, in.version);
+    uint64_t actual = (top.a == unk_ || top.b == unk_) ? 0 : in.freq();
+    if (actual != in.freq()) {
+      in.set_freq(actual);
+      in.bump_version();
+      if (actual >= min_freq_) push(top.a, top.b, actual, in.version());
       continue;
     }
     if (actual < min_freq_) continue;
@@ -242,6 +250,11 @@ bool Selector::select(int32_t* a, int32_t* b, uint64_t* freq) {
 }
 
 void Selector::apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n) {
+  apply_combine(a, b, X, recs, n);
+  apply_finish(a, b, X);
+}
+
+void Selector::apply_combine(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n) {
   const uint64_t c0 = __builtin_ia32_rdtsc();
   // 1. records -> FreqChange entries keyed exactly like the reference's pair_hash.
   changes_.clear();
@@ -281,8 +294,30 @@ void Selector::apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, s
   }
   ctr_.records += n;
   ctr_.changes += changes_.size();
+  ctr_.cyc_combine += __builtin_ia32_rdtsc() - c0;
+}
+
+bool Selector::predict_after(int32_t X, uint64_t above, int32_t* pa, int32_t* pb, uint64_t* pf) const {
+  // Pairs holding X are new: their count after this merge is their combined delta, exactly.
+  uint64_t best_f = above;
+  bool found = false;
+  for (const Change& c : changes_) {
+    const int32_t f = (int32_t)(uint32_t)(c.hk >> 32), s = (int32_t)(uint32_t)c.hk;
+    if ((f != X && s != X) || f == unk_ || s == unk_ || c.delta <= 0) continue;
+    const uint64_t v = (uint64_t)c.delta;
+    if (v > best_f && v >= min_freq_) {
+      best_f = v;
+      *pa = f;
+      *pb = s;
+      found = true;
+    }
+  }
+  if (found) *pf = best_f;
+  return found;
+}
+
+void Selector::apply_finish(int32_t a, int32_t b, int32_t X) {
   const uint64_t c1 = __builtin_ia32_rdtsc();
-  ctr_.cyc_combine += c1 - c0;
   // 2. reference application order: bucket (hk % 1024) ascending, latest first touch first.
   //    Two stable 5-bit counting passes by bucket (the usual ~100 changes never pay for a
   //    1024-entry prefix), then insertion sort inside the (almost always tiny) buckets.
@@ -323,18 +358,18 @@ void Selector::apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, s
     Info& in = get(f, s);
     if (c.delta < 0) {
       const uint64_t m = (uint64_t)(-c.delta);
-      in.freq = in.freq >= m ? in.freq - m : 0;
+      in.set_freq(in.freq() >= m ? in.freq() - m : 0);
     } else {
-      in.freq += (uint64_t)c.delta;
+      in.set_freq(in.freq() + (uint64_t)c.delta);
     }
-    if (in.freq >= min_freq_) {
-      in.version++;
-      push(f, s, in.freq, in.version);
+    if (in.freq() >= min_freq_) {
+      in.bump_version();
+      push(f, s, in.freq(), in.version());
     }
   }
   Info& merged = get(a, b);
-  merged.freq = 0;
-  merged.version++;
+  merged.set_freq(0);
+  merged.bump_version();
   ctr_.cyc_walk += __builtin_ia32_rdtsc() - c2;
 }
 

@@ -102,6 +102,14 @@ class Selector {
 
   // Applies one merge's device deltas and finalises the merged key (bpe.cpp:297-318).
   void apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n);
+  // apply() in two steps: the records combined into per-pair changes, then the changes applied
+  // in the reference's order.  Between them predict_after() can see the changes.
+  void apply_combine(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n);
+  void apply_finish(int32_t a, int32_t b, int32_t X);
+  // Between the two steps: the most frequent new pair holding X (its count is exact: the pair
+  // did not exist before this merge) if its count is above `above` -- a better guess of the next
+  // merge than one made before (a, b)'s records were known.
+  bool predict_after(int32_t X, uint64_t above, int32_t* pa, int32_t* pb, uint64_t* pf) const;
 
   // Guess of the merge after (a, b), made before (a, b)'s deltas are known: the best valid heap
   // entry among the first `window` heap slots that shares no token with (a, b).  Used only to
@@ -130,7 +138,24 @@ class Selector {
  private:
   // One flat open-addressing table: a lookup touches one cache line.  kEmptyKey is the packed
   // pair (INT32_MIN, INT32_MIN), which no token pair can be (ids are >= -2^30).
-  struct Info { uint64_t key; uint64_t freq; uint32_t version; uint32_t seq; };
+  // 16 bytes: four to a cache line.  freq (40 bits) << 24 | version (24 bits); the creation
+  // sequence number the heap build orders by lives beside, in seq_.
+  struct Info {
+    uint64_t key;
+    uint64_t fv;
+    uint64_t freq() const { return fv >> 24; }
+    uint32_t version() const { return (uint32_t)(fv & 0xFFFFFFu); }
+    void set_freq(uint64_t f) {
+      if (f >> 40) info_overflow();
+      fv = f << 24 | (fv & 0xFFFFFFu);
+    }
+    void set_version(uint32_t v) { fv = (fv & ~0xFFFFFFull) | (v & 0xFFFFFFu); }
+    void bump_version() {
+      if ((fv & 0xFFFFFFu) == 0xFFFFFFu) info_overflow();
+      ++fv;
+    }
+  };
+  [[noreturn]] static void info_overflow();
   struct HeapEnt { int32_t a, b; uint64_t freq; uint32_t version; };
   // A heap node in 16 bytes: frequency (40 bits) << 24 | version (24 bits), then the pair.
   struct HeapNode { uint64_t fv; int32_t a, b; };
@@ -148,6 +173,7 @@ class Selector {
   int32_t unk_ = 0;
   uint64_t min_freq_ = 2000;
   HugeVec<Info> table_;
+  HugeVec<uint32_t> seq_;  // creation order of table_[j] (bimap_get order), for the heap build
   size_t count_ = 0;
   uint64_t mask_ = 0;
   // The reference's binary heap (heap.cpp), logical slot k stored at heap_[k + 1]: with 16-byte

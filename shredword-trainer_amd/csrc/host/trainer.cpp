@@ -211,6 +211,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   if (const char* v = std::getenv("SHREDWORD_LAYOUT")) set_option(t, "layout", v);
   if (const char* v = std::getenv("SHREDWORD_TRACE")) set_option(t, "trace", v);
   t->engine.set_speculation(env_int("SHREDWORD_SPECULATE", 1) != 0);
+  t->engine.set_correction(env_int("SHREDWORD_CORRECT", 1) != 0);
   if (const char* v = std::getenv("SHREDWORD_CHAIN")) set_option(t, "chain", v);
   t->engine.set_verify(env_int("SHREDWORD_VERIFY_ARGMAX", 0));
   if (const char* v = std::getenv("SHREDWORD_DIST")) set_option(t, "dist", v);
