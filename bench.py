@@ -92,6 +92,48 @@ def cpu_model():
     return "unknown"
 
 
+def l3_domain(cpu):
+    """The CPUs sharing `cpu`'s last-level cache (sysfs), within this process's affinity set."""
+    allowed = os.sched_getaffinity(0)
+    try:
+        idx = sorted(os.listdir(f"/sys/devices/system/cpu/cpu{cpu}/cache"))
+        for name in reversed(idx):
+            if not name.startswith("index"):
+                continue
+            with open(f"/sys/devices/system/cpu/cpu{cpu}/cache/{name}/shared_cpu_list") as f:
+                cpus = set()
+                for part in f.read().strip().split(","):
+                    lo, _, hi = part.partition("-")
+                    cpus.update(range(int(lo), int(hi or lo) + 1))
+            return sorted(cpus & allowed) or [cpu]
+    except (OSError, ValueError):
+        pass
+    return [cpu]
+
+
+def pin_host_loop(local_rank):
+    """Keeps this rank's threads on one last-level-cache domain (the host replay's heap and pair
+    table live in that cache; a migration to another CCD starts cold).  Rank r takes the r-th
+    domain of the allowed CPUs; the last CPU stays free for the CPU baseline."""
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) < 4:
+        return None
+    seen, domains = set(), []
+    for c in allowed[:-1]:
+        if c in seen:
+            continue
+        d = [x for x in l3_domain(c) if x != allowed[-1]]
+        seen.update(d)
+        domains.append(d)
+    # the domain of CPU 0 takes most of the OS's interrupts and housekeeping: start past it
+    dom = domains[(local_rank + 1) % len(domains)] if len(domains) > 1 else domains[0]
+    try:
+        os.sched_setaffinity(0, set(dom))
+    except OSError:
+        return None
+    return dom
+
+
 def cpu_baseline_start(cfg, path, seconds):
     """Starts the CPU port (oracle/bpe_oracle.c: the reference-faithful merge loop, SURVEY.md §8
     d5) on ONE host core — the last core of this process's affinity set, away from the core
@@ -378,6 +420,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--encode-reps", type=int, default=5, help="encoder leg repetitions (0 = skip)")
+    ap.add_argument("--no-pin", action="store_true", help="do not keep the host loop on one L3 domain")
     ap.add_argument("--pair-count-reps", type=int, default=10,
                     help="K1 roofline leg on the stream layout of the same corpus (0: skip)")
     args = ap.parse_args()
@@ -411,6 +454,7 @@ def main():
         except Exception as e:  # the GPU number stands on its own
             cpu_h = {"error": repr(e)}
 
+    pinned = None if args.no_pin else pin_host_loop(local)
     from shredword import dist as sdist
     from shredword.trainer import BPETrainer
     if world > 1:
@@ -549,6 +593,8 @@ def main():
             "resident": {"launches": st["resident_launches"], "ms": st["resident_ms"],
                          "note": "k_resident launch durations (HIP events): one persistent launch per train()"},
             "load_s": load_s, "corpus_gen_s": gen_s,
+            "host_cpus": (f"pinned to the L3 domain {pinned[0]}-{pinned[-1]} ({len(pinned)} CPUs)" if pinned
+                          else "not pinned"),
             "host_breakdown_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
             "init_s_last_step": st["init_seconds"],
             "selector_last_step": {k: st[k] for k in ("heap_pops", "heap_stale_pops", "heap_pushes", "delta_records",
