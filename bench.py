@@ -113,7 +113,7 @@ def l3_domain(cpu):
 
 def pin_host_loop(local_rank):
     """Keeps this rank's threads on one last-level-cache domain (the host replay's heap and pair
-    table live in that cache; a migration to another CCD starts cold).  Rank r takes the r-th
+    table live in that cache; a migration to another CCD starts cold).  Rank r takes the (r+1)-th
     domain of the allowed CPUs; the last CPU stays free for the CPU baseline."""
     allowed = sorted(os.sched_getaffinity(0))
     if len(allowed) < 4:
