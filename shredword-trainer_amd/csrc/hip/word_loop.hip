@@ -258,6 +258,7 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
   bool skip = false;
 #pragma unroll
   for (int j = 0; j < (int)kStripTok; ++j) {
+    if ((j & 3) == 0 && !__any((uint32_t)j < L)) break;  // every lane's word has ended
     const int32_t t0 = run_at(x, 1 + j);
     const int32_t t1 = j + 1 < (int)kStripTok ? run_at(x, 2 + j) : 0;
     const bool emit = (uint32_t)j < L && !skip;
