@@ -347,7 +347,7 @@ def pair_count_leg(cfg, path, reps, device=0, layout="stream", dist=None):
     }
 
 
-def encode_leg(model, vocab, unk, path, reps, device=0):
+def encode_leg(model, vocab, unk, path, reps, device=0, cfg_name="c3"):
     """Encoder: the model this run trained applied to its own HBM-resident corpus
     (word-cache kernels + hipCUB scan + k_encode_emit, HIP events on the encoder's stream).  Checks
     the size-independent property that the id counts equal the .vocab frequency column."""
@@ -383,17 +383,19 @@ def encode_leg(model, vocab, unk, path, reps, device=0):
     enc.destroy()
     del text, out
     torch.cuda.empty_cache()
-    traffic = sum(pmc_traffic("c2", "types", k) or 0.0 for k in
-                  ("k_cache_insert", "k_cache_encode<true>", "k_cache_words", "k_encode_emit"))
-    return {"kernel": ("k_cache_insert + k_cache_encode + k_cache_words + hipCUB scan + k_encode_emit "
+    per = {k: pmc_traffic(cfg_name, "types", k) for k in
+           ("k_cache_insert", "k_cache_encode<true>", "k_cache_words", "k_block_emit")}
+    traffic = sum(v or 0.0 for v in per.values())
+    return {"kernel": ("k_cache_insert + k_cache_encode + k_cache_words + hipCUB scan + k_block_emit "
                        "(word cache; median of reps, HIP events)"),
+            "traffic_by_kernel": per, "traffic_x_algorithmic": (traffic / alg) if traffic else None,
             "traffic_bytes": traffic or None,
             "text_bytes": n, "ids": nids, "ms": ms, "text_GBps": n / (ms * 1e-3) / 1e9,
             "algorithmic_bytes": alg, "achieved_GBps": alg / (ms * 1e-3) / 1e9,
             "frac_of_hbm_peak": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "counts_match_vocab": bool(np.array_equal(counts, np.array(freq, dtype=np.int64))),
             "note": ("latency of word-cache probes and first-occurrence reads (L2/MALL), not HBM bandwidth; "
-                     "traffic_bytes = PMC bytes of the five kernels per call from the committed C2 profile")}
+                     f"traffic_bytes = PMC bytes of the word-cache kernels per call from the committed {cfg_name} profile")}
 
 
 def hbm_probe_leg(device=0, nbytes=4 << 30, reps=10):
@@ -510,7 +512,7 @@ def main():
     if args.encode_reps > 0 and rank == 0:
         try:
             encode = encode_leg(os.path.join(tmpd, f"bench_r{rank}.model"), os.path.join(tmpd, f"bench_r{rank}.vocab"),
-                                cfg["unk"], path, args.encode_reps, device=local)
+                                cfg["unk"], path, args.encode_reps, device=local, cfg_name=args.config)
         except Exception as e:
             encode = {"error": repr(e)}
 
@@ -593,6 +595,10 @@ def main():
             "resident": {"launches": st["resident_launches"], "ms": st["resident_ms"],
                          "note": "k_resident launch durations (HIP events): one persistent launch per train()"},
             "load_s": load_s, "corpus_gen_s": gen_s,
+            "load": {"kernel": "k_word_count (one pass, LDS-staged tiles, byte-exact in-pass verification)",
+                     "algorithmic_bytes": cfg["bytes"],
+                     "traffic_bytes": pmc_traffic(args.config, args.layout, "k_word_count"),
+                     "note": "load_corpus: PCIe upload + device word count + host table; outside the timed step"},
             "host_cpus": (f"pinned to the L3 domain {pinned[0]}-{pinned[-1]} ({len(pinned)} CPUs)" if pinned
                           else "not pinned"),
             "host_breakdown_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
