@@ -22,7 +22,11 @@ void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
   unk_ = unk_id;
   min_freq_ = min_pair_freq;
   ctr_ = Counters();
-  table_.assign(1 << 20, Info{kEmptyKey, 0});  // 16 MB: no rehash below 512 k pairs
+  // at least 1 M slots (16 MB: no rehash below 512 k pairs), and as many as the previous
+  // training grew to: a repeated train() (benchmarks, sweeps) rehashes nothing and reuses the
+  // mapped pages (a 4 M -> 16 M slot grow costs ~12 ms mid-training at C3)
+  const size_t want = std::max<size_t>(size_t(1) << 20, table_.size());
+  table_.assign(want, Info{kEmptyKey, 0});
   seq_.assign(table_.size(), 0);
   mask_ = table_.size() - 1;
   count_ = 0;
