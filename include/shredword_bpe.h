@@ -121,11 +121,12 @@ int shred_probe_rollback(Trainer* trainer, int32_t a, int32_t b);
 int64_t shred_debug_tokens(Trainer* trainer, int32_t* out, size_t cap);
 
 /* Diagnostic: the indexed loop's per-merge trace of the merges collected since timing was last
- * switched on or the stats cleared (set_option timing / clear_stats): 12 uint32 per merge — X,
+ * switched on or the stats cleared (set_option timing / clear_stats): 15 uint32 per merge — X,
  * listed words, scanned words, changed words, occurrences, device ns command -> flag, of which
  * lookup ns and scan ns, then wave 0's stamps (ns after the command: pool entries loaded, first
- * run loaded, first word merged, scan loop left).  Copies min(cap, n) values into out; returns n
- * (-1 on error). */
+ * run loaded, first word merged, unused), the device ns since the previous merge's flag spent
+ * waiting for commands and undoing guesses, and the host ns from post to flag.  Copies
+ * min(cap, n) values into out; returns n (-1 on error). */
 int64_t shred_index_trace(Trainer* trainer, uint32_t* out, size_t cap);
 
 typedef struct ShredStats {

@@ -3252,6 +3252,8 @@ void Device::flush_timing(bool block) {
   ev_pending_.resize(keep);
 }
 
+bool Device::index_id_room(int32_t max_id) const { return wl_ && (uint32_t)max_id + 2 <= wl_->id_room(); }
+
 void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {
   HIP_OK(hipSetDevice(ordinal_));
   if (n < 1 || n > kChainMax) fatal("merge_chain: bad chain length");

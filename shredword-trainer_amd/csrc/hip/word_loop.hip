@@ -341,6 +341,7 @@ struct LoopS {
   u64 lk[2];  // word list: pool offset, count
   u64 need;   // filter bits the listed words must hold
   u64 occ, t[2];
+  u64 t_wait, t_idle, t_undo;  // s_memrealtime: this command's wait began; idle / undo since the last flag
 };
 
 }  // namespace
@@ -354,7 +355,11 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t tid = threadIdx.x;
   int32_t* const mys = s_strip + tid;
-  if (tid == 0) S.pool_top = ld_agent(&p.dstate[kStPoolTop]);
+  if (tid == 0) {
+    S.pool_top = ld_agent(&p.dstate[kStPoolTop]);
+    S.t_idle = 0;
+    S.t_undo = 0;
+  }
   uint32_t expect = p.seq0;
   uint32_t exit_op = kOpStop;
   const MergeCtx mc{&S.nspill};
@@ -363,9 +368,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     // ---- wave 0 waits for the next command (one round trip reads all four granules)
     if (wid == 0) {
       const u64* g = p.ring[expect % kRing].g;
+      const u64 t_wait = __builtin_amdgcn_s_memrealtime();
       uint32_t op = 0, a = 0, b = 0, X = 0, idle = 0;
+      u64 v = lane < 4 ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
       for (;;) {
-        const u64 v = lane < 4 ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
         const bool tagged = lane >= 4 || (uint32_t)v == expect;
         if (__all(tagged)) {
           const uint32_t val = (uint32_t)(v >> 32);
@@ -380,6 +386,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           break;
         }
         __builtin_amdgcn_s_sleep(1);
+        v = lane < 4 ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
       }
       if (lane == 0) {
         S.cmd[0] = op & 0xFFu;
@@ -388,6 +395,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.cmd[3] = X;
         S.cmd[4] = (op >> 8) & 0xFFu;  // slot
         S.cmd[5] = expect;
+        S.t_wait = t_wait;
       }
     }
     __syncthreads();
@@ -502,6 +510,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         if (off + cnt == (u64)S.pool_top) S.pool_top = (uint32_t)off;  // the guess's list was the last one
         p.lseq[X] = kNoList;
       }
+      if (tid == 0) {
+        S.t_idle += t_cmd - S.t_wait;
+        S.t_undo += __builtin_amdgcn_s_memrealtime() - t_cmd;
+      }
       __syncthreads();
       continue;
     }
@@ -607,16 +619,16 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.pool_top = top + nchg;
       }
     }
-    for (int i = tid; i < kDh; i += kWlThreads) {
-      const uint32_t key = s_h.key[i];
-      if (key == kEmpty32) continue;
-      const uint32_t r = atomicAdd(&S.nout, 1u);
-      u64* dst = reinterpret_cast<u64*>(sd.recs + r);
-      dst[0] = (u64)key;
-      dst[1] = s_h.sum[i];
-      dst[2] = s_h.ft[i];
-    }
     {
+      for (int i = tid; i < kDh; i += kWlThreads) {
+        const uint32_t key = s_h.key[i];
+        if (key == kEmpty32) continue;
+        const uint32_t r = atomicAdd(&S.nout, 1u);
+        u64* dst = reinterpret_cast<u64*>(sd.recs + r);
+        dst[0] = (u64)key;
+        dst[1] = s_h.sum[i];
+        dst[2] = s_h.ft[i];
+      }
       const uint32_t nsp = S.nspill;  // complete: every delta was added before the barrier above
       for (uint32_t i = tid; i < nsp; i += kWlThreads) {
         const uint32_t key = p.dlist[i];
@@ -628,8 +640,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         dst[1] = sum;
         dst[2] = ft;
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
       sd.hdr[0] = S.nout;
@@ -645,6 +657,11 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       sd.hdr[16] = S.st[0];
       sd.hdr[17] = S.st[1];
       sd.hdr[18] = S.st[2];
+      // device time outside merges since the previous flag: waiting for commands, undoing guesses
+      sd.hdr[20] = (uint32_t)(S.t_idle + (t_cmd - S.t_wait));
+      sd.hdr[21] = (uint32_t)S.t_undo;
+      S.t_idle = 0;
+      S.t_undo = 0;
       __threadfence_system();
       __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -1224,7 +1241,8 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   if (timing_) {
     const uint32_t rec[kTraceFields] = {(uint32_t)X, h[2], h[12], h[3], (uint32_t)h64[2], (uint32_t)(10 * h64[3]),
                                         (uint32_t)(10 * h64[4]), (uint32_t)(10 * (h64[5] - h64[4])),
-                                        10 * h[16], 10 * h[17], 10 * h[18], 0u};
+                                        10 * h[16], 10 * h[17], 10 * h[18], 0u, 10 * h[20], 10 * h[21],
+                                        (uint32_t)(1e9 * (now_seconds() - pp.t_post))};
     trace_.insert(trace_.end(), rec, rec + kTraceFields);
   }
   if (n > sl.rec_cap) fatal("k_word_loop: record overflow");

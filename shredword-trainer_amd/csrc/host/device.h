@@ -93,9 +93,12 @@ class Device : public Backend {
   int max_chain() const override {
     return speculate_ && !resident_eligible() && !index_eligible() ? kChainMax : 1;
   }
+  bool index_id_room(int32_t max_id) const;
   bool can_overlap() const override {
     if (switch_pending_) return false;  // drain the resident loop: the indexed loop takes over
-    if (index_eligible()) return speculate_;
+    // the indexed loop's delta slots grow only with nothing in flight: no guess runs past them
+    // (the next merge is then posted alone, and reserves room first)
+    if (index_eligible()) return speculate_ && index_id_room(max_id_seen_ + 1 + spec_depth_);
     return speculate_ && (!resident_eligible() || (uint32_t)max_id_seen_ + 3 < min_slot_cap());
   }
   // k_resident takes up to kResSlots merges in flight (the current one and the guesses behind

@@ -187,6 +187,7 @@ int Engine::train(Backend& be) {
   if (log_ >= 1) std::printf("[INFO]\t Starting BPE training (target vocab size: %zu)\n", target_vocab_);
   sel_.reset(unk_, min_freq_);  // bpe_init (bpe.cpp:98-108)
   mtrace_on_ = std::getenv("SHREDWORD_ENGINE_TRACE") != nullptr;
+  if (const char* e = std::getenv("SHREDWORD_SIM_SELECT")) sel_.set_simulate_pops(std::atoi(e) != 0);
   mtrace_.clear();
   count_bigrams(be);
   times_.init_s += now_seconds() - t0;

@@ -28,6 +28,7 @@ void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
   const size_t want = std::max<size_t>(size_t(1) << 20, table_.size());
   table_.assign(want, Info{kEmptyKey, 0});
   seq_.assign(table_.size(), 0);
+  seq_live_ = true;
   mask_ = table_.size() - 1;
   count_ = 0;
   heap_.assign(1, HeapNode{0, 0, 0});
@@ -35,9 +36,9 @@ void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
 
 void Selector::grow() {
   HugeVec<Info> old(table_.size() * 4, Info{kEmptyKey, 0});
-  HugeVec<uint32_t> old_seq(old.size(), 0);
+  HugeVec<uint32_t> old_seq(seq_live_ ? old.size() : 0, 0);
   old.swap(table_);
-  old_seq.swap(seq_);
+  if (seq_live_) old_seq.swap(seq_);
   mask_ = table_.size() - 1;
   for (size_t i = 0; i < old.size(); ++i) {
     const Info& in = old[i];
@@ -45,7 +46,7 @@ void Selector::grow() {
     uint64_t j = mix64(in.key) & mask_;
     while (table_[j].key != kEmptyKey) j = (j + 1) & mask_;
     table_[j] = in;
-    seq_[j] = old_seq[i];
+    if (seq_live_) seq_[j] = old_seq[i];
   }
 }
 
@@ -66,7 +67,8 @@ Selector::Info& Selector::get(int32_t a, int32_t b) {
     while (table_[j].key != kEmptyKey) j = (j + 1) & mask_;
   }
   table_[j] = Info{key, 0};
-  seq_[j] = (uint32_t)count_++;
+  if (seq_live_) seq_[j] = (uint32_t)count_;
+  ++count_;
   return table_[j];
 }
 
@@ -113,19 +115,34 @@ Selector::HeapEnt Selector::pop() {
   if (n == 0) return top;
   const uint64_t xf = node_freq(x);
   size_t i = 0;
-  for (;;) {  // left child if strictly greater, then right if strictly greater (heap.cpp:101-106)
-    size_t l = 2 * i + 1, r = l + 1, best = i;
+  // The reference's sift-down (heap.cpp:101-106): left child if strictly greater than x, then
+  // right if strictly greater than that.  With both children present this is "the larger
+  // child, left on a tie, while it is strictly greater than x", so the child is chosen without
+  // a branch (the choice is a coin flip to the predictor); only the stop test branches, and it
+  // almost always goes the same way.
+  while (2 * i + 2 < n) {
+    const size_t l = 2 * i + 1;
     if (4 * i + 3 < n) __builtin_prefetch(h + 4 * i + 4);  // the four grandchildren: one line
     if (8 * i + 7 < n) {                                  // their eight children: two lines
       __builtin_prefetch(h + 8 * i + 8);
       __builtin_prefetch(h + 8 * i + 12);
     }
-    uint64_t bf = xf;
-    if (l < n && node_freq(h[l + 1]) > bf) { best = l; bf = node_freq(h[l + 1]); }
-    if (r < n && node_freq(h[r + 1]) > bf) best = r;
-    if (best == i) break;
-    h[i + 1] = h[best + 1];
-    i = best;
+    if (16 * i + 15 < n) {  // and their sixteen: four lines
+      __builtin_prefetch(h + 16 * i + 16);
+      __builtin_prefetch(h + 16 * i + 20);
+      __builtin_prefetch(h + 16 * i + 24);
+      __builtin_prefetch(h + 16 * i + 28);
+    }
+    const uint64_t lf = node_freq(h[l + 1]), rf = node_freq(h[l + 2]);
+    const bool right = rf > lf;
+    const size_t c = l + right;
+    if ((right ? rf : lf) <= xf) break;
+    h[i + 1] = h[c + 1];
+    i = c;
+  }
+  if (2 * i + 2 == n && node_freq(h[2 * i + 2]) > xf) {  // a lone left child (the last slot)
+    h[i + 1] = h[2 * i + 2];
+    i = 2 * i + 1;
   }
   h[i + 1] = x;
   return top;
@@ -154,6 +171,9 @@ void Selector::add_counts(std::vector<PairCount> pairs) {
     const Info& in = table_[o.second];
     push(pair_first(in.key), pair_second(in.key), in.freq(), in.version());
   }
+  // Creation order is read only by this heap build: the merge loop's new pairs skip the store
+  // (one random line of a 64 MB array per new pair at C3).
+  seq_live_ = false;
 }
 
 bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, int32_t* pb) const {
@@ -195,7 +215,86 @@ bool Selector::predict_avoid(const int32_t* used, size_t n_used, size_t window, 
   if (best == SIZE_MAX) return false;
   *pa = h[best].a;
   *pb = h[best].b;
+  if (simulate_pops_) simulate_select(used, n_used, best_f, pa, pb);
   return true;
+}
+
+bool Selector::simulate_select(const int32_t* used, size_t n_used, uint64_t floor, int32_t* pa, int32_t* pb) const {
+  // Among entries of one frequency the exact pop order decides, and a slot-order guess misses
+  // it (late merges are mostly ties).  So the coming select() is replayed on a copy-on-write
+  // overlay of the heap as it stands, with tokens in `used` counted as stale (the merge in
+  // flight changes their pairs).  Only entries >= floor (a valid entry exists there) can come
+  // out first, and they move exactly as in the real heap while every element sifted down from
+  // the end is below floor: a child >= floor always beats it, and which entries < floor sit
+  // where never decides between entries >= floor.  So a sift stops where both children are
+  // below floor.  Any other case (an end element >= floor, the overlay full, too many pops)
+  // keeps the caller's guess.
+  ++ov_gen_;
+  if (ov_gen_ == 0) {  // generation wrap: clear the stamps
+    std::fill(ov_stamp_.begin(), ov_stamp_.end(), 0u);
+    ov_gen_ = 1;
+  }
+  constexpr size_t kCap = 1024, kMask = kCap - 1;
+  if (ov_stamp_.size() != kCap) {
+    ov_stamp_.assign(kCap, 0u);
+    ov_pos_.assign(kCap, 0);
+    ov_node_.assign(kCap, HeapNode{0, 0, 0});
+  }
+  size_t used_slots = 0;
+  const HeapNode* h = heap_.data() + 1;  // logical slots
+  auto slot_of = [&](size_t pos) -> size_t {
+    size_t j = (pos * 0x9E3779B97F4A7C15ull >> 40) & kMask;
+    while (ov_stamp_[j] == ov_gen_ && ov_pos_[j] != pos) j = (j + 1) & kMask;
+    return j;
+  };
+  auto rd = [&](size_t pos) -> const HeapNode& {
+    const size_t j = slot_of(pos);
+    return ov_stamp_[j] == ov_gen_ ? ov_node_[j] : h[pos];
+  };
+  auto wr = [&](size_t pos, const HeapNode& v) -> bool {
+    const size_t j = slot_of(pos);
+    if (ov_stamp_[j] != ov_gen_) {
+      if (++used_slots > kCap / 2) return false;
+      ov_stamp_[j] = ov_gen_;
+      ov_pos_[j] = pos;
+    }
+    ov_node_[j] = v;
+    return true;
+  };
+  size_t n = heap_size();
+  for (int k = 0; k < 256 && n > 0; ++k) {
+    const HeapNode top = rd(0);
+    const uint64_t f = node_freq(top);
+    if (f < floor) return false;
+    bool skip = top.a == unk_ || top.b == unk_;
+    for (size_t u = 0; u < n_used && !skip; ++u) skip = top.a == used[u] || top.b == used[u];
+    if (!skip) {
+      const Info* in = find(pack_pair(top.a, top.b));
+      if (in && in->version() == node_version(top) && in->freq() == f) {
+        *pa = top.a;
+        *pb = top.b;
+        return true;
+      }
+    }
+    const HeapNode x = rd(n - 1);  // pop: the last element sifts down from the root
+    --n;
+    if (n == 0) return false;
+    if (node_freq(x) >= floor) return false;
+    size_t i = 0;
+    for (;;) {
+      const size_t l = 2 * i + 1;
+      if (l >= n) break;
+      const uint64_t lf = node_freq(rd(l));
+      const uint64_t rf = l + 1 < n ? node_freq(rd(l + 1)) : 0;
+      const bool right = l + 1 < n && rf > lf;
+      if ((right ? rf : lf) < floor) break;
+      const size_t c = l + right;
+      if (!wr(i, rd(c))) return false;
+      i = c;
+    }
+    if (!wr(i, x)) return false;
+  }
+  return false;
 }
 
 size_t Selector::predict_chain(int32_t a, int32_t b, size_t window, size_t k, int32_t* out) const {
@@ -283,6 +382,8 @@ void Selector::apply_combine(int32_t a, int32_t b, int32_t X, const DeltaRecord*
     for (;;) {
       uint32_t s = change_index_[j];
       if (!s) {
+        // the pair's info line, requested now: the combine and the ordering hide its miss
+        __builtin_prefetch(&table_[mix64(pack_pair((int32_t)(hk >> 32), (int32_t)hk)) & mask_]);
         changes_.push_back({hk, d, recs[i].ft});
         change_index_[j] = (uint32_t)changes_.size();
         break;
@@ -341,21 +442,25 @@ void Selector::apply_finish(int32_t a, int32_t b, int32_t X) {
     for (int k = 0; k < 32; ++k) cnt[k + 1] += cnt[k];
     for (const Change& c : staged_) ordered_[cnt[(c.hk >> 5) & 31u]++] = c;
   }
-  for (size_t i = 1; i < nc; ++i) {
-    const Change c = ordered_[i];
-    const uint64_t bk = c.hk % kDeltaBuckets;
-    size_t j = i;
-    while (j > 0 && ordered_[j - 1].hk % kDeltaBuckets == bk && ordered_[j - 1].ft < c.ft) {
-      ordered_[j] = ordered_[j - 1];
-      --j;
-    }
-    ordered_[j] = c;
+  // Inside a bucket, first touch descending (unique per change, so any sort gives the same
+  // order).  Buckets are not small: every (p, a) change lands in a's bucket and every (p, X)
+  // change in X's (the bucket is the second id's low bits), so each holds about a quarter of
+  // the merge's changes -- sorted, not insertion-sorted.
+  for (size_t i = 0; i < nc;) {
+    const uint64_t bk = ordered_[i].hk % kDeltaBuckets;
+    size_t e = i + 1;
+    while (e < nc && ordered_[e].hk % kDeltaBuckets == bk) ++e;
+    if (e - i > 1) std::sort(ordered_.begin() + i, ordered_.begin() + e, [](const Change& x, const Change& y) { return x.ft > y.ft; });
+    i = e;
   }
   const uint64_t c2 = __builtin_ia32_rdtsc();
   ctr_.cyc_order += c2 - c1;
-  // the table lines this merge touches, requested before the ordered walk needs them
+  // (the table lines this merge touches were requested by apply_combine)
   if (2 * (count_ + ordered_.size() + 1) > table_.size()) grow();
-  for (const Change& c : ordered_) __builtin_prefetch(&table_[mix64(pack_pair((int32_t)(c.hk >> 32), (int32_t)c.hk)) & mask_]);
+  // The pair-info updates first, then the heap pushes in the same order: the pushes read nothing
+  // the updates write, so this is the reference's interleaved loop exactly, and the info lines'
+  // misses overlap each other instead of waiting behind sift-ups.
+  pushes_.clear();
   for (const Change& c : ordered_) {
     const int32_t f = (int32_t)(uint32_t)(c.hk >> 32), s = (int32_t)(uint32_t)c.hk;
     if (f == a && s == b) continue;
@@ -368,13 +473,16 @@ void Selector::apply_finish(int32_t a, int32_t b, int32_t X) {
     }
     if (in.freq() >= min_freq_) {
       in.bump_version();
-      push(f, s, in.freq(), in.version());
+      pushes_.push_back(HeapNode{in.fv, f, s});
     }
   }
   Info& merged = get(a, b);
   merged.set_freq(0);
   merged.bump_version();
-  ctr_.cyc_walk += __builtin_ia32_rdtsc() - c2;
+  const uint64_t c3 = __builtin_ia32_rdtsc();
+  ctr_.cyc_walk += c3 - c2;
+  for (const HeapNode& p : pushes_) push(p.a, p.b, node_freq(p), node_version(p));
+  ctr_.cyc_push += __builtin_ia32_rdtsc() - c3;
 }
 
 }  // namespace shred

@@ -122,6 +122,10 @@ class Selector {
   // share no token with (a, b) or with each other, by frequency.  out: k (a, b) pairs.
   size_t predict_chain(int32_t a, int32_t b, size_t window, size_t k, int32_t* out) const;
 
+  // predict_avoid refines its guess by replaying the coming select() on an overlay of the heap
+  // (simulate_select); off: the slot-order guess alone.
+  void set_simulate_pops(bool on) { simulate_pops_ = on; }
+
   size_t heap_size() const { return heap_.empty() ? 0 : heap_.size() - 1; }
   bool heap_empty() const { return heap_.size() <= 1; }
   uint64_t heap_top_freq() const { return heap_empty() ? 0 : node_freq(heap_[1]); }
@@ -131,7 +135,7 @@ class Selector {
   int32_t unk_id() const { return unk_; }
   struct Counters {
     uint64_t pops = 0, stale = 0, pushes = 0, records = 0, changes = 0;
-    uint64_t cyc_combine = 0, cyc_order = 0, cyc_walk = 0;  // TSC cycles inside apply()
+    uint64_t cyc_combine = 0, cyc_order = 0, cyc_walk = 0, cyc_push = 0;  // TSC cycles inside apply()
   };
   const Counters& counters() const { return ctr_; }
 
@@ -174,6 +178,7 @@ class Selector {
   uint64_t min_freq_ = 2000;
   HugeVec<Info> table_;
   HugeVec<uint32_t> seq_;  // creation order of table_[j] (bimap_get order), for the heap build
+  bool seq_live_ = true;   // seq_ is kept until the heap build has read it
   size_t count_ = 0;
   uint64_t mask_ = 0;
   // The reference's binary heap (heap.cpp), logical slot k stored at heap_[k + 1]: with 16-byte
@@ -185,6 +190,14 @@ class Selector {
   std::vector<uint32_t> change_index_;
   std::vector<Change> staged_;  // apply: the first counting pass
   std::vector<Change> ordered_;
+  std::vector<HeapNode> pushes_;  // apply: the pushes of one merge, in order
+  bool simulate_select(const int32_t* used, size_t n_used, uint64_t floor, int32_t* pa, int32_t* pb) const;
+  bool simulate_pops_ = true;
+  // simulate_select's overlay: heap slot -> node, valid where the stamp equals the generation
+  mutable std::vector<uint32_t> ov_stamp_;
+  mutable std::vector<size_t> ov_pos_;
+  mutable std::vector<HeapNode> ov_node_;
+  mutable uint32_t ov_gen_ = 0;
   Counters ctr_;
 };
 

@@ -95,6 +95,7 @@ class WordLoop {
   // Undoes every posted merge with id >= X, newest first (queued; nothing waits).
   void rollback(int32_t X);
   size_t in_flight() const { return posted_.size(); }
+  uint32_t id_room() const { return cap_; }  // merges may post ids X with X + 2 <= id_room()
   // Ends the persistent launch (nothing may be in flight).
   void stop();
   bool running() const { return running_; }
@@ -118,8 +119,10 @@ class WordLoop {
   // Per collected merge while timing is on, kTraceFields u32 each: X, listed words, scanned
   // words, changed words, occurrences, device ns command -> flag, of which lookup ns, scan ns;
   // then thread 0's stamps (ns after the command): pool entries loaded, first run loaded, first
-  // word merged; and ns spent building pair groups this merge needed first.
-  static constexpr int kTraceFields = 12;
+  // word merged; and ns spent building pair groups this merge needed first; then the device ns
+  // outside merges since the previous merge's flag (waiting for commands; undoing guesses), and
+  // the host ns from posting this merge to seeing its flag.
+  static constexpr int kTraceFields = 15;
   const std::vector<uint32_t>& trace() const { return trace_; }
   void set_timing(bool on) { timing_ = on; }
   size_t device_bytes() const { return bytes_; }

@@ -68,17 +68,18 @@ class BPETrainer:
 
     def index_trace(self):
         """Per-merge trace of the indexed merge loop (diagnostic, recorded while the 'timing'
-        option is on): numpy uint32 array (merges, 12) of X, listed words, scanned words, changed
-        words, occurrences, device ns command -> flag, lookup ns, scan ns, and wave 0's stamps
-        (ns after the command: pool entries loaded, first run loaded, first word merged, scan
-        loop left)."""
+        option is on): numpy uint32 array (merges, 15) of X, listed words, scanned words, changed
+        words, occurrences, device ns command -> flag, lookup ns, scan ns, wave 0's stamps
+        (ns after the command: pool entries loaded, first run loaded, first word merged, unused),
+        device ns since the previous flag spent waiting for commands and undoing guesses, and
+        host ns from post to flag."""
         import numpy as np
         n = lib.shred_index_trace(self.trainer, None, 0)
         if n < 0:
             raise RuntimeError("no device")
         out = np.empty(n, dtype=np.uint32)
         lib.shred_index_trace(self.trainer, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n)
-        return out.reshape(-1, 12)
+        return out.reshape(-1, 15)
 
     def stats(self) -> dict:
         s = ShredStats()

@@ -43,7 +43,7 @@ def main():
     t.destroy()
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     np.save(args.out, tr)
-    X, listed, scanned, changed, occ, dev, look, scan, s0, s1, s2, s3 = tr.T
+    X, listed, scanned, changed, occ, dev, look, scan, s0, s1, s2, s3, idle, undo, hflag = tr.T
     rows = []
     edges = [0, 16, 64, 256, 1024, 4096, 16384, len(tr)]
     for lo, hi in zip(edges[:-1], edges[1:]):
@@ -55,7 +55,9 @@ def main():
                      "scan_us_mean": float(scan[s].mean() / 1e3), "listed_mean": float(listed[s].mean()),
                      "scanned_mean": float(scanned[s].mean()), "changed_mean": float(changed[s].mean()),
                      "occ_mean": float(occ[s].mean()),
-                     "stamps_us_mean": [float(v[s].mean() / 1e3) for v in (s0, s1, s2, s3)]})
+                     "stamps_us_mean": [float(v[s].mean() / 1e3) for v in (s0, s1, s2, s3)],
+                     "dev_idle_us_mean": float(idle[s].mean() / 1e3), "dev_undo_us_mean": float(undo[s].mean() / 1e3),
+                     "host_post_to_flag_us_mean": float(hflag[s].mean() / 1e3)})
     print(json.dumps({"config": args.config, "merges": int(n), "train_s": st["train_seconds"],
                       "merges_per_s": n / st["train_seconds"], "dev_s_total": float(dev.sum() / 1e9),
                       "host": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},

@@ -71,7 +71,15 @@ class EmuBackend : public Backend {
     if (cb_) cb_(ctx_, cnt.data(), ft.data(), D);
     for (size_t k = 0; k < D; ++k)
       if (ft[k] != ~0ull) out->push_back({(int32_t)(k / 257), (int32_t)(k % 257), cnt[k], ft[k]});
+    if (const char* rp = std::getenv("HH_RECORD")) {  // selector replay input (tests/native/selector_replay.cpp)
+      rec_ = std::fopen(rp, "wb");
+      if (!rec_) fatal("HH_RECORD: cannot open the file");
+      const uint64_t n = out->size();
+      std::fwrite(&n, 8, 1, rec_);
+      std::fwrite(out->data(), sizeof(PairCount), n, rec_);
+    }
   }
+  FILE* rec_ = nullptr;
 
   void emit(uint32_t key, uint64_t w, uint64_t ft) {
     if (raw_) {  // direct mode: unreduced records, duplicates combined by the host
@@ -205,6 +213,12 @@ class EmuBackend : public Backend {
       if (nb) std::memcpy(pd.recs.data(), all, nb);
     }
     index_.set_tiles(X, pd.matched.data(), pd.matched.size());
+    if (rec_) {
+      const int32_t hdr[4] = {pd.a, pd.b, X, (int32_t)pd.recs.size()};
+      std::fwrite(hdr, 4, 4, rec_);
+      std::fwrite(pd.recs.data(), sizeof(DeltaRecord), pd.recs.size(), rec_);
+      std::fflush(rec_);
+    }
     recs_ = std::move(pd.recs);
     *recs = recs_.data();
     return recs_.size();
