@@ -215,6 +215,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   if (const char* v = std::getenv("SHREDWORD_CHAIN")) set_option(t, "chain", v);
   t->engine.set_verify(env_int("SHREDWORD_VERIFY_ARGMAX", 0));
   if (const char* v = std::getenv("SHREDWORD_DIST")) set_option(t, "dist", v);
+  if (const char* v = std::getenv("SHREDWORD_RESIDENT")) set_option(t, "resident", v);
   if (t->engine.log() >= 1) std::printf("[INFO]\t BPE trainer initialized. Heap initialized successfully.\n");
   return t;
 }
