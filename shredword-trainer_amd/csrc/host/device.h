@@ -341,7 +341,7 @@ class Device : public Backend {
   bool hybrid_ = true;             // option (SHREDWORD_HYBRID / set_option hybrid)
   bool idx_phase_ = false;         // hybrid: the indexed loop has taken over this train()
   bool switch_pending_ = false;    // hybrid: a resident merge changed < switch_occ_ occurrences
-  uint64_t switch_occ_ = 400;      // option (SHREDWORD_SWITCH_OCC / set_option switch_occ)
+  uint64_t switch_occ_ = 4000;     // option (SHREDWORD_SWITCH_OCC / set_option switch_occ)
   static constexpr int kSwitchWindow = 64;
   uint64_t sw_win_[kSwitchWindow] = {};  // entries merged by the last resident merges
   uint64_t sw_n_ = 0;
