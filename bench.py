@@ -18,14 +18,24 @@ Legs beside the timed steps (all on the same corpus):
 * ``merge_loop``: the dominant kernel of the timed step (the persistent merge loop), which is
   bound by the per-merge round trip, not by bandwidth: µs per merge, device dispatch -> flag.
 * ``cpu_baseline``: oracle/bpe_oracle (the reference-faithful CPU restatement) on one host core,
-  run concurrently with the GPU legs on another core, train() capped at --cpu-seconds and
-  extrapolated to the full run along the measured cost curve committed in
-  tests/golden/fullsize/<config>/case.json.
+  started AFTER the timed region (the host replay is most of the merge chain, so the baseline
+  must not share the host while it runs), train() capped at --cpu-seconds.  ``value`` is the
+  measured merges/s of that capped prefix; the full-run estimate along the cost curve committed
+  in tests/golden/fullsize/<config>/case.json is reported beside it (``extrapolated_value``).
 
-N > 1 runs under torch.distributed.run, one process per GPU.  Each rank trains its own replica
-of the word table (the merge loop is a serial chain of dependent merges: "replicas only", see
-DESIGN.md §5), so ``value`` = merges per step x ranks / max-over-ranks time and ``scaling`` is
-"weak"; the K1 leg counts every rank's shard of the stream and reports aggregate GB/s.
+N GPUs: ``--gpus N`` with N > 1 launches N ranks itself (torch.distributed.run, one process per
+GPU, rank r on device r) unless WORLD_SIZE is already set (the driver's own torchrun).
+``--dist`` picks what the ranks do:
+* ``replicas`` (default): every rank trains its own replica of the workload.  The merge loop is a
+  serial chain of dependent merges (merge m+1's selection needs merge m's exact frequency
+  changes), so one training does not split across GPUs; N GPUs run N trainings.
+  ``value`` = merges of all ranks / max-over-ranks time, ``scaling`` "weak".
+* ``replicate``: ONE training: the load is sharded (rank r counts byte range r of the corpus on
+  its GPU, the word lists are all-gathered over RCCL and merged) and the merge loop runs on every
+  rank; ``value`` = merges of the one training / max-over-ranks time, ``scaling`` "strong".
+* ``exchange``: ONE training over word-range shards with one RCCL all-gather of the merge's
+  records per merge (stream layout); ``value`` as for replicate.
+The K1 leg counts every rank's copy (replicas) or shard of the stream and reports aggregate GB/s.
 Rank 0 prints one JSON line.
 """
 import argparse
@@ -136,9 +146,9 @@ def pin_host_loop(local_rank):
 
 def cpu_baseline_start(cfg, path, seconds):
     """Starts the CPU port (oracle/bpe_oracle.c: the reference-faithful merge loop, SURVEY.md §8
-    d5) on ONE host core — the last core of this process's affinity set, away from the core
-    the GPU host loop runs on — with train() capped at `seconds`.  It runs while the GPU legs
-    run; cpu_baseline_finish() collects it."""
+    d5) on ONE host core — the last core of this process's affinity set — with train() capped at
+    `seconds`.  main() starts it after the timed region (it overlaps only the untimed legs);
+    cpu_baseline_finish() collects it."""
     exe = os.path.join(REPO, "oracle", "_build", "bpe_oracle")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "port"], check=True)
@@ -192,7 +202,8 @@ def cpu_baseline_finish(h, cfg_name, target_merges, gpu_merges, timeout=600):
         "sample": (f"train() of the same corpus/config capped at {h['seconds']:.0f} s: {merges} of "
                    f"{target_merges} merges in {train_s:.1f} s (load {load_s:.1f} s excluded); "
                    f"oracle/bpe_oracle.c pinned to core {h['core']} of {cpu_model()} (nproc={os.cpu_count()}), "
-                   f"run concurrently with the GPU legs"),
+                   f"started after the timed GPU steps (it overlaps only the untimed K1/encode/HBM legs); "
+                   f"value = merges/s of this measured prefix"),
         "capped_merges": merges, "capped_train_s": train_s, "load_s": load_s,
         "calibration": calibration_note(),
     }
@@ -210,15 +221,14 @@ def cpu_baseline_finish(h, cfg_name, target_merges, gpu_merges, timeout=600):
         if at and at > 0:
             est = train_s * full_s / at
             res.update({
-                "value": full_m / est, "extrapolated": True,
-                "extrapolated_train_s": est,
-                "sample": res["sample"] + (f"; extrapolated to all {full_m} merges along the measured cost curve of the "
-                                           f"full run (tests/golden/fullsize/{cfg_name}/case.json: {full_s:.0f} s on "
-                                           f"{case['oracle'].get('cpu', 'the build container')}, x{train_s / at:.2f} "
-                                           f"on this host)"),
+                "extrapolated_value": full_m / est, "extrapolated_train_s": est,
+                "extrapolation": (f"the full train() estimated along the measured cost curve of the full run "
+                                  f"(tests/golden/fullsize/{cfg_name}/case.json: {full_s:.0f} s for {full_m} merges on "
+                                  f"{case['oracle'].get('cpu', 'the build container')}, a different machine), scaled "
+                                  f"by this host's time on the measured prefix (x{train_s / at:.2f}); the per-merge "
+                                  f"cost falls as the word table shrinks, so the prefix rate understates the full run"),
             })
     elif merges < target_merges:
-        res["extrapolated"] = False
         res["note"] = "capped run, no committed full-run curve for this config: value = merges/s of the capped prefix"
     if gpu_merges:
         res["gpu_merges_per_step"] = gpu_merges
@@ -277,6 +287,19 @@ PMC_NOTE = ("HBM bytes per k_merge launch from rocprofv3 --pmc FETCH_SIZE / WRIT
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def pmc_source(cfg_name, layout, kernel):
+    """The committed PMC summary pmc_traffic() reads for this kernel (newest round first)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", f"*_{cfg_name}_{layout}*_pmc_traffic.json")), reverse=True):
+        try:
+            if kernel in json.load(open(path))["kernels"]:
+                return ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (FETCH doubled for gfx950 16-B reads): "
+                        + os.path.relpath(path, HERE))
+        except (OSError, ValueError, KeyError):
+            continue
+    return None
+
+
 def pmc_traffic(cfg_name, layout, kernel=None):
     """Measured HBM bytes per launch of `kernel` (default k_merge) for this workload, from the
     committed PMC summaries (profiles/*_<config>_<layout>*_pmc_traffic.json)."""
@@ -294,7 +317,7 @@ def pmc_traffic(cfg_name, layout, kernel=None):
     return None
 
 
-def pair_count_leg(cfg, path, reps, device=0, layout="stream", dist=None):
+def pair_count_leg(cfg, path, reps, device=0, layout="stream", dist=None, shard=False):
     """K1 at HBM scale: the same corpus in the stream layout (every occurrence as int32 tokens,
     the north-star data layout), `reps` x (reset + bpe_init).  k_pair_hist counts the bulk of the
     stream (every occurrence past each type's first) and is timed alone with HIP events on the
@@ -336,14 +359,15 @@ def pair_count_leg(cfg, path, reps, device=0, layout="stream", dist=None):
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS if achieved else None,
         "traffic": pmc_traffic(cfg.get("name", "c2"), "stream", "k_pair_hist"),
-        "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/k1_bench.py, "
-                          "profiles/r01_<config>_stream_k1_pmc_traffic.json",
+        "traffic_source": pmc_source(cfg.get("name", "c2"), "stream", "k_pair_hist"),
         "avg_launch_us": us, "bytes_per_launch": b, "launches": st["hist_launches"],
         "k1_total_us": k1_us,
         "k1_total_GBps": (st["count_kernel_bytes"] / max(1, st["count_launches"])) / (k1_us * 1e-6) / 1e9 if k1_us > 0 else None,
         "stream_tokens": st["live_tokens"], "tiles": st["num_tiles"], "load_s": load_s,
         "ranks": 1 if dist is None else dist.get_world_size(),
-        "aggregate": "sum of per-rank bytes / slowest rank's avg launch" if dist is not None else None,
+        "aggregate": (("sum of per-rank bytes / slowest rank's avg launch; each rank counts "
+                       + ("its shard of the stream" if shard else "its own copy of the stream"))
+                      if dist is not None else None),
     }
 
 
@@ -398,6 +422,83 @@ def encode_leg(model, vocab, unk, path, reps, device=0, cfg_name="c3"):
                      f"traffic_bytes = PMC bytes of the word-cache kernels per call from the committed {cfg_name} profile")}
 
 
+def merge_loop_report(st, merges, elapsed, args):
+    """The timed step's merge loops with their own algorithmic bytes, each over
+    its own merges and its own launch time (HIP events around each persistent launch, the
+    durations rocprofv3 --kernel-trace reports for the same kernels):
+    * resident (k_resident, merges while they change many words): 4 B per live token per merge
+      (K2: the scan of the token table a merge stands for; LDS signatures let it skip tiles);
+    * index (k_word_loop, the rest): per merge 16 B per listed pool entry + 8 B weight per scanned
+      word + 4 B per run int read (length + tokens) and written back + 16 B per new pool entry
+      (changed word) + 24 B per delta record to host memory.
+    Both loops are bound by the per-merge round trip (host select/apply <-> device), not by HBM:
+    the fractions are reported to show that, not as targets."""
+    res_n, idx_n = st["resident_merges"], st["index_merges"]
+    out = {
+        "bound": "latency (serial merge chain: host heap replay <-> device merge per merge)",
+        "us_per_merge": 1e6 * elapsed / max(1, merges),
+        "host_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
+        "launches": st["merge_launches"],
+    }
+    if res_n:
+        ms = st["resident_kernel_ms"]
+        b = st["resident_bytes"]
+        gbps = b / (ms * 1e-3) / 1e9 if ms > 0 else None
+        out["resident"] = {
+            "kernel": "k_resident (persistent, whole chip: LDS signatures, wave-level match + deltas + compaction)",
+            "merges": res_n, "launches": st["resident_launches"], "kernel_ms": ms,
+            "us_per_merge": 1e3 * ms / res_n, "algorithmic_bytes": b, "algorithmic_bytes_per_merge": b / res_n,
+            "achieved_GBps": gbps, "frac_of_hbm_peak": gbps / HBM_PEAK_GBS if gbps else None,
+            "traffic_bytes_per_launch": (pmc_traffic(args.config, args.layout, "k_resident<true>")
+                                         or pmc_traffic(args.config, args.layout, "k_resident")),
+            "traffic_source": (pmc_source(args.config, args.layout, "k_resident<true>")
+                               or pmc_source(args.config, args.layout, "k_resident")),
+            "dispatch_to_flag_us": st.get("resident_latency_us"),
+        }
+    if idx_n:
+        ri, rw = st["index_run_ints_read"], st["index_run_ints_written"]
+        b = (16.0 * st["index_candidates"] + 8.0 * st["index_scanned"] + 4.0 * (ri + rw)
+             + 16.0 * st["index_changed"] + 24.0 * st["index_records"])
+        ms = st["index_ms"]
+        gbps = b / (ms * 1e-3) / 1e9 if ms > 0 else None
+        busy = st["index_dev_us"]
+        out["index"] = {
+            "kernel": "k_word_loop (indexed persistent loop, one workgroup: word lists, filter, register merge, "
+                      "neighbour deltas, in-place compaction)",
+            "merges": idx_n, "undos": st["index_undos"], "launches": st["index_launches"], "kernel_ms": ms,
+            "us_per_merge": 1e3 * ms / idx_n,
+            "algorithmic_bytes": b, "algorithmic_bytes_per_merge": b / idx_n,
+            "bytes_breakdown_per_merge": {
+                "pool_entries_listed": 16.0 * st["index_candidates"] / idx_n,
+                "weights": 8.0 * st["index_scanned"] / idx_n,
+                "runs_read": 4.0 * ri / idx_n, "runs_written": 4.0 * rw / idx_n,
+                "pool_entries_appended": 16.0 * st["index_changed"] / idx_n,
+                "records_to_host": 24.0 * st["index_records"] / idx_n},
+            "achieved_GBps": gbps, "frac_of_hbm_peak": gbps / HBM_PEAK_GBS if gbps else None,
+            "device_busy_us_per_merge": busy / idx_n,
+            "achieved_GBps_while_busy": b / (busy * 1e-6) / 1e9 if busy > 0 else None,
+            "words_listed_per_merge": st["index_candidates"] / idx_n,
+            "words_scanned_per_merge": st["index_scanned"] / idx_n,
+            "words_changed_per_merge": st["index_changed"] / idx_n,
+            "occurrences_per_merge": st["index_occurrences"] / idx_n,
+            "device_lookup_us_per_merge": st["index_dev_lookup_us"] / idx_n,
+            "device_scan_us_per_merge": st["index_dev_scan_us"] / idx_n,
+            "host_post_to_flag_us_per_merge": st["index_wait_us"] / idx_n,
+            "hybrid_switch_merge": st["index_switch_merge"],
+            "hybrid_switch_ms_total": st["index_switch_ms"],
+        }
+    if not res_n and not idx_n and st["merge_launches"]:
+        ms = st["merge_kernel_ms"]
+        b = st["merge_kernel_bytes"]
+        gbps = b / (ms * 1e-3) / 1e9 if ms > 0 else None
+        out["launch"] = {"kernel": "k_merge (one launch per merge)", "merges": st["merge_launches"],
+                         "kernel_ms": ms, "us_per_merge": 1e3 * ms / st["merge_launches"],
+                         "algorithmic_bytes_per_merge": b / st["merge_launches"], "achieved_GBps": gbps,
+                         "frac_of_hbm_peak": gbps / HBM_PEAK_GBS if gbps else None,
+                         "traffic_bytes_per_launch": pmc_traffic(args.config, args.layout)}
+    return out
+
+
 def hbm_probe_leg(device=0, nbytes=4 << 30, reps=10):
     """Achievable HBM bandwidth on this box: streaming read and copy kernels
     of the library (shred_hbm_probe), beside the nominal 8 TB/s peak."""
@@ -411,6 +512,26 @@ def hbm_probe_leg(device=0, nbytes=4 << 30, reps=10):
             "kernels": "k_hbm_read (4 x 16 B nontemporal loads per lane in flight), k_hbm_copy"}
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """--gpus N without a surrounding launcher: N ranks under torch.distributed.run (one process
+    per GPU, rank r on device r), started as a child before this process touches the GPU; the
+    exit code is the launcher's.  Rank 0's JSON line reaches stdout through the inherited pipe."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    log(f"bench: launching {n} ranks: {' '.join(cmd[1:7])} ...")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -418,6 +539,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--layout", default="types", choices=["types", "stream"])
+    ap.add_argument("--dist", default="replicas", choices=["replicas", "replicate", "exchange"],
+                    help="N > 1: independent trainings per rank (replicas), or one training with a sharded load "
+                         "(replicate) or a per-merge RCCL exchange (exchange); see the module docstring")
     ap.add_argument("--bytes", type=int, default=0, help="override the corpus size (testing)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -425,7 +549,12 @@ def main():
     ap.add_argument("--no-pin", action="store_true", help="do not keep the host loop on one L3 domain")
     ap.add_argument("--pair-count-reps", type=int, default=10,
                     help="K1 roofline leg on the stream layout of the same corpus (0: skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank bookkeeping only (no GPU, no corpus): rank 0 prints the ranks it saw")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     cfg = dict(CONFIGS[args.config], name=args.config)
     if args.bytes:
@@ -433,6 +562,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher's world size is used")
 
     import torch
     dist = None
@@ -440,6 +571,21 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    if args.dry_run:
+        seen = [None] * world
+        me = {"rank": rank, "local_rank": local, "world": world, "pid": os.getpid(),
+              "device": f"cuda:{local}"}
+        if dist is not None:
+            dist.all_gather_object(seen, me)
+        else:
+            seen = [me]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "dist": args.dist, "ranks": seen}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
     torch.cuda.set_device(local)
 
     def barrier():
@@ -449,26 +595,26 @@ def main():
     path = corpus_path(cfg, args.config)
     gen_s = ensure_corpus(cfg, path) if local == 0 else 0.0
     barrier()
-    cpu_h = None
-    if world == 1 and not args.no_cpu_baseline:
-        try:
-            cpu_h = cpu_baseline_start(cfg, path, args.cpu_seconds)
-        except Exception as e:  # the GPU number stands on its own
-            cpu_h = {"error": repr(e)}
 
     pinned = None if args.no_pin else pin_host_loop(local)
     from shredword import dist as sdist
+    from shredword.cbase import lib
     from shredword.trainer import BPETrainer
-    if world > 1:
+    one_job = world > 1 and args.dist != "replicas"  # the ranks train ONE model together
+    if one_job:
         sdist.init_from_env(device=local)
+    rccl_ranks = lib.shred_dist_ranks() if one_job else 0
 
     t = BPETrainer(vocab_size=cfg["vocab"], unk_id=cfg["unk"], character_coverage=cfg["cov"], min_pair_freq=cfg["mpf"])
     t.set_option("log", 0)
     t.set_option("device", local)
     t.set_option("layout", args.layout)
+    if one_job:
+        t.set_option("dist", args.dist)
     t0 = time.time()
     t.load_corpus(path)
     load_s = time.time() - t0
+
     def train_step():
         t.reset()
         n = t._train(t.trainer)  # the BPETrainer.train() ABI call, without its stdout line
@@ -490,21 +636,33 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - start
+    all_merges = merges
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        tm = torch.tensor([merges], dtype=torch.int64)
+        dist.all_reduce(tm, op=dist.ReduceOp.SUM)
+        all_merges = int(tm.item())
+    # the CPU baseline starts only now: the timed steps ran with the host to themselves
+    cpu_h = None
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu_h = cpu_baseline_start(cfg, path, args.cpu_seconds)
+        except Exception as e:  # the GPU number stands on its own
+            cpu_h = {"error": repr(e)}
     st = t.stats()
     tmpd = os.environ.get("TMPDIR", "/tmp")
     t._save(t.trainer, os.path.join(tmpd, f"bench_r{rank}.model").encode(),
             os.path.join(tmpd, f"bench_r{rank}.vocab").encode())
     t.destroy()
 
-    # K1 HBM leg (the metric's "pair-count HBM GB/s"): every rank counts its stream shard
+    # K1 HBM leg (the metric's "pair-count HBM GB/s"): every rank counts its stream copy / shard
     pair_count = None
     if args.pair_count_reps > 0:
         try:
-            pair_count = pair_count_leg(cfg, path, args.pair_count_reps, device=local, dist=dist)
+            pair_count = pair_count_leg(cfg, path, args.pair_count_reps, device=local, dist=dist,
+                                        shard=one_job)
         except Exception as e:
             pair_count = {"error": repr(e)}
 
@@ -517,61 +675,27 @@ def main():
             encode = {"error": repr(e)}
 
     if rank == 0:
-        res_traffic = (pmc_traffic(args.config, args.layout, "k_resident<true>")
-                       or pmc_traffic(args.config, args.layout, "k_resident"))
-        mk_ms = st["merge_kernel_ms"] / max(1, st["merge_launches"])
-        mk_bytes = st["merge_kernel_bytes"] / max(1, st["merge_launches"])
-        achieved = (mk_bytes / (mk_ms * 1e-3)) / 1e9 if mk_ms > 0 else None
-        k1_ms = st["count_kernel_ms"] / max(1, st["count_launches"])
-        k1_bytes = st["count_kernel_bytes"] / max(1, st["count_launches"])
         per_step_merges = merges / max(1, args.steps)
-        im = max(1, st["index_merges"])
-        merge_loop = {
-            "kernel": ("k_word_loop (indexed persistent merge loop, one workgroup: word lists, match, neighbour "
-                       "deltas, in-place compaction)" if st["index_merges"] else
-                       "k_resident (persistent merge loop, K2+K3: match, neighbour deltas, in-place compaction)"
-                       if st["resident_launches"] else "k_merge (per-merge launches, K2+K3)"),
-            "bound": "latency",
-            "us_per_merge": 1e6 * elapsed / max(1, merges),
-            "device_us_per_merge": 1e3 * mk_ms,
-            "dispatch_to_flag_us": st.get("resident_latency_us"),
-            "algorithmic_bytes_per_merge": mk_bytes,
-            "hbm_GBps_equiv": achieved, "frac_of_hbm_peak": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic_per_merge": (res_traffic / max(1.0, per_step_merges) if st["resident_launches"] and res_traffic
-                                  else None if st["resident_launches"] else pmc_traffic(args.config, args.layout)),
-            "note": ("a serial chain of dependent merges: each needs the previous one's exact heap replay on the "
-                     "host, so the bound is the per-merge round trip (host select/apply + device dispatch -> flag), "
-                     "not bandwidth; the HBM fraction is shown for completeness only"),
-            "launches": merges,
-        }
-        if st["index_merges"]:
-            merge_loop["index"] = {
-                "merges": st["index_merges"], "undos": st["index_undos"], "launches": st["index_launches"],
-                "words_listed_per_merge": st["index_candidates"] / im,
-                "words_scanned_per_merge": st["index_scanned"] / im,
-                "words_changed_per_merge": st["index_changed"] / im,
-                "occurrences_per_merge": st["index_occurrences"] / im,
-                "device_us_per_merge": st["index_dev_us"] / im,
-                "device_lookup_us_per_merge": st["index_dev_lookup_us"] / im,
-                "device_scan_us_per_merge": st["index_dev_scan_us"] / im,
-                "host_post_to_flag_us_per_merge": st["index_wait_us"] / im,
-                "device_build_us_per_merge": st["index_build_us"] / im,
-                "merges_without_pair_groups": st["index_no_sub"],
-                "group_entries_per_merge": st["index_staged"] / im,
-                "hybrid_switch_merge": st["index_switch_merge"],
-                "hybrid_switch_ms_total": st["index_switch_ms"],
-                "launch_ms_total": st["index_ms"],
-            }
+        value = (all_merges if not one_job else merges) / elapsed
+        if one_job:
+            parallelism = (f"dp{world} one training: sharded load (byte ranges, RCCL all-gather of word lists) + "
+                           f"merge loop replicated on every rank" if args.dist == "replicate" else
+                           f"dp{world} one training: word-range shards + one RCCL all-gather of records per merge")
+        elif world > 1:
+            parallelism = (f"replicas{world}: every rank trains its own replica of the workload (the merge chain is "
+                           f"serial, DESIGN.md §5); value = merges of all ranks / slowest rank's time")
+        else:
+            parallelism = "single GPU"
         result = {
             "metric": "BPE merges/sec",
-            "value": merges / elapsed,
+            "value": value,
             "unit": "merges/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if one_job else "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (committed deterministic generator, SURVEY.md §8 d2)",
@@ -580,20 +704,17 @@ def main():
                 "corpus_bytes": cfg["bytes"], "seed": cfg["seed"], "script": cfg["script"],
                 "vocab_size": cfg["vocab"], "min_pair_freq": cfg["mpf"], "character_coverage": cfg["cov"],
                 "unk_id": cfg["unk"], "layout": args.layout,
-                "parallelism": (f"dp{world}: sharded load (byte ranges) + merge loop replicated on every rank"
-                                if world > 1 else "single GPU"),
+                "parallelism": parallelism, "dist": args.dist if world > 1 else None, "rccl_ranks": rccl_ranks,
                 "merges_per_step": per_step_merges, "distinct_words": st["num_words"],
                 "symbols": st["num_symbols"], "occurrences": st["num_occurrences"], "tiles": st["num_tiles"],
             },
             "roofline": None,
-            "merge_loop": merge_loop,
+            "merge_loop": merge_loop_report(st, merges, elapsed, args),
             "pair_count_types": {
                 "kernel": "k_pair_dense (K1 of this train(): types layout, weighted, first touch)",
-                "avg_launch_us": 1e3 * k1_ms, "bytes_per_launch": k1_bytes,
-                "achieved_GBps": (k1_bytes / (k1_ms * 1e-3)) / 1e9 if k1_ms > 0 else None,
+                "avg_launch_us": 1e3 * st["count_kernel_ms"] / max(1, st["count_launches"]),
+                "bytes_per_launch": st["count_kernel_bytes"] / max(1, st["count_launches"]),
             },
-            "resident": {"launches": st["resident_launches"], "ms": st["resident_ms"],
-                         "note": "k_resident launch durations (HIP events): one persistent launch per train()"},
             "load_s": load_s, "corpus_gen_s": gen_s,
             "load": {"kernel": "k_word_count (one pass, LDS-staged tiles, byte-exact in-pass verification)",
                      "algorithmic_bytes": cfg["bytes"],
@@ -610,6 +731,9 @@ def main():
             "speculation": {"hits": st["spec_hits"], "misses": st["spec_misses"],
                             "hit_rate": st["spec_hits"] / max(1, st["spec_hits"] + st["spec_misses"])},
         }
+        k1 = result["pair_count_types"]
+        k1["achieved_GBps"] = (k1["bytes_per_launch"] / (k1["avg_launch_us"] * 1e-6) / 1e9
+                               if k1["avg_launch_us"] > 0 else None)
         case = fullsize_case(args.config)
         if case and not args.bytes:
             result["config"]["corpus_md5_expected"] = case["corpus_md5"]
@@ -631,8 +755,8 @@ def main():
                 result["roofline"]["algorithmic_bytes_per_launch"] = pair_count["bytes_per_launch"]
                 result["roofline"]["avg_launch_us"] = pair_count["avg_launch_us"]
                 result["roofline"]["note"] = ("K1, the pair-count scan the north star sets the HBM-roofline target on; "
-                                              "the timed step's dominant kernel is the latency-bound merge loop "
-                                              "(merge_loop)")
+                                              "the timed step's dominant kernels are the latency-bound merge loops "
+                                              "(merge_loop.resident, merge_loop.index)")
         if encode is not None:
             result["encode"] = encode
         try:
@@ -657,8 +781,9 @@ def main():
                 except Exception as e:
                     encode["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if one_job:
         sdist.finalize()
+    if dist is not None:
         dist.destroy_process_group()
 
 

@@ -170,6 +170,13 @@ typedef struct ShredStats {
   uint64_t resident_aborts;    /* k_resident launches that found their grid not co-resident (then off) */
   uint64_t verify_checks;      /* verify_argmax: selections checked against a device recount */
   uint64_t verify_failures;    /* of verify_checks: frequency != device max or != the pair's count */
+  /* algorithmic bytes of the two merge loops, collected while timing is on */
+  uint64_t resident_merges;    /* merges collected from k_resident */
+  double resident_bytes;       /* Σ 4 B x live tokens over those merges (K2: the scan a merge stands for) */
+  double resident_kernel_ms;   /* Σ durations of the k_resident launches that merged (HIP events) */
+  uint64_t index_run_ints_read;     /* k_word_loop: Σ ints of the scanned words' runs (length + tokens) */
+  uint64_t index_run_ints_written;  /* k_word_loop: Σ ints of the changed runs written back */
+  uint64_t index_records;           /* k_word_loop: Σ 24-B delta records written to host memory */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 
@@ -194,6 +201,8 @@ void shred_release(void* handle);
 int shred_dist_unique_id(void* out, size_t cap);
 int shred_dist_init(int rank, int world_size, const void* unique_id, size_t len, int device);
 int shred_dist_finalize(void);
+/* Ranks of the communicator shred_dist_init made (ncclCommCount); 0 when there is none. */
+int shred_dist_ranks(void);
 
 #ifdef __cplusplus
 }

@@ -2773,7 +2773,19 @@ void Device::free_slot(MergeSlot& s, bool keep_host) {
   }
 }
 
+// The streams of aborted resident launches: their missing workgroups may still start once the CUs
+// free up, and they read the token table, the weights, the signatures and the resident plan
+// before they see the abort.  Every path that frees or reallocates those buffers drains them first.
+void Device::drain_retired() {
+  for (void* s : retired_streams_) {
+    (void)hipStreamSynchronize(S(s));
+    (void)hipStreamDestroy(S(s));
+  }
+  retired_streams_.clear();
+}
+
 void Device::free_all() {
+  drain_retired();
   void* ptrs[] = {tok_, tok0_, tile_off_, tile_len_, tile_len0_, weight_, sig_};
   for (void* p : ptrs)
     if (p) HIP_OK(hipFree(p));
@@ -2797,11 +2809,7 @@ Device::~Device() {
   delete wl_;  // ends its launch first
   wl_ = nullptr;
   (void)hipStreamSynchronize(S(stream_));
-  for (void* s : retired_streams_) {  // aborted resident launches: their late workgroups leave first
-    (void)hipStreamSynchronize(S(s));
-    (void)hipStreamDestroy(S(s));
-  }
-  retired_streams_.clear();
+  drain_retired();  // aborted resident launches: their late workgroups leave first
   free_resident();
   if (res_mbox_) (void)hipHostFree(res_mbox_);
   if (res_status_) (void)hipHostFree(res_status_);
@@ -3758,6 +3766,7 @@ void Device::download_tokens(std::vector<int32_t>* out) {
 // k_resident host side: plan (which workgroup holds which tiles in LDS), launch, post, collect,
 // roll back, park.  See the kernel's comment for the protocol.
 void Device::free_resident() {
+  drain_retired();
   for (void* p : {(void*)res_wg_tiles_, (void*)res_wg_rank_, (void*)res_tile_lofs_, (void*)res_cmd_, (void*)res_q_,
                   (void*)res_dbg_, (void*)res_stamps_, (void*)res_arrive_})
     if (p) HIP_OK(hipFree(p));
@@ -4092,7 +4101,11 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
     res_phase_[3] += 1e-2 * (double)hs[2];
     res_phase_n_ += 1;
   }
-  if (timing_) times_.merge_bytes += 4.0 * (double)live_tokens_est_;
+  if (timing_) {
+    times_.merge_bytes += 4.0 * (double)live_tokens_est_;
+    times_.res_bytes += 4.0 * (double)live_tokens_est_;
+    times_.res_merges += 1;
+  }
   ++res_merges_;
   if (hybrid_ && !idx_phase_ && index_on_ && wl_ && wl_->ready()) {
     // entries merged per merge is far from monotone (a frequent pair of a few common words sits
@@ -4156,6 +4169,7 @@ void Device::park() {
   if (timing_ && res_merges_) {  // one launch: its wall time is the merge loop's device time
     times_.merge_ms += ms;
     times_.merge_launches += res_merges_;
+    times_.res_ms += ms;
   }
   if (res_merges_ && std::getenv("SHREDWORD_RESIDENT_REPORT")) {
     const double n = (double)res_merges_;

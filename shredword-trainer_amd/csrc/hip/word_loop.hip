@@ -73,6 +73,7 @@ struct WlSlotDev {
                       //   [4..5] occurrences (u64), [6..7] device ticks command -> flag (u64),
                       //   [8..9] ticks command -> list known, [10..11] ticks command -> words merged,
                       //   [12] words whose runs were read, [13] 1: a filtered words-of list,
+                      //   [14] run ints read (length + tokens), [15] run ints written back,
                       //   [16..18] stamps (10 ns ticks after the command, thread 0): pool entries
                       //   loaded, first run loaded, first word merged
   uint32_t rec_cap;
@@ -337,6 +338,7 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
 struct LoopS {
   uint32_t cmd[8];
   uint32_t nout, nchg, pool_top, err, scan, filter, nspill, qn;
+  uint32_t rd, wr;  // run ints read (length + tokens of every scanned word) / written back (changed words)
   uint32_t st[4];
   u64 lk[2];  // word list: pool offset, count
   u64 need;   // filter bits the listed words must hold
@@ -475,6 +477,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.nout = 0;
         S.nchg = 0;
         S.scan = 0;
+        S.rd = 0;
+        S.wr = 0;
         S.nspill = 0;
         S.filter = need != 0;
         S.occ = 0;
@@ -523,7 +527,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     // densely, a lane per word: the run in one round trip, the walk in registers.
     const bool append = S.err == 0;
     const u64 need = S.need;
-    uint32_t my_occ = 0, my_scan = 0;
+    uint32_t my_occ = 0, my_scan = 0, my_rd = 0, my_wr = 0;
     if (tid == 0) S.qn = 0;
     for (u64 base = 0; base < cnt; base += (u64)kWlThreads * kB) {
       u64 ex[kB], sx[kB];
@@ -584,6 +588,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
             }
           }
           my_occ += occ;
+          my_rd += 1u + L;
+          my_wr += occ ? 1u + nl : 0u;
           if (qi == 0 && base == 0) S.st[2] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
         }
         const u64 chg = __ballot(occ != 0);
@@ -607,6 +613,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     }
     if (my_occ) atomicAdd(&S.occ, (u64)my_occ);
     if (my_scan) atomicAdd(&S.scan, my_scan);
+    if (my_rd) atomicAdd(&S.rd, my_rd);
+    if (my_wr) atomicAdd(&S.wr, my_wr);
     __syncthreads();
     // ---- the records to host memory (LDS hash, then the spilled keys), then the flag
     const WlSlotDev& sd = p.sl[slot & (WordLoop::kSlots - 1)];
@@ -654,6 +662,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       h64[5] = S.t[1];
       sd.hdr[12] = S.scan;
       sd.hdr[13] = S.filter;
+      sd.hdr[14] = S.rd;
+      sd.hdr[15] = S.wr;
       sd.hdr[16] = S.st[0];
       sd.hdr[17] = S.st[1];
       sd.hdr[18] = S.st[2];
@@ -669,6 +679,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   }
   if (tid == 0) {
     p.dstate[kStPoolTop] = S.pool_top;
+    p.status[1] = expect - 1u;  // the command this launch did not take (a time-out's resume point)
     __threadfence_system();
     __hip_atomic_store(&p.status[0], exit_op, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -828,6 +839,9 @@ WordLoop::WordLoop(int ordinal, void* stream, int32_t unk_id) : ordinal_(ordinal
   WL_OK(hipHostMalloc((void**)&status_, 64, pin));
   std::memset(status_, 0, 64);
   WL_OK(hipHostGetDevicePointer(&status_dev_, status_, 0));
+  // the idle bound (polls without a command before the launch ends itself); tests shrink it to
+  // race the time-out against the posts
+  if (const char* e = std::getenv("SHREDWORD_WL_IDLE_POLLS")) idle_polls_ = (uint32_t)std::strtoul(e, nullptr, 10);
   for (auto& e : ev_) {
     hipEvent_t ev;
     WL_OK(hipEventCreate(&ev));
@@ -909,6 +923,8 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
   ntok_ = ntok;
   ntiles_ = (uint32_t)ts.num_tiles();
   if (nwords_ == 0 || nint_ >= (1ull << 31)) return false;  // hipcub sizes are int
+  // the pool (below) is addressed with 32-bit offsets (pool top, lst_, directory values)
+  if (3 * ntok_ + 4096 >= (1ull << 32)) return false;
   for (uint32_t w = 0; w < nwords_; ++w)
     if (wtok[woff[w]] == 0) return false;  // words are never empty (strtok)
   wtok.resize(nint_ + kRunPad, 0);
@@ -1139,7 +1155,7 @@ void WordLoop::reserve(int32_t max_id) {
   WL_OK(hipStreamSynchronize(s));
 }
 
-void WordLoop::launch() {
+void WordLoop::launch(uint32_t seq0) {
   WlParams p{};
   p.wtok = wtok_;
   p.weight = weight_;
@@ -1160,8 +1176,8 @@ void WordLoop::launch() {
   p.unk = unk_;
   p.ring = static_cast<const WlCmd*>(ring_dev_);
   p.status = static_cast<uint32_t*>(status_dev_);
-  p.seq0 = seq_ + 1;
-  p.idle_polls = 1u << 22;  // ~10 s without a command: the launch ends itself (the host relaunches)
+  p.seq0 = seq0;
+  p.idle_polls = idle_polls_;
   for (int k = 0; k < kSlots; ++k) {
     p.sl[k].recs = static_cast<DeltaRecord*>(slot_[k].dev_recs);
     p.sl[k].hdr = static_cast<uint32_t*>(slot_[k].dev_hdr);
@@ -1176,15 +1192,24 @@ void WordLoop::launch() {
   ++st_.launches;
 }
 
-uint32_t WordLoop::post(uint32_t op, int32_t a, int32_t b, int32_t X) {
-  if (running_ && __atomic_load_n(&status_[0], __ATOMIC_ACQUIRE) == kOpTimeout) {
-    if (!posted_.empty()) fatal("k_word_loop ended on its time-out with merges in flight");
-    WL_OK(hipStreamSynchronize(S(stream_)));
-    running_ = false;
+// The launch ended itself after ~10 s without a command.  It may have done so between a post's
+// check and its ring store, so commands can be waiting: the loop published the first command it
+// did not take (status_[1]), and a new launch resumes there (the ring still holds them).
+void WordLoop::recover_timeout() {
+  WL_OK(hipStreamSynchronize(S(stream_)));
+  running_ = false;
+  const uint32_t next = __atomic_load_n(&status_[1], __ATOMIC_ACQUIRE);
+  if (next != seq_ + 1) {  // posted commands were not taken
+    if (seq_ + 1 - next > kRing) fatal("k_word_loop: more commands behind its time-out than the ring holds");
+    launch(next);
   }
+}
+
+uint32_t WordLoop::post(uint32_t op, int32_t a, int32_t b, int32_t X) {
+  if (running_ && __atomic_load_n(&status_[0], __ATOMIC_ACQUIRE) == kOpTimeout) recover_timeout();
   if (!running_) {
     if (op == kOpStop) return 0;
-    launch();
+    launch(seq_ + 1);
   }
   const uint32_t seq = ++seq_;
   const uint32_t slot = (uint32_t)X & (kSlots - 1);
@@ -1211,7 +1236,12 @@ void WordLoop::wait_flag(const Slot& sl, uint32_t seq) {
   while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
     __builtin_ia32_pause();
     if (++spins % 4096 != 0) continue;
-    if (__atomic_load_n(&status_[0], __ATOMIC_ACQUIRE) != 0) fatal("k_word_loop ended with a merge in flight");
+    const uint32_t st = __atomic_load_n(&status_[0], __ATOMIC_ACQUIRE);
+    if (st == kOpTimeout) {
+      recover_timeout();  // resumes at the first command it did not take (this one or earlier)
+    } else if (st != 0) {
+      fatal("k_word_loop ended with a merge in flight");
+    }
     if (now_seconds() - t0 > 60.0) {
       const hipError_t e = hipStreamQuery(S(stream_));
       if (e != hipSuccess && e != hipErrorNotReady) WL_OK(e);
@@ -1233,6 +1263,9 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   st_.merges += 1;
   st_.candidates += h[2];
   st_.scanned += h[12];
+  st_.run_ints_read += h[14];
+  st_.run_ints_written += h[15];
+  st_.records += h[0];
   st_.changed += h[3];
   st_.occurrences += h64[2];
   st_.dev_us += 1e-2 * (double)h64[3];  // s_memrealtime: 100 MHz

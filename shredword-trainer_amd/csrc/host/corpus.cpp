@@ -322,11 +322,13 @@ std::vector<Entry> shard_entries(const uint8_t* d, size_t n, const LoadOptions& 
 // the same word: Counter::add compares the bytes), then the table in reference order.
 void merge_entries(const uint8_t* d, const Entry* all, size_t total, const LoadOptions& opt, int threads,
                    WordTable* out) {
-  std::vector<std::vector<uint32_t>> by_part(kParts);
-  for (size_t i = 0; i < total; ++i) by_part[all[i].hash >> (64 - kPartBits)].push_back((uint32_t)i);
+  // 64-bit indices: Σ over ranks of distinct words per rank can pass 2^32 even when the merged
+  // table stays small
+  std::vector<std::vector<uint64_t>> by_part(kParts);
+  for (size_t i = 0; i < total; ++i) by_part[all[i].hash >> (64 - kPartBits)].push_back((uint64_t)i);
   std::vector<Counter> merged(kParts);
   parallel_for(threads, kParts, [&](size_t p, int) {
-    for (uint32_t i : by_part[p]) merged[p].add(d, all[i].hash, all[i].first, all[i].len, all[i].count, all[i].first);
+    for (uint64_t i : by_part[p]) merged[p].add(d, all[i].hash, all[i].first, all[i].len, all[i].count, all[i].first);
   });
   std::vector<OrderKey> keys;
   order_and_finish(d, merged, opt, threads, out, &keys);

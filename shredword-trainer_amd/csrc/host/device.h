@@ -38,6 +38,9 @@ struct KernelTimes {
   double hist_ms = 0;      // Σ k_pair_hist durations (stream layout K1 bulk: counts only)
   double hist_bytes = 0;   // Σ its algorithmic bytes (4 B per token + 12 B per tile)
   uint64_t hist_launches = 0;
+  uint64_t res_merges = 0;  // merges collected from k_resident
+  double res_bytes = 0;     // their algorithmic bytes: 4 B per live token per merge
+  double res_ms = 0;        // Σ durations of the k_resident launches that merged (HIP events)
 };
 
 class Device : public Backend {
@@ -367,6 +370,7 @@ class Device : public Backend {
   };
   void plan_resident(const TiledStream& ts);
   void free_resident();
+  void drain_retired();  // syncs and destroys retired_streams_ (before their buffers go)
   void start_resident();
   uint32_t post_resident(uint32_t op, int32_t a, int32_t b, int32_t X, int slot);
   bool wait_resident(const MergeSlot& sl, int32_t X);  // false: the launch aborted

@@ -26,6 +26,7 @@ struct Rccl {
   decltype(&ncclAllGather) AllGather = nullptr;
   decltype(&ncclAllReduce) AllReduce = nullptr;
   decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&ncclCommCount) CommCount = nullptr;
 };
 const Rccl& rccl() {
   static Rccl r;
@@ -49,6 +50,7 @@ const Rccl& rccl() {
     r.AllGather = reinterpret_cast<decltype(r.AllGather)>(sym("ncclAllGather"));
     r.AllReduce = reinterpret_cast<decltype(r.AllReduce)>(sym("ncclAllReduce"));
     r.GetErrorString = reinterpret_cast<decltype(r.GetErrorString)>(sym("ncclGetErrorString"));
+    r.CommCount = reinterpret_cast<decltype(r.CommCount)>(sym("ncclCommCount"));
   });
   return r;
 }
@@ -100,6 +102,14 @@ int dist_init(int rank, int world, const void* id, size_t len, int device) {
   s.device = device;
   s.comm = comm;
   return 0;
+}
+
+int dist_comm_ranks() {
+  const DistState& s = dist_state();
+  if (!s.comm) return 0;
+  int n = 0;
+  nccl_ok(rccl().CommCount((ncclComm_t)s.comm, &n), "ncclCommCount");
+  return n;
 }
 
 int dist_finalize() {

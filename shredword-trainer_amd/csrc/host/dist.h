@@ -32,6 +32,8 @@ inline bool dist_active() { return dist_state().world > 1 && dist_state().comm !
 
 int dist_unique_id(void* out, size_t cap);
 int dist_init(int rank, int world, const void* id, size_t len, int device);
+// Ranks of the job's communicator (ncclCommCount), 0 without one.
+int dist_comm_ranks();
 int dist_finalize();
 
 // All-gather of `bytes` per rank (device buffers; recv holds world x bytes) on `stream`, over

@@ -400,6 +400,9 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
     s->resident_ms = t->dev->resident_ms();
     s->resident_latency_us = t->dev->resident_latency_us();
     s->resident_aborts = t->dev->resident_aborts();
+    s->resident_merges = k.res_merges;
+    s->resident_bytes = k.res_bytes;
+    s->resident_kernel_ms = k.res_ms;
     if (const WordLoop* wl = t->dev->word_loop()) {
       const WordLoopStats& w = wl->stats();
       s->index_on = t->dev->index_eligible() ? 1 : 0;
@@ -418,6 +421,9 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
       s->index_build_us = w.build_us;
       s->index_no_sub = w.no_sub;
       s->index_staged = w.staged;
+      s->index_run_ints_read = w.run_ints_read;
+      s->index_run_ints_written = w.run_ints_written;
+      s->index_records = w.records;
       s->index_switch_merge = t->dev->switch_merge();
       s->index_switch_ms = t->dev->switch_ms();
     }
@@ -467,5 +473,6 @@ int shred_dist_init(int rank, int world, const void* id, size_t len, int device)
   return dist_init(rank, world, id, len, device);
 }
 int shred_dist_finalize(void) { return dist_finalize(); }
+int shred_dist_ranks(void) { return dist_comm_ranks(); }
 
 }  // extern "C"

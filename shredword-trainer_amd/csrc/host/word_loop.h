@@ -57,6 +57,9 @@ struct WordLoopStats {
   double build_us = 0;        // Σ device time building pair groups (after the flags)
   uint64_t no_sub = 0;        // merges whose pair groups were not built (their words-of list serves)
   uint64_t staged = 0;        // Σ pair-group entries written
+  uint64_t run_ints_read = 0;     // Σ ints of the scanned words' runs (length + tokens)
+  uint64_t run_ints_written = 0;  // Σ ints of the changed words' runs written back
+  uint64_t records = 0;           // Σ delta records handed to the host
 };
 
 class WordLoop {
@@ -146,7 +149,8 @@ class WordLoop {
   void free_all();
   void build_index();
   void restore_index();
-  void launch();
+  void launch(uint32_t seq0);  // the first command the launch takes
+  void recover_timeout();
   uint32_t post(uint32_t op, int32_t a, int32_t b, int32_t X);
   void wait_flag(const Slot& s, uint32_t seq);
   void ensure_slots(uint32_t cap);
@@ -192,6 +196,7 @@ class WordLoop {
   uint32_t* status_ = nullptr;     // pinned: [0] exit reason, [1] error code
   void* status_dev_ = nullptr;
   uint32_t seq_ = 0;
+  uint32_t idle_polls_ = 1u << 22;  // ~10 s without a command: the launch ends itself (relaunched on demand)
   std::vector<Post> posted_;
   void* ev_[2] = {};
   WordLoopStats st_;

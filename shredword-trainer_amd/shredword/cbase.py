@@ -74,7 +74,10 @@ class ShredStats(Structure):
                 ("index_dev_lookup_us", c_double), ("index_dev_scan_us", c_double),
                 ("index_scanned", c_uint64), ("index_build_us", c_double), ("index_no_sub", c_uint64),
                 ("index_staged", c_uint64), ("index_switch_merge", c_int64), ("index_switch_ms", c_double),
-                ("resident_aborts", c_uint64), ("verify_checks", c_uint64), ("verify_failures", c_uint64)]
+                ("resident_aborts", c_uint64), ("verify_checks", c_uint64), ("verify_failures", c_uint64),
+                ("resident_merges", c_uint64), ("resident_bytes", c_double), ("resident_kernel_ms", c_double),
+                ("index_run_ints_read", c_uint64), ("index_run_ints_written", c_uint64),
+                ("index_records", c_uint64)]
 
 
 Trainer = c_void_p
@@ -119,6 +122,7 @@ lib.shred_release.argtypes, lib.shred_release.restype = [c_void_p], None
 lib.shred_dist_unique_id.argtypes, lib.shred_dist_unique_id.restype = [c_void_p, c_size_t], c_int
 lib.shred_dist_init.argtypes, lib.shred_dist_init.restype = [c_int, c_int, c_void_p, c_size_t, c_int], c_int
 lib.shred_dist_finalize.argtypes, lib.shred_dist_finalize.restype = [], c_int
+lib.shred_dist_ranks.argtypes, lib.shred_dist_ranks.restype = [], c_int
 
 # encoder (include/shredword_encode.h)
 Encoder = c_void_p

@@ -38,6 +38,13 @@ OUT = os.path.join(HERE, "fullsize")
 CASES = {
     "c2": (1_000_000_000, 2, "utf8", (8192, 0, 0.995, 2000)),
     "c3": (10_000_000_000, 3, "utf8", (32000, 0, 0.995, 2)),
+    # C5's parameters (vocab 64000, coverage 0.9995, mixed script, seed 5, min_pair_freq 2000 =
+    # the Python default) at 10 GB: the 100 GB corpus is out of the oracle's reach (hours per GB
+    # of merges), this one pins the 64k-vocab / high-cardinality path at a size past C3
+    "c5_10g": (10_000_000_000, 5, "mixed", (64000, 0, 0.9995, 2000)),
+    # C4's parameters (vocab 32000, min_pair_freq 2000, seed 4) on one 10 GB shard-sized corpus:
+    # the GPU test loads it as 8 byte ranges (the sharded load of C4) and must match this run
+    "c4_10g": (10_000_000_000, 4, "utf8", (32000, 0, 0.995, 2000)),
 }
 
 

@@ -391,14 +391,23 @@ def _fullsize(name):
     return case, corpus
 
 
-@pytest.mark.parametrize("name", ["c2", "c3"])
-def test_full_size_matches_oracle_run(name, tmp_path):
-    """C2 (1 GB, vocab 8192) and C3 (10 GB, vocab 32000, min_pair_freq 2) at full size, bit-exact:
-    .model bytes, .vocab md5 and every merge / batch line against the oracle's full run committed
-    in tests/golden/fullsize/ (the oracle is pinned to the reference by every golden, including
-    the reference's own 31,744- and 63,744-merge runs)."""
+# C4's parameters at 10 GB are loaded as the C4 job loads its 80 GB: 8 byte ranges counted on the
+# device in turn and merged (the per-rank step of the sharded load, SHREDWORD_LOAD_SIM_SHARDS)
+_FULLSIZE_ENV = {"c4_10g": {"SHREDWORD_LOAD_SIM_SHARDS": "8"}}
+
+
+@pytest.mark.parametrize("name", ["c2", "c3", "c5_10g", "c4_10g"])
+def test_full_size_matches_oracle_run(name, tmp_path, monkeypatch):
+    """Full-size corpora, bit-exact: .model bytes, .vocab md5 and every merge / batch line against
+    the oracle's full run committed in tests/golden/fullsize/ (the oracle is pinned to the
+    reference by every golden, including the reference's own 31,744- and 63,744-merge runs).
+    c2 = C2 (1 GB, vocab 8192), c3 = C3 (10 GB, vocab 32000, min_pair_freq 2), c5_10g = C5's
+    parameters (vocab 64000, coverage 0.9995, mixed script) on 10 GB, c4_10g = C4's parameters
+    on 10 GB through the 8-way sharded load."""
     import hashlib
     case, corpus = _fullsize(name)
+    for k, v in _FULLSIZE_ENV.get(name, {}).items():
+        monkeypatch.setenv(k, v)
     cfg = case["config"]
     t = _trainer(vocab_size=cfg["vocab_size"], unk_id=cfg["unk_id"], character_coverage=cfg["character_coverage"],
                  min_pair_freq=cfg["min_pair_freq"])
@@ -415,20 +424,50 @@ def test_full_size_matches_oracle_run(name, tmp_path):
     assert hashlib.md5(vocab).hexdigest() == case["vocab_md5"]
 
 
-def test_full_size_c2_invariants(tmp_path):
-    """C2 at full size (1 GB): invariants that hold for any correct run."""
-    corpus = os.path.join(os.environ.get("TMPDIR", "/tmp"), "shredword_bench", "c2_utf8_1000000000_s2.txt")
-    if not (os.path.exists(corpus) and os.path.getsize(corpus) == 1_000_000_000):
+def _word_bytes(corpus):
+    """Bytes of the corpus that are not delimiters ([\t\r\n ]), streamed in 1 GB pieces."""
+    total = 0
+    with open(corpus, "rb") as f:
+        while True:
+            buf = f.read(1 << 30)
+            if not buf:
+                return total
+            d = np.frombuffer(buf, dtype=np.uint8)
+            total += d.size - int(np.count_nonzero((d == 32) | (d == 10) | (d == 9) | (d == 13)))
+
+
+# Size-independent invariants at full size: byte conservation, operands before their merge,
+# non-increasing merge frequencies >= min_pair_freq, and the K5 device recount every 500 merges
+# (the host heap's pick is the largest pair count and its own count).
+_INVARIANT_CASES = {
+    # name: (bytes, seed, script, vocab, coverage, min_pair_freq, env, expected merges or None)
+    "c2": (1_000_000_000, 2, "utf8", 8192, 0.995, 2000, {}, 7936),
+    "c5_10g": (10_000_000_000, 5, "mixed", 64000, 0.9995, 2000, {}, None),
+    "c4_10g": (10_000_000_000, 4, "utf8", 32000, 0.995, 2000, {"SHREDWORD_LOAD_SIM_SHARDS": "8"}, None),
+}
+
+
+@pytest.mark.parametrize("name", sorted(_INVARIANT_CASES))
+def test_full_size_invariants(name, tmp_path, monkeypatch):
+    nbytes, seed, script, vocab_size, cov, mpf, env, expect = _INVARIANT_CASES[name]
+    corpus = os.path.join(os.environ.get("TMPDIR", "/tmp"), "shredword_bench", f"{name}_{script}_{nbytes}_s{seed}.txt")
+    if not (os.path.exists(corpus) and os.path.getsize(corpus) == nbytes):
         os.makedirs(os.path.dirname(corpus), exist_ok=True)
-        corpora.gen_synthetic(corpus, 1_000_000_000, 2, "utf8")
-    t = _trainer(vocab_size=8192, min_pair_freq=2000)
+        corpora.gen_synthetic(corpus, nbytes, seed, script)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    t = _trainer(vocab_size=vocab_size, unk_id=0, character_coverage=cov, min_pair_freq=mpf)
     trace = str(tmp_path / "trace.txt")
     t.set_option("trace", trace)
+    t.set_option("verify_argmax", 500)
     t.load_corpus(corpus)
-    n, model, vocab = _train_bytes(t, tmp_path, "c2")
+    n, model, vocab = _train_bytes(t, tmp_path, name)
     st = t.stats()
     t.destroy()
-    assert n == 7936
+    if expect is not None:
+        assert n == expect
+    assert 0 < n <= vocab_size - 256
+    assert st["verify_checks"] >= n // 500 and st["verify_failures"] == 0
     T = 256 + n
     ops = np.frombuffer(model, dtype="<i4").reshape(-1, 3)
     assert (ops[:, 2] == np.arange(256, T)).all()
@@ -437,14 +476,11 @@ def test_full_size_c2_invariants(tmp_path):
     assert len(toks) == T
     # Byte conservation: every byte of every word occurrence ends in exactly one final token.
     # unk_id = 0 has the empty spelling and counts one byte per unk symbol (byte 0 never occurs).
-    data = np.fromfile(corpus, dtype=np.uint8)
-    delims = int(np.count_nonzero((data == 32) | (data == 10) | (data == 9) | (data == 13)))
-    word_bytes = data.size - delims
-    assert sum(len(tok) * f for tok, f in toks[1:]) + toks[0][1] == word_bytes
+    assert sum(len(tok) * f for tok, f in toks[1:]) + toks[0][1] == _word_bytes(corpus)
     freqs = [int(ln.split()[3]) for ln in open(trace) if ln.startswith("M ")]
     assert len(freqs) == n
     assert all(x >= y for x, y in zip(freqs, freqs[1:])), "merge frequencies must not increase"
-    assert freqs[-1] >= 2000
+    assert freqs[-1] >= mpf
 
 
 @pytest.mark.parametrize("kind", ["medium", "adversarial_no_nul", "utf8"])
@@ -523,10 +559,30 @@ def test_resident_abort_falls_back(medium_corpus, medium_oracle, tmp_path, monke
     t.load_corpus(medium_corpus)
     n, model, vocab = _train_bytes(t, tmp_path, "ab")
     st = t.stats()
-    t.destroy()
     assert (model, vocab) == medium_oracle
     assert n > 1000
     assert st["resident_aborts"] >= 1 and st["index_merges"] > 0
+    # a second load on the same trainer frees and reallocates the buffers the aborted launch's
+    # late workgroups read: its retired streams drain first (Device::drain_retired)
+    t.load_corpus(medium_corpus)
+    n2, model2, vocab2 = _train_bytes(t, tmp_path, "ab2")
+    t.destroy()
+    assert (n2, model2, vocab2) == (n, model, vocab)
+
+
+def test_word_loop_idle_timeout_resumes(medium_corpus, medium_oracle, tmp_path, monkeypatch):
+    """k_word_loop ends itself after SHREDWORD_WL_IDLE_POLLS polls without a command.  With a
+    bound of one poll it ends between almost every pair of merges, racing the host's posts: the
+    host resumes a new launch at the first command the old one did not take (status[1]), and the
+    files are still the oracle's."""
+    monkeypatch.setenv("SHREDWORD_WL_IDLE_POLLS", "1")
+    t = _trainer(vocab_size=6000, unk_id=0, character_coverage=0.9995, min_pair_freq=20)
+    t.load_corpus(medium_corpus)
+    n, model, vocab = _train_bytes(t, tmp_path, "to")
+    st = t.stats()
+    t.destroy()
+    assert (model, vocab) == medium_oracle
+    assert st["index_merges"] > 0 and st["index_launches"] >= 2
 
 
 def test_resident_partial_residency(medium_corpus, medium_oracle, tmp_path):
