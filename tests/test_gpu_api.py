@@ -564,7 +564,9 @@ def test_resident_abort_falls_back(medium_corpus, medium_oracle, tmp_path, monke
     assert st["resident_aborts"] >= 1 and st["index_merges"] > 0
     # a second load on the same trainer frees and reallocates the buffers the aborted launch's
     # late workgroups read: its retired streams drain first (Device::drain_retired)
+    # (reset: a reload keeps the merge count, as the reference's num_merges, bpe.cpp:176-185)
     t.load_corpus(medium_corpus)
+    t.reset()
     n2, model2, vocab2 = _train_bytes(t, tmp_path, "ab2")
     t.destroy()
     assert (n2, model2, vocab2) == (n, model, vocab)
