@@ -985,6 +985,8 @@ constexpr uint32_t kResRing = 16;
 // participants' records to the host), 2 .. grid-1 own the tiles.
 constexpr uint32_t kResGatherWg = 1, kResFirstWorker = 2;
 constexpr int kResGatherBatch = 16;  // records per gatherer thread per round trip
+constexpr int kResThreadsHbm = 512;  // k_resident block size when the tokens stay in HBM
+constexpr uint32_t kAllTiles = 0xFFFFFFFFu;  // hcount[2]: merge X matched (nearly) every tile
 static_assert(kResDeltaW < (1 << 12) && kResMaxTiles * kWaveTok < (1u << 22), "region header fields (k_resident)");
 constexpr uint32_t kOpUnmerge = 4;
 // k_resident: not every workgroup became resident within the leader's bound (another kernel or
@@ -1041,6 +1043,8 @@ struct ResParams {
   uint32_t seq0;             // first command number of this launch
   uint32_t leader_polls;     // idle leader iterations before the launch ends itself
   uint32_t keys_per_merge, slot_cap;
+  uint32_t region_keys;      // a participant with more LDS delta keys adds them to the global tables
+  uint32_t mt_dense;         // more matched tiles than this: the host index marks X in every tile
   ResSlot sl[Device::kResSlots];  // merge X uses sl[X % kResSlots]
   uint32_t* dbg;      // diagnostic (SHREDWORD_RESIDENT_DEBUG): per workgroup [phase, last seq, pi, T]
   u64* stamps;        // diagnostic: per participant [go seen, work done, loop cycles, -] (s_memrealtime)
@@ -1099,22 +1103,48 @@ __device__ __forceinline__ void res_sig_build(uint32_t* sg, const int32_t* t, ui
 // One wave applies (a, b) -> X to a single-chunk tile held in LDS at tb (live length *len):
 // k_merge's per-chunk logic with no carries (the tile is its own first and last chunk).
 // Returns the occurrences merged; the tile is compacted in place and *len updated.
+// This lane's 16 tokens of a tile (four 16-B loads).
+struct TileRegs {
+  int4 q[kPer / 4];
+};
+__device__ __forceinline__ void res_load_tile(const int32_t* tb, int lane, TileRegs* r) {
+  const int p0 = lane * kPer;
+#pragma unroll
+  for (int q = 0; q < kPer / 4; ++q) r->q[q] = *reinterpret_cast<const int4*>(tb + p0 + 4 * q);
+}
+
+template <bool kWeighted>
+__device__ __forceinline__ uint32_t res_merge_body(int32_t* tb, const TileRegs& tr, uint32_t* lenp, uint32_t* sg,
+                                                   uint32_t* sgadd, int32_t* st, const u64* s_w, uint32_t r0, int32_t a,
+                                                   int32_t b, int32_t X, ResDelta& h, const ResSlot& p,
+                                                   uint32_t slot_cap, int lane, u64* n_written);
+
 template <bool kWeighted>
 __device__ __forceinline__ uint32_t res_merge_tile(int32_t* tb, uint32_t* lenp, uint32_t* sg, uint32_t* sgadd, int32_t* st,
                                                    const u64* s_w,
                                                    uint32_t r0, int32_t a, int32_t b, int32_t X, ResDelta& h,
                                                    const ResSlot& p, uint32_t slot_cap, int lane, u64* n_written) {
   if (!res_sig_test(sg, a, b)) return 0;  // the pair cannot be in this tile
+  TileRegs tr;
+  res_load_tile(tb, lane, &tr);
+  return res_merge_body<kWeighted>(tb, tr, lenp, sg, sgadd, st, s_w, r0, a, b, X, h, p, slot_cap, lane, n_written);
+}
+
+// The merge of one tile whose 16 tokens per lane are already in registers (tr).
+template <bool kWeighted>
+__device__ __forceinline__ uint32_t res_merge_body(int32_t* tb, const TileRegs& tr, uint32_t* lenp, uint32_t* sg,
+                                                   uint32_t* sgadd, int32_t* st, const u64* s_w, uint32_t r0, int32_t a,
+                                                   int32_t b, int32_t X, ResDelta& h, const ResSlot& p,
+                                                   uint32_t slot_cap, int lane, u64* n_written) {
   const uint32_t len = *lenp;
   const int p0 = lane * kPer;
   int32_t v[kPer];
 #pragma unroll
   for (int q = 0; q < kPer / 4; ++q) {
-    const int4 x = *reinterpret_cast<const int4*>(tb + p0 + 4 * q);
-    v[4 * q] = x.x;
-    v[4 * q + 1] = x.y;
-    v[4 * q + 2] = x.z;
-    v[4 * q + 3] = x.w;
+    v[4 * q] = tr.q[q].x;
+    v[4 * q + 1] = tr.q[q].y;
+    v[4 * q + 2] = tr.q[q].z;
+    v[4 * q + 3] = tr.q[q].w;
   }
 #pragma unroll
   for (int j = 0; j < kPer; ++j)
@@ -1369,26 +1399,29 @@ __device__ __forceinline__ void res_unmerge_tile(int32_t* tb, uint32_t* lenp, ui
 // (read and rewritten in place by their owner workgroup only) and LDS holds the weights and the
 // tile signatures, which is what decides which tiles a merge reads at all.
 template <bool kWeighted, bool kLdsTok>
-__global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
+__global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(ResParams p) {
+  constexpr int kRT = kLdsTok ? 256 : kResThreadsHbm;  // threads: more waves hide the HBM tile loads
+  constexpr int kRW = kRT / 64;
+  constexpr int kGB = kLdsTok ? kResGatherBatch : kResGatherBatch / 4;  // gatherer loads in flight per thread
   extern __shared__ __align__(16) int32_t s_dyn[];
   int32_t* s_res = s_dyn;                                     // the tiles' tokens
   u64* s_w = reinterpret_cast<u64*>(s_dyn + p.tok_words);     // the words' weights
   uint32_t* s_sig = reinterpret_cast<uint32_t*>(s_dyn + p.tok_words + 2 * p.w_words);  // per-tile signatures
-  __shared__ int32_t s_tok[kWaves][kStPad + 64];  // + a trash word per lane (branch-free compaction)
+  __shared__ int32_t s_tok[kRW][kStPad + 64];  // + a trash word per lane (branch-free compaction)
   __shared__ ResDelta h;
   __shared__ uint32_t s_len[kResMaxTiles], s_lofs[kResMaxTiles], s_sigadd[kResMaxTiles];
   __shared__ u64 s_toff[kResMaxTiles];
   __shared__ uint32_t s_mt[kResMaxTiles];
   __shared__ uint8_t s_lm[kResMaxTiles];   // per tile: bit X % 8 set when merge X matched there
   __shared__ uint32_t s_qc[kMaxMergeGroups];  // leader: entries written to each workgroup's queue
-  __shared__ uint32_t s_nmt, s_nrec;
+  __shared__ uint32_t s_nmt, s_nrec, s_nkeys;
   __shared__ uint32_t s_cmd[8];
   __shared__ u64 s_cnt[2];
   __shared__ u64 s_tlead;
   __shared__ u64 s_ts[4];      // diagnostic (stamps): the gatherer's phase ends
   __shared__ uint32_t s_nout;  // the last participant: records written to the host
   __shared__ uint32_t s_pre[kMaxMergeGroups + 1], s_pmt[kMaxMergeGroups + 1];
-  __shared__ uint32_t s_wtot[2][kWaves];
+  __shared__ uint32_t s_wtot[2][kRW];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t G = gridDim.x, me = blockIdx.x;
   const uint32_t t0 = p.wg_tiles[me], nt = p.wg_tiles[me + 1] - t0;
@@ -1399,28 +1432,28 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(p.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   // ---- residency: tiles, weights and signatures into LDS
-  for (uint32_t i = threadIdx.x; i < nt; i += kThreads) {
+  for (uint32_t i = threadIdx.x; i < nt; i += kRT) {
     s_len[i] = p.tile_len[t0 + i];
     s_lofs[i] = p.tile_lofs[t0 + i];
     s_toff[i] = p.tile_off[t0 + i];
     s_sigadd[i] = 0;
     s_lm[i] = 0;
   }
-  for (uint32_t i = threadIdx.x; i < G; i += kThreads) s_qc[i] = 0;
-  for (int i = threadIdx.x; i < kResDeltaW; i += kThreads) {
+  for (uint32_t i = threadIdx.x; i < G; i += kRT) s_qc[i] = 0;
+  for (int i = threadIdx.x; i < kResDeltaW; i += kRT) {
     h.key[i] = kEmpty32;
     h.sum[i] = 0;
     h.ft[i] = kEmpty64;
   }
   if (kWeighted)
-    for (uint32_t i = threadIdx.x; i < nr; i += kThreads) s_w[i] = p.weight[r0 + i];
+    for (uint32_t i = threadIdx.x; i < nr; i += kRT) s_w[i] = p.weight[r0 + i];
   if (threadIdx.x == 0) h.spill = 0;
   __syncthreads();
   auto tile_ptr = [&](uint32_t i) -> int32_t* {
     if constexpr (kLdsTok) return s_res + s_lofs[i];
     else return p.tok + s_toff[i];
   };
-  for (uint32_t i = wid; i < nt; i += kWaves) {
+  for (uint32_t i = wid; i < nt; i += kRW) {
     if constexpr (kLdsTok) {
       const int32_t* src = p.tok + s_toff[i];
       int32_t* dst = s_res + s_lofs[i];
@@ -1542,6 +1575,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       }
       s_nmt = 0;
       s_nrec = 0;
+      s_nkeys = 0;
       s_cnt[0] = 0;
       s_cnt[1] = 0;
     }
@@ -1564,7 +1598,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
     }
     const uint32_t lm_bit = 1u << ((uint32_t)X & 7u);
     if (op == kOpUnmerge) {  // undo merge X, a wrong guess (the host undoes them newest first)
-      for (uint32_t i = wid; i < nt; i += kWaves)
+      for (uint32_t i = wid; i < nt; i += kRW)
         if (s_lm[i] & lm_bit) res_unmerge_tile(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords, &s_sigadd[i], st,
                                       a, b, X, lane);
       __syncthreads();
@@ -1574,14 +1608,43 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
 
     // ---- the merge over this workgroup's tiles (wave per tile)
     u64 n_merged = 0, n_written = 0;
-    for (uint32_t i = wid; i < nt; i += kWaves) {
-      const uint32_t m = res_merge_tile<kWeighted>(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords,
-                                                   &s_sigadd[i], st, s_w, r0, a, b, X, h, sl, p.slot_cap, lane,
-                                                   &n_written);
+    auto note = [&](uint32_t i, uint32_t m) {
       if (lane == 0) s_lm[i] = m ? (s_lm[i] | lm_bit) : (s_lm[i] & ~lm_bit);
       if (m) {
         n_merged += m;
         if (lane == 0) s_mt[atomicAdd(&s_nmt, 1u)] = t0 + i;
+      }
+    };
+    if constexpr (kLdsTok) {
+      for (uint32_t i = wid; i < nt; i += kRW) {
+        const uint32_t m = res_merge_tile<kWeighted>(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords,
+                                                     &s_sigadd[i], st, s_w, r0, a, b, X, h, sl, p.slot_cap, lane,
+                                                     &n_written);
+        note(i, m);
+      }
+    } else {
+      // tokens in HBM: a software pipeline per wave, the next candidate tile's tokens load while
+      // this one merges (tiles the signature rules out are only noted)
+      auto skip_to = [&](uint32_t i) {
+        for (; i < nt; i += kRW) {
+          if (res_sig_test(s_sig + (size_t)i * kResSigWords, a, b)) break;
+          note(i, 0);
+        }
+        return i;
+      };
+      uint32_t i = skip_to(wid);
+      TileRegs cur;
+      if (i < nt) res_load_tile(tile_ptr(i), lane, &cur);
+      while (i < nt) {
+        const uint32_t j = skip_to(i + kRW);
+        TileRegs nxt;
+        if (j < nt) res_load_tile(tile_ptr(j), lane, &nxt);
+        const uint32_t m = res_merge_body<kWeighted>(tile_ptr(i), cur, &s_len[i], s_sig + (size_t)i * kResSigWords,
+                                                     &s_sigadd[i], st, s_w, r0, a, b, X, h, sl, p.slot_cap, lane,
+                                                     &n_written);
+        note(i, m);
+        cur = nxt;
+        i = j;
       }
     }
     if (lane == 0) {
@@ -1589,22 +1652,37 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       if (n_written) atomicAdd(&s_cnt[1], n_written);
     }
     __syncthreads();
-    // ---- publish this participant's region (write-through), clearing the LDS hash
+    // ---- publish this participant's deltas, clearing the LDS hash.  Few keys: a region the
+    // gatherer reads and combines.  Many keys (the early merges touch most neighbours in every
+    // workgroup): straight into the slot's global tables (device-scope Σ and min, the first
+    // toucher lists the key), so the gatherer only reads the combined keys instead of combining
+    // every participant's records in one workgroup.
     {
+      uint32_t mine = 0;
+      for (int i = threadIdx.x; i < kResDeltaW; i += kRT) mine += h.key[i] != kEmpty32 ? 1u : 0u;
+      mine = wave_scan_add(mine);
+      if (lane == 63 && mine) atomicAdd(&s_nkeys, mine);
+      __syncthreads();
+      const bool to_global = s_nkeys > p.region_keys;
       u64* rr = sl.rrec + (size_t)pi * kDeltaLdsW * 3;
-      for (int i = threadIdx.x; i < kResDeltaW; i += kThreads) {
+      for (int i = threadIdx.x; i < kResDeltaW; i += kRT) {
         const uint32_t key = h.key[i];
         if (key == kEmpty32) continue;
-        const uint32_t k = atomicAdd(&s_nrec, 1u);
-        __hip_atomic_store(rr + 3 * k, (u64)key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(rr + 3 * k + 1, h.sum[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(rr + 3 * k + 2, h.ft[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (to_global) {
+          delta_global(sl, key, h.sum[i], h.ft[i]);
+        } else {
+          const uint32_t k = atomicAdd(&s_nrec, 1u);
+          __hip_atomic_store(rr + 3 * k, (u64)key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(rr + 3 * k + 1, h.sum[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(rr + 3 * k + 2, h.ft[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         h.key[i] = kEmpty32;
         h.sum[i] = 0;
         h.ft[i] = kEmpty64;
       }
+      if (to_global && threadIdx.x == 0) h.spill = 1;
       const uint32_t nmt = s_nmt;
-      for (uint32_t i = threadIdx.x; i < nmt; i += kThreads)
+      for (uint32_t i = threadIdx.x; i < nmt; i += kRT)
         __hip_atomic_store(sl.rtile + (size_t)pi * kMtLds + i, s_mt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       u64* hd = reinterpret_cast<u64*>(sl.rhdr + (size_t)pi * kRegHdr);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's region stores (and spills) are done
@@ -1701,11 +1779,11 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
         }
         return lo;
       };
-      for (uint32_t i0 = 0; i0 < n; i0 += kThreads * kResGatherBatch) {
-        u64 r[kResGatherBatch][3];
+      for (uint32_t i0 = 0; i0 < n; i0 += kRT * kGB) {
+        u64 r[kGB][3];
 #pragma unroll
-        for (int k = 0; k < kResGatherBatch; ++k) {
-          const uint32_t i = i0 + k * kThreads + threadIdx.x;
+        for (int k = 0; k < kGB; ++k) {
+          const uint32_t i = i0 + k * kRT + threadIdx.x;
           if (i < n) {
             const uint32_t o = owner(s_pre, i);
             const u64* src = sl.rrec + ((size_t)o * kDeltaLdsW + (i - s_pre[o])) * 3;
@@ -1719,8 +1797,8 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
           if (threadIdx.x == 0) s_ts[2] = __builtin_amdgcn_s_memrealtime();
         }
 #pragma unroll
-        for (int k = 0; k < kResGatherBatch; ++k) {  // combine the participants' records per key in the LDS hash
-          const uint32_t i = i0 + k * kThreads + threadIdx.x;
+        for (int k = 0; k < kGB; ++k) {  // combine the participants' records per key in the LDS hash
+          const uint32_t i = i0 + k * kRT + threadIdx.x;
           if (i >= n) continue;
           const uint32_t key = (uint32_t)r[k][0];
           uint32_t hs = (key * 2654435761u) >> (32 - __builtin_ctz(kResDeltaW));
@@ -1740,7 +1818,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       }
       if (p.stamps && threadIdx.x == 0) s_ts[3] = __builtin_amdgcn_s_memrealtime();
       __syncthreads();
-      for (int i = threadIdx.x; i < kResDeltaW; i += kThreads) {
+      for (int i = threadIdx.x; i < kResDeltaW; i += kRT) {
         const uint32_t key = h.key[i];
         if (key == kEmpty32) continue;
         sys_record(sl.out + atomicAdd(&s_nout, 1u), key, h.sum[i], h.ft[i]);
@@ -1750,7 +1828,8 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
       }
       __syncthreads();
       n = s_nout;
-      for (uint32_t i = threadIdx.x; i < nm; i += kThreads) {
+      if (nm > p.mt_dense) nm = kAllTiles;  // X is in most tiles: the host marks it everywhere
+      for (uint32_t i = threadIdx.x; nm != kAllTiles && i < nm; i += kRT) {
         const uint32_t o = owner(s_pmt, i);
         sys_store(sl.hmlist + i,
                   __hip_atomic_load(sl.rtile + (size_t)o * kMtLds + (i - s_pmt[o]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1760,7 +1839,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
         if (threadIdx.x == 0) s_cmd[7] = atomicAdd(sl.dcount, 0u);
         __syncthreads();
         const uint32_t ngl = s_cmd[7];
-        for (uint32_t i = threadIdx.x; i < ngl; i += kThreads) {
+        for (uint32_t i = threadIdx.x; i < ngl; i += kRT) {
           const uint32_t key = atomicOr(&sl.dlist[i], 0u);
           const u64 sum = atomicExch(&sl.dsum[key], 0ull);
           const u64 ft = atomicExch(&sl.dft[key], kEmpty64);
@@ -1788,7 +1867,7 @@ __global__ __launch_bounds__(kThreads) void k_resident(ResParams p) {
     }
   }
   // ---- STOP (or the leader's time-out): the tiles go back to HBM
-  for (uint32_t i = wid; i < nt; i += kWaves) {
+  for (uint32_t i = wid; i < nt; i += kRW) {
     const uint32_t len = s_len[i];
     if constexpr (kLdsTok) {
       int32_t* dst = p.tok + s_toff[i];
@@ -2726,6 +2805,7 @@ Device::Device(int device_ordinal) : ordinal_(device_ordinal) {
   if (const char* e = std::getenv("SHREDWORD_INDEX")) index_on_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_HYBRID")) hybrid_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_RESIDENT_ARRIVE_POLLS")) res_arrive_polls_ = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char* e = std::getenv("SHREDWORD_RESIDENT_REGION_KEYS")) res_region_keys_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_SWITCH_OCC")) switch_occ_ = std::strtoull(e, nullptr, 10);
   int nb = 0;  // resident workgroups of k_merge per CU
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&k_merge<true>), kThreads, 0));
@@ -3785,11 +3865,14 @@ void Device::plan_resident(const TiledStream& ts) {
   const uint32_t W = G - kResFirstWorker;  // workers 2 .. G-1 (0 dispatches, 1 gathers)
   int max_lds = 0;
   HIP_OK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, ordinal_));
-  hipFuncAttributes fa;
+  hipFuncAttributes fa, fh;
   HIP_OK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_resident<true, true>)));
-  const long budget = (long)max_lds - (long)fa.sharedSizeBytes - 64;  // dynamic LDS per workgroup
-  // the dynamic region follows the statics unpadded: its 16-B LDS accesses need a 16-B base
-  if (budget <= 0 || fa.sharedSizeBytes % 16 != 0) return;
+  HIP_OK(hipFuncGetAttributes(&fh, reinterpret_cast<const void*>(&k_resident<true, false>)));
+  // dynamic LDS per workgroup: tokens in LDS (256 threads) / tokens in HBM (kResThreadsHbm threads,
+  // more staging); the dynamic region follows the statics unpadded: its 16-B accesses need a 16-B base
+  const long budget = (long)max_lds - (long)fa.sharedSizeBytes - 64;
+  const long budget_hbm = (long)max_lds - (long)fh.sharedSizeBytes - 64;
+  if (budget <= 0 || fa.sharedSizeBytes % 16 != 0 || fh.sharedSizeBytes % 16 != 0) return;
   // per tile: first and last word rank (tiles hold whole words in rank order), LDS words
   const size_t T = ntiles_;
   std::vector<uint32_t> rfirst(T), rlast(T), words(T);
@@ -3847,7 +3930,7 @@ void Device::plan_resident(const TiledStream& ts) {
   if (!res_lds_tok_) {  // the tokens stay in HBM; LDS holds weights and signatures
     tok_words = 0;
     shm = (size_t)nr_max * 8 + (size_t)nt_max * kResSigWords * 4;
-    if ((long)shm > budget) return;
+    if ((long)shm > budget_hbm) return;
   }
   res_grid_ = G;
   res_tok_words_ = tok_words;
@@ -3893,7 +3976,7 @@ void Device::plan_resident(const TiledStream& ts) {
                                  : reinterpret_cast<const void*>(&k_resident<true, false>);
   HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   int per_cu = 0;  // the persistent grid must be co-resident: at least one workgroup per CU
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kThreads, shm));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, res_lds_tok_ ? 256 : kResThreadsHbm, shm));
   if (per_cu < 1 || (long)per_cu * cu_count_ < (long)G) return;
   resident_ok_ = true;
   if (std::getenv("SHREDWORD_RESIDENT_REPORT"))
@@ -3945,6 +4028,8 @@ void Device::start_resident() {
   rp.leader_polls = 1u << 23;  // ~10 s without a command: the launch ends itself (the host relaunches)
   rp.keys_per_merge = keys_per_merge_;
   rp.slot_cap = min_slot_cap();
+  rp.region_keys = res_region_keys_;
+  rp.mt_dense = (uint32_t)(ntiles_ / 2);
   for (int k = 0; k < kResSlots; ++k) {
     MergeSlot& sl = slot_[k];
     ResSlot& r = rp.sl[k];
@@ -3973,8 +4058,8 @@ void Device::start_resident() {
   HIP_OK(hipEventRecord((hipEvent_t)res_ev_[0], S(stream_)));
   // a plain launch: one workgroup per CU by its LDS footprint, checked against the occupancy
   // query at plan time (plan_resident), so every workgroup is resident together
-  if (res_lds_tok_) k_resident<true, true><<<res_grid_, kThreads, res_shm_, S(stream_)>>>(rp);
-  else k_resident<true, false><<<res_grid_, kThreads, res_shm_, S(stream_)>>>(rp);
+  if (res_lds_tok_) k_resident<true, true><<<res_grid_, 256, res_shm_, S(stream_)>>>(rp);
+  else k_resident<true, false><<<res_grid_, kResThreadsHbm, res_shm_, S(stream_)>>>(rp);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord((hipEvent_t)res_ev_[1], S(stream_)));
   res_running_ = true;
@@ -4092,7 +4177,8 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   const u64* hs = (const u64*)(sl.host_count + 4);
   const size_t n = sl.host_count[0];
   const uint32_t nm = sl.host_count[2];
-  index_.set_tiles(X, sl.host_mlist, nm);
+  if (nm == kAllTiles) index_.set_all(X);
+  else index_.set_tiles(X, sl.host_mlist, nm);
   res_lat_us_ += 1e-2 * (double)hs[2];  // s_memrealtime: 100 MHz
   res_lat_n_ += 1;
   if (res_stamps_) {

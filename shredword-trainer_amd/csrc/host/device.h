@@ -357,6 +357,8 @@ class Device : public Backend {
   uint64_t res_aborts_ = 0;
   uint32_t* res_arrive_ = nullptr;      // k_resident: workgroups that started
   uint32_t res_arrive_polls_ = 20000;   // the leader's co-residency bound (~20 ms; env SHREDWORD_RESIDENT_ARRIVE_POLLS)
+  uint32_t res_region_keys_ = 32;       // participants with more delta keys add them to the global tables
+                                        // (env SHREDWORD_RESIDENT_REGION_KEYS)
   uint64_t wl_ms_seen_ = 0;        // merges already folded into times_
   double wl_kms_seen_ = 0;         // launch time already folded into times_
 

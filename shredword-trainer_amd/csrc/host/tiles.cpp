@@ -197,6 +197,16 @@ void TileIndex::set_tiles(int32_t id, const uint32_t* tiles, size_t n) {
   make(&ids_[id], std::move(v));
 }
 
+void TileIndex::set_all(int32_t id) {
+  if (id < 0) return;
+  if ((size_t)id >= ids_.size()) ids_.resize(id + 1);
+  Set& s = ids_[id];
+  s.list.clear();
+  s.bits.assign((ntiles_ + 63) / 64, ~0ull);
+  if (ntiles_ & 63) s.bits.back() = (1ull << (ntiles_ & 63)) - 1;
+  s.size = ntiles_;
+}
+
 bool TileIndex::candidates(int32_t a, int32_t b, std::vector<uint32_t>* out) const {
   out->clear();
   const size_t limit = ntiles_ / 2;  // beyond this a full scan is as cheap
