@@ -64,8 +64,11 @@ constexpr int kStPoolTop = 1, kStError = 3;
 constexpr uint32_t kErrPool = 1, kErrList = 2, kErrLookup = 4;
 
 struct WlCmd {
-  u64 g[4];  // granules (seq | value << 32): op | slot << 8, a, b, X
+  // granules (seq | value << 32): op | slot << 8, a, b, X, then the words-of list of max(a, b)
+  // when the host knows it (offset, count + 1; 0: look it up), one 64-B line
+  u64 g[8];
 };
+constexpr int kCmdGranules = 6;
 
 struct WlSlotDev {
   DeltaRecord* recs;  // host-visible
@@ -339,6 +342,7 @@ struct LoopS {
   uint32_t cmd[8];
   uint32_t nout, nchg, pool_top, err, scan, filter, nspill, qn;
   uint32_t rd, wr;  // run ints read (length + tokens of every scanned word) / written back (changed words)
+  u64 lst_x;        // the words-of list written for X (offset | (count + 1) << 32), for the host
   uint32_t st[4];
   u64 lk[2];  // word list: pool offset, count
   u64 need;   // filter bits the listed words must hold
@@ -372,15 +376,18 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       const u64* g = p.ring[expect % kRing].g;
       const u64 t_wait = __builtin_amdgcn_s_memrealtime();
       uint32_t op = 0, a = 0, b = 0, X = 0, idle = 0;
-      u64 v = lane < 4 ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+      u64 v = lane < kCmdGranules ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+      uint32_t loff = 0, lcnt1 = 0;
       for (;;) {
-        const bool tagged = lane >= 4 || (uint32_t)v == expect;
+        const bool tagged = lane >= kCmdGranules || (uint32_t)v == expect;
         if (__all(tagged)) {
           const uint32_t val = (uint32_t)(v >> 32);
           op = __shfl(val, 0, 64);
           a = __shfl(val, 1, 64);
           b = __shfl(val, 2, 64);
           X = __shfl(val, 3, 64);
+          loff = __shfl(val, 4, 64);
+          lcnt1 = __shfl(val, 5, 64);
           break;
         }
         if (++idle >= p.idle_polls) {
@@ -388,7 +395,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        v = lane < 4 ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+        v = lane < kCmdGranules ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
       }
       if (lane == 0) {
         S.cmd[0] = op & 0xFFu;
@@ -397,6 +404,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.cmd[3] = X;
         S.cmd[4] = (op >> 8) & 0xFFu;  // slot
         S.cmd[5] = expect;
+        S.cmd[6] = lcnt1;
+        S.cmd[7] = loff;
         S.t_wait = t_wait;
       }
     }
@@ -418,21 +427,22 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     if (wid == 0) {
       const bool undo = op == kOpUnmerge;
       const int32_t M = undo ? X : (a > b ? a : b);
+      const uint32_t given = undo ? 0u : S.cmd[6];  // the host sent M's words-of list: no lookup
       u64 lv64 = 0;
       bool lv = false;
-      if ((lane == 16 || lane == 17) && M >= 0 && (uint32_t)M < p.id_cap) {
+      if (!given && (lane == 16 || lane == 17) && M >= 0 && (uint32_t)M < p.id_cap) {
         if (lane == 16) lv = p.lseq[M] != kNoList;
         if (lane == 17) lv64 = p.lst[M];
       }
       const u64 key = pair_key(a, b);
       const u64 h = mix64(key) & p.dir_mask;
       u64 dk = kEmpty64, dv = 0;
-      if (!undo && lane < 16) {
+      if (!given && !undo && lane < 16) {
         dk = p.dkey[(h + (u64)lane) & p.dir_mask];
         dv = p.dval[(h + (u64)lane) & p.dir_mask];
       }
-      const bool has_list = (__ballot(lv) >> 16) & 1ull;
-      const u64 wl = __shfl(lv64, 17, 64);
+      const bool has_list = given || ((__ballot(lv) >> 16) & 1ull);
+      const u64 wl = given ? ((u64)S.cmd[7] | ((u64)(given - 1u) << 32)) : __shfl(lv64, 17, 64);
       u64 off = 0, cnt = 0, need = 0;
       bool err = false;
       if (has_list) {
@@ -621,10 +631,12 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     const uint32_t nchg = append ? S.nchg : 0u;
     if (tid == 0) {
       S.t[1] = __builtin_amdgcn_s_memrealtime() - t_cmd;
+      S.lst_x = 0;
       if (X >= 0 && (uint32_t)X < p.id_cap) {
         p.lst[X] = (u64)top | ((u64)nchg << 32);
         p.lseq[X] = seq;
         S.pool_top = top + nchg;
+        S.lst_x = (u64)top | ((u64)(nchg + 1u) << 32);  // for the host: offset, count + 1
       }
     }
     {
@@ -670,9 +682,11 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       // device time outside merges since the previous flag: waiting for commands, undoing guesses
       sd.hdr[20] = (uint32_t)(S.t_idle + (t_cmd - S.t_wait));
       sd.hdr[21] = (uint32_t)S.t_undo;
+      h64[12] = S.lst_x;  // X's words-of list (0: none)
       S.t_idle = 0;
       S.t_undo = 0;
       __threadfence_system();
+      h64[11] = (u64)__builtin_amdgcn_s_memrealtime() - t_cmd;  // diagnostic: after the write-back
       __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
@@ -1024,6 +1038,7 @@ void WordLoop::build_index() {
 // The directory, the words-of lists and the counters as right after build_index().
 void WordLoop::restore_index() {
   hipStream_t s = S(stream_);
+  std::fill(lists_.begin(), lists_.end(), 0ull);  // no words-of lists: every merge looks its pair up
   WL_OK(hipMemsetAsync(dkey_, 0xFF, dir_cap_ * sizeof(u64), s));
   if (init_keys_n_) {
     k_wl_dir_init<<<1024, 256, 0, s>>>(init_key_, init_val_, init_keys_n_, dkey_, dval_, dir_cap_ - 1);
@@ -1151,6 +1166,7 @@ void WordLoop::reserve(int32_t max_id) {
 
   id_cap_ = cap;
   cap_ = cap;
+  lists_.resize(cap, 0ull);
   ensure_slots(cap);
   WL_OK(hipStreamSynchronize(s));
 }
@@ -1205,7 +1221,7 @@ void WordLoop::recover_timeout() {
   }
 }
 
-uint32_t WordLoop::post(uint32_t op, int32_t a, int32_t b, int32_t X) {
+uint32_t WordLoop::post(uint32_t op, int32_t a, int32_t b, int32_t X, uint32_t loff, uint32_t lcnt1) {
   if (running_ && __atomic_load_n(&status_[0], __ATOMIC_ACQUIRE) == kOpTimeout) recover_timeout();
   if (!running_) {
     if (op == kOpStop) return 0;
@@ -1214,8 +1230,8 @@ uint32_t WordLoop::post(uint32_t op, int32_t a, int32_t b, int32_t X) {
   const uint32_t seq = ++seq_;
   const uint32_t slot = (uint32_t)X & (kSlots - 1);
   u64* g = static_cast<WlCmd*>(ring_)[seq % kRing].g;
-  const uint32_t vals[4] = {op | (slot << 8), (uint32_t)a, (uint32_t)b, (uint32_t)X};
-  for (int k = 0; k < 4; ++k) __atomic_store_n(&g[k], (u64)seq | ((u64)vals[k] << 32), __ATOMIC_RELAXED);
+  const uint32_t vals[kCmdGranules] = {op | (slot << 8), (uint32_t)a, (uint32_t)b, (uint32_t)X, loff, lcnt1};
+  for (int k = 0; k < kCmdGranules; ++k) __atomic_store_n(&g[k], (u64)seq | ((u64)vals[k] << 32), __ATOMIC_RELAXED);
   std::atomic_thread_fence(std::memory_order_release);
   return seq;
 }
@@ -1224,7 +1240,10 @@ void WordLoop::post_merge(int32_t a, int32_t b, int32_t X) {
   if (!ready_) fatal("WordLoop::post_merge before upload");
   if (posted_.size() >= (size_t)kSlots) fatal("WordLoop: every merge slot is in flight");
   if (X < 0 || (uint32_t)X + 2 > cap_) fatal("WordLoop: merge id beyond the reserved ids");
-  const uint32_t seq = post(kOpMerge, a, b, X);
+  // the words-of list of max(a, b), when a collected merge made it: the loop skips its lookup
+  const int32_t M = a > b ? a : b;
+  const uint64_t l = M >= 0 && (size_t)M < lists_.size() ? lists_[M] : 0;
+  const uint32_t seq = post(kOpMerge, a, b, X, (uint32_t)l, (uint32_t)(l >> 32));
   posted_.push_back({X, a, b, seq, now_seconds()});
   dirty_ = true;
 }
@@ -1274,11 +1293,13 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   if (timing_) {
     const uint32_t rec[kTraceFields] = {(uint32_t)X, h[2], h[12], h[3], (uint32_t)h64[2], (uint32_t)(10 * h64[3]),
                                         (uint32_t)(10 * h64[4]), (uint32_t)(10 * (h64[5] - h64[4])),
-                                        10 * h[16], 10 * h[17], 10 * h[18], 0u, 10 * h[20], 10 * h[21],
+                                        10 * h[16], 10 * h[17], 10 * h[18], (uint32_t)(10 * h64[11]), 10 * h[20],
+                                        10 * h[21],
                                         (uint32_t)(1e9 * (now_seconds() - pp.t_post))};
     trace_.insert(trace_.end(), rec, rec + kTraceFields);
   }
   if (n > sl.rec_cap) fatal("k_word_loop: record overflow");
+  if (h64[12] && (size_t)X < lists_.size()) lists_[X] = h64[12];
   *recs = sl.host_recs;
   return n;
 }

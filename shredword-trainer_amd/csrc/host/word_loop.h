@@ -151,7 +151,8 @@ class WordLoop {
   void restore_index();
   void launch(uint32_t seq0);  // the first command the launch takes
   void recover_timeout();
-  uint32_t post(uint32_t op, int32_t a, int32_t b, int32_t X);
+  // Writes one command; (loff, lcnt1): the words-of list of max(a, b) if known (count + 1; 0: none).
+  uint32_t post(uint32_t op, int32_t a, int32_t b, int32_t X, uint32_t loff = 0, uint32_t lcnt1 = 0);
   void wait_flag(const Slot& s, uint32_t seq);
   void ensure_slots(uint32_t cap);
 
@@ -159,6 +160,9 @@ class WordLoop {
   void* stream_ = nullptr;
   int32_t unk_ = 0;
   bool ready_ = false, running_ = false, dirty_ = false, timing_ = false;
+  // per id: the words-of list a collected merge wrote (offset | (count + 1) << 32; 0: none) --
+  // exactly the device's lst[] for confirmed merges, so a merge's command carries its list
+  std::vector<uint64_t> lists_;
 
   uint32_t nwords_ = 0;
   uint64_t nint_ = 0;          // int32 elements of the word runs (lengths + tokens + padding)
