@@ -683,10 +683,11 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       sd.hdr[20] = (uint32_t)(S.t_idle + (t_cmd - S.t_wait));
       sd.hdr[21] = (uint32_t)S.t_undo;
       h64[12] = S.lst_x;  // X's words-of list (0: none)
+      h64[13] = t_cmd;    // diagnostic: absolute device clock at the command and at the wait's start
+      h64[14] = S.t_wait;
       S.t_idle = 0;
       S.t_undo = 0;
-      __threadfence_system();
-      h64[11] = (u64)__builtin_amdgcn_s_memrealtime() - t_cmd;  // diagnostic: after the write-back
+      // one system-scope release (L2 write-back of the records and header, then the flag)
       __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
@@ -1275,7 +1276,8 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   posted_.erase(posted_.begin());
   const Slot& sl = slot_[(uint32_t)X & (kSlots - 1)];
   wait_flag(sl, pp.seq);
-  st_.wait_us += 1e6 * (now_seconds() - pp.t_post);
+  const double t_seen = now_seconds();
+  st_.wait_us += 1e6 * (t_seen - pp.t_post);
   const uint32_t* h = sl.host_hdr;
   const uint64_t* h64 = reinterpret_cast<const uint64_t*>(h);
   const size_t n = h[0];
@@ -1293,9 +1295,12 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   if (timing_) {
     const uint32_t rec[kTraceFields] = {(uint32_t)X, h[2], h[12], h[3], (uint32_t)h64[2], (uint32_t)(10 * h64[3]),
                                         (uint32_t)(10 * h64[4]), (uint32_t)(10 * (h64[5] - h64[4])),
-                                        10 * h[16], 10 * h[17], 10 * h[18], (uint32_t)(10 * h64[11]), 10 * h[20],
-                                        10 * h[21],
-                                        (uint32_t)(1e9 * (now_seconds() - pp.t_post))};
+                                        10 * h[16], 10 * h[17], 10 * h[18], 0u, 10 * h[20],
+                                        10 * h[21], (uint32_t)(1e9 * (t_seen - pp.t_post)),
+                                        // absolute clocks for a timeline: host 10 ns units since the
+                                        // loop was made, device ticks (100 MHz), low 32 bits
+                                        (uint32_t)(1e8 * (pp.t_post - t_epoch_)), (uint32_t)(1e8 * (t_seen - t_epoch_)),
+                                        (uint32_t)h64[13], (uint32_t)h64[14]};
     trace_.insert(trace_.end(), rec, rec + kTraceFields);
   }
   if (n > sl.rec_cap) fatal("k_word_loop: record overflow");

@@ -124,8 +124,10 @@ class WordLoop {
   // then thread 0's stamps (ns after the command): pool entries loaded, first run loaded, first
   // word merged; and ns spent building pair groups this merge needed first; then the device ns
   // outside merges since the previous merge's flag (waiting for commands; undoing guesses), and
-  // the host ns from posting this merge to seeing its flag.
-  static constexpr int kTraceFields = 15;
+  // the host ns from posting this merge to seeing its flag; then absolute clocks: host post and
+  // flag seen (10 ns since the loop was made), device command seen and wait begun (100 MHz
+  // ticks), low 32 bits each.
+  static constexpr int kTraceFields = 19;
   const std::vector<uint32_t>& trace() const { return trace_; }
   void set_timing(bool on) { timing_ = on; }
   size_t device_bytes() const { return bytes_; }
@@ -163,6 +165,7 @@ class WordLoop {
   // per id: the words-of list a collected merge wrote (offset | (count + 1) << 32; 0: none) --
   // exactly the device's lst[] for confirmed merges, so a merge's command carries its list
   std::vector<uint64_t> lists_;
+  double t_epoch_ = now_seconds();  // the trace's host clock origin
 
   uint32_t nwords_ = 0;
   uint64_t nint_ = 0;          // int32 elements of the word runs (lengths + tokens + padding)

@@ -71,15 +71,16 @@ class BPETrainer:
         option is on): numpy uint32 array (merges, 15) of X, listed words, scanned words, changed
         words, occurrences, device ns command -> flag, lookup ns, scan ns, wave 0's stamps
         (ns after the command: pool entries loaded, first run loaded, first word merged, unused),
-        device ns since the previous flag spent waiting for commands and undoing guesses, and
-        host ns from post to flag."""
+        device ns since the previous flag spent waiting for commands and undoing guesses, host ns
+        from post to flag, then absolute clocks (low 32 bits): host post and flag seen (10 ns
+        units), device command seen and wait begun (100 MHz ticks)."""
         import numpy as np
         n = lib.shred_index_trace(self.trainer, None, 0)
         if n < 0:
             raise RuntimeError("no device")
         out = np.empty(n, dtype=np.uint32)
         lib.shred_index_trace(self.trainer, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n)
-        return out.reshape(-1, 15)
+        return out.reshape(-1, 19)
 
     def stats(self) -> dict:
         s = ShredStats()

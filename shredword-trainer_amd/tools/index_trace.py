@@ -43,7 +43,7 @@ def main():
     t.destroy()
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     np.save(args.out, tr)
-    X, listed, scanned, changed, occ, dev, look, scan, s0, s1, s2, s3, idle, undo, hflag = tr.T
+    X, listed, scanned, changed, occ, dev, look, scan, s0, s1, s2, s3, idle, undo, hflag = tr.T[:15]
     rows = []
     edges = [0, 16, 64, 256, 1024, 4096, 16384, len(tr)]
     for lo, hi in zip(edges[:-1], edges[1:]):

@@ -42,6 +42,20 @@ __global__ void k_read_lat(const u64* host, int n, u64* out) {
   out[1] = idx;
 }
 
+// The shader clock one lone workgroup runs at: s_memtime (core clock) against s_memrealtime
+// (100 MHz) over a dependent ALU loop.
+__global__ void k_clock(int iters, u64* out) {
+  const u64 c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned x = threadIdx.x;
+  for (int i = 0; i < iters; ++i) x = x * 1664525u + 1013904223u;
+  const u64 c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    out[0] = c1 - c0;
+    out[1] = r1 - r0;
+    out[2] = x;
+  }
+}
+
 // mode: 0 sleep, 1 spin, 2 pipe; ans: 0 fence, 1 wt
 __global__ void k_pong(const u64* cmd, u64* ans, int iters, int mode, int wt, u64* dev_ticks) {
   if (threadIdx.x >= 64) return;
@@ -112,6 +126,13 @@ int main(int argc, char** argv) {
   u64 r[2];
   OK(hipMemcpy(r, dbuf, 16, hipMemcpyDeviceToHost));
   std::printf("{\"read_rtt_us\": %.3f", 1e-2 * (double)r[0] / nr);
+  for (int rep = 0; rep < 3; ++rep) {
+    k_clock<<<1, 512>>>(20000000, dbuf);
+    OK(hipDeviceSynchronize());
+    u64 c[3];
+    OK(hipMemcpy(c, dbuf, 24, hipMemcpyDeviceToHost));
+    std::printf(", \"lone_wg_clock_mhz_%d\": %.0f", rep, 100.0 * (double)c[0] / (double)c[1]);
+  }
   const char* names[3] = {"sleep", "spin", "pipe"};
   hipStream_t s;
   OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
