@@ -295,8 +295,9 @@ std::vector<Entry> shard_entries(const uint8_t* d, size_t n, const LoadOptions& 
   if (opt.gpu_device >= 0 && e > b && e - b >= opt.gpu_min_bytes) {
     std::vector<WordRec> recs;
     std::string why;
-    if (gpu_count_words(opt.gpu_device, d + b, e - b, &recs, &why)) {
+    if (gpu_count_words(opt.gpu_device, d + b, e - b, &recs, &why, /*staged=*/b > 0)) {
       *on_gpu = true;
+      const double th = now_seconds();
       mine.resize(recs.size());
       parallel_for(threads, (recs.size() + 4095) / 4096, [&](size_t blk, int) {
         const size_t i1 = std::min(recs.size(), (blk + 1) * 4096);
@@ -305,6 +306,9 @@ std::vector<Entry> shard_entries(const uint8_t* d, size_t n, const LoadOptions& 
           mine[i] = Entry{word_hash(d + f, recs[i].len), f, recs[i].count, recs[i].len};
         }
       });
+      if (std::getenv("SHREDWORD_LOAD_REPORT"))
+        std::fprintf(stderr, "[LOAD] range %llu/%llu: %zu word hashes %.1f ms\n", (unsigned long long)r,
+                     (unsigned long long)W, recs.size(), 1e3 * (now_seconds() - th));
       return mine;
     }
     std::fprintf(stderr, "[WARNING]\t GPU word count unavailable (%s): counting on the host\n", why.c_str());

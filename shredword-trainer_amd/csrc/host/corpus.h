@@ -69,7 +69,9 @@ struct WordRec {
 // GPU word count: the distinct words of d[0, n) in reference word order
 // (djb2(word) & 4095, first occurrence).  d must not contain NUL bytes (those files keep the
 // host's fgets/strlen path).  False (reason in *why) when no device is usable.
-bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec>* out, std::string* why);
+// staged: d is a range inside a larger mapping (a sharded load): uploaded through pinned buffers.
+bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec>* out, std::string* why,
+                     bool staged = false);
 
 // Returns 0 on success, -1 if the file cannot be opened/mapped (message in *err).
 int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::string* err);

@@ -82,3 +82,37 @@ def case_corpus(corpus_dir):
 def oracle_bin():
     subprocess.run(["make", "-s", "-C", ORACLE, "port"], check=True)
     return os.path.join(ORACLE, "_build", "bpe_oracle")
+
+
+def progress(msg):
+    """A progress line for long GPU tests: appended to $SHREDWORD_HEARTBEAT_FILE when set (pytest
+    captures fds 1 and 2, so a harness that kills silent commands watches a file instead)."""
+    path = os.environ.get("SHREDWORD_HEARTBEAT_FILE")
+    if path:
+        with open(path, "a") as f:
+            f.write(msg + "\n")
+
+
+@pytest.fixture(autouse=True)
+def _heartbeat(request):
+    """Long GPU tests (full-size corpora: generation, load, training) write a progress line every
+    30 s (see progress())."""
+    if request.node.get_closest_marker("gpu") is None or not os.environ.get("SHREDWORD_HEARTBEAT_FILE"):
+        yield
+        return
+    import threading
+    import time
+    done = threading.Event()
+    t0 = time.time()
+
+    def beat():
+        while not done.wait(30.0):
+            progress(f"[heartbeat] {request.node.nodeid} running {time.time() - t0:.0f} s")
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        yield
+    finally:
+        done.set()
+        th.join(timeout=1.0)

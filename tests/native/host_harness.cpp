@@ -440,7 +440,7 @@ uint64_t hh_word(void* p, uint64_t i, uint8_t* buf, uint64_t cap, uint64_t* coun
 // The harness has no device: the loader's GPU word count (hip/load_device.hip) is absent here,
 // so load_corpus always takes the host count.
 namespace shred {
-bool gpu_count_words(int, const uint8_t*, size_t, std::vector<WordRec>*, std::string* why) {
+bool gpu_count_words(int, const uint8_t*, size_t, std::vector<WordRec>*, std::string* why, bool) {
   if (why) *why = "host harness: no device";
   return false;
 }

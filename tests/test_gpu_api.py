@@ -405,7 +405,11 @@ def test_full_size_matches_oracle_run(name, tmp_path, monkeypatch):
     parameters (vocab 64000, coverage 0.9995, mixed script) on 10 GB, c4_10g = C4's parameters
     on 10 GB through the 8-way sharded load."""
     import hashlib
+    import time
+    from conftest import progress
+    t0 = time.time()
     case, corpus = _fullsize(name)
+    progress(f"[{name}] corpus ready {time.time() - t0:.0f} s")
     for k, v in _FULLSIZE_ENV.get(name, {}).items():
         monkeypatch.setenv(k, v)
     cfg = case["config"]
@@ -414,7 +418,9 @@ def test_full_size_matches_oracle_run(name, tmp_path, monkeypatch):
     trace = str(tmp_path / "trace.txt")
     t.set_option("trace", trace)
     t.load_corpus(corpus)
+    progress(f"[{name}] loaded {time.time() - t0:.0f} s")
     n, model, vocab = _train_bytes(t, tmp_path, name)
+    progress(f"[{name}] trained {time.time() - t0:.0f} s")
     st = t.stats()
     t.destroy()
     assert (st["num_words"], st["num_symbols"]) == (case["distinct_words"], case["symbols"])
