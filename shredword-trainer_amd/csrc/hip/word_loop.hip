@@ -956,9 +956,6 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
   WL_OK(hipMemcpyAsync(tile_first_, tfirst.data(), ntiles_ * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   WL_OK(hipMemcpyAsync(tile_nw_, tnw.data(), ntiles_ * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   WL_OK(hipMemcpyAsync(wtok_, wtok0_, (nint_ + kRunPad) * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-  // pool: the initial index (<= one entry per adjacent pair) and the words-of lists of the run:
-  // a merge lists only the words it shortened, so Σ over a run <= Σ (length - 1); the lists of
-  // undone guesses are released (each is the last one when its undo runs)
   // pool: the initial index (<= one entry per adjacent pair), the words-of lists (a merge lists
   // the words it shortened: Σ over a run <= Σ (length - 1)) and the pair groups (<= 2 entries
   // per occurrence merged: Σ <= 2 Σ (length - 1)); undone guesses release theirs (each is the
