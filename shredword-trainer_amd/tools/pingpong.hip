@@ -8,6 +8,9 @@
 //            fence  = the answer after a plain store + __threadfence_system (release)
 //            wt     = the answer as a system-scope (write-through) store after s_waitcnt vmcnt(0)
 //   The answer is a tagged 8-byte word, so the host reads it with no further ordering.
+//   vram   : (./pingpong N vram) the command word in fine-grained device memory
+//            (hipExtMallocWithFlags hipDeviceMallocFinegrained) written by the CPU through its
+//            mapping; the device polls its own memory, so a poll costs no PCIe round trip.
 // Build: hipcc -O3 --offload-arch=gfx950 -o pingpong pingpong.hip ; run: ./pingpong [iters]
 #include <hip/hip_runtime.h>
 
@@ -15,6 +18,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define OK(x)                                                                 \
@@ -162,6 +166,44 @@ int main(int argc, char** argv) {
       std::printf(", \"pp_%s_%s_us\": {\"mean\": %.3f, \"p50\": %.3f, \"p10\": %.3f, \"p90\": %.3f}", names[mode],
                   wt ? "wt" : "fence", sum / iters, lat[iters / 2], lat[iters / 10], lat[iters * 9 / 10]);
     }
+  }
+  if (argc > 2 && std::string(argv[2]) == "vram") {
+    u64* vcmd = nullptr;
+    OK(hipExtMallocWithFlags((void**)&vcmd, 4096, hipDeviceMallocFinegrained));
+    hipPointerAttribute_t at;
+    OK(hipPointerGetAttributes(&at, vcmd));
+    std::printf(", \"vram_host_ptr\": \"%p\", \"vram_dev_ptr\": \"%p\"", at.hostPointer, at.devicePointer);
+    volatile u64* hv = static_cast<volatile u64*>(at.hostPointer ? at.hostPointer : (void*)vcmd);
+    *hv = 0;  // the CPU mapping (a fault here ends this mode only)
+    std::fflush(stdout);
+    k_read_lat<<<1, 64>>>(vcmd, nr, dbuf);
+    OK(hipDeviceSynchronize());
+    OK(hipMemcpy(r, dbuf, 16, hipMemcpyDeviceToHost));
+    std::printf(", \"vram_read_rtt_us\": %.3f", 1e-2 * (double)r[0] / nr);
+    for (int mode = 0; mode < 2; ++mode) {
+      volatile u64* ans = hbuf + 64;
+      *hv = 0;
+      *ans = 0;
+      k_pong<<<1, 64, 0, s>>>(vcmd, hdev + 64, iters, mode, 0, dbuf);
+      OK(hipGetLastError());
+      std::vector<double> lat;
+      lat.reserve(iters);
+      for (int i = 1; i <= iters; ++i) {
+        const double t0 = now_us();
+        __atomic_store_n(const_cast<u64*>(hv), (u64)i, __ATOMIC_RELEASE);
+        while (__atomic_load_n(const_cast<u64*>(ans), __ATOMIC_ACQUIRE) != (u64)i) __builtin_ia32_pause();
+        lat.push_back(now_us() - t0);
+        const double tw = now_us();
+        while (now_us() - tw < 3.0) __builtin_ia32_pause();
+      }
+      OK(hipStreamSynchronize(s));
+      std::sort(lat.begin(), lat.end());
+      double sum = 0;
+      for (double x : lat) sum += x;
+      std::printf(", \"pp_vram_%s_fence_us\": {\"mean\": %.3f, \"p50\": %.3f, \"p10\": %.3f, \"p90\": %.3f}",
+                  names[mode], sum / iters, lat[iters / 2], lat[iters / 10], lat[iters * 9 / 10]);
+    }
+    OK(hipFree(vcmd));
   }
   std::printf("}\n");
   OK(hipHostFree(hbuf));
