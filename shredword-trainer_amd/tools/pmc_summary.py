@@ -33,6 +33,11 @@ def main():
     res = {"workload": a.workload, "layout": a.layout,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (KiB per dispatch); "
                      "read bytes = 2 x FETCH_SIZE (gfx950 16-B/lane reads), write bytes = WRITE_SIZE",
+           "calibration": "the x2 on FETCH_SIZE is calibrated for 16-B/lane streaming reads only "
+                          "(MI355X_MICROARCH.md, HBM); other access widths are uncalibrated, so for kernels that "
+                          "read by hash probes, atomics and random lines (k_word_count, k_cache_*) the read bytes "
+                          "lie between hbm_bytes_per_launch_fetch_raw and hbm_bytes_per_launch; Infinity Cache "
+                          "hits are counted, not excluded",
            "kernels": {}}
     for k in sorted(set(f) | set(w)):
         fv, wv = f.get(k, []), w.get(k, [])
@@ -40,7 +45,10 @@ def main():
         wr = 1024.0 * (sum(wv) / len(wv)) if wv else None
         res["kernels"][k] = {"launches": max(len(fv), len(wv)), "read_bytes_per_launch": rd,
                              "write_bytes_per_launch": wr,
-                             "hbm_bytes_per_launch": (rd or 0.0) + (wr or 0.0)}
+                             "hbm_bytes_per_launch": (rd or 0.0) + (wr or 0.0),
+                             # FETCH_SIZE as counted (no x2): the lower bound for kernels whose
+                             # reads are not 16-B/lane streams (hash probes, atomics, random lines)
+                             "hbm_bytes_per_launch_fetch_raw": (rd or 0.0) / 2.0 + (wr or 0.0)}
     json.dump(res, open(a.out, "w"), indent=1)
     for k, v in res["kernels"].items():
         print(f"{k:28s} launches {v['launches']:6d}  HBM bytes/launch {v['hbm_bytes_per_launch'] / 1e6:10.3f} MB")
