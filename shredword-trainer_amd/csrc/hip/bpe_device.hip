@@ -975,7 +975,7 @@ constexpr int kResDeltaW = 1024;         // LDS delta slots per workgroup (spill
 constexpr int kResSigBits = 4096;        // per-tile pair signature held in LDS (Bloom, 2 hashes)
 constexpr int kResSigWords = kResSigBits / 32;
 constexpr uint32_t kResSigRebuild = 192;  // pairs added to a tile's signature before it is rebuilt
-constexpr uint32_t kResMaxTiles = 256;   // tiles one workgroup may own
+constexpr uint32_t kResMaxTiles = 320;   // tiles one workgroup may own (C5 at 100 GB: 271)
 constexpr uint32_t kOpMerge = 1, kOpStop = 2, kOpTimeout = 3;
 
 // host command ring, device command ring, per-workgroup queues: at most 10 commands are ever
@@ -1043,6 +1043,8 @@ struct ResParams {
   uint32_t seq0;             // first command number of this launch
   uint32_t leader_polls;     // idle leader iterations before the launch ends itself
   uint32_t keys_per_merge, slot_cap;
+  uint32_t sig_words;        // LDS signature words per tile (kResSigWords, or a half / quarter of it)
+  uint32_t w_global;         // 1: the weights stay in HBM (w_words = 0), read per matched occurrence
   uint32_t region_keys;      // a participant with more LDS delta keys adds them to the global tables
   uint32_t mt_dense;         // more matched tiles than this: the host index marks X in every tile
   ResSlot sl[Device::kResSlots];  // merge X uses sl[X % kResSlots]
@@ -1068,30 +1070,32 @@ __device__ __forceinline__ void q_pack(uint32_t cnt, uint32_t pi, uint32_t op, u
   *h1 = c | ((u64)((uint32_t)b & 0xFFFFFu) << 16) | ((u64)((uint32_t)X & 0xFFFFFu) << 36);
 }
 
-__device__ __forceinline__ void res_sig_bits(int32_t x, int32_t y, uint32_t* h1, uint32_t* h2) {
+// sm = the tile signature's bit count - 1 (kResSigBits, or a half / quarter of it when the table
+// needs a smaller LDS plan: Device::plan_resident)
+__device__ __forceinline__ void res_sig_bits(int32_t x, int32_t y, uint32_t* h1, uint32_t* h2, uint32_t sm) {
   uint32_t k = (uint32_t)x * 0x9E3779B1u ^ ((uint32_t)y + 0x7F4A7C15u) * 0x85EBCA77u;
   k ^= k >> 15;
   k *= 0x2C1B3C6Du;
   k ^= k >> 12;
   k *= 0x297A2D39u;
   k ^= k >> 15;
-  *h1 = k & (kResSigBits - 1);
-  *h2 = (k >> 16) & (kResSigBits - 1);
+  *h1 = k & sm;
+  *h2 = (k >> 16) & sm;
 }
-__device__ __forceinline__ bool res_sig_test(const uint32_t* sg, int32_t x, int32_t y) {
+__device__ __forceinline__ bool res_sig_test(const uint32_t* sg, int32_t x, int32_t y, uint32_t sm) {
   uint32_t h1, h2;
-  res_sig_bits(x, y, &h1, &h2);
+  res_sig_bits(x, y, &h1, &h2, sm);
   return ((sg[h1 >> 5] >> (h1 & 31)) & 1u) && ((sg[h2 >> 5] >> (h2 & 31)) & 1u);
 }
 // Rebuilds a tile's LDS signature from its tokens t[0, len) (one wave).
-__device__ __forceinline__ void res_sig_build(uint32_t* sg, const int32_t* t, uint32_t len, int lane) {
-  for (int w = lane; w < kResSigWords; w += 64) sg[w] = 0;
+__device__ __forceinline__ void res_sig_build(uint32_t* sg, const int32_t* t, uint32_t len, int lane, uint32_t sm) {
+  for (int w = lane; w < (int)((sm + 1) >> 5); w += 64) sg[w] = 0;
   wave_lds_sync();
   for (uint32_t i = (uint32_t)lane; i + 1 < len; i += 64) {
     const int32_t x = t[i], y = t[i + 1];
     if (!is_hdr(x) && !is_hdr(y)) {
       uint32_t h1, h2;
-      res_sig_bits(x, y, &h1, &h2);
+      res_sig_bits(x, y, &h1, &h2, sm);
       atomicOr(&sg[h1 >> 5], 1u << (h1 & 31));
       atomicOr(&sg[h2 >> 5], 1u << (h2 & 31));
     }
@@ -1113,21 +1117,29 @@ __device__ __forceinline__ void res_load_tile(const int32_t* tb, int lane, TileR
   for (int q = 0; q < kPer / 4; ++q) r->q[q] = *reinterpret_cast<const int4*>(tb + p0 + 4 * q);
 }
 
+// The per-launch plan the merge body needs beside the tile: signature mask, and where the word
+// weights live (LDS s_w from rank r0, or HBM when the table's weights do not fit LDS).
+struct ResPlan {
+  uint32_t sm;
+  const u64* gw;  // non-null: weights from HBM (indexed by rank)
+};
+
 template <bool kWeighted>
 __device__ __forceinline__ uint32_t res_merge_body(int32_t* tb, const TileRegs& tr, uint32_t* lenp, uint32_t* sg,
                                                    uint32_t* sgadd, int32_t* st, const u64* s_w, uint32_t r0, int32_t a,
                                                    int32_t b, int32_t X, ResDelta& h, const ResSlot& p,
-                                                   uint32_t slot_cap, int lane, u64* n_written);
+                                                   uint32_t slot_cap, int lane, u64* n_written, const ResPlan& rp);
 
 template <bool kWeighted>
 __device__ __forceinline__ uint32_t res_merge_tile(int32_t* tb, uint32_t* lenp, uint32_t* sg, uint32_t* sgadd, int32_t* st,
                                                    const u64* s_w,
                                                    uint32_t r0, int32_t a, int32_t b, int32_t X, ResDelta& h,
-                                                   const ResSlot& p, uint32_t slot_cap, int lane, u64* n_written) {
-  if (!res_sig_test(sg, a, b)) return 0;  // the pair cannot be in this tile
+                                                   const ResSlot& p, uint32_t slot_cap, int lane, u64* n_written,
+                                                   const ResPlan& rp) {
+  if (!res_sig_test(sg, a, b, rp.sm)) return 0;  // the pair cannot be in this tile
   TileRegs tr;
   res_load_tile(tb, lane, &tr);
-  return res_merge_body<kWeighted>(tb, tr, lenp, sg, sgadd, st, s_w, r0, a, b, X, h, p, slot_cap, lane, n_written);
+  return res_merge_body<kWeighted>(tb, tr, lenp, sg, sgadd, st, s_w, r0, a, b, X, h, p, slot_cap, lane, n_written, rp);
 }
 
 // The merge of one tile whose 16 tokens per lane are already in registers (tr).
@@ -1135,7 +1147,7 @@ template <bool kWeighted>
 __device__ __forceinline__ uint32_t res_merge_body(int32_t* tb, const TileRegs& tr, uint32_t* lenp, uint32_t* sg,
                                                    uint32_t* sgadd, int32_t* st, const u64* s_w, uint32_t r0, int32_t a,
                                                    int32_t b, int32_t X, ResDelta& h, const ResSlot& p,
-                                                   uint32_t slot_cap, int lane, u64* n_written) {
+                                                   uint32_t slot_cap, int lane, u64* n_written, const ResPlan& rp) {
   const uint32_t len = *lenp;
   const int p0 = lane * kPer;
   int32_t v[kPer];
@@ -1225,7 +1237,7 @@ __device__ __forceinline__ uint32_t res_merge_body(int32_t* tb, const TileRegs& 
       const uint32_t hidx = (uint32_t)(hdr >> 32) - 1u;
       const uint32_t rank = (uint32_t)hdr;
       const uint32_t gi = p0 + j;
-      const u64 w = kWeighted ? s_w[rank - r0] : 1ull;
+      const u64 w = kWeighted ? (rp.gw ? rp.gw[rank] : s_w[rank - r0]) : 1ull;
       const u64 ftb = ((u64)rank << 32) | ((u64)(gi - hidx - 1u) << 2);
       const bool vl = gi - 1u > hidx;  // a left neighbour inside the word (X if it was just merged)
       const int32_t left = ((m_ext >> j) & 1u) ? X : st[SK(1 + p0 + j)];
@@ -1266,8 +1278,8 @@ __device__ __forceinline__ uint32_t res_merge_body(int32_t* tb, const TileRegs& 
       }
       // the tile's signature gains the new pairs (a superset stays valid; rebuilt when loose)
       uint32_t h1, h2, h3, h4;
-      res_sig_bits(left, X, &h1, &h2);
-      res_sig_bits(X, right, &h3, &h4);
+      res_sig_bits(left, X, &h1, &h2, rp.sm);
+      res_sig_bits(X, right, &h3, &h4, rp.sm);
       atomicOr(&sg[h1 >> 5], vl ? 1u << (h1 & 31) : 0u);
       atomicOr(&sg[h2 >> 5], vl ? 1u << (h2 & 31) : 0u);
       atomicOr(&sg[h3 >> 5], vr ? 1u << (h3 & 31) : 0u);
@@ -1286,9 +1298,9 @@ __device__ __forceinline__ uint32_t res_merge_body(int32_t* tb, const TileRegs& 
   }
   // a tile whose signature gathered many added pairs since its last build is re-signed below
   const uint32_t added = *sgadd + 2u * (uint32_t)matches;
-  const bool rebuild = added > kResSigRebuild;
+  const bool rebuild = added > (kResSigRebuild * (rp.sm + 1)) / (uint32_t)kResSigBits;  // scaled with the signature
   if (rebuild)
-    for (int w = lane; w < kResSigWords; w += 64) sg[w] = 0;
+    for (int w = lane; w < (int)((rp.sm + 1) >> 5); w += 64) sg[w] = 0;
   wave_lds_sync();
   int32_t c[kPer + 1];  // this lane's compacted tokens (kPad past the end) and the next one
 #pragma unroll
@@ -1313,7 +1325,7 @@ __device__ __forceinline__ uint32_t res_merge_body(int32_t* tb, const TileRegs& 
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {  // signature of the compacted tile (OR of 0 where no pair)
       uint32_t h1, h2;
-      res_sig_bits(c[j], c[j + 1], &h1, &h2);
+      res_sig_bits(c[j], c[j + 1], &h1, &h2, rp.sm);
       const bool pr = !is_hdr(c[j]) && !is_hdr(c[j + 1]);
       atomicOr(&sg[h1 >> 5], pr ? 1u << (h1 & 31) : 0u);
       atomicOr(&sg[h2 >> 5], pr ? 1u << (h2 & 31) : 0u);
@@ -1328,7 +1340,7 @@ __device__ __forceinline__ uint32_t res_merge_body(int32_t* tb, const TileRegs& 
 // speculative merge that the host did not confirm; the tile's length grows back, within its
 // original LDS capacity.  The signature is rebuilt exactly.
 __device__ __forceinline__ void res_unmerge_tile(int32_t* tb, uint32_t* lenp, uint32_t* sg, uint32_t* sgadd, int32_t* st,
-                                                 int32_t a, int32_t b, int32_t X, int lane) {
+                                                 int32_t a, int32_t b, int32_t X, int lane, uint32_t sm) {
   const uint32_t len = *lenp;
   const int p0 = lane * kPer;
   int32_t v[kPer];
@@ -1361,7 +1373,7 @@ __device__ __forceinline__ void res_unmerge_tile(int32_t* tb, uint32_t* lenp, ui
     o += live ? (isx ? 2 : 1) : 0;
   }
   wave_lds_sync();
-  for (int i = lane; i < kResSigWords; i += 64) sg[i] = 0;
+  for (int i = lane; i < (int)((sm + 1) >> 5); i += 64) sg[i] = 0;
   int32_t c[kPer + 1];
 #pragma unroll
   for (int j = 0; j <= kPer; ++j) {
@@ -1383,7 +1395,7 @@ __device__ __forceinline__ void res_unmerge_tile(int32_t* tb, uint32_t* lenp, ui
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     uint32_t h1, h2;
-    res_sig_bits(c[j], c[j + 1], &h1, &h2);
+    res_sig_bits(c[j], c[j + 1], &h1, &h2, sm);
     const bool pr = !is_hdr(c[j]) && !is_hdr(c[j + 1]);
     atomicOr(&sg[h1 >> 5], pr ? 1u << (h1 & 31) : 0u);
     atomicOr(&sg[h2 >> 5], pr ? 1u << (h2 & 31) : 0u);
@@ -1407,6 +1419,8 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
   int32_t* s_res = s_dyn;                                     // the tiles' tokens
   u64* s_w = reinterpret_cast<u64*>(s_dyn + p.tok_words);     // the words' weights
   uint32_t* s_sig = reinterpret_cast<uint32_t*>(s_dyn + p.tok_words + 2 * p.w_words);  // per-tile signatures
+  const uint32_t sw = p.sig_words;
+  const ResPlan rplan{sw * 32u - 1u, p.w_global ? reinterpret_cast<const u64*>(p.weight) : nullptr};
   __shared__ int32_t s_tok[kRW][kStPad + 64];  // + a trash word per lane (branch-free compaction)
   __shared__ ResDelta h;
   __shared__ uint32_t s_len[kResMaxTiles], s_lofs[kResMaxTiles], s_sigadd[kResMaxTiles];
@@ -1446,7 +1460,7 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
     h.ft[i] = kEmpty64;
   }
   if (kWeighted)
-    for (uint32_t i = threadIdx.x; i < nr; i += kRT) s_w[i] = p.weight[r0 + i];
+    for (uint32_t i = threadIdx.x; nr && !p.w_global && i < nr; i += kRT) s_w[i] = p.weight[r0 + i];
   if (threadIdx.x == 0) h.spill = 0;
   __syncthreads();
   auto tile_ptr = [&](uint32_t i) -> int32_t* {
@@ -1462,7 +1476,7 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
         *reinterpret_cast<int4*>(dst + 4 * q) = *reinterpret_cast<const int4*>(src + 4 * q);
       wave_lds_sync();
     }
-    res_sig_build(s_sig + (size_t)i * kResSigWords, tile_ptr(i), s_len[i], lane);
+    res_sig_build(s_sig + (size_t)i * sw, tile_ptr(i), s_len[i], lane, rplan.sm);
   }
   __syncthreads();
 
@@ -1599,8 +1613,8 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
     const uint32_t lm_bit = 1u << ((uint32_t)X & 7u);
     if (op == kOpUnmerge) {  // undo merge X, a wrong guess (the host undoes them newest first)
       for (uint32_t i = wid; i < nt; i += kRW)
-        if (s_lm[i] & lm_bit) res_unmerge_tile(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords, &s_sigadd[i], st,
-                                      a, b, X, lane);
+        if (s_lm[i] & lm_bit) res_unmerge_tile(tile_ptr(i), &s_len[i], s_sig + (size_t)i * sw, &s_sigadd[i], st,
+                                      a, b, X, lane, rplan.sm);
       __syncthreads();
       continue;
     }
@@ -1617,9 +1631,9 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
     };
     if constexpr (kLdsTok) {
       for (uint32_t i = wid; i < nt; i += kRW) {
-        const uint32_t m = res_merge_tile<kWeighted>(tile_ptr(i), &s_len[i], s_sig + (size_t)i * kResSigWords,
+        const uint32_t m = res_merge_tile<kWeighted>(tile_ptr(i), &s_len[i], s_sig + (size_t)i * sw,
                                                      &s_sigadd[i], st, s_w, r0, a, b, X, h, sl, p.slot_cap, lane,
-                                                     &n_written);
+                                                     &n_written, rplan);
         note(i, m);
       }
     } else {
@@ -1627,7 +1641,7 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
       // this one merges (tiles the signature rules out are only noted)
       auto skip_to = [&](uint32_t i) {
         for (; i < nt; i += kRW) {
-          if (res_sig_test(s_sig + (size_t)i * kResSigWords, a, b)) break;
+          if (res_sig_test(s_sig + (size_t)i * sw, a, b, rplan.sm)) break;
           note(i, 0);
         }
         return i;
@@ -1639,9 +1653,9 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
         const uint32_t j = skip_to(i + kRW);
         TileRegs nxt;
         if (j < nt) res_load_tile(tile_ptr(j), lane, &nxt);
-        const uint32_t m = res_merge_body<kWeighted>(tile_ptr(i), cur, &s_len[i], s_sig + (size_t)i * kResSigWords,
+        const uint32_t m = res_merge_body<kWeighted>(tile_ptr(i), cur, &s_len[i], s_sig + (size_t)i * sw,
                                                      &s_sigadd[i], st, s_w, r0, a, b, X, h, sl, p.slot_cap, lane,
-                                                     &n_written);
+                                                     &n_written, rplan);
         note(i, m);
         cur = nxt;
         i = j;
@@ -1683,7 +1697,7 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
       if (to_global && threadIdx.x == 0) h.spill = 1;
       const uint32_t nmt = s_nmt;
       for (uint32_t i = threadIdx.x; i < nmt; i += kRT)
-        __hip_atomic_store(sl.rtile + (size_t)pi * kMtLds + i, s_mt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sl.rtile + (size_t)pi * kResMaxTiles + i, s_mt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       u64* hd = reinterpret_cast<u64*>(sl.rhdr + (size_t)pi * kRegHdr);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's region stores (and spills) are done
       __syncthreads();
@@ -1832,7 +1846,7 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
       for (uint32_t i = threadIdx.x; nm != kAllTiles && i < nm; i += kRT) {
         const uint32_t o = owner(s_pmt, i);
         sys_store(sl.hmlist + i,
-                  __hip_atomic_load(sl.rtile + (size_t)o * kMtLds + (i - s_pmt[o]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                  __hip_atomic_load(sl.rtile + (size_t)o * kResMaxTiles + (i - s_pmt[o]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       }
       if (s_nrec) {  // spilled deltas in the global tables: all of them follow the records
         __syncthreads();
@@ -2956,7 +2970,8 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
     if (!s.rhdr) {
       s.rhdr = dalloc<uint32_t>((size_t)kMaxMergeGroups * kRegHdr, &bytes_alloc_);
       s.rrec = dalloc<uint64_t>((size_t)kMaxMergeGroups * kDeltaLdsW * 3, &bytes_alloc_);
-      s.rtile = dalloc<uint32_t>((size_t)kMaxMergeGroups * kMtLds, &bytes_alloc_);
+      // k_merge's regions hold kMtLds tiles each, k_resident's every tile of its owner
+      s.rtile = dalloc<uint32_t>((size_t)kMaxMergeGroups * std::max<uint32_t>(kMtLds, kResMaxTiles), &bytes_alloc_);
     }
   }
   if (host_ulist_) HIP_OK(hipHostFree(host_ulist_));
@@ -3876,7 +3891,6 @@ void Device::plan_resident(const TiledStream& ts) {
   // per tile: first and last word rank (tiles hold whole words in rank order), LDS words
   const size_t T = ntiles_;
   std::vector<uint32_t> rfirst(T), rlast(T), words(T);
-  double total = 0;
   for (size_t t = 0; t < T; ++t) {
     const uint32_t len = ts.len[t];
     if (len > (uint32_t)kWaveTok || len == 0) return;  // a long word: k_merge handles those
@@ -3889,49 +3903,82 @@ void Device::plan_resident(const TiledStream& ts) {
     rlast[t] = last;
     if (t && rfirst[t] != rlast[t - 1] + 1) return;
     words[t] = (len + 3u) & ~3u;
-    total += 4.0 * words[t] + 8.0 * (rlast[t] - rfirst[t] + 1) + 4.0 * kResSigWords;
   }
-  // contiguous ranges balanced by LDS bytes: tile t goes to worker 2 + floor((prefix + cost/2) * W / total)
-  std::vector<uint32_t> wg_tiles(G + 1, 0), wg_rank(G + 1, 0), lofs(T);
-  res_owner_.assign(T, 0);
-  double pre = 0;
-  uint32_t w = kResFirstWorker;
-  for (size_t t = 0; t < T; ++t) {
-    const double c = 4.0 * words[t] + 8.0 * (rlast[t] - rfirst[t] + 1) + 4.0 * kResSigWords;
-    uint32_t want = kResFirstWorker + (uint32_t)std::min<double>(W - 1, std::floor((pre + c / 2) * W / total));
-    if (want < w) want = w;
-    while (w < want) wg_tiles[++w] = (uint32_t)t;
-    res_owner_[t] = w;
-    pre += c;
+  // The LDS plan, largest first: tokens + weights + 4096-bit signatures in LDS; tokens in HBM;
+  // then (big tables: C5 at 100 GB has 68,905 tiles of 4.1 M words) the weights in HBM too, and
+  // the signatures halved, then quartered (a looser filter: more tiles scanned per merge).
+  // SHREDWORD_RESIDENT_SIG_WORDS / SHREDWORD_RESIDENT_W_GLOBAL force a smaller plan (tests).
+  uint32_t sig_min = (uint32_t)kResSigWords / 4;
+  uint32_t sig_cap = (uint32_t)kResSigWords;
+  if (const char* e = std::getenv("SHREDWORD_RESIDENT_SIG_WORDS")) {
+    const uint32_t v = (uint32_t)std::atoi(e);
+    if (v == 32 || v == 64 || v == 128) sig_cap = sig_min = v;
   }
-  while (w < G) wg_tiles[++w] = (uint32_t)T;
-  uint32_t tok_words = 0, nr_max = 0, nt_max = 0;
-  res_wg_ntiles_.assign(G, 0);
-  for (uint32_t g = 0; g < G; ++g) {
-    const uint32_t a = wg_tiles[g], b = wg_tiles[g + 1];
-    res_wg_ntiles_[g] = b - a;
-    if (b - a > kResMaxTiles) return;
-    nt_max = std::max(nt_max, b - a);
-    uint32_t o = 0;
-    for (uint32_t t = a; t < b; ++t) {
-      lofs[t] = o;
-      o += words[t];
+  const bool force_wg = std::getenv("SHREDWORD_RESIDENT_W_GLOBAL") != nullptr;
+  const bool force_hbm = std::getenv("SHREDWORD_RESIDENT_HBM") != nullptr || force_wg || sig_cap < (uint32_t)kResSigWords;
+  std::vector<uint32_t> wg_tiles, wg_rank, lofs;
+  uint32_t tok_words = 0, nr_max = 0, sw = 0;
+  size_t shm = 0;
+  bool lds_tok = false, w_global = false, fit = false;
+  for (int plan = 0; plan < 8 && !fit; ++plan) {
+    // plan 0: tokens in LDS; 1: tokens in HBM; 2..: weights in HBM, signatures sig_cap >> (plan - 2)
+    lds_tok = plan == 0;
+    w_global = plan >= 2;
+    sw = plan >= 2 ? sig_cap >> (plan - 2) : sig_cap;
+    if (sw < sig_min) break;
+    if ((lds_tok && force_hbm) || (!w_global && force_wg) || (!w_global && sw != sig_cap)) continue;
+    const long bud = lds_tok ? budget : budget_hbm;
+    // contiguous ranges balanced by LDS bytes: tile t goes to worker 2 + floor((prefix + cost/2) * W / total)
+    auto cost = [&](size_t t) {  // tokens (LDS bytes, or the scan work when they stay in HBM) + weights + signature
+      return 4.0 * words[t] + (w_global ? 0.0 : 8.0 * (rlast[t] - rfirst[t] + 1)) + 4.0 * sw;
+    };
+    double total = 0;
+    for (size_t t = 0; t < T; ++t) total += cost(t);
+    wg_tiles.assign(G + 1, 0);
+    wg_rank.assign(G + 1, 0);
+    lofs.assign(T, 0);
+    res_owner_.assign(T, 0);
+    double pre = 0;
+    uint32_t w = kResFirstWorker;
+    for (size_t t = 0; t < T; ++t) {
+      const double c = cost(t);
+      uint32_t want = kResFirstWorker + (uint32_t)std::min<double>(W - 1, std::floor((pre + c / 2) * W / total));
+      if (want < w) want = w;
+      while (w < want) wg_tiles[++w] = (uint32_t)t;
+      res_owner_[t] = w;
+      pre += c;
     }
-    tok_words = std::max(tok_words, o);
-    wg_rank[g] = a < b ? rfirst[a] : (a < T ? rfirst[a] : rlast[T - 1] + 1);
-    const uint32_t r_end = a < b ? rlast[b - 1] + 1 : wg_rank[g];
-    nr_max = std::max(nr_max, r_end - wg_rank[g]);
-  }
-  wg_rank[G] = rlast[T - 1] + 1;
-  tok_words += (uint32_t)kWaveTok;  // every lane reads its 16 tokens of a full chunk from any tile start
-  nr_max = (nr_max + 1u) & ~1u;
-  size_t shm = (size_t)tok_words * 4 + (size_t)nr_max * 8 + (size_t)nt_max * kResSigWords * 4;
-  res_lds_tok_ = (long)shm <= budget && !std::getenv("SHREDWORD_RESIDENT_HBM");
-  if (!res_lds_tok_) {  // the tokens stay in HBM; LDS holds weights and signatures
+    while (w < G) wg_tiles[++w] = (uint32_t)T;
     tok_words = 0;
-    shm = (size_t)nr_max * 8 + (size_t)nt_max * kResSigWords * 4;
-    if ((long)shm > budget_hbm) return;
+    nr_max = 0;
+    uint32_t nt_max = 0;
+    res_wg_ntiles_.assign(G, 0);
+    for (uint32_t g = 0; g < G; ++g) {
+      const uint32_t a = wg_tiles[g], b = wg_tiles[g + 1];
+      res_wg_ntiles_[g] = b - a;
+      nt_max = std::max(nt_max, b - a);
+      uint32_t o = 0;
+      for (uint32_t t = a; t < b; ++t) {
+        lofs[t] = o;
+        o += words[t];
+      }
+      tok_words = std::max(tok_words, o);
+      wg_rank[g] = a < b ? rfirst[a] : (a < T ? rfirst[a] : rlast[T - 1] + 1);
+      const uint32_t r_end = a < b ? rlast[b - 1] + 1 : wg_rank[g];
+      nr_max = std::max(nr_max, r_end - wg_rank[g]);
+    }
+    wg_rank[G] = rlast[T - 1] + 1;
+    if (nt_max > kResMaxTiles) continue;
+    tok_words += (uint32_t)kWaveTok;  // every lane reads its 16 tokens of a full chunk from any tile start
+    nr_max = w_global ? 0u : (nr_max + 1u) & ~1u;
+    if (!lds_tok) tok_words = 0;
+    shm = (size_t)tok_words * 4 + (size_t)nr_max * 8 + (size_t)nt_max * sw * 4;
+    fit = (long)shm <= bud;
   }
+  if (!fit) return;
+  res_lds_tok_ = lds_tok;
+  res_sig_words_ = sw;
+  res_w_global_ = w_global;
   res_grid_ = G;
   res_tok_words_ = tok_words;
   res_w_words_ = nr_max;
@@ -3980,7 +4027,9 @@ void Device::plan_resident(const TiledStream& ts) {
   if (per_cu < 1 || (long)per_cu * cu_count_ < (long)G) return;
   resident_ok_ = true;
   if (std::getenv("SHREDWORD_RESIDENT_REPORT"))
-    std::fprintf(stderr, "[RESIDENT] plan: grid %u, %zu B of LDS per workgroup, %d per CU\n", G, (size_t)shm, per_cu);
+    std::fprintf(stderr, "[RESIDENT] plan: grid %u, %zu B of LDS per workgroup, %d per CU; tokens in %s, weights in %s, "
+                 "%u-bit tile signatures\n", G, (size_t)shm, per_cu, res_lds_tok_ ? "LDS" : "HBM",
+                 res_w_global_ ? "HBM" : "LDS", 32u * res_sig_words_);
 }
 
 void Device::set_resident(bool on) {
@@ -4018,6 +4067,8 @@ void Device::start_resident() {
   rp.tile_lofs = res_tile_lofs_;
   rp.tok_words = res_tok_words_;
   rp.w_words = res_w_words_;
+  rp.sig_words = res_sig_words_;
+  rp.w_global = res_w_global_ ? 1u : 0u;
   rp.mbox = (const ResMbox*)res_mbox_dev_;
   rp.cmd = res_cmd_;
   rp.q = reinterpret_cast<u64*>(res_q_);

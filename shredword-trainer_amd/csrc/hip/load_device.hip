@@ -52,6 +52,9 @@ constexpr int kLdsSlots = 1536;      // per-workgroup table: 36 B a slot (54 KB)
 constexpr int kLdsProbes = 8;
 constexpr int kSpell = 16;           // leading bytes of a word an LDS slot keeps
 constexpr size_t kPadBytes = kTileBytes + 256;  // ' ' past the corpus: every tile load and word scan stays inside
+// HBM table probes before the table counts as too full (it is grown 4x and the count rerun); with
+// the 3/4 fill flag the usual probe run is a few slots
+constexpr u64 kTableProbes = 512;
 
 __device__ __forceinline__ bool delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }
 
@@ -94,13 +97,13 @@ __device__ __forceinline__ bool same_global(const uint8_t* d, u64 a, u64 b, uint
 }
 
 // Adds (cnt, first) to key's slot.  Exactness: every add but the slot's very first compares its
-// occurrence with the offset the atomic hands back — an occurrence some earlier add stored — so
-// all the occurrences behind one key are linked by byte-equal pairs, or flags[1] is raised (a
-// 64-bit key collision: the count is repeated with another seed).
+// occurrence with one some earlier add stored as the slot's first offset (the value the atomic
+// hands back, or a loaded one) — so all the occurrences behind one key are linked by byte-equal
+// pairs, or flags[1] is raised (a 64-bit key collision: the count is repeated with another seed).
 __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 key, uint32_t bkt, uint32_t len,
                                           u64 cnt, u64 first) {
   u64 s = key & t.mask;
-  for (u64 probe = 0; probe <= t.mask; ++probe) {
+  for (u64 probe = 0; probe < kTableProbes; ++probe) {
     Slot& e = t.slot[s];
     u64 prev = e.key;
     if (prev == 0ull) {
@@ -114,8 +117,12 @@ __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 
     }
     if (prev == key) {
       atomicAdd(&e.cnt, cnt);
-      const u64 old = ~atomicMax(&e.nfirst, ~first);
-      if (old != ~0ull && !same_global(d, first, old, len)) atomicOr(&t.flags[1], 1u);
+      // The link: an occurrence some earlier add stored.  A loaded first offset (even a stale one:
+      // every value nfirst held was stored by an add) at or before this one means the minimum
+      // needs no update, so the atomic is skipped; otherwise the atomic hands back the previous.
+      const u64 seen = __hip_atomic_load(&e.nfirst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const u64 link = (seen != 0ull && ~seen <= first) ? ~seen : ~atomicMax(&e.nfirst, ~first);
+      if (link != ~0ull && !same_global(d, first, link, len)) atomicOr(&t.flags[1], 1u);
       return;
     }
     s = (s + 1) & t.mask;
@@ -155,9 +162,12 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
   const u64 t0 = (u64)blockIdx.x * tiles_per_wg;
   const u64 t1 = t0 + tiles_per_wg < ntiles ? t0 + tiles_per_wg : ntiles;
   const u64 range = t0 * kTileBytes;  // LDS first offsets are relative to it (< 2^32: host-checked)
+  __shared__ uint32_t s_full;
   for (u64 tile = t0; tile < t1; ++tile) {
     const u64 base = tile * kTileBytes;
+    if (tid == 0) s_full = __hip_atomic_load(&t.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();  // the previous tile's scans are done
+    if (s_full) return;  // the table is too full: this count is rerun on a bigger one
     const int4* g = reinterpret_cast<const int4*>(d + base);
 #pragma unroll
     for (int j = 0; j < kTileBytes / 16 / kLoadThreads; ++j) {
@@ -356,6 +366,13 @@ bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec
   // a small table keeps the slots the spills touch in L2 / MALL
   u64 cap = 1ull << 20;
   while (cap < (u64)(n / 8192) && cap < (1ull << 29)) cap <<= 1;
+  if (const char* e = std::getenv("SHREDWORD_LOAD_TABLE_SLOTS")) {  // tests: a table that must grow
+    const u64 want = std::strtoull(e, nullptr, 10);
+    if (want >= 1024) {
+      cap = 1024;
+      while (cap < want && cap < (1ull << 29)) cap <<= 1;
+    }
+  }
   u64 kmask = ~0ull;
   if (const char* e = std::getenv("SHREDWORD_LOAD_KEY_BITS")) {
     const int bits = std::atoi(e);

@@ -295,7 +295,9 @@ std::vector<Entry> shard_entries(const uint8_t* d, size_t n, const LoadOptions& 
   if (opt.gpu_device >= 0 && e > b && e - b >= opt.gpu_min_bytes) {
     std::vector<WordRec> recs;
     std::string why;
-    if (gpu_count_words(opt.gpu_device, d + b, e - b, &recs, &why, /*staged=*/b > 0)) {
+    // any range short of the whole mapping goes through pinned buffers (the runtime's pageable
+    // copy of a part of a mapping is slow: load_device.hip)
+    if (gpu_count_words(opt.gpu_device, d + b, e - b, &recs, &why, /*staged=*/b > 0 || e < n)) {
       *on_gpu = true;
       const double th = now_seconds();
       mine.resize(recs.size());

@@ -389,6 +389,8 @@ class Device : public Backend {
   int32_t res_abandoned_[kResSlots] = {-1, -1, -1, -1};  // by slot: an undone guess not yet completed
   int res_next_slot_ = 0;
   uint32_t res_grid_ = 0, res_tok_words_ = 0, res_w_words_ = 0;
+  uint32_t res_sig_words_ = 0;   // LDS signature words per tile in this plan
+  bool res_w_global_ = false;    // the plan reads word weights from HBM
   size_t res_shm_ = 0;
   uint32_t* res_wg_tiles_ = nullptr;   // device: grid + 1
   uint32_t* res_wg_rank_ = nullptr;    // device: grid + 1

@@ -519,6 +519,33 @@ def test_gpu_word_count_matches_host(kind, medium_corpus, tmp_path, monkeypatch)
 
 
 
+def test_gpu_word_count_grows_a_full_table(medium_corpus, tmp_path, monkeypatch):
+    """The device word table started far below the corpus's distinct words
+    (SHREDWORD_LOAD_TABLE_SLOTS=1024): the count stops at the 3/4 fill (bounded probes, every
+    workgroup leaves at its next tile), grows the table 4x and reruns until it fits -- the same
+    word table as the host count, in bounded time (a full table once cost minutes of probing)."""
+    import time
+    monkeypatch.setenv("SHREDWORD_GPU_LOAD_MIN", "1")
+    outs = []
+    for slots in ("1024", None):
+        if slots:
+            monkeypatch.setenv("SHREDWORD_LOAD_TABLE_SLOTS", slots)
+        else:
+            monkeypatch.delenv("SHREDWORD_LOAD_TABLE_SLOTS", raising=False)
+        t = _trainer(vocab_size=2000, unk_id=0, character_coverage=0.9995, min_pair_freq=2)
+        t.set_option("gpu_load", 1 if slots else 0)
+        t0 = time.time()
+        t.load_corpus(medium_corpus)
+        dt = time.time() - t0
+        n, model, vocab = _train_bytes(t, tmp_path, f"g{slots}")
+        st = t.stats()
+        t.destroy()
+        if slots:
+            assert st["load_on_gpu"] == 1 and st["num_words"] > 4 * 1024 and dt < 30
+        outs.append((n, model, vocab, st["num_words"], st["num_occurrences"]))
+    assert outs[0] == outs[1]
+
+
 def test_gpu_word_count_detects_key_collisions(medium_corpus, tmp_path, monkeypatch):
     """Word keys narrowed to 12 bits (SHREDWORD_LOAD_KEY_BITS): thousands of distinct words share
     keys, the byte compare inside k_word_count flags it on every seed, and the load falls back to

@@ -153,6 +153,23 @@ def test_types_layout_resident_hbm_matches_reference(name, case_corpus, tmp_path
         assert st["resident_launches"] > 0
 
 
+@pytest.mark.parametrize("plan", [("32", "1", "1"), ("64", "1", "3")], ids=["sig1024_wglobal", "sig2048_depth3"])
+@pytest.mark.parametrize("name", [n for n in API_CASES if not n.startswith("adv_")])
+def test_types_layout_resident_small_plan_matches_reference(name, plan, case_corpus, tmp_path, monkeypatch):
+    """k_resident's plans for tables too big for the default LDS plan (C5 at 100 GB: 68,905 tiles
+    of 4.1 M words): weights read from HBM and the per-tile signatures quartered / halved
+    (SHREDWORD_RESIDENT_SIG_WORDS forces them here), with one and with three guesses in flight."""
+    sig, wg, depth = plan
+    monkeypatch.setenv("SHREDWORD_RESIDENT_SIG_WORDS", sig)
+    monkeypatch.setenv("SHREDWORD_RESIDENT_W_GLOBAL", wg)
+    monkeypatch.setenv("SHREDWORD_SPEC_DEPTH", depth)
+    case, corpus = case_corpus(name)
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, index=0))
+    if case["merges"] > 0:
+        assert st["resident_launches"] > 0
+
+
 @pytest.mark.parametrize("name", [n for n in API_CASES if not n.startswith("adv_")])
 def test_types_layout_resident_deep_speculation_matches_reference(name, case_corpus, tmp_path, monkeypatch):
     """k_resident with three guessed merges in flight behind the current one."""
