@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--dir", default="")
     ap.add_argument("--out", default="gpurun_out/fullsize.json")
     ap.add_argument("--keep", action="store_true", help="keep the corpus file")
+    ap.add_argument("--known", default="", help="a committed record of the same corpus (generator, seed, size): "
+                    "its md5, unique bytes and word bytes are used instead of a streaming pass")
     args = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (one HIP runtime per process: torch's)
@@ -148,7 +150,12 @@ def main():
         toks.append((tok, int(vb[pos + 1:end])))
         pos = end + 1
     freqs = [int(ln.split()[3]) for ln in open(trace) if ln.startswith("M ")]
-    md5, uniq, word_bytes = stream_stats(path)
+    known = json.load(open(args.known)) if args.known else None
+    if known and all(known.get(k) == res[k] for k in ("corpus_bytes", "seed", "script")):
+        md5, uniq, word_bytes = known["corpus_md5"], known["unique_bytes"], known["word_bytes"]
+        res["corpus_stats_from"] = args.known
+    else:
+        md5, uniq, word_bytes = stream_stats(path)
     res.update({"corpus_md5": md5, "unique_bytes": uniq, "word_bytes": word_bytes})
     conserved = sum(len(tok) * f for tok, f in toks[1:]) + toks[0][1]
     checks = {
@@ -163,6 +170,9 @@ def main():
         "k5_checks": st["verify_checks"], "k5_failures": st["verify_failures"],
         "k5_all_passed": st["verify_checks"] >= n // args.verify and st["verify_failures"] == 0,
     }
+    if known and "corpus_stats_from" in res:  # another run of the same corpus and config: the same bytes
+        checks["model_vocab_md5_equal_known_run"] = (res["model_md5"], res["vocab_md5"]) == (known["model_md5"],
+                                                                                            known["vocab_md5"])
     res["invariants"] = checks
     res["all_invariants_hold"] = all(v for k, v in checks.items() if not k.startswith("k5_") or k == "k5_all_passed")
     res["last_merge_freq"] = freqs[-1] if freqs else None
