@@ -448,6 +448,8 @@ def merge_loop_report(st, merges, elapsed, args):
             "kernel": "k_resident (persistent, whole chip: LDS signatures, wave-level match + deltas + compaction)",
             "merges": res_n, "launches": st["resident_launches"], "kernel_ms": ms,
             "us_per_merge": 1e3 * ms / res_n, "algorithmic_bytes": b, "algorithmic_bytes_per_merge": b / res_n,
+            # K3: the dirty tiles a merge rewrites, read + written (4 B a token each way)
+            "k3_dirty_tile_bytes_per_merge": st.get("resident_k3_bytes", 0.0) / res_n,
             "achieved_GBps": gbps, "frac_of_hbm_peak": gbps / HBM_PEAK_GBS if gbps else None,
             "traffic_bytes_per_launch": (pmc_traffic(args.config, args.layout, "k_resident<true>")
                                          or pmc_traffic(args.config, args.layout, "k_resident")),

@@ -177,6 +177,7 @@ typedef struct ShredStats {
   uint64_t index_run_ints_read;     /* k_word_loop: Σ ints of the scanned words' runs (length + tokens) */
   uint64_t index_run_ints_written;  /* k_word_loop: Σ ints of the changed runs written back */
   uint64_t index_records;           /* k_word_loop: Σ 24-B delta records written to host memory */
+  double resident_k3_bytes;    /* k_resident: Σ 8 B x tokens of the tiles a merge rewrote (K3: read + write) */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -4241,6 +4241,7 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   if (timing_) {
     times_.merge_bytes += 4.0 * (double)live_tokens_est_;
     times_.res_bytes += 4.0 * (double)live_tokens_est_;
+    times_.res_k3_bytes += 8.0 * (double)hs[1];  // hs[1]: tokens the merge's matched tiles hold after it
     times_.res_merges += 1;
   }
   ++res_merges_;

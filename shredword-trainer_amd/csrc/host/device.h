@@ -40,6 +40,7 @@ struct KernelTimes {
   uint64_t hist_launches = 0;
   uint64_t res_merges = 0;  // merges collected from k_resident
   double res_bytes = 0;     // their algorithmic bytes: 4 B per live token per merge
+  double res_k3_bytes = 0;  // K3: 4 B read + 4 B written per token of the tiles a merge rewrote
   double res_ms = 0;        // Σ durations of the k_resident launches that merged (HIP events)
 };
 

@@ -402,6 +402,7 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
     s->resident_aborts = t->dev->resident_aborts();
     s->resident_merges = k.res_merges;
     s->resident_bytes = k.res_bytes;
+    s->resident_k3_bytes = k.res_k3_bytes;
     s->resident_kernel_ms = k.res_ms;
     if (const WordLoop* wl = t->dev->word_loop()) {
       const WordLoopStats& w = wl->stats();
