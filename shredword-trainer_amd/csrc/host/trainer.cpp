@@ -49,6 +49,10 @@ struct Trainer {
   int spec_depth = 0;            // resident guesses in flight (0: env SHREDWORD_SPEC_DEPTH or default)
   bool gpu_load = true;          // count the corpus words on the device (types layout)
   double load_s = 0;
+  // shred_set_load_gather: a sharded load over the caller's all-gather (no RCCL)
+  LoadGather ext_gather = nullptr;
+  void* ext_ctx = nullptr;
+  int ext_rank = 0, ext_world = 1;
 };
 
 namespace {
@@ -246,6 +250,11 @@ int bpe_load_corpus(Trainer* t, const char* path) {
     opt.shard_rank = dist_state().rank;
     opt.shard_world = dist_state().world;
     opt.gather = dist_allgather_bytes;
+  } else if (t->ext_gather && t->ext_world > 1 && !opt.want_stream) {  // the same over the caller's gather
+    opt.shard_rank = t->ext_rank;
+    opt.shard_world = t->ext_world;
+    opt.gather = t->ext_gather;
+    opt.gather_ctx = t->ext_ctx;
   }
   std::string err;
   WordTable wt;
@@ -312,6 +321,16 @@ void bpe_save(const Trainer* tc, const char* model_path, const char* vocab_path)
 int shred_set_option(Trainer* t, const char* key, const char* value) {
   if (!t || !key || !value) return -1;
   return set_option(t, key, value);
+}
+
+int shred_set_load_gather(Trainer* t, int rank, int world, shred_gather_fn gather, void* ctx) {
+  if (!t) return -1;
+  if (world > 1 && (rank < 0 || rank >= world)) return -1;
+  t->ext_gather = world > 1 ? gather : nullptr;
+  t->ext_ctx = ctx;
+  t->ext_rank = world > 1 ? rank : 0;
+  t->ext_world = world > 1 ? world : 1;
+  return 0;
 }
 
 int shred_reset(Trainer* t) {

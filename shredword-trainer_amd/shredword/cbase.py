@@ -108,6 +108,11 @@ lib.loadVocab.argtypes, lib.loadVocab.restype = [c_void_p, c_char_p], c_bool
 # extensions (include/shredword_bpe.h)
 lib.shred_set_option.argtypes, lib.shred_set_option.restype = [Trainer, c_char_p, c_char_p], c_int
 lib.shred_reset.argtypes, lib.shred_reset.restype = [Trainer], c_int
+# shred_gather_fn: (ctx, send, nbytes, size_t* out_bytes) -> every rank's bytes, concatenated
+GATHER_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                             ctypes.POINTER(ctypes.c_size_t))
+lib.shred_set_load_gather.argtypes = [Trainer, c_int, c_int, GATHER_FN, ctypes.c_void_p]
+lib.shred_set_load_gather.restype = c_int
 lib.shred_probe_merge.argtypes, lib.shred_probe_merge.restype = [Trainer, c_int32, c_int32, c_int], c_double
 if hasattr(lib, "shred_probe_rollback"):  # diagnostics (absent from older builds)
     lib.shred_probe_rollback.argtypes, lib.shred_probe_rollback.restype = [Trainer, c_int32, c_int32], c_int

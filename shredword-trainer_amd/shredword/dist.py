@@ -35,3 +35,24 @@ def init_from_env(device=None):
 
 def finalize():
     lib.shred_dist_finalize()
+
+
+def host_load_gather(group=None):
+    """A shred_gather_fn over torch.distributed's host collectives (gloo): the sharded load's
+    word-list all-gather without RCCL (BPETrainer.set_load_gather).  The returned callback keeps
+    its last result alive until its next call, as the C ABI requires."""
+    import torch.distributed as dist
+
+    from .cbase import GATHER_FN
+    keep = {}
+
+    def gather(_ctx, send, nbytes, out_bytes):
+        mine = ctypes.string_at(send, nbytes) if nbytes else b""
+        parts = [None] * dist.get_world_size(group)
+        dist.all_gather_object(parts, mine, group=group)
+        blob = b"".join(parts)
+        keep["buf"] = ctypes.create_string_buffer(blob, max(1, len(blob)))
+        out_bytes[0] = len(blob)
+        return ctypes.addressof(keep["buf"])
+
+    return GATHER_FN(gather)

@@ -51,6 +51,14 @@ class BPETrainer:
         if lib.shred_set_option(self.trainer, key.encode(), str(value).encode()) != 0:
             raise ValueError(f"bad option {key}={value}")
 
+    def set_load_gather(self, rank: int, world: int, gather) -> None:
+        """Later load_corpus calls count only byte range `rank` of `world` and merge every rank's
+        word list through `gather` (a shred_gather_fn, e.g. shredword.dist.host_load_gather());
+        the merge loop then runs on every rank (dist=replicate without RCCL)."""
+        self._gather = gather  # the C side keeps the pointer: keep the callback alive
+        if lib.shred_set_load_gather(self.trainer, rank, world, gather, None) != 0:
+            raise ValueError(f"bad rank {rank} of {world}")
+
     def reset(self) -> None:
         """Restore the loaded corpus to its unmerged state (benchmark repeats)."""
         lib.shred_reset(self.trainer)

@@ -207,3 +207,18 @@ def test_cli_matches_reference(name, case_corpus, tmp_path):
     assert proc.returncode == 0, proc.stderr  # the reference CLI segfaults here (rc 139)
     assert open(model, "rb").read() == case["model_bytes"]
     assert open(vocab, "rb").read() == case["vocab_bytes"]
+
+
+@pytest.mark.parametrize("name", ["utf8_4m_v8192_mpf5", "mixed2m_v4000"])
+def test_sharded_load_two_processes_on_gpu(name, case_corpus, tmp_path):
+    """Two processes on the GPU, the product library end to end (dist=replicate without RCCL):
+    each rank counts its byte range with k_word_count, the word lists meet over a gloo all-gather
+    (shred_set_load_gather), and each rank trains the merged table on the device -- both ranks
+    write the reference's bytes."""
+    from test_multirank_cpu import _run_product_ranks
+    case, corpus = case_corpus(name)
+    infos = _run_product_ranks(corpus, case["config"], 2, tmp_path, train=True, env={"SHREDWORD_GPU_LOAD_MIN": "1"})
+    assert all(i["load_on_gpu"] == 1 and i["merges"] == case["merges"] for i in infos)
+    for r in range(2):
+        assert open(tmp_path / f"r{r}.model", "rb").read() == case["model_bytes"]
+        assert open(tmp_path / f"r{r}.vocab", "rb").read() == case["vocab_bytes"]

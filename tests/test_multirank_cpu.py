@@ -102,3 +102,33 @@ def test_sharded_load_replicated_loop(name, world, case_corpus, tmp_path):
         assert open(tmp_path / f"trace_r{r}.txt").read() == case["trace"]
     assert open(tmp_path / "mr.model", "rb").read() == case["model_bytes"]
     assert open(tmp_path / "mr.vocab", "rb").read() == case["vocab_bytes"]
+
+
+def _run_product_ranks(corpus, cfg, world, outdir, train=False, timeout=600, env=None):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
+               OMP_NUM_THREADS="1", **(env or {}))
+    if train:
+        env["TRAIN"] = "1"
+    procs = [subprocess.Popen([sys.executable, os.path.join(TESTS, "sharded_product_worker.py"), corpus,
+                               str(cfg["vocab_size"]), str(cfg["unk_id"]), repr(cfg["character_coverage"]),
+                               str(cfg["min_pair_freq"]), str(outdir)],
+                              env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(world)]
+    outs = [p.communicate(timeout=timeout)[0].decode(errors="replace") for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+    import json
+    return [json.load(open(os.path.join(outdir, f"info_r{r}.json"))) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_product_sharded_load_over_host_gather(world, case_corpus, tmp_path):
+    """The product library's sharded load (shred_set_load_gather) with gloo as the all-gather:
+    every rank counts its byte range on the host here, the merged table equals the one-process
+    table (distinct words, symbols, occurrences)."""
+    case, corpus = case_corpus("utf8_4m_v8192_mpf5")
+    (tmp_path / "one").mkdir()
+    one = _run_product_ranks(corpus, case["config"], 1, tmp_path / "one")
+    many = _run_product_ranks(corpus, case["config"], world, tmp_path)
+    keys = ("num_words", "num_symbols", "num_occurrences")
+    assert all(tuple(i[k] for k in keys) == tuple(one[0][k] for k in keys) for i in many)
