@@ -97,9 +97,9 @@ __device__ __forceinline__ bool same_global(const uint8_t* d, u64 a, u64 b, uint
 }
 
 // Adds (cnt, first) to key's slot.  Exactness: every add but the slot's very first compares its
-// occurrence with one some earlier add stored as the slot's first offset (the value the atomic
-// hands back, or a loaded one) — so all the occurrences behind one key are linked by byte-equal
-// pairs, or flags[1] is raised (a 64-bit key collision: the count is repeated with another seed).
+// occurrence with the offset the atomic hands back — an occurrence some earlier add stored — so
+// all the occurrences behind one key are linked by byte-equal pairs, or flags[1] is raised (a
+// 64-bit key collision: the count is repeated with another seed).
 __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 key, uint32_t bkt, uint32_t len,
                                           u64 cnt, u64 first) {
   u64 s = key & t.mask;
@@ -117,11 +117,7 @@ __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 
     }
     if (prev == key) {
       atomicAdd(&e.cnt, cnt);
-      // The link: an occurrence some earlier add stored.  A loaded first offset (even a stale one:
-      // every value nfirst held was stored by an add) at or before this one means the minimum
-      // needs no update, so the atomic is skipped; otherwise the atomic hands back the previous.
-      const u64 seen = __hip_atomic_load(&e.nfirst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const u64 link = (seen != 0ull && ~seen <= first) ? ~seen : ~atomicMax(&e.nfirst, ~first);
+      const u64 link = ~atomicMax(&e.nfirst, ~first);  // ~0: none yet (this is the key's first add)
       if (link != ~0ull && !same_global(d, first, link, len)) atomicOr(&t.flags[1], 1u);
       return;
     }
