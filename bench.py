@@ -588,7 +588,13 @@ def main():
             dist.destroy_process_group()
         return
 
-    torch.cuda.set_device(local)
+    # rank r on device r; on a box with fewer GPUs than ranks (a rehearsal of the N-GPU run on
+    # one card) the ranks share devices round-robin (device_count() does not initialise the GPU)
+    ndev = max(1, torch.cuda.device_count())
+    dev = local % ndev
+    if ndev < world:
+        log(f"bench: {world} ranks on {ndev} device(s): rank {rank} shares device {dev} (rehearsal, not a scaling number)")
+    torch.cuda.set_device(dev)
 
     def barrier():
         if dist is not None:
@@ -604,12 +610,12 @@ def main():
     from shredword.trainer import BPETrainer
     one_job = world > 1 and args.dist != "replicas"  # the ranks train ONE model together
     if one_job:
-        sdist.init_from_env(device=local)
+        sdist.init_from_env(device=dev)
     rccl_ranks = lib.shred_dist_ranks() if one_job else 0
 
     t = BPETrainer(vocab_size=cfg["vocab"], unk_id=cfg["unk"], character_coverage=cfg["cov"], min_pair_freq=cfg["mpf"])
     t.set_option("log", 0)
-    t.set_option("device", local)
+    t.set_option("device", dev)
     t.set_option("layout", args.layout)
     if one_job:
         t.set_option("dist", args.dist)
@@ -663,7 +669,7 @@ def main():
     pair_count = None
     if args.pair_count_reps > 0:
         try:
-            pair_count = pair_count_leg(cfg, path, args.pair_count_reps, device=local, dist=dist,
+            pair_count = pair_count_leg(cfg, path, args.pair_count_reps, device=dev, dist=dist,
                                         shard=one_job)
         except Exception as e:
             pair_count = {"error": repr(e)}
@@ -672,7 +678,7 @@ def main():
     if args.encode_reps > 0 and rank == 0:
         try:
             encode = encode_leg(os.path.join(tmpd, f"bench_r{rank}.model"), os.path.join(tmpd, f"bench_r{rank}.vocab"),
-                                cfg["unk"], path, args.encode_reps, device=local, cfg_name=args.config)
+                                cfg["unk"], path, args.encode_reps, device=dev, cfg_name=args.config)
         except Exception as e:
             encode = {"error": repr(e)}
 
@@ -707,6 +713,8 @@ def main():
                 "vocab_size": cfg["vocab"], "min_pair_freq": cfg["mpf"], "character_coverage": cfg["cov"],
                 "unk_id": cfg["unk"], "layout": args.layout,
                 "parallelism": parallelism, "dist": args.dist if world > 1 else None, "rccl_ranks": rccl_ranks,
+                "devices": ndev if world > 1 else 1,
+                "ranks_share_devices": world > ndev,
                 "merges_per_step": per_step_merges, "distinct_words": st["num_words"],
                 "symbols": st["num_symbols"], "occurrences": st["num_occurrences"], "tiles": st["num_tiles"],
             },
@@ -762,7 +770,7 @@ def main():
         if encode is not None:
             result["encode"] = encode
         try:
-            result["hbm_achievable"] = hbm_probe_leg(device=local)
+            result["hbm_achievable"] = hbm_probe_leg(device=dev)
             if (result.get("pair_count") or {}).get("achieved"):
                 result["pair_count"]["frac_of_achievable_read"] = (
                     result["pair_count"]["achieved"] / world / result["hbm_achievable"]["read_GBps"])
