@@ -558,6 +558,15 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
+    # Under N ranks, libraries print to the process's stdout (gloo's "[Gloo] Rank r is connected
+    # to ..." lines, from C++): fd 1 goes to stderr for the whole run and rank 0 writes its one
+    # JSON line to the saved stdout, so the launcher's stdout carries exactly that line.
+    json_out = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        sys.stdout.flush()
+        json_out = os.dup(1)
+        os.dup2(2, 1)
+
     cfg = dict(CONFIGS[args.config], name=args.config)
     if args.bytes:
         cfg["bytes"] = args.bytes
@@ -583,7 +592,12 @@ def main():
         else:
             seen = [me]
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world, "dist": args.dist, "ranks": seen}), flush=True)
+            line = json.dumps({"dry_run": True, "n_gpus": world, "dist": args.dist, "ranks": seen}) + "\n"
+            if json_out is not None:
+                os.write(json_out, line.encode())
+            else:
+                sys.stdout.write(line)
+                sys.stdout.flush()
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -790,7 +804,10 @@ def main():
                                                                  cfg["unk"], path)
                 except Exception as e:
                     encode["cpu_baseline"] = {"value": None, "error": repr(e)}
-        print(json.dumps(result), flush=True)
+        if json_out is not None:
+            os.write(json_out, (json.dumps(result) + "\n").encode())
+        else:
+            print(json.dumps(result), flush=True)
     if one_job:
         sdist.finalize()
     if dist is not None:

@@ -19,8 +19,8 @@ def test_bench_launches_n_ranks(n):
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--dry-run"],
                          capture_output=True, text=True, env=env, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
-    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, out.stdout  # rank 0 prints one line
+    lines = out.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout  # stdout: rank 0's one JSON line, nothing else
     rep = json.loads(lines[0])
     assert rep["n_gpus"] == n
     ranks = rep["ranks"]
