@@ -201,14 +201,16 @@ __global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __rest
 // A corpus repeats its words (C3: 1.13 G occurrences of 1.25 M distinct words), so the default
 // path encodes each distinct word once and copies its ids to every occurrence:
 //   k_cache_insert  per occurrence: 64-bit hash of (bytes, length) into an open-addressing table
-//                   of 16-byte slots (key, payload = the inserting occurrence's offset): a read
-//                   that hits L2 for a hot word, a CAS only for an empty slot; a full probe
-//                   window flags an overflow (the table then grows 4x);
+//                   of 64-byte slots (key, payload = the inserting occurrence's offset, then the
+//                   short word's bytes and ids inline): a read that hits L2 for a hot word, a CAS
+//                   only for an empty slot; a full probe window flags an overflow (the table then
+//                   grows 4x);
 //   k_cache_encode  per used slot: the lowest-rank loop on that occurrence; the ids, then the
 //                   word's bytes, go to a dense arena (one entry per distinct word), and the
 //                   payload becomes (arena offset, length, id count);
 //   k_cache_words   per occurrence: the slot (key and payload in one 16-byte load), a byte compare
-//                   with the arena copy (a 64-bit collision is flagged, never trusted); then the
+//                   with the slot's inline copy (words <= 16 bytes with <= 8 ids: no arena read)
+//                   or the arena's (a 64-bit collision is flagged, never trusted); then the
 //                   block's ids are written as one contiguous run from its first word start
 //                   (per-block count + start);
 //   k_block_emit    one workgroup per block copies its run to the output, coalesced.
@@ -217,6 +219,13 @@ __global__ __launch_bounds__(kThreads) void k_encode_words(const uint8_t* __rest
 // (run write, emit read, emit write); the slot table and arena stay in L2/MALL for a corpus of
 // repeated words.
 constexpr int kCacheProbes = 128;
+// A word-cache slot is one 64-byte line of 8 u64: [0] key, [1] payload (first the inserting
+// occurrence's offset), [2..3] the word's bytes and [4..7] its ids inline when it is short
+// (<= kInlineBytes bytes, <= kInlineIds ids; most occurrences at any vocab size), so a hot word
+// costs k_cache_words one line -- which stays in L2 -- and no arena read.
+constexpr int kSlotU64 = 8;
+constexpr int kInlineBytes = 16;
+constexpr int kInlineIds = 8;
 constexpr int kSpanWords = kSpan / 2 + 1;  // words starting in one span, at most
 
 // The chunk's text staged in LDS (coalesced 4-byte loads), with a few bytes before it and
@@ -303,11 +312,11 @@ __global__ __launch_bounds__(kThreads) void k_cache_insert(const uint8_t* __rest
     const u64 h = word_hash(tv, s, (uint32_t)L);
     u64 i = (h >> 17) & cmask;
     for (int p = 0; p < kCacheProbes; ++p, i = (i + 1) & cmask) {
-      u64 k = slot[2 * i];  // hot words: a read that hits L2, no atomic
+      u64 k = slot[kSlotU64 * i];  // hot words: a read that hits L2, no atomic
       if (k == 0) {
-        k = atomicCAS(reinterpret_cast<unsigned long long*>(slot + 2 * i), 0ull, (unsigned long long)h);
+        k = atomicCAS(reinterpret_cast<unsigned long long*>(slot + kSlotU64 * i), 0ull, (unsigned long long)h);
         if (k == 0) {
-          slot[2 * i + 1] = s;  // any occurrence spells the word (k_cache_words checks them all)
+          slot[kSlotU64 * i + 1] = s;  // any occurrence spells the word (k_cache_words checks them all)
           return;
         }
       }
@@ -334,8 +343,8 @@ __global__ __launch_bounds__(kThreads) void k_cache_encode(const uint8_t* __rest
   for (int i = tid; i < 256; i += kThreads) s_map[i] = byte_map[i];
   __syncthreads();
   const u64 i = (u64)blockIdx.x * kThreads + tid;
-  if (i >= cap || slot[2 * i] == 0) return;
-  const u64 s = slot[2 * i + 1];
+  if (i >= cap || slot[kSlotU64 * i] == 0) return;
+  const u64 s = slot[kSlotU64 * i + 1];
   u64 e = s;
   while (e < n && !is_delim(text[e])) ++e;  // <= kEncMaxWord (insert checked)
   const int L = (int)(e - s);
@@ -371,7 +380,17 @@ __global__ __launch_bounds__(kThreads) void k_cache_encode(const uint8_t* __rest
     bytes[k / 4] = w;
   }
   arena[off] = m | L << 16;
-  slot[2 * i + 1] = pack_payload(off, (u64)L, (u64)m);
+  u64* sl = slot + kSlotU64 * i;
+  if (L <= kInlineBytes && m <= kInlineIds) {  // the bytes and the ids inline (zero-padded)
+    u64 b[2] = {0, 0};
+    for (int k = 0; k < L; ++k) b[k >> 3] |= (u64)text[s + k] << (8 * (k & 7));
+    sl[2] = b[0];
+    sl[3] = b[1];
+    u64 w[kInlineIds / 2] = {0, 0, 0, 0};
+    for (int k = 0; k < m; ++k) w[k >> 1] |= (u64)(uint32_t)ids[k] << (32 * (k & 1));
+    for (int k = 0; k < kInlineIds / 2; ++k) sl[4 + k] = w[k];
+  }
+  sl[1] = pack_payload(off, (u64)L, (u64)m);
 }
 
 __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restrict__ text, u64 n,
@@ -396,7 +415,7 @@ __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restr
     const u64 h = word_hash(tv, s, (uint32_t)L);
     u64 pay = 0, i = (h >> 17) & cmask;
     for (int p = 0; p < kCacheProbes; ++p, i = (i + 1) & cmask) {
-      const ulonglong2 sl = *reinterpret_cast<const ulonglong2*>(slot + 2 * i);  // key and payload: one load
+      const ulonglong2 sl = *reinterpret_cast<const ulonglong2*>(slot + kSlotU64 * i);  // key and payload: one load
       if (sl.x == h) {
         pay = sl.y;
         break;
@@ -405,14 +424,23 @@ __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restr
     }
     if (!pay) return;  // not inserted: an overflow, flagged by k_cache_insert / k_cache_encode
     const uint32_t m = (uint32_t)(pay >> 48), pl = (uint32_t)(pay >> 32) & 0xFFFFu;
-    const uint8_t* ab = reinterpret_cast<const uint8_t*>(arena + (uint32_t)pay + 1 + m);
     uint32_t diff = pl != (uint32_t)L;
-    for (uint32_t k = 0; k < pl && !diff; ++k) diff |= ab[k] ^ tv[s + k];
+    uint32_t entry;
+    if (pl <= (uint32_t)kInlineBytes && m <= (uint32_t)kInlineIds) {  // inline: the slot's own line
+      const ulonglong2 sb = *reinterpret_cast<const ulonglong2*>(slot + kSlotU64 * i + 2);
+      for (uint32_t k = 0; k < pl && !diff; ++k)
+        diff |= (uint32_t)(((k < 8 ? sb.x : sb.y) >> (8 * (k & 7))) & 0xFFu) ^ tv[s + k];
+      entry = 0x80000000u | (uint32_t)i;  // (slot indices < 2^31: the table is far smaller)
+    } else {
+      const uint8_t* ab = reinterpret_cast<const uint8_t*>(arena + (uint32_t)pay + 1 + m);
+      for (uint32_t k = 0; k < pl && !diff; ++k) diff |= ab[k] ^ tv[s + k];
+      entry = (uint32_t)pay;
+    }
     if (diff) {
       flag(misc, 4);  // 64-bit collision
       return;
     }
-    s_list[nw * kThreads + tid] = (uint32_t)pay;
+    s_list[nw * kThreads + tid] = entry;
     ++nw;
     cnt += m;
   });
@@ -429,7 +457,16 @@ __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restr
   const uint32_t start = s_start == 0xFFFFFFFFu ? 0u : s_start;
   int32_t* dst = pad + cbase + start + (s_inc[tid] - cnt);
   for (uint32_t w = 0; w < nw; ++w) {
-    const int32_t* src = arena + s_list[w * kThreads + tid];
+    const uint32_t e = s_list[w * kThreads + tid];
+    if (e & 0x80000000u) {  // inline ids: the slot line the lookup just read
+      const u64* sl = slot + kSlotU64 * (u64)(e & 0x7FFFFFFFu);
+      const uint32_t m = (uint32_t)(sl[1] >> 48);
+      const int32_t* src = reinterpret_cast<const int32_t*>(sl + 4);
+      for (uint32_t k = 0; k < m; ++k) dst[k] = src[k];
+      dst += m;
+      continue;
+    }
+    const int32_t* src = arena + e;
     const uint32_t m = (uint32_t)src[0] & 0xFFFFu;
     ++src;
     for (uint32_t k = 0; k < m; ++k) dst[k] = src[k];
@@ -571,7 +608,7 @@ bool EncodeDevice::reserve(size_t n, std::string* why) {
   while (ccap_ < cap / 256) ccap_ <<= 1;
   ccap_min_ = 1 << 20;
   while (ccap_min_ < cap / 4096) ccap_min_ <<= 1;
-  if (hipMalloc(&cslot_, ccap_ * 16) != hipSuccess) {
+  if (hipMalloc(&cslot_, ccap_ * kSlotU64 * 8) != hipSuccess) {
     *why = "word-cache allocation failed";
     return false;
   }
@@ -620,7 +657,7 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
   for (;;) {
     ENC_OK(hipMemsetAsync(misc_, 0, 32, st));
     if (cached) {
-      ENC_OK(hipMemsetAsync(cslot_, 0, cc * 16, st));
+      ENC_OK(hipMemsetAsync(cslot_, 0, cc * kSlotU64 * 8, st));
       k_cache_insert<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, cslot_, cc - 1, misc_);
       ENC_OK(hipGetLastError());
       auto enck = packed_ ? k_cache_encode<true> : k_cache_encode<false>;
