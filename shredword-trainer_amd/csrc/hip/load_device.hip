@@ -45,16 +45,21 @@ typedef unsigned long long u64;
   } while (0)
 
 constexpr int kChunkBytes = 64;      // bytes whose word starts one thread owns
-constexpr int kLoadThreads = 256;
-constexpr int kTileBytes = kChunkBytes * kLoadThreads;  // 16 KB of text per workgroup step
 constexpr int kTileStride = kChunkBytes + 4;  // LDS bytes per chunk: the lanes' chunks start in distinct banks
-constexpr int kLdsSlots = 1536;      // per-workgroup table: 36 B a slot (54 KB) + 17 KB tile: two workgroups per CU
+// Two workgroup shapes (36 B an LDS slot; the tile is kChunkBytes per thread, staged at kTileStride):
+//   narrow: 256 threads, 16 KB tiles, 1536 slots (54 KB + 17 KB): two workgroups per CU;
+//   wide:   512 threads, 32 KB tiles, 3072 slots (108 KB + 34 KB): one workgroup per CU, a table
+//           twice the size over twice the range (fewer words spill to HBM: 16.5% -> 12.3% of
+//           occurrences at C3 by a host simulation of the table).
+constexpr int kNarrowThreads = 256, kNarrowSlots = 1536;
+constexpr int kWideThreads = 512, kWideSlots = 3072;
 constexpr int kLdsProbes = 8;
 constexpr int kSpell = 16;           // leading bytes of a word an LDS slot keeps
-constexpr size_t kPadBytes = kTileBytes + 256;  // ' ' past the corpus: every tile load and word scan stays inside
+constexpr size_t kPadBytes = (size_t)kChunkBytes * kWideThreads + 256;  // ' ' past the corpus: every tile load and word scan stays inside
 // HBM table probes before the table counts as too full (it is grown 4x and the count rerun); with
 // the 3/4 fill flag the usual probe run is a few slots
 constexpr u64 kTableProbes = 512;
+constexpr bool kLoadWideDefault = true;  // the wide shape (C3: PMC 87.8 -> 77.9 GB); SHREDWORD_LOAD_WIDE=0/1 overrides
 
 __device__ __forceinline__ bool delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }
 
@@ -85,6 +90,7 @@ __device__ __forceinline__ u64 word_key(u64 h, uint32_t len, u64 seed, u64 kmask
 }
 
 // Byte p of the workgroup's tile (p may run past the tile: then from HBM).
+template <int kTileBytes>
 __device__ __forceinline__ uint32_t tile_byte(const uint8_t* s, const uint8_t* d, u64 base, uint32_t p) {
   return p < (uint32_t)kTileBytes ? s[(p / kChunkBytes) * kTileStride + (p % kChunkBytes)] : d[base + p];
 }
@@ -126,7 +132,7 @@ __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 
   atomicOr(&t.flags[0], 1u);
 }
 
-// One pass over the corpus.  Workgroup w owns a contiguous range of 16 KB tiles; each tile is
+// One pass over the corpus.  Workgroup w owns a contiguous range of tiles (kChunkBytes per thread); each tile is
 // staged in LDS with coalesced 16-B loads (the text is read from HBM once), and each thread takes
 // the words that START in its 64-byte chunk (maximal runs of bytes outside "\t\r\n "), hashes each
 // (64-bit FNV-1a + length mix) and counts it in the workgroup's LDS table (count, min first
@@ -138,8 +144,10 @@ __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 
 // spill compare with the HBM slot's occurrence.  A slot is used once its length is published
 // (0 = being created: the occurrence then goes to HBM directly).  The reference StrMap bucket
 // (djb2 & 4095) is computed at the flush, from the slot's first occurrence.
+template <int kLoadThreads, int kLdsSlots>
 __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u64 n, Table t, u64 seed, u64 kmask,
                                                              u64 tiles_per_wg) {
+  constexpr int kTileBytes = kChunkBytes * kLoadThreads;
   __shared__ u64 s_key[kLdsSlots];
   __shared__ uint32_t s_first[kLdsSlots];
   __shared__ uint32_t s_cnt[kLdsSlots];
@@ -178,17 +186,17 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
     __syncthreads();
     uint32_t p = (uint32_t)tid * kChunkBytes;
     const uint32_t end = p + kChunkBytes;
-    const uint32_t prev = p ? tile_byte(s_tile, d, base, p - 1) : (base ? d[base - 1] : 32u);
+    const uint32_t prev = p ? tile_byte<kTileBytes>(s_tile, d, base, p - 1) : (base ? d[base - 1] : 32u);
     if (!delim(prev))  // a word running in from the previous chunk belongs to that chunk
-      while (p < end && !delim(tile_byte(s_tile, d, base, p))) ++p;
+      while (p < end && !delim(tile_byte<kTileBytes>(s_tile, d, base, p))) ++p;
     for (;;) {
-      while (p < end && delim(tile_byte(s_tile, d, base, p))) ++p;
+      while (p < end && delim(tile_byte<kTileBytes>(s_tile, d, base, p))) ++p;
       if (p >= end || base + p >= n) break;
       u64 h = 0xCBF29CE484222325ull ^ seed;
       uint32_t w[kSpell / 4] = {0, 0, 0, 0};  // the leading bytes, packed
       uint32_t len = 0;
       for (;; ++len) {
-        const uint32_t c = tile_byte(s_tile, d, base, p + len);
+        const uint32_t c = tile_byte<kTileBytes>(s_tile, d, base, p + len);
         if (delim(c)) break;
         h = (h ^ c) * 0x100000001B3ull;
         if (len < (uint32_t)kSpell) w[len / 4] |= c << (8 * (len % 4));
@@ -223,7 +231,7 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
           if (rel < link) link = atomicMin(&s_first[s], rel);
           if (len > (uint32_t)kSpell && link != ~0u && !diff) {
             const u64 rep = range + link;
-            for (uint32_t q = kSpell; q < len; ++q) diff |= tile_byte(s_tile, d, base, p + q) ^ d[rep + q];
+            for (uint32_t q = kSpell; q < len; ++q) diff |= tile_byte<kTileBytes>(s_tile, d, base, p + q) ^ d[rep + q];
           }
           if (diff) atomicOr(&t.flags[1], 1u);
           atomicAdd(&s_cnt[s], 1u);
@@ -234,7 +242,7 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
       }
       if (!done) {
         uint32_t dj = 5381u;  // djb2 in 32 bits: its & 4095 equals the reference's 64-bit value's
-        for (uint32_t q = 0; q < len; ++q) dj = dj * 33u + tile_byte(s_tile, d, base, p + q);
+        for (uint32_t q = 0; q < len; ++q) dj = dj * 33u + tile_byte<kTileBytes>(s_tile, d, base, p + q);
         table_add(d, t, key, dj & 4095u, len, 1ull, off);
       }
       p += len;
@@ -374,8 +382,11 @@ bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec
     const int bits = std::atoi(e);
     if (bits > 0 && bits < 64) kmask = (1ull << bits) - 1;
   }
+  const char* wenv = std::getenv("SHREDWORD_LOAD_WIDE");
+  const bool wide = wenv ? std::atoi(wenv) != 0 : kLoadWideDefault;
+  const u64 kTileBytes = (u64)kChunkBytes * (wide ? kWideThreads : kNarrowThreads);
   const u64 ntiles = (n + kTileBytes - 1) / kTileBytes;
-  u64 grid = std::min<u64>(ntiles, (u64)cus * 2);
+  u64 grid = std::min<u64>(ntiles, (u64)cus * (wide ? 1 : 2));
   u64 per = (ntiles + grid - 1) / grid;
   while (per * (u64)kTileBytes >= (1ull << 32)) {  // LDS first offsets are 32-bit range-relative
     grid *= 2;
@@ -394,7 +405,10 @@ bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec
     t.mask = cap - 1;
     t.nkeys = (uint32_t*)bmeta.p;
     t.flags = (uint32_t*)bmeta.p + 4;
-    k_word_count<<<(unsigned)grid, kLoadThreads, 0, st>>>(db, n, t, seed, kmask, per);
+    if (wide)
+      k_word_count<kWideThreads, kWideSlots><<<(unsigned)grid, kWideThreads, 0, st>>>(db, n, t, seed, kmask, per);
+    else
+      k_word_count<kNarrowThreads, kNarrowSlots><<<(unsigned)grid, kNarrowThreads, 0, st>>>(db, n, t, seed, kmask, per);
     LOAD_OK(hipGetLastError());
     uint32_t meta[16];
     LOAD_OK(hipMemcpyAsync(meta, bmeta.p, 64, hipMemcpyDeviceToHost, st));
