@@ -26,15 +26,20 @@ Legs beside the timed steps (all on the same corpus):
 N GPUs: ``--gpus N`` with N > 1 launches N ranks itself (torch.distributed.run, one process per
 GPU, rank r on device r) unless WORLD_SIZE is already set (the driver's own torchrun).
 ``--dist`` picks what the ranks do:
-* ``replicas`` (default): every rank trains its own replica of the workload.  The merge loop is a
-  serial chain of dependent merges (merge m+1's selection needs merge m's exact frequency
-  changes), so one training does not split across GPUs; N GPUs run N trainings.
-  ``value`` = merges of all ranks / max-over-ranks time, ``scaling`` "weak".
-* ``replicate``: ONE training: the load is sharded (rank r counts byte range r of the corpus on
-  its GPU, the word lists are all-gathered over RCCL and merged) and the merge loop runs on every
-  rank; ``value`` = merges of the one training / max-over-ranks time, ``scaling`` "strong".
+* ``replicate`` (the default for N > 1): ONE training.  The load is sharded (rank r counts byte
+  range r of the corpus on its GPU, the word lists are all-gathered over RCCL and merged) and the
+  merge loop runs on every rank.  The merge loop is a serial chain of dependent merges (merge
+  m+1's selection needs merge m's exact frequency changes), so ``value`` (merges
+  of the one training / max-over-ranks train() time) does not grow with N; ``load`` reports
+  the part that does shard (max-over-ranks load_corpus time) and ``end_to_end_s`` = load + one
+  train.  ``scaling`` "strong".  When ranks share a device (a rehearsal on fewer GPUs than
+  ranks, where RCCL refuses duplicate GPUs) the word lists meet over gloo instead
+  (shredword.dist.host_load_gather).
 * ``exchange``: ONE training over word-range shards with one RCCL all-gather of the merge's
   records per merge (stream layout); ``value`` as for replicate.
+* ``replicas`` (opt-in): N INDEPENDENT jobs, every rank trains its own replica of the workload;
+  ``value`` = merges of all ranks / max-over-ranks time, ``scaling`` "weak".  Not a scaling of
+  one training.
 The K1 leg counts every rank's copy (replicas) or shard of the stream and reports aggregate GB/s.
 Rank 0 prints one JSON line.
 """
@@ -541,9 +546,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--layout", default="types", choices=["types", "stream"])
-    ap.add_argument("--dist", default="replicas", choices=["replicas", "replicate", "exchange"],
-                    help="N > 1: independent trainings per rank (replicas), or one training with a sharded load "
-                         "(replicate) or a per-merge RCCL exchange (exchange); see the module docstring")
+    ap.add_argument("--dist", default="replicate", choices=["replicas", "replicate", "exchange"],
+                    help="N > 1: one training with a sharded load (replicate, the default) or a per-merge RCCL "
+                         "exchange (exchange), or N independent jobs (replicas); see the module docstring")
     ap.add_argument("--bytes", type=int, default=0, help="override the corpus size (testing)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -623,19 +628,35 @@ def main():
     from shredword.cbase import lib
     from shredword.trainer import BPETrainer
     one_job = world > 1 and args.dist != "replicas"  # the ranks train ONE model together
-    if one_job:
+    share = world > ndev  # RCCL refuses two ranks on one GPU: the load's gather goes over gloo
+    if one_job and share and args.dist == "exchange":
+        raise SystemExit("bench: --dist exchange needs one GPU per rank (RCCL per merge); use --dist replicate")
+    gather_via = None
+    if one_job and not share:
         sdist.init_from_env(device=dev)
-    rccl_ranks = lib.shred_dist_ranks() if one_job else 0
+        gather_via = "RCCL all-gather over xGMI (dist_allgather_bytes)"
+    rccl_ranks = lib.shred_dist_ranks() if one_job and not share else 0
 
     t = BPETrainer(vocab_size=cfg["vocab"], unk_id=cfg["unk"], character_coverage=cfg["cov"], min_pair_freq=cfg["mpf"])
     t.set_option("log", 0)
     t.set_option("device", dev)
     t.set_option("layout", args.layout)
-    if one_job:
+    if one_job and not share:
         t.set_option("dist", args.dist)
+    elif one_job:
+        t.set_load_gather(rank, world, sdist.host_load_gather())
+        gather_via = "gloo all-gather (shredword.dist.host_load_gather: ranks share a device)"
+        if args.layout == "types":
+            t.set_option("resident", 0)  # ranks share one GPU: a whole-chip persistent loop per rank would not be co-resident
+    barrier()
     t0 = time.time()
     t.load_corpus(path)
     load_s = time.time() - t0
+    load_s_max = load_s
+    if dist is not None:
+        tl = torch.tensor([load_s], dtype=torch.float64)
+        dist.all_reduce(tl, op=dist.ReduceOp.MAX)
+        load_s_max = float(tl.item())
 
     def train_step():
         t.reset()
@@ -704,20 +725,21 @@ def main():
                            f"merge loop replicated on every rank" if args.dist == "replicate" else
                            f"dp{world} one training: word-range shards + one RCCL all-gather of records per merge")
         elif world > 1:
-            parallelism = (f"replicas{world}: every rank trains its own replica of the workload (the merge chain is "
-                           f"serial, DESIGN.md §5); value = merges of all ranks / slowest rank's time")
+            parallelism = (f"replicas{world}: N INDEPENDENT jobs, every rank trains its own replica of the workload "
+                           f"(not one training; the merge chain is serial, DESIGN.md §5); value = merges of all ranks "
+                           f"/ slowest rank's time")
         else:
             parallelism = "single GPU"
         result = {
             "metric": "BPE merges/sec",
             "value": value,
             "unit": "merges/s",
-            "n_gpus": world,
+            "n_gpus": min(world, ndev),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "strong" if one_job else "weak",
+            "scaling": "strong" if one_job else ("weak" if world > 1 else "weak"),
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (committed deterministic generator, SURVEY.md §8 d2)",
@@ -727,8 +749,9 @@ def main():
                 "vocab_size": cfg["vocab"], "min_pair_freq": cfg["mpf"], "character_coverage": cfg["cov"],
                 "unk_id": cfg["unk"], "layout": args.layout,
                 "parallelism": parallelism, "dist": args.dist if world > 1 else None, "rccl_ranks": rccl_ranks,
-                "devices": ndev if world > 1 else 1,
+                "ranks": world, "devices": ndev if world > 1 else 1,
                 "ranks_share_devices": world > ndev,
+                "load_gather": gather_via,
                 "merges_per_step": per_step_merges, "distinct_words": st["num_words"],
                 "symbols": st["num_symbols"], "occurrences": st["num_occurrences"], "tiles": st["num_tiles"],
             },
@@ -739,11 +762,17 @@ def main():
                 "avg_launch_us": 1e3 * st["count_kernel_ms"] / max(1, st["count_launches"]),
                 "bytes_per_launch": st["count_kernel_bytes"] / max(1, st["count_launches"]),
             },
-            "load_s": load_s, "corpus_gen_s": gen_s,
+            "load_s": load_s_max, "corpus_gen_s": gen_s,
+            "train_s": elapsed / args.steps,
+            "end_to_end_s": load_s_max + elapsed / args.steps,
             "load": {"kernel": "k_word_count (one pass, LDS-staged tiles, byte-exact in-pass verification)",
                      "algorithmic_bytes": cfg["bytes"],
+                     "load_s_max_over_ranks": load_s_max, "load_s_rank0": load_s,
+                     "bytes_per_rank": cfg["bytes"] / world if one_job else cfg["bytes"],
                      "traffic_bytes": pmc_traffic(args.config, args.layout, "k_word_count"),
-                     "note": "load_corpus: PCIe upload + device word count + host table; outside the timed step"},
+                     "note": ("load_corpus: page-in + PCIe upload + device word count + host table; outside the timed "
+                              "step" + ("; each rank counts its byte range, the word lists are all-gathered and "
+                                        "merged on every rank" if one_job else ""))},
             "host_cpus": (f"pinned to the L3 domain {pinned[0]}-{pinned[-1]} ({len(pinned)} CPUs)" if pinned
                           else "not pinned"),
             "host_breakdown_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
@@ -808,7 +837,7 @@ def main():
             os.write(json_out, (json.dumps(result) + "\n").encode())
         else:
             print(json.dumps(result), flush=True)
-    if one_job:
+    if one_job and not share:
         sdist.finalize()
     if dist is not None:
         dist.destroy_process_group()

@@ -112,8 +112,10 @@ int shred_reset(Trainer* trainer);
 /* The sharded load (dist=replicate) over a caller-supplied all-gather instead of RCCL (host-side
  * collectives, e.g. torch.distributed gloo): later load_corpus calls count only byte range `rank`
  * of `world` on this trainer's device, and `gather(ctx, send, nbytes, &out_bytes)` must return
- * every rank's buffer concatenated in rank order (valid until its next call).  world <= 1 or a
- * NULL gather turns it off.  Returns 0, or -1 for a bad rank. */
+ * every rank's buffer concatenated in rank order (valid until its next call), or NULL when the
+ * gather failed: load_corpus then fails (-1) instead of building a table from a partial gather.
+ * world <= 1 or a NULL gather turns it off.  The stream layout has no sharded load: load_corpus
+ * returns -1 when a gather is set with layout=stream.  Returns 0, or -1 for a bad rank. */
 typedef const void* (*shred_gather_fn)(void* ctx, const void* send, size_t nbytes, size_t* out_bytes);
 int shred_set_load_gather(Trainer* trainer, int rank, int world, shred_gather_fn gather, void* ctx);
 /* Diagnostic: runs `iters` device merges of a pair (a, b) that must not occur in the corpus

@@ -35,6 +35,14 @@ int or_load(OrTrainer* t, const char* path);
  * once max_seconds (<=0: none) of train time have elapsed.  Returns merges performed. */
 int or_train(OrTrainer* t, long max_merges, double max_seconds);
 void or_save(const OrTrainer* t, const char* model_path, const char* vocab_path);
+/* The reference's other entry points, for call sequences through one trainer:
+ * bpe_init (bpe.cpp:98-108), bpe_count_bigrams (:187-230, adds to the current pair map and heap),
+ * bpe_merge_batch (:232-323, returns merges done).  or_load keeps the merges and the heap and
+ * starts a fresh pair map, as bpe_load_corpus does (:176-183). */
+void or_init(OrTrainer* t);
+void or_count(OrTrainer* t);
+int or_merge_batch(OrTrainer* t, int batch);
+size_t or_num_merges(const OrTrainer* t);
 /* Trace file: "M a b freq new_id" per merge (bpe.cpp:260) and
  * "B batch done heap_size top_freq" per batch (bpe.cpp:369).  NULL disables. */
 void or_set_trace(OrTrainer* t, const char* path);

@@ -661,8 +661,11 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
       k_cache_insert<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, cslot_, cc - 1, misc_);
       ENC_OK(hipGetLastError());
       auto enck = packed_ ? k_cache_encode<true> : k_cache_encode<false>;
+      // arena offsets must stay below 2^31: bit 31 of a payload tags "ids inline in the slot", so
+      // a larger arena flags "arena full" and the call reruns on the direct path
+      const u64 arena_cap = std::min<u64>(cap_bytes_, (u64)1 << 31);
       enck<<<dim3((unsigned)(cc / kThreads)), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, cslot_, cc,
-                                                                       rank_, cap_bytes_, pad_, misc_);
+                                                                       rank_, arena_cap, pad_, misc_);
       ENC_OK(hipGetLastError());
       k_cache_words<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, cslot_, cc - 1, rank_, pad_, tcnt_, bcnt_,
                                                                    misc_);

@@ -342,7 +342,8 @@ void merge_entries(const uint8_t* d, const Entry* all, size_t total, const LoadO
 
 // The sharded load (LoadOptions::shard_world > 1): this rank's words, then every rank's merged.
 // SHREDWORD_LOAD_SIM_SHARDS=k (tests, one process): the k ranges counted in turn, merged the same way.
-void load_sharded(const uint8_t* d, size_t n, const LoadOptions& opt, int threads, WordTable* out, int sim) {
+bool load_sharded(const uint8_t* d, size_t n, const LoadOptions& opt, int threads, WordTable* out, int sim,
+                  std::string* err) {
   bool on_gpu = false;
   if (sim > 1) {
     std::vector<Entry> all;
@@ -358,22 +359,29 @@ void load_sharded(const uint8_t* d, size_t n, const LoadOptions& opt, int thread
                                             &on_gpu);
     size_t got = 0;
     const Entry* all = (const Entry*)opt.gather(opt.gather_ctx, mine.data(), mine.size() * sizeof(Entry), &got);
+    // A failed gather (the caller's callback raised, a peer left) must not become an empty
+    // table: every rank would then train on nothing without an error.
+    if (!all || got % sizeof(Entry) != 0 || got < mine.size() * sizeof(Entry)) {
+      if (err)
+        *err = "sharded load: the word-list all-gather failed (" + std::to_string(got) + " bytes returned for " +
+               std::to_string(mine.size() * sizeof(Entry)) + " sent)";
+      return false;
+    }
     merge_entries(d, all, got / sizeof(Entry), opt, threads, out);
   }
   out->counted_on_gpu = on_gpu;
+  return true;
 }
 
 }  // namespace
 
-void load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordTable* out) {
+int load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordTable* out, std::string* err) {
   int threads = opt.threads > 0 ? opt.threads : (int)std::thread::hardware_concurrency();
   threads = std::max(1, std::min(threads, 32));
   const char* sim_env = std::getenv("SHREDWORD_LOAD_SIM_SHARDS");
   const int sim = sim_env ? std::atoi(sim_env) : 0;
-  if (((opt.shard_world > 1 && opt.gather) || sim > 1) && !opt.want_stream && n > 0 && !std::memchr(d, 0, n)) {
-    load_sharded(d, n, opt, threads, out, sim);
-    return;
-  }
+  if (((opt.shard_world > 1 && opt.gather) || sim > 1) && !opt.want_stream && n > 0 && !std::memchr(d, 0, n))
+    return load_sharded(d, n, opt, threads, out, sim, err) ? 0 : -1;
   // the device count (types layout, NUL-free files: every line is read whole, so the words are
   // the maximal runs of non-delimiters of the whole file)
   if (opt.gpu_device >= 0 && !opt.want_stream && n >= opt.gpu_min_bytes && !std::memchr(d, 0, n)) {
@@ -387,7 +395,7 @@ void load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordT
       if (std::getenv("SHREDWORD_LOAD_REPORT"))
         std::fprintf(stderr, "[LOAD] device count %.1f ms, host table %.1f ms\n", 1e3 * (t1 - t0),
                      1e3 * (now_seconds() - t1));
-      return;
+      return 0;
     }
     std::fprintf(stderr, "[WARNING]\t GPU word count unavailable (%s): counting on the host\n", why.c_str());
   }
@@ -421,6 +429,7 @@ void load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordT
       });
     });
   }
+  return 0;
 }
 
 int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::string* err) {
@@ -438,8 +447,7 @@ int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::s
   size_t n = (size_t)st.st_size;
   if (n == 0) {
     ::close(fd);
-    load_corpus_bytes(nullptr, 0, opt, out);
-    return 0;
+    return load_corpus_bytes(nullptr, 0, opt, out, err);
   }
   void* m = ::mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
   ::close(fd);
@@ -448,9 +456,9 @@ int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::s
     return -1;
   }
   ::madvise(m, n, MADV_SEQUENTIAL);
-  load_corpus_bytes((const uint8_t*)m, n, opt, out);
+  const int rc = load_corpus_bytes((const uint8_t*)m, n, opt, out, err);
   ::munmap(m, n);
-  return 0;
+  return rc;
 }
 
 }  // namespace shred

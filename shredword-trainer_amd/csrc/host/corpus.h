@@ -77,6 +77,7 @@ bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec
 int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::string* err);
 
 // Builds a WordTable from in-memory text (same rules); used by tests and tools.
-void load_corpus_bytes(const uint8_t* data, size_t n, const LoadOptions& opt, WordTable* out);
+// 0, or -1 with *err set (a sharded load whose word-list all-gather failed).
+int load_corpus_bytes(const uint8_t* data, size_t n, const LoadOptions& opt, WordTable* out, std::string* err = nullptr);
 
 }  // namespace shred

@@ -217,6 +217,7 @@ const void* dist_allgather_bytes(void*, const void* send, size_t nbytes, size_t*
   keep.clear();
   if (!dist_active()) {
     keep.assign((const uint8_t*)send, (const uint8_t*)send + nbytes);
+    keep.push_back(0);  // never NULL: NULL means a failed gather
     *out_bytes = nbytes;
     return keep.data();
   }
@@ -245,7 +246,8 @@ const void* dist_allgather_bytes(void*, const void* send, size_t nbytes, size_t*
     keep.insert(keep.end(), all.data() + (size_t)r * slot + 8, all.data() + (size_t)r * slot + 8 + n);
   }
   *out_bytes = keep.size();
-  return keep.data();
+  static const uint8_t kNothing = 0;  // NULL means a failed gather (shred_gather_fn)
+  return keep.empty() ? &kNothing : keep.data();
 }
 
 }  // namespace shred

@@ -62,6 +62,19 @@ void Engine::verify_selection(Backend& be, int32_t a, int32_t b, uint64_t freq) 
 bool Engine::merge_one(Backend& be, int remaining) {
   int32_t a, b;
   uint64_t freq;
+  // A pair map that is not the corpus's count (call sequences such as count twice, or a batch
+  // after a reload without a count): the select needs recompute_freq's rescan (bpe.cpp:251), so
+  // no guess runs and the corpus's counts come from one device recount, kept current by the
+  // merges' deltas.
+  const bool exact = sel_.exact();
+  if (!exact) {
+    finish_speculation(be);
+    if (!sel_.truth_live()) {
+      std::vector<PairCount> pc;
+      be.count_pairs(unk_, &pc);
+      sel_.set_truth(pc);
+    }
+  }
   const double t0 = now_seconds();
   const bool ok = sel_.select(&a, &b, &freq);
   const double t1 = now_seconds();
@@ -94,7 +107,8 @@ bool Engine::merge_one(Backend& be, int remaining) {
       finish_speculation(be);
     }
   }
-  const int chain = speculate_ ? std::max(1, std::min(std::min(chain_max_, be.max_chain()), remaining)) : 1;
+  const bool spec = speculate_ && exact;
+  const int chain = spec ? std::max(1, std::min(std::min(chain_max_, be.max_chain()), remaining)) : 1;
   if (!launched) {
     chain_ab_.assign(2 * (size_t)chain, 0);
     chain_ab_[0] = a;
@@ -106,7 +120,7 @@ bool Engine::merge_one(Backend& be, int remaining) {
   }
   // overlap: the next merges' guesses run while this one is consumed (up to the backend's depth;
   // each guess shares no token with this merge or the guesses before it)
-  if (speculate_ && chain == 1) {
+  if (spec && chain == 1) {
     const size_t depth = (size_t)std::max(1, be.overlap_depth());
     while (pending_.size() < depth && (int)pending_.size() + 1 < remaining && be.can_overlap()) {
       used_.assign({a, b});
@@ -130,7 +144,7 @@ bool Engine::merge_one(Backend& be, int remaining) {
   // frequent than the guess in flight (made before them; its own count is unchanged by this
   // merge) replaces it now, so the device undoes and redoes the guess while this merge is
   // applied and the next one selected.  The exact selection still confirms or rolls back.
-  if (correct_ && speculate_ && chain == 1 && pending_.size() == 1 && pending_.front().X == X + 1 && remaining > 1 &&
+  if (correct_ && spec && chain == 1 && pending_.size() == 1 && pending_.front().X == X + 1 && remaining > 1 &&
       be.can_overlap()) {
     const Guess g = pending_.front();
     int32_t pa, pb;
@@ -193,7 +207,8 @@ int Engine::train(Backend& be) {
   times_.init_s += now_seconds() - t0;
   int total = 0;
   const int target = (int)target_vocab_ - kBaseVocab;  // bpe.cpp:353
-  if (target > 0) be.reserve_ids((int32_t)target_vocab_);
+  // ids continue after the merges of earlier trainings (new_id = 256 + num_merges, bpe.cpp:259)
+  if (target > 0) be.reserve_ids((int32_t)(kBaseVocab + merge_a_.size() + (size_t)target));
   while (total < target) {
     if (sel_.heap_empty()) {
       if (log_ >= 1) std::printf("[INFO]\t Heap exhausted, stopping training\n");

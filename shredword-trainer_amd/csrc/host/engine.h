@@ -66,6 +66,8 @@ class Engine {
  public:
   void configure(size_t target_vocab_size, int32_t unk_id, uint64_t min_pair_freq);
   void reset_selection() { sel_.reset(unk_, min_freq_); }
+  // bpe_load_corpus: the pair map starts fresh, the heap and the merges stay (bpe.cpp:176-183).
+  void reload() { sel_.reset_info(); }
   void forget_merges();
 
   void count_bigrams(Backend& be);            // bpe_count_bigrams (bpe.cpp:187-230)

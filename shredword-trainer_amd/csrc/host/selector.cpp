@@ -27,18 +27,42 @@ void Selector::reset(int32_t unk_id, uint64_t min_pair_freq) {
   // mapped pages (a 4 M -> 16 M slot grow costs ~12 ms mid-training at C3)
   const size_t want = std::max<size_t>(size_t(1) << 20, table_.size());
   table_.assign(want, Info{kEmptyKey, 0});
-  seq_.assign(table_.size(), 0);
-  seq_live_ = true;
+  created_.clear();
   mask_ = table_.size() - 1;
   count_ = 0;
   heap_.assign(1, HeapNode{0, 0, 0});
+  exact_ = true;  // an empty map and an empty heap: nothing is popped before a count
+  truth_live_ = false;
+  truth_.clear();
+}
+
+void Selector::reset_info() {
+  std::fill(table_.begin(), table_.end(), Info{kEmptyKey, 0});
+  created_.clear();
+  count_ = 0;
+  exact_ = false;  // the kept heap's entries meet a map that has not counted the new corpus
+  truth_live_ = false;
+  truth_.clear();
+}
+
+void Selector::set_truth(const std::vector<PairCount>& pairs) {
+  truth_.clear();
+  truth_.reserve(pairs.size() * 2);
+  for (const PairCount& p : pairs)
+    if (p.a != unk_ && p.b != unk_) truth_[pack_pair(p.a, p.b)] = p.count;
+  truth_live_ = true;
+}
+
+uint64_t Selector::recount(int32_t a, int32_t b) const {
+  if (a == unk_ || b == unk_) return 0;  // bpe.cpp:53
+  if (!truth_live_) fatal("Selector: a rescan without the truth table");
+  const auto it = truth_.find(pack_pair(a, b));
+  return it == truth_.end() ? 0 : it->second;
 }
 
 void Selector::grow() {
   HugeVec<Info> old(table_.size() * 4, Info{kEmptyKey, 0});
-  HugeVec<uint32_t> old_seq(seq_live_ ? old.size() : 0, 0);
   old.swap(table_);
-  if (seq_live_) old_seq.swap(seq_);
   mask_ = table_.size() - 1;
   for (size_t i = 0; i < old.size(); ++i) {
     const Info& in = old[i];
@@ -46,7 +70,6 @@ void Selector::grow() {
     uint64_t j = mix64(in.key) & mask_;
     while (table_[j].key != kEmptyKey) j = (j + 1) & mask_;
     table_[j] = in;
-    if (seq_live_) seq_[j] = old_seq[i];
   }
 }
 
@@ -67,7 +90,7 @@ Selector::Info& Selector::get(int32_t a, int32_t b) {
     while (table_[j].key != kEmptyKey) j = (j + 1) & mask_;
   }
   table_[j] = Info{key, 0};
-  if (seq_live_) seq_[j] = (uint32_t)count_;
+  created_.push_back(key);
   ++count_;
   return table_[j];
 }
@@ -149,6 +172,10 @@ Selector::HeapEnt Selector::pop() {
 }
 
 void Selector::add_counts(std::vector<PairCount> pairs) {
+  // A count on a map that already holds pairs adds to them (bpe.cpp:206-211): the map is then
+  // no longer the corpus's count.  On a fresh map it is exactly the count.
+  if (count_ != 0 && !pairs.empty()) exact_ = false;
+  else if (count_ == 0) exact_ = true;
   // bimap_get is reached in (word rank, position) order, so that is creation order.
   std::sort(pairs.begin(), pairs.end(), [](const PairCount& x, const PairCount& y) { return x.ft < y.ft; });
   for (const PairCount& p : pairs) {
@@ -156,24 +183,23 @@ void Selector::add_counts(std::vector<PairCount> pairs) {
     if (in.freq() == 0) in.set_version(0);  // bpe.cpp:207-210
     in.set_freq(in.freq() + p.count);
   }
-  // Heap build: bucket 0..4095, chain (creation) order, freq >= min (bpe.cpp:218-225).
-  std::vector<std::pair<uint64_t, uint64_t>> order;  // ((bucket << 32) | seq, slot)
-  order.reserve(count_);
-  for (uint64_t i = 0; i < table_.size(); ++i) {
-    const Info& in = table_[i];
-    if (in.key != kEmptyKey && in.freq() >= min_freq_) {
-      uint32_t bk = pair_fnv(pair_first(in.key), pair_second(in.key)) & (kPairBuckets - 1);
-      order.push_back({((uint64_t)bk << 32) | seq_[i], i});
+  // Heap build: bucket 0..4095, chain (creation) order, freq >= min (bpe.cpp:218-225), over every
+  // pair of the map (those the merges created included).
+  std::vector<std::pair<uint64_t, uint64_t>> order;  // ((bucket << 32) | creation, key)
+  order.reserve(created_.size());
+  for (size_t c = 0; c < created_.size(); ++c) {
+    const uint64_t key = created_[c];
+    const Info* in = find(key);
+    if (in && in->freq() >= min_freq_) {
+      const uint32_t bk = pair_fnv(pair_first(key), pair_second(key)) & (kPairBuckets - 1);
+      order.push_back({((uint64_t)bk << 32) | c, key});
     }
   }
   std::sort(order.begin(), order.end());
   for (auto& o : order) {
-    const Info& in = table_[o.second];
-    push(pair_first(in.key), pair_second(in.key), in.freq(), in.version());
+    const Info* in = find(o.second);
+    push(pair_first(o.second), pair_second(o.second), in->freq(), in->version());
   }
-  // Creation order is read only by this heap build: the merge loop's new pairs skip the store
-  // (one random line of a 64 MB array per new pair at C3).
-  seq_live_ = false;
 }
 
 bool Selector::predict_next(int32_t a, int32_t b, size_t window, int32_t* pa, int32_t* pb) const {
@@ -336,7 +362,8 @@ bool Selector::select(int32_t* a, int32_t* b, uint64_t* freq) {
       ++ctr_.stale;
       continue;
     }
-    uint64_t actual = (top.a == unk_ || top.b == unk_) ? 0 : in.freq();
+    // recompute_freq (bpe.cpp:251): info.freq while the map is exact, else the truth table
+    uint64_t actual = exact_ ? ((top.a == unk_ || top.b == unk_) ? 0 : in.freq()) : recount(top.a, top.b);
     if (actual != in.freq()) {
       in.set_freq(actual);
       in.bump_version();
@@ -479,6 +506,15 @@ void Selector::apply_finish(int32_t a, int32_t b, int32_t X) {
   Info& merged = get(a, b);
   merged.set_freq(0);
   merged.bump_version();
+  if (truth_live_) {  // the corpus's counts follow the same exact deltas (pairs holding unk: none)
+    for (const Change& c : ordered_) {
+      const int32_t f = (int32_t)(uint32_t)(c.hk >> 32), s = (int32_t)(uint32_t)c.hk;
+      if ((f == a && s == b) || f == unk_ || s == unk_) continue;
+      uint64_t& v = truth_[pack_pair(f, s)];
+      v = c.delta < 0 ? (v >= (uint64_t)(-c.delta) ? v - (uint64_t)(-c.delta) : 0) : v + (uint64_t)c.delta;
+    }
+    truth_[pack_pair(a, b)] = 0;
+  }
   const uint64_t c3 = __builtin_ia32_rdtsc();
   ctr_.cyc_walk += c3 - c2;
   for (const HeapNode& p : pushes_) push(p.a, p.b, node_freq(p), node_version(p));

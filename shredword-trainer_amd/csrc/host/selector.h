@@ -10,7 +10,13 @@
 //                   if strictly greater (reference heap.cpp:53-114)
 //  * select         bpe_merge_batch's pop loop (bpe.cpp:244-258); the O(S) recompute_freq
 //                   (bpe.cpp:52-65) is replaced by its provable value: 0 for keys holding unk,
-//                   info.freq otherwise (deltas keep non-unk counts exact, SURVEY.md §0 finding 3)
+//                   info.freq otherwise (deltas keep non-unk counts exact, SURVEY.md §0 finding 3).
+//                   That holds while the pair info IS the corpus's count (exact()): after a bpe_init,
+//                   or a count on the fresh pair map of a load.  Call sequences that break it (a
+//                   count on a counted map doubles it, bpe.cpp:207-211; merge_batch after a load
+//                   without a count pops the old corpus's heap over a fresh map, :176-183) take the
+//                   rescan's value from a truth table: one device recount, then the merges' exact
+//                   deltas (set_truth / truth_live).
 //  * apply          the FreqChangeMap semantics of bpe.cpp:265-313: deltas keyed by
 //                   ((i64)first << 32) | (i64)second (sign-extension folds every (x, negative) key
 //                   to (-1, negative)), applied bucket (key % 1024) ascending and, inside a bucket,
@@ -22,6 +28,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <new>
+#include <unordered_map>
 #include <vector>
 
 namespace shred {
@@ -90,7 +97,10 @@ struct PairCount {
 
 class Selector {
  public:
+  // bpe_init's fresh pair map and heap (bpe.cpp:103-106).
   void reset(int32_t unk_id, uint64_t min_pair_freq);
+  // bpe_load_corpus: a fresh pair map (bpe.cpp:183); the heap and its entries stay.
+  void reset_info();
 
   // bpe_count_bigrams (bpe.cpp:187-230): adds counts (new pairs created in first-touch order),
   // then pushes every pair with freq >= min in (FNV bucket & 4095, creation order).
@@ -125,6 +135,14 @@ class Selector {
   // predict_avoid refines its guess by replaying the coming select() on an overlay of the heap
   // (simulate_select); off: the slot-order guess alone.
   void set_simulate_pops(bool on) { simulate_pops_ = on; }
+
+  // True while every pair's info equals its count in the corpus (recompute_freq is then
+  // info.freq).  Otherwise select() needs the truth table.
+  bool exact() const { return exact_; }
+  bool truth_live() const { return truth_live_; }
+  // The corpus's pair counts now (a fresh K1): recompute_freq's values until the corpus changes;
+  // each applied merge then updates them by its exact deltas.
+  void set_truth(const std::vector<PairCount>& pairs);
 
   size_t heap_size() const { return heap_.empty() ? 0 : heap_.size() - 1; }
   bool heap_empty() const { return heap_.size() <= 1; }
@@ -177,9 +195,15 @@ class Selector {
   int32_t unk_ = 0;
   uint64_t min_freq_ = 2000;
   HugeVec<Info> table_;
-  HugeVec<uint32_t> seq_;  // creation order of table_[j] (bimap_get order), for the heap build
-  bool seq_live_ = true;   // seq_ is kept until the heap build has read it
+  // Creation order (bimap_get order) of every pair since the last fresh map: the heap build of a
+  // count pushes in (bucket, creation) order, and a count may come after merges created pairs.
+  // An append-only log (a sequential store per new pair, not a random one).
+  std::vector<uint64_t> created_;
   size_t count_ = 0;
+  bool exact_ = true;
+  bool truth_live_ = false;
+  std::unordered_map<uint64_t, uint64_t> truth_;  // pair -> its count in the corpus (non-exact state)
+  uint64_t recount(int32_t a, int32_t b) const;
   uint64_t mask_ = 0;
   // The reference's binary heap (heap.cpp), logical slot k stored at heap_[k + 1]: with 16-byte
   // nodes on a 2 MiB-aligned array, the two children of a slot share one 32-byte half line and

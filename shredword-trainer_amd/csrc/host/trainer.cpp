@@ -75,6 +75,10 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
     t->trace = val.empty() ? nullptr : std::fopen(val.c_str(), "w");
     t->engine.set_trace(t->trace);
     if (!val.empty() && !t->trace) return -1;
+  } else if (key == "trace_note") {  // a caller's line in the trace file (tests of call sequences)
+    if (!t->trace) return -1;
+    std::fprintf(t->trace, "%s\n", val.c_str());
+    std::fflush(t->trace);
   } else if (key == "timing") {
     t->timing = std::atoi(val.c_str()) != 0;
     if (t->dev) t->dev->set_timing(t->timing);
@@ -256,6 +260,10 @@ int bpe_load_corpus(Trainer* t, const char* path) {
     opt.gather = t->ext_gather;
     opt.gather_ctx = t->ext_ctx;
   }
+  if (t->ext_gather && t->ext_world > 1 && opt.want_stream) {
+    std::fprintf(stderr, "[ERROR]\t a sharded load (shred_set_load_gather) needs the types layout, not layout=stream\n");
+    return -1;
+  }
   std::string err;
   WordTable wt;
   if (load_corpus(path, opt, &wt, &err) != 0) {
@@ -265,7 +273,7 @@ int bpe_load_corpus(Trainer* t, const char* path) {
   t->wt = std::move(wt);  // last load wins (bpe.cpp:176-178)
   t->loaded = true;
   t->device_stale = true;
-  t->engine.reset_selection();
+  t->engine.reload();     // a fresh pair map; the merges and the heap stay (bpe.cpp:183)
   if (t->engine.log() >= 1)
     std::printf("[DEBUG]\t Character histogram built with %zu unique characters.\n", t->wt.distinct_bytes);
   // Put the word table in HBM now when a GPU is present, so train() starts HBM-resident.
@@ -281,8 +289,24 @@ void bpe_init(Trainer* t) {
   bpe_count_bigrams(t);
 }
 
+// Before any load the reference's corpus is empty (zero-initialised Trainer): a count adds
+// nothing, a batch finds the heap empty, a train performs no merge.  No device is needed then.
+namespace {
+struct NoCorpus : Backend {
+  void count_pairs(int32_t, std::vector<PairCount>* out) override { out->clear(); }
+  void merge_chain(const int32_t*, int, int32_t) override { fatal("merge without a corpus"); }
+  size_t collect(int32_t, const DeltaRecord**) override { return 0; }
+  void token_freq(size_t T, std::vector<uint64_t>* freq) override { freq->assign(T, 0); }
+};
+}  // namespace
+
 void bpe_count_bigrams(Trainer* t) {
   if (!t) fatal("NULL trainer pointer");
+  if (!t->loaded) {
+    NoCorpus none;
+    t->engine.count_bigrams(none);
+    return;
+  }
   if (!ensure_device(t, "bpe_count_bigrams")) return;
   t->engine.count_bigrams(*t->dev);
 }
@@ -292,6 +316,7 @@ int bpe_merge_batch(Trainer* t, int batch_size) {
     std::fprintf(stderr, "[ERROR]\t Trainer pointer is NULL!\n");
     return -1;
   }
+  if (!t->loaded) return 0;  // the heap of a trainer that never loaded is empty
   if (!ensure_device(t, "bpe_merge_batch")) return -1;
   return t->engine.merge_batch(*t->dev, batch_size);
 }
@@ -300,6 +325,10 @@ int bpe_train(Trainer* t) {
   if (!t) {
     std::fprintf(stderr, "[ERROR]\t Trainer pointer is NULL!\n");
     return -1;
+  }
+  if (!t->loaded) {
+    NoCorpus none;
+    return t->engine.train(none);
   }
   if (!ensure_device(t, "bpe_train")) return -1;
   return t->engine.train(*t->dev);

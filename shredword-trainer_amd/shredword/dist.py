@@ -47,12 +47,21 @@ def host_load_gather(group=None):
     keep = {}
 
     def gather(_ctx, send, nbytes, out_bytes):
-        mine = ctypes.string_at(send, nbytes) if nbytes else b""
-        parts = [None] * dist.get_world_size(group)
-        dist.all_gather_object(parts, mine, group=group)
-        blob = b"".join(parts)
-        keep["buf"] = ctypes.create_string_buffer(blob, max(1, len(blob)))
-        out_bytes[0] = len(blob)
-        return ctypes.addressof(keep["buf"])
+        # An exception must not cross the C boundary (ctypes would print it and return 0 bytes,
+        # which reads as "no words"): report a NULL result and the library fails load_corpus.
+        try:
+            mine = ctypes.string_at(send, nbytes) if nbytes else b""
+            parts = [None] * dist.get_world_size(group)
+            dist.all_gather_object(parts, mine, group=group)
+            blob = b"".join(parts)
+            keep["buf"] = ctypes.create_string_buffer(blob, max(1, len(blob)))
+            out_bytes[0] = len(blob)
+            return ctypes.addressof(keep["buf"])
+        except BaseException as e:  # noqa: BLE001 (reported, then turned into the C error)
+            import sys
+            print(f"[ERROR]\t host_load_gather: {e!r}", file=sys.stderr)
+            keep.pop("buf", None)
+            out_bytes[0] = 0
+            return None
 
     return GATHER_FN(gather)

@@ -78,6 +78,49 @@ def case_corpus(corpus_dir):
     return get
 
 
+SEQ = os.path.join(GOLDEN, "seq")
+
+
+def seq_cases():
+    """The stateful call-sequence goldens (tests/golden/seq, make_golden.py SEQ_CASES)."""
+    return sorted(d for d in os.listdir(SEQ) if os.path.isfile(os.path.join(SEQ, d, "case.json")))
+
+
+def load_seq_case(name):
+    d = os.path.join(SEQ, name)
+    with open(os.path.join(d, "case.json")) as f:
+        case = json.load(f)
+    case["outputs"] = []
+    for i in range(len(case["saves"])):
+        with open(os.path.join(d, f"model{i}.bin"), "rb") as fm, open(os.path.join(d, f"vocab{i}.txt"), "rb") as fv:
+            case["outputs"].append((fm.read(), fv.read()))
+    with gzip.open(os.path.join(d, "trace.txt.gz"), "rt") as f:
+        case["trace"] = f.read()
+    return case
+
+
+@pytest.fixture(scope="session")
+def seq_case(corpus_dir):
+    """name -> (case, ops) with every load op's corpus built (md5-checked) and named by path."""
+    def get(name):
+        case = load_seq_case(name)
+        ops = []
+        for op in case["script"]:
+            if op[0] == "load":
+                recipe = op[1]
+                key = json.dumps({k: v for k, v in recipe.items() if k not in ("md5", "size")}, sort_keys=True)
+                if key not in _CORPUS_CACHE:
+                    path = os.path.join(corpus_dir, f"corpus_{len(_CORPUS_CACHE)}.txt")
+                    build_corpus(recipe, path)
+                    assert corpora.md5_file(path) == recipe["md5"], f"generator drift for {name}"
+                    _CORPUS_CACHE[key] = path
+                ops.append(("load", _CORPUS_CACHE[key]))
+            else:
+                ops.append(tuple(op))
+        return case, ops
+    return get
+
+
 @pytest.fixture(scope="session")
 def oracle_bin():
     subprocess.run(["make", "-s", "-C", ORACLE, "port"], check=True)

@@ -29,6 +29,13 @@ def load():
     lib.hh_merge_batch.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.hh_merge_batch.restype = ctypes.c_int
     lib.hh_init.argtypes = [ctypes.c_void_p]
+    lib.hh_create.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_uint64]
+    lib.hh_create.restype = ctypes.c_void_p
+    lib.hh_load.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.hh_load.restype = ctypes.c_int
+    lib.hh_count.argtypes = [ctypes.c_void_p]
+    lib.hh_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.hh_trace_line.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     lib.hh_save.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
     for fn in ("hh_num_words", "hh_num_symbols", "hh_num_tiles", "hh_live_tokens", "hh_heap_size",
                "hh_distinct_bytes", "hh_kept_bytes", "hh_tiles_visited"):

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -52,8 +53,37 @@ class EmuBackend : public Backend {
 
   uint64_t weight(uint32_t rank) const { return layout_ == Layout::kTypes ? wt_.count[rank] : 1; }
 
+  // Any ids (a count after merges: a second train, a count without init): a hash map.
+  void count_pairs_any(int32_t unk, std::vector<PairCount>* out) {
+    std::unordered_map<uint64_t, std::pair<uint64_t, uint64_t>> m;  // pair -> (count, first touch)
+    for (size_t t = 0; t < ts_.num_tiles(); ++t) {
+      const int32_t* p = ts_.tok.data() + ts_.off[t];
+      uint32_t hidx = 0, rank = 0;
+      for (uint32_t i = 0; i < ts_.len[t]; ++i) {
+        if (is_hdr(p[i])) { hidx = i; rank = (uint32_t)(p[i] - kHeaderBase); continue; }
+        if (i + 1 >= ts_.len[t] || is_hdr(p[i + 1]) || p[i] == unk || p[i + 1] == unk) continue;
+        auto it = m.emplace(pack_pair(p[i], p[i + 1]), std::make_pair(uint64_t(0), ~uint64_t(0))).first;
+        it->second.first += weight(rank);
+        it->second.second = std::min<uint64_t>(it->second.second, ((uint64_t)rank << 32) | (i - hidx - 1));
+      }
+    }
+    for (const auto& kv : m)
+      out->push_back({pair_first(kv.first), (int32_t)(uint32_t)kv.first, kv.second.first, kv.second.second});
+  }
+
   void count_pairs(int32_t unk, std::vector<PairCount>* out) override {
     out->clear();
+    bool small = true;
+    for (size_t t = 0; t < ts_.num_tiles() && small; ++t)
+      for (uint32_t i = 0; i < ts_.len[t]; ++i) {
+        const int32_t v = ts_.tok[ts_.off[t] + i];
+        if (!is_hdr(v) && v != unk && (uint32_t)v >= 256) { small = false; break; }
+      }
+    if (!small) {
+      if (cb_) fatal("emulated multi-rank count supports ids < 256 only");
+      count_pairs_any(unk, out);
+      return;
+    }
     const size_t D = 257 * 257;  // ids < 256 plus slot 0 (first count only)
     std::vector<uint64_t> cnt(D, 0), ft(D, ~0ull);
     for (size_t t = 0; t < ts_.num_tiles(); ++t) {
@@ -273,7 +303,17 @@ struct Harness {
   std::unique_ptr<EmuBackend> be;
   Engine engine;
   FILE* trace = nullptr;
+  uint64_t vocab = 0;
+  int32_t unk = 0;
+  float cov = 0.995f;
 };
+
+// Delta slots for every id a call sequence can create: later trainings continue the ids.
+uint32_t slot_cap(uint64_t vocab, int32_t unk) {
+  uint32_t cap = 1024;
+  while (cap < 4 * (vocab + 256) || (unk >= 0 && cap < (uint64_t)unk + 1)) cap *= 2;
+  return cap;
+}
 
 }  // namespace
 
@@ -296,12 +336,64 @@ void* hh_open(const char* path, uint64_t vocab, int32_t unk, float cov, uint64_t
   const Layout lay = layout == 1 ? Layout::kStream : Layout::kTypes;
   size_t b = 0, e = 0;
   shard_range(h->wt, lay, rank, world, &b, &e);
-  uint32_t cap = 1024;
-  while (cap < vocab + 1 || (unk >= 0 && cap < (uint64_t)unk + 1)) cap *= 2;
-  h->be.reset(new EmuBackend(h->wt, lay, b, e, cap));
+  h->be.reset(new EmuBackend(h->wt, lay, b, e, slot_cap(vocab, unk)));
   h->engine.configure(vocab, unk, mpf);
   h->engine.set_log(0);
+  h->vocab = vocab;
+  h->unk = unk;
+  h->cov = cov;
   return h;
+}
+
+// Call sequences (bpe.cpp's entry points in any order) over the emulated device: a trainer with
+// no corpus, then hh_load / hh_init / hh_count / hh_merge_batch / hh_train / hh_save.
+void* hh_create(uint64_t vocab, int32_t unk, float cov, uint64_t mpf) {
+  Harness* h = new Harness();
+  if (cov <= 0.0f || cov >= 1.0f) cov = 0.995f;
+  if (mpf == 0) mpf = kDefaultMinPairFreq;
+  h->engine.configure(vocab, unk, mpf);
+  h->engine.set_log(0);
+  h->vocab = vocab;
+  h->unk = unk;
+  h->cov = cov;
+  return h;
+}
+
+// bpe_load_corpus as trainer.cpp runs it: a new word table and device copy, engine.reload().
+int hh_load(void* p, const char* path) {
+  Harness* h = (Harness*)p;
+  LoadOptions opt;
+  opt.unk_id = h->unk;
+  opt.coverage = h->cov;
+  opt.threads = 2;
+  std::string err;
+  WordTable wt;
+  if (load_corpus(path, opt, &wt, &err) != 0) return -1;
+  h->be.reset();
+  h->wt = std::move(wt);
+  h->be.reset(new EmuBackend(h->wt, Layout::kTypes, 0, h->wt.num_words(), slot_cap(h->vocab, h->unk)));
+  h->engine.reload();
+  return 0;
+}
+
+void hh_count(void* p) {
+  Harness* h = (Harness*)p;
+  if (h->be) h->engine.count_bigrams(*h->be);
+}
+
+void hh_set_trace(void* p, const char* path) {
+  Harness* h = (Harness*)p;
+  if (h->trace) std::fclose(h->trace);
+  h->trace = path ? std::fopen(path, "w") : nullptr;
+  h->engine.set_trace(h->trace);
+}
+
+void hh_trace_line(void* p, const char* line) {
+  Harness* h = (Harness*)p;
+  if (h->trace) {
+    std::fputs(line, h->trace);
+    std::fflush(h->trace);
+  }
 }
 
 // Sharded load (corpus.h LoadOptions::shard_*): this rank counts its byte range, the ranks'
@@ -324,9 +416,7 @@ void* hh_open_sharded(const char* path, uint64_t vocab, int32_t unk, float cov, 
     delete h;
     return nullptr;
   }
-  uint32_t cap = 1024;
-  while (cap < vocab + 1 || (unk >= 0 && cap < (uint64_t)unk + 1)) cap *= 2;
-  h->be.reset(new EmuBackend(h->wt, Layout::kTypes, 0, h->wt.num_words(), cap));
+  h->be.reset(new EmuBackend(h->wt, Layout::kTypes, 0, h->wt.num_words(), slot_cap(vocab, unk)));
   h->engine.configure(vocab, unk, mpf);
   h->engine.set_log(0);
   return h;
@@ -342,27 +432,29 @@ void hh_set_exchange(void* p, ExchangeCb cb, GatherCb gather, void* ctx) {
   ((Harness*)p)->be->set_exchange(cb, gather, ctx);
 }
 
+// trace_path: a new trace file, or "" to keep the current one (hh_set_trace).
 int hh_train(void* p, const char* trace_path) {
   Harness* h = (Harness*)p;
-  if (h->trace) std::fclose(h->trace);
-  h->trace = trace_path ? std::fopen(trace_path, "w") : nullptr;
-  h->engine.set_trace(h->trace);
+  if (!trace_path || *trace_path) hh_set_trace(p, trace_path);
   const int n = h->engine.train(*h->be);
   if (h->trace) std::fflush(h->trace);
   return n;
 }
 
-int hh_merge_batch(void* p, int batch) { return ((Harness*)p)->engine.merge_batch(*((Harness*)p)->be, batch); }
+int hh_merge_batch(void* p, int batch) {
+  Harness* h = (Harness*)p;
+  return h->be ? h->engine.merge_batch(*h->be, batch) : 0;
+}
 void hh_init(void* p) {
   Harness* h = (Harness*)p;
   h->engine.reset_selection();
-  h->engine.count_bigrams(*h->be);
+  if (h->be) h->engine.count_bigrams(*h->be);
 }
 
 void hh_save(void* p, const char* model, const char* vocab, int write) {
   Harness* h = (Harness*)p;
   std::vector<uint64_t> freq;
-  h->be->token_freq(kBaseVocab + h->engine.num_merges(), &freq);
+  if (h->be) h->be->token_freq(kBaseVocab + h->engine.num_merges(), &freq);
   if (write) h->engine.write_outputs(freq, model, vocab);
 }
 

@@ -111,3 +111,49 @@ def test_encoder_without_gpu_fails_loudly(tmp_path):
         BPEEncoder(str(model))
     with pytest.raises(RuntimeError):
         BPEEncoder.from_merges([[97, 98, 256]])
+
+
+def test_failed_load_gather_fails_load_corpus(tmp_path):
+    """A sharded load whose word-list all-gather fails (here: host_load_gather with no process
+    group, so torch.distributed raises inside the callback) makes load_corpus fail instead of
+    training every rank on a partial table."""
+    import corpora
+    from shredword import dist as sdist
+    from shredword.trainer import BPETrainer
+    corpus = str(tmp_path / "c.txt")
+    corpora.write_small_corpus(corpus)
+    t = BPETrainer(vocab_size=300, min_pair_freq=2)
+    t.set_option("log", 0)
+    t.set_load_gather(0, 2, sdist.host_load_gather())
+    with pytest.raises(IOError):
+        t.load_corpus(corpus)
+    # a gather that returns NULL outright
+    from shredword.cbase import GATHER_FN
+    t.set_load_gather(1, 2, GATHER_FN(lambda ctx, send, n, out: None))
+    with pytest.raises(IOError):
+        t.load_corpus(corpus)
+    # a gather is not usable with the stream layout: an error, not a silent whole-file load
+    t.set_load_gather(0, 2, GATHER_FN(lambda ctx, send, n, out: None))
+    t.set_option("layout", "stream")
+    with pytest.raises(IOError):
+        t.load_corpus(corpus)
+    t.destroy()
+
+
+def test_call_sequence_before_any_load(tmp_path):
+    """The reference's trainer with no corpus (zero-initialised): a count adds nothing, a batch
+    finds an empty heap, a train performs no merge, a save writes the 256 byte tokens -- no GPU
+    is needed for any of that."""
+    from shredword.cbase import lib
+    from shredword.trainer import BPETrainer
+    t = BPETrainer(vocab_size=300, min_pair_freq=2)
+    t.set_option("log", 0)
+    lib.bpe_count_bigrams(t.trainer)
+    lib.bpe_init(t.trainer)
+    assert lib.bpe_merge_batch(t.trainer, 5) == 0
+    assert lib.bpe_train(t.trainer) == 0
+    m, v = str(tmp_path / "e.model"), str(tmp_path / "e.vocab")
+    t.save(m, v)
+    t.destroy()
+    assert os.path.getsize(m) == 0
+    assert open(v, "rb").read().count(b"\n") == 257  # token 10 is itself a newline

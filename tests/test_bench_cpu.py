@@ -23,6 +23,9 @@ def test_bench_launches_n_ranks(n):
     assert len(lines) == 1 and lines[0].startswith("{"), out.stdout  # stdout: rank 0's one JSON line, nothing else
     rep = json.loads(lines[0])
     assert rep["n_gpus"] == n
+    # N > 1 measures ONE training by default (sharded load + merge loop on every rank), not N
+    # independent jobs
+    assert rep["dist"] == "replicate"
     ranks = rep["ranks"]
     assert sorted(r["rank"] for r in ranks) == list(range(n))
     assert sorted(r["local_rank"] for r in ranks) == list(range(n))

@@ -10,7 +10,7 @@ import os
 import pytest
 
 import hostharness
-from conftest import golden_cases
+from conftest import golden_cases, seq_cases
 
 
 @pytest.fixture(scope="module")
@@ -109,3 +109,46 @@ def test_merge_batch_matches_train(hh, case_corpus, tmp_path):
         assert got[:len(case["model_bytes"])] == case["model_bytes"]
     finally:
         hh.hh_close(h)
+
+
+def run_script_harness(hh, case, ops, tmp_path):
+    """One emulated trainer through a golden's call sequence: (trace, outputs, returns)."""
+    cfg = case["config"]
+    h = hh.hh_create(cfg["vocab_size"], cfg["unk_id"], cfg["character_coverage"], cfg["min_pair_freq"])
+    trace = str(tmp_path / "seq_trace.txt")
+    hh.hh_set_trace(h, trace.encode())
+    outputs, returns = [], []
+    try:
+        for op in ops:
+            ret = 0
+            if op[0] == "load":
+                ret = hh.hh_load(h, op[1].encode())
+            elif op[0] == "init":
+                hh.hh_init(h)
+            elif op[0] == "count":
+                hh.hh_count(h)
+            elif op[0] == "batch":
+                ret = hh.hh_merge_batch(h, op[1])
+            elif op[0] == "train":
+                ret = hh.hh_train(h, b"")
+            elif op[0] == "save":
+                m, v = str(tmp_path / f"m{len(outputs)}"), str(tmp_path / f"v{len(outputs)}")
+                hh.hh_save(h, m.encode(), v.encode(), 1)
+                outputs.append((open(m, "rb").read(), open(v, "rb").read()))
+            returns.append([op[0], str(ret)])
+            hh.hh_trace_line(h, f"S {op[0]} {ret}\n".encode())
+    finally:
+        hh.hh_close(h)
+    return open(trace).read(), outputs, returns
+
+
+@pytest.mark.parametrize("name", seq_cases())
+def test_host_logic_call_sequences(name, hh, seq_case, tmp_path):
+    """The product's host code (Engine reload / count / merge_batch / train, the Selector's pair-map
+    exactness and truth table) through the reference's stateful call sequences, over the emulated
+    kernels: the reference's trace, every save's bytes and every return value."""
+    case, ops = seq_case(name)
+    trace, outputs, returns = run_script_harness(hh, case, ops, tmp_path)
+    assert returns == case["returns"]
+    assert trace == case["trace"]
+    assert outputs == case["outputs"]

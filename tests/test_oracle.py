@@ -11,7 +11,7 @@ import subprocess
 
 import pytest
 
-from conftest import golden_cases
+from conftest import golden_cases, seq_cases
 
 
 @pytest.fixture(scope="session")
@@ -35,6 +35,33 @@ def oracle_runs(case_corpus, oracle_bin, tmp_path_factory):
     futs = {n: pool.submit(run, n, *cases[n]) for n in order}
     yield lambda n: futs[n].result()
     pool.shutdown(wait=True)
+
+
+@pytest.mark.parametrize("name", seq_cases())
+def test_oracle_call_sequence_matches_reference(name, seq_case, oracle_bin, tmp_path):
+    """The restatement driven through the same call sequence as the reference's golden (load twice,
+    train twice, init + merge_batch, counts on a stale pair map ...): every save's files, every
+    [MERGE]/batch line and every call's return value."""
+    case, ops = seq_case(name)
+    cfg = case["config"]
+    argv, nsave = [], 0
+    for op in ops:
+        if op[0] == "load":
+            argv.append("load=" + op[1])
+        elif op[0] == "batch":
+            argv.append(f"batch={op[1]}")
+        elif op[0] == "save":
+            argv.append(f"save={tmp_path}/m{nsave},{tmp_path}/v{nsave}")
+            nsave += 1
+        else:
+            argv.append(op[0])
+    trace = str(tmp_path / "trace")
+    subprocess.run([oracle_bin, "--script", str(cfg["vocab_size"]), str(cfg["unk_id"]), repr(cfg["character_coverage"]),
+                    str(cfg["min_pair_freq"]), trace] + argv, check=True)
+    assert open(trace).read() == case["trace"]
+    for i, (model, vocab) in enumerate(case["outputs"]):
+        assert open(tmp_path / f"m{i}", "rb").read() == model, f"save {i}: .model"
+        assert open(tmp_path / f"v{i}", "rb").read() == vocab, f"save {i}: .vocab"
 
 
 @pytest.mark.parametrize("name", golden_cases())
