@@ -506,6 +506,38 @@ def merge_loop_report(st, merges, elapsed, args):
     return out
 
 
+def tiebreak_report(st, merges, elapsed, args, out_prefix):
+    """tiebreak=device: the device's own selection (k_word_loop<true>), with the size-independent
+    checks of its output: non-increasing merge frequencies >= min_pair_freq (from the .model's
+    order and the .vocab) are not recomputable without a trace, so the line reports the weighted
+    symbol count of the .vocab (invariant under any merge order) beside the exact mode's."""
+    import numpy as np
+    model, vocab = out_prefix + ".model", out_prefix + ".vocab"
+    ops = np.fromfile(model, dtype="<i4").reshape(-1, 3)
+    spell = [bytes([i]) if i else b"" for i in range(256)]
+    size = [1] * 256
+    for a, b, _x in ops:
+        spell.append(spell[a] + spell[b])
+        size.append(size[a] + size[b])
+    vb, pos, sym = open(vocab, "rb").read(), 0, 0
+    for tok, sz in zip(spell, size):
+        pos += len(tok)
+        end = vb.index(b"\n", pos + 1)
+        sym += int(vb[pos + 1:end]) * sz
+        pos = end + 1
+    n = max(1, st["sel_merges"])
+    return {
+        "mode": "device: every merge selected on the GPU inside k_word_loop<true> (pair table + frontier argmax, "
+                "ties to the smaller pair key); NOT the reference's merge order",
+        "merges_per_s": merges / elapsed, "sel_merges": st["sel_merges"], "launches": st["sel_launches"],
+        "rebuilds": st["sel_rebuilds"], "rebuild_ms": st["sel_rebuild_ms"], "kernel_ms": st["sel_kernel_ms"],
+        "device_select_us_per_merge": st["sel_select_us"] / n, "device_merge_us_per_merge": st["sel_merge_us"] / n,
+        "table_pairs": st["sel_table_pairs"], "table_slots": st["sel_table_slots"],
+        "operands_before_merge": bool((ops[:, :2] < ops[:, 2:3]).all()),
+        "weighted_symbols": sym,
+    }
+
+
 def hbm_probe_leg(device=0, nbytes=4 << 30, reps=10):
     """Achievable HBM bandwidth on this box: streaming read and copy kernels
     of the library (shred_hbm_probe), beside the nominal 8 TB/s peak."""
@@ -549,6 +581,9 @@ def main():
     ap.add_argument("--dist", default="replicate", choices=["replicas", "replicate", "exchange"],
                     help="N > 1: one training with a sharded load (replicate, the default) or a per-merge RCCL "
                          "exchange (exchange), or N independent jobs (replicas); see the module docstring")
+    ap.add_argument("--tiebreak", default="exact", choices=["exact", "device"],
+                    help="merge selection: exact (the reference's heap replay, bit-exact files; default) or device "
+                         "(opt-in K5 mode: every merge selected on the GPU, ties to the smaller pair key)")
     ap.add_argument("--bytes", type=int, default=0, help="override the corpus size (testing)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -641,6 +676,7 @@ def main():
     t.set_option("log", 0)
     t.set_option("device", dev)
     t.set_option("layout", args.layout)
+    t.set_option("tiebreak", args.tiebreak)
     if one_job and not share:
         t.set_option("dist", args.dist)
     elif one_job:
@@ -739,7 +775,8 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "strong" if one_job else ("weak" if world > 1 else "weak"),
+            "scaling": "strong" if one_job else "weak",
+            "tiebreak": args.tiebreak,
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (committed deterministic generator, SURVEY.md §8 d2)",
@@ -787,8 +824,10 @@ def main():
         k1 = result["pair_count_types"]
         k1["achieved_GBps"] = (k1["bytes_per_launch"] / (k1["avg_launch_us"] * 1e-6) / 1e9
                                if k1["avg_launch_us"] > 0 else None)
+        if args.tiebreak == "device":
+            result["tiebreak_device"] = tiebreak_report(st, merges, elapsed, args, os.path.join(tmpd, f"bench_r{rank}"))
         case = fullsize_case(args.config)
-        if case and not args.bytes:
+        if case and not args.bytes and args.tiebreak == "exact":
             result["config"]["corpus_md5_expected"] = case["corpus_md5"]
             result["config"]["unique_bytes"] = case["unique_bytes"]
             # size-independent parity at full size: the bench's own .model/.vocab against the

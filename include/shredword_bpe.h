@@ -100,6 +100,11 @@ int loadVocab(void* trainer, const char* path);
  *                               table with no per-merge collective; exchange shards the word table
  *                               and all-gathers each merge's neighbour records (RCCL over xGMI).
  *                               Output bytes are identical in every mode and world size.
+ *   tiebreak = exact|device     merge selection of train(): exact (default) replays the reference's
+ *                               heap (bit-exact files); device (opt-in, NOT bit-exact) selects every
+ *                               merge on the GPU inside the indexed loop, with no host round trip per
+ *                               merge: the pair of largest count, ties to the smaller (first, second)
+ *                               key (env SHREDWORD_TIEBREAK; types layout, one GPU)
  *   verify_argmax = <n>         debug (K5 check): every n merges (0 = off, the default; env
  *                               SHREDWORD_VERIFY_ARGMAX) the device recounts the corpus's pairs
  *                               and reduces them (k_pair_max): the host heap's selected frequency
@@ -187,6 +192,16 @@ typedef struct ShredStats {
   uint64_t index_run_ints_written;  /* k_word_loop: Σ ints of the changed runs written back */
   uint64_t index_records;           /* k_word_loop: Σ 24-B delta records written to host memory */
   double resident_k3_bytes;    /* k_resident: Σ 8 B x tokens of the tiles a merge rewrote (K3: read + write) */
+  /* tiebreak=device (k_word_loop<true>: the device selects its merges) */
+  uint64_t sel_merges;         /* merges selected on the device */
+  uint64_t sel_launches;       /* launches of the self-selecting loop */
+  uint64_t sel_rebuilds;       /* frontier rebuilds (whole chip, between launches) */
+  double sel_kernel_ms;        /* Σ launch durations (HIP events) */
+  double sel_rebuild_ms;       /* Σ host wall time of the rebuilds */
+  double sel_select_us;        /* device: Σ time selecting (frontier scan + argmax) */
+  double sel_merge_us;         /* device: Σ time merging and updating the pair table */
+  uint64_t sel_table_pairs;    /* pairs in the device pair table at the end */
+  uint64_t sel_table_slots;    /* its capacity */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

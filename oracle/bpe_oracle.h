@@ -43,6 +43,12 @@ void or_init(OrTrainer* t);
 void or_count(OrTrainer* t);
 int or_merge_batch(OrTrainer* t, int batch);
 size_t or_num_merges(const OrTrainer* t);
+/* The selection rule of the product's opt-in tiebreak=device mode (NOT the reference's): from
+ * merge `after` on (0: from the first), each merge takes the pair of largest count, ties to the
+ * smallest key ((u32)first << 32 | (u32)second), among pairs without unk whose count is >=
+ * min_pair_freq; the heap rule decides the merges before.  The merge itself and every count
+ * stay the reference's.  mode 0 = the reference rule throughout. */
+void or_set_tiebreak(OrTrainer* t, int mode, long after);
 /* Trace file: "M a b freq new_id" per merge (bpe.cpp:260) and
  * "B batch done heap_size top_freq" per batch (bpe.cpp:369).  NULL disables. */
 void or_set_trace(OrTrainer* t, const char* path);

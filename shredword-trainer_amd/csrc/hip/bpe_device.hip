@@ -3355,6 +3355,21 @@ void Device::flush_timing(bool block) {
   ev_pending_.resize(keep);
 }
 
+int Device::device_select(const std::vector<PairCount>& pairs, int32_t X0, int n, uint64_t min_freq,
+                          std::vector<SelectedMerge>* out) {
+  HIP_OK(hipSetDevice(ordinal_));
+  park();
+  if (!wl_ || !wl_->ready() || exchange_ || layout_ != Layout::kTypes || !index_on_) return -1;
+  if (words_stale_) index_refresh();  // the words from the tiles (a tile-path merge, or a reset)
+  const int r = wl_->run_select(pairs, X0, (uint32_t)std::max(n, 0), min_freq, out);
+  if (r > 0) {
+    max_id_seen_ = std::max(max_id_seen_, X0 + r - 1);
+    idx_phase_ = true;  // later merges of this train() go to the indexed loop
+    wl_pristine_index_ = false;
+  }
+  return r;
+}
+
 bool Device::index_id_room(int32_t max_id) const { return wl_ && (uint32_t)max_id + 2 <= wl_->id_room(); }
 
 void Device::merge_chain(const int32_t* ab, int n, int32_t X0) {

@@ -93,6 +93,34 @@ struct WEnt {
   u64 sig;
 };
 
+// tiebreak=device (K5 as the selector, WordLoop::run_select): the loop picks its own merges from
+// a pair table on the device.  Table: open addressing on the pair key, count beside it (pairs
+// holding unk are never in it).  Frontier: the slots of every pair ranked at or above a threshold
+// (count desc, key asc) plus stale ones; each merge takes the best live frontier entry, and pairs
+// a merge creates above the threshold join it (only new pairs ever gain: every other count only
+// falls).  An empty frontier sends the launch back to the host, which rebuilds it whole-chip.
+struct SelParams {
+  u64* pkey;          // pair key, kEmpty64 = empty slot
+  u64* pcnt;          // its count in the corpus
+  uint32_t* inf;      // per slot: 1 while in the frontier
+  u64 pmask;
+  uint32_t* fr[2];    // frontier buffers (slots); st[kSelBuf] says which is current
+  uint32_t fcap;
+  uint32_t* st;       // see kSel* below
+  const u64* thr;     // threshold (count, key): every pair ranked at or above it is in the frontier
+  u64* out;           // per merge: key, count
+  uint32_t* upd;      // scratch: slots of the pairs the current merge created
+  int32_t X0;         // id of merge 0 of this training
+  uint32_t n_max;     // merges wanted
+  u64 min_freq;
+  uint32_t fill_max;  // inserts allowed before the table counts as full
+};
+// st words
+constexpr int kSelM = 0, kSelNF = 1, kSelBuf = 2, kSelStatus = 3, kSelIns = 4, kSelErr = 5, kSelStats = 6;
+constexpr int kSelWords = kSelStats + 2 * 6;  // st: 6 words, then 6 u64 statistics
+// exit status: merges done (target reached / below min_pair_freq), frontier to rebuild, table full
+constexpr uint32_t kSelDone = 1, kSelRebuild = 2, kSelFull = 3;
+
 struct WlParams {
   int32_t* wtok;
   const u64* weight;
@@ -115,6 +143,7 @@ struct WlParams {
   uint32_t seq0;
   uint32_t idle_polls;
   WlSlotDev sl[WordLoop::kSlots];
+  SelParams sel;  // k_word_loop<true> only
 };
 
 __device__ __forceinline__ u64 mix64(u64 k) {
@@ -136,6 +165,49 @@ __device__ __forceinline__ u64 nbit(int32_t id, uint32_t s) {
 }
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 ld_agent64(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// tiebreak=device order: larger count first, then the smaller key
+__device__ __forceinline__ bool sel_better(u64 c, u64 k, u64 c2, u64 k2) { return c > c2 || (c == c2 && k < k2); }
+__device__ __forceinline__ bool sel_at_least(u64 c, u64 k, u64 tc, u64 tk) { return c > tc || (c == tc && k <= tk); }
+// The table slot of pair key pk, inserted when absent (~0 when the table is past its probe bound).
+__device__ __forceinline__ u64 sel_slot(const SelParams& q, u64 pk) {
+  u64 h = mix64(pk) & q.pmask;
+#pragma unroll 1
+  for (uint32_t probe = 0; probe < 4096u; ++probe) {
+    const u64 cur = ld_agent64(q.pkey + h);
+    if (cur == pk) return h;
+    if (cur == kEmpty64) {
+      const u64 prev = atomicCAS(q.pkey + h, kEmpty64, pk);
+      if (prev == kEmpty64) {
+        atomicAdd(q.st + kSelIns, 1u);
+        return h;
+      }
+      if (prev == pk) return h;
+    }
+    h = (h + 1) & q.pmask;
+  }
+  atomicMax(q.st + kSelErr, 1u);
+  return ~0ull;
+}
+// One combined record of merge (a, b) -> X as a change of a pair's count (the reference's
+// FreqChangeMap entry, bpe.cpp:297-313, minus the pair merged and pairs holding unk).  New pairs
+// (categories 1 and 3: they hold X) are listed for the frontier.
+__device__ __forceinline__ void sel_apply(const SelParams& q, uint32_t* nnew, int32_t unk, uint32_t cap, uint32_t key,
+                                          u64 sum, int32_t a, int32_t b, int32_t X) {
+  const uint32_t sl = key >> 2, cat = key & 3u;
+  const int32_t id = sl == 0 ? unk : (int32_t)(sl - 1u);
+  if (id == unk || sum == 0) return;
+  const int32_t f = cat < 2u ? id : (cat == 2u ? b : X);
+  const int32_t g = cat == 0u ? a : (cat == 1u ? X : id);
+  if (f == a && g == b) return;
+  const u64 h = sel_slot(q, pair_key(f, g));
+  if (h == ~0ull) return;
+  atomicAdd(q.pcnt + h, (cat & 1u) ? sum : (u64)(-(int64_t)sum));
+  if (cat & 1u) q.upd[atomicAdd(nnew, 1u)] = (uint32_t)h;
+  (void)cap;
 }
 
 struct DeltaH {
@@ -348,11 +420,19 @@ struct LoopS {
   u64 need;   // filter bits the listed words must hold
   u64 occ, t[2];
   u64 t_wait, t_idle, t_undo;  // s_memrealtime: this command's wait began; idle / undo since the last flag
+  // tiebreak=device
+  uint32_t sm, snf, sbuf, snk, snew, status;
+  u64 sel_slot;
+  u64 bc[kWlThreads / 64], bk[kWlThreads / 64];
+  uint32_t bs[kWlThreads / 64];
 };
 
 }  // namespace
 
 // The merge loop (see the file comment).  One workgroup; command numbers start at p.seq0.
+// kSelf (tiebreak=device): no host commands; the loop selects each merge from the device pair
+// table's frontier (p.sel) and folds the merge's records back into the table.
+template <bool kSelf>
 __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   __shared__ int32_t s_strip[kStrip * kWlThreads];  // [position][lane]: conflict-free per wave
   __shared__ DeltaH s_h;
@@ -371,8 +451,98 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   const MergeCtx mc{&S.nspill};
   __syncthreads();
   for (;;) {
-    // ---- wave 0 waits for the next command (one round trip reads all four granules)
-    if (wid == 0) {
+    if constexpr (kSelf) {
+      // ---- tiebreak=device: the best live frontier entry is the merge (count desc, key asc);
+      // the entries still at or above the threshold are kept in the other buffer
+      const SelParams& q = p.sel;
+      if (tid == 0) {
+        S.sm = ld_agent(q.st + kSelM);
+        S.snf = ld_agent(q.st + kSelNF);
+        S.sbuf = ld_agent(q.st + kSelBuf);
+        S.snk = 0;
+        S.status = 0;
+        S.t_wait = __builtin_amdgcn_s_memrealtime();
+      }
+      __syncthreads();
+      const uint32_t nf = S.snf, buf = S.sbuf;
+      const u64 tc = q.thr[0], tk = q.thr[1];
+      const uint32_t* fi = q.fr[buf];
+      uint32_t* fo = q.fr[buf ^ 1u];
+      u64 bc = 0, bk = kEmpty64;
+      uint32_t bs = kEmpty32;
+      for (uint32_t i0 = 0; i0 < nf; i0 += kWlThreads) {
+        const uint32_t i = i0 + tid;
+        bool keep = false;
+        u64 c = 0, k = kEmpty64;
+        uint32_t sl = 0;
+        if (i < nf) {
+          sl = ld_agent(fi + i);
+          c = ld_agent64(q.pcnt + sl);
+          k = ld_agent64(q.pkey + sl);
+          keep = sel_at_least(c, k, tc, tk);
+        }
+        if (keep && sel_better(c, k, bc, bk)) {
+          bc = c;
+          bk = k;
+          bs = sl;
+        }
+        const u64 bl = __ballot(keep);
+        if (bl) {
+          const int lead = __ffsll((long long)bl) - 1;
+          uint32_t base = 0;
+          if (lane == lead) base = atomicAdd(&S.snk, (uint32_t)__popcll(bl));
+          base = __shfl(base, lead, 64);
+          if (keep) fo[base + (uint32_t)__popcll(bl & ((1ull << lane) - 1ull))] = sl;
+        }
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        const u64 c2 = __shfl_xor(bc, d, 64), k2 = __shfl_xor(bk, d, 64);
+        const uint32_t s2 = __shfl_xor(bs, d, 64);
+        if (sel_better(c2, k2, bc, bk)) {
+          bc = c2;
+          bk = k2;
+          bs = s2;
+        }
+      }
+      if (lane == 0) {
+        S.bc[wid] = bc;
+        S.bk[wid] = bk;
+        S.bs[wid] = bs;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        for (int w = 1; w < kWlThreads / 64; ++w)
+          if (sel_better(S.bc[w], S.bk[w], bc, bk)) {
+            bc = S.bc[w];
+            bk = S.bk[w];
+            bs = S.bs[w];
+          }
+        const uint32_t m = S.sm;
+        uint32_t status = 0;
+        if (m >= q.n_max) status = kSelDone;
+        else if (S.snk == 0) status = kSelRebuild;  // nothing at or above the threshold is left
+        else if (bc < q.min_freq) status = kSelDone;
+        S.cmd[0] = status ? kOpStop : kOpMerge;
+        S.status = status;
+        if (!status) {
+          const int32_t a = (int32_t)(uint32_t)(bk >> 32), b = (int32_t)(uint32_t)bk;
+          S.cmd[1] = (uint32_t)a;
+          S.cmd[2] = (uint32_t)b;
+          S.cmd[3] = (uint32_t)(q.X0 + (int32_t)m);
+          S.cmd[4] = 0;
+          S.cmd[5] = expect;
+          S.cmd[6] = 0;  // no list given: the loop looks it up
+          S.cmd[7] = 0;
+          S.sel_slot = bs;
+          q.out[2 * (u64)m] = bk;
+          q.out[2 * (u64)m + 1] = bc;
+          q.st[kSelNF] = S.snk;  // the kept entries are the frontier now
+          q.st[kSelBuf] = buf ^ 1u;
+        }
+      }
+    } else if (wid == 0) {
+      // ---- wave 0 waits for the next command (one round trip reads all four granules)
       const u64* g = p.ring[expect % kRing].g;
       const u64 t_wait = __builtin_amdgcn_s_memrealtime();
       uint32_t op = 0, a = 0, b = 0, X = 0, idle = 0;
@@ -415,7 +585,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     const uint32_t slot = S.cmd[4], seq = S.cmd[5];
     ++expect;
     if (op != kOpMerge && op != kOpUnmerge) {
-      exit_op = op;
+      exit_op = kSelf ? S.status : op;
       break;
     }
     // ---- the word list.  Merge (a, b), M = max(a, b): when the loop created M, M's words-of
@@ -626,9 +796,74 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     if (my_rd) atomicAdd(&S.rd, my_rd);
     if (my_wr) atomicAdd(&S.wr, my_wr);
     __syncthreads();
+    const uint32_t nchg = append ? S.nchg : 0u;
+    if constexpr (kSelf) {
+      // ---- tiebreak=device: the records change the pair table; the pairs this merge created
+      // that rank at or above the threshold join the frontier
+      const SelParams& q = p.sel;
+      if (tid == 0) {
+        if (X >= 0 && (uint32_t)X < p.id_cap) {
+          p.lst[X] = (u64)top | ((u64)nchg << 32);
+          p.lseq[X] = seq;
+          S.pool_top = top + nchg;
+        }
+        S.snew = 0;
+      }
+      __syncthreads();
+      for (int i = tid; i < kDh; i += kWlThreads) {
+        const uint32_t key = s_h.key[i];
+        if (key != kEmpty32) sel_apply(q, &S.snew, p.unk, p.cap, key, s_h.sum[i], a, b, X);
+      }
+      const uint32_t nsp = S.nspill;
+      for (uint32_t i = tid; i < nsp; i += kWlThreads) {
+        const uint32_t key = p.dlist[i];
+        const u64 sum = atomicExch(&p.dsum[key], 0ull);
+        atomicExch(&p.dft[key], kEmpty64);
+        sel_apply(q, &S.snew, p.unk, p.cap, key, sum, a, b, X);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(q.pcnt + S.sel_slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const u64 tc = q.thr[0], tk = q.thr[1];
+      uint32_t* fo = q.fr[S.sbuf ^ 1u];
+      const uint32_t nnew = S.snew;
+      for (uint32_t i = tid; i < nnew; i += kWlThreads) {
+        const uint32_t sl = q.upd[i];
+        const u64 c = ld_agent64(q.pcnt + sl), k = ld_agent64(q.pkey + sl);
+        if (sel_at_least(c, k, tc, tk) && atomicCAS(q.inf + sl, 0u, 1u) == 0u) {
+          const uint32_t pos = atomicAdd(&S.snk, 1u);
+          if (pos < q.fcap) fo[pos] = sl;
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        q.st[kSelNF] = S.snk < q.fcap ? S.snk : q.fcap;
+        q.st[kSelM] = S.sm + 1u;
+        // statistics (st words 6..): select ticks, merge ticks (u64 each), listed / changed words,
+        // occurrences (u64), new pairs
+        u64* t64 = reinterpret_cast<u64*>(q.st + kSelStats);
+        const u64 now = __builtin_amdgcn_s_memrealtime();
+        t64[0] += t_cmd - S.t_wait;
+        t64[1] += now - t_cmd;
+        t64[2] += cnt;
+        t64[3] += nchg;
+        t64[4] += S.occ;
+        t64[5] += nnew;
+        // after a complete merge: a frontier past its capacity lost entries (rebuild), a table past
+        // its fill bound must grow (the host stops)
+        const uint32_t full = ld_agent(q.st + kSelIns) > q.fill_max || ld_agent(q.st + kSelErr) != 0;
+        S.status = full ? kSelFull : (S.snk > q.fcap ? kSelRebuild : 0u);
+      }
+      __syncthreads();
+      if (S.status) {
+        exit_op = S.status;
+        break;
+      }
+      continue;
+    }
     // ---- the records to host memory (LDS hash, then the spilled keys), then the flag
     const WlSlotDev& sd = p.sl[slot & (WordLoop::kSlots - 1)];
-    const uint32_t nchg = append ? S.nchg : 0u;
     if (tid == 0) {
       S.t[1] = __builtin_amdgcn_s_memrealtime() - t_cmd;
       S.lst_x = 0;
@@ -694,6 +929,11 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   }
   if (tid == 0) {
     p.dstate[kStPoolTop] = S.pool_top;
+    if constexpr (kSelf) {
+      p.sel.st[kSelStatus] = exit_op;
+      __threadfence_system();
+      return;
+    }
     p.status[1] = expect - 1u;  // the command this launch did not take (a time-out's resume point)
     __threadfence_system();
     __hip_atomic_store(&p.status[0], exit_op, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -830,6 +1070,84 @@ __global__ void k_tiles_to_words(const int32_t* tok, const uint64_t* tile_off, c
   }
 }
 
+// ---- tiebreak=device: the frontier's rebuild (whole chip) and the table's initial pairs
+constexpr uint32_t kSelBuckets = 65536u + 48u * 256u;  // exact counts below 2^16, 256 per octave above
+constexpr uint32_t kSelLds = 16384;                    // buckets counted in LDS per workgroup
+__host__ __device__ __forceinline__ uint32_t sel_bucket(u64 c) {
+  if (c < 65536) return (uint32_t)c;
+  int lg = 63;
+  while (!((c >> lg) & 1ull)) --lg;
+  return 65536u + (uint32_t)(lg - 16) * 256u + (uint32_t)((c >> (lg - 8)) & 255u);
+}
+// the smallest count in bucket b
+inline u64 sel_bucket_lo(uint32_t b) {
+  if (b < 65536u) return b;
+  const uint32_t lg = 16u + (b - 65536u) / 256u, mant = (b - 65536u) % 256u;
+  return (u64)(256u + mant) << (lg - 8u);
+}
+
+__global__ void k_sel_hist(const u64* pkey, const u64* pcnt, u64 n, u64 minf, uint32_t* hist) {
+  __shared__ uint32_t h[kSelLds];
+  for (uint32_t i = threadIdx.x; i < kSelLds; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    const u64 c = pcnt[i];
+    if (pkey[i] == kEmpty64 || c < minf) continue;
+    const uint32_t b = sel_bucket(c);
+    if (b < kSelLds) atomicAdd(&h[b], 1u);
+    else atomicAdd(&hist[b], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < kSelLds; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+__global__ void k_sel_collect(const u64* pkey, const u64* pcnt, u64 n, u64 minf, uint32_t bstar, uint32_t* out,
+                              uint32_t* nout, u64 cap) {
+  const int lane = threadIdx.x & 63;
+  for (u64 i0 = blockIdx.x * (u64)blockDim.x; i0 < n; i0 += (u64)gridDim.x * blockDim.x) {
+    const u64 i = i0 + threadIdx.x;
+    bool take = false;
+    if (i < n) {
+      const u64 c = pcnt[i];
+      take = pkey[i] != kEmpty64 && c >= minf && sel_bucket(c) >= bstar;
+    }
+    const u64 bl = __ballot(take);
+    if (!bl) continue;
+    const int lead = __ffsll((long long)bl) - 1;
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(nout, (uint32_t)__popcll(bl));
+    base = __shfl(base, lead, 64);
+    const uint32_t pos = base + (uint32_t)__popcll(bl & ((1ull << lane) - 1ull));
+    if (take && pos < cap) out[pos] = (uint32_t)i;
+  }
+}
+
+__global__ void k_sel_gather(const uint32_t* slots, uint32_t n, const u64* pkey, const u64* pcnt, u64* key,
+                             u64* negc, uint32_t* idx) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    key[i] = pkey[slots[i]];
+    negc[i] = ~pcnt[slots[i]];
+    idx[i] = i;
+  }
+}
+
+// idx: the sorted order; the first n of the collected slots in that order -> the frontier
+__global__ void k_sel_pick(const uint32_t* slots, const uint32_t* idx, uint32_t n, uint32_t* fr, uint32_t* inf) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t s = slots[idx ? idx[i] : i];
+    fr[i] = s;
+    inf[s] = 1u;
+  }
+}
+
+__global__ void k_sel_insert(const PairCount* pc, uint64_t n, SelParams q) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const u64 h = sel_slot(q, pair_key(pc[i].a, pc[i].b));
+    if (h != ~0ull) q.pcnt[h] = pc[i].count;
+  }
+}
+
 template <class T>
 T* wl_alloc(size_t n, size_t* acc) {
   void* p = nullptr;
@@ -880,6 +1198,7 @@ WordLoop::~WordLoop() {
 }
 
 void WordLoop::free_all() {
+  sel_free();
   void* ptrs[] = {wtok_, wtok0_, woff_, tile_first_, tile_nw_, pool_, dkey_, dval_, init_key_, init_val_,
                   lst_, lseq_, dsum_, dft_, dlist_, dstate_};
   for (void* p : ptrs)
@@ -1199,7 +1518,7 @@ void WordLoop::launch(uint32_t seq0) {
   }
   status_[0] = 0;
   WL_OK(hipEventRecord((hipEvent_t)ev_[0], S(stream_)));
-  k_word_loop<<<1, kWlThreads, 0, S(stream_)>>>(p);
+  k_word_loop<false><<<1, kWlThreads, 0, S(stream_)>>>(p);
   WL_OK(hipGetLastError());
   WL_OK(hipEventRecord((hipEvent_t)ev_[1], S(stream_)));
   running_ = true;
@@ -1336,6 +1655,254 @@ void WordLoop::stop() {
                  ds[kStError]);
     fatal("k_word_loop failed");
   }
+}
+
+// ==========================================================================================
+// tiebreak=device
+
+void WordLoop::sel_free() {
+  void* ptrs[] = {pkey_, pcnt_, pinf_, fr_[0], fr_[1], sst_dev_, thr_, sout_, upd_, shist_, scol_};
+  for (void* q : ptrs)
+    if (q) WL_OK(hipFree(q));
+  pkey_ = pcnt_ = thr_ = sout_ = nullptr;
+  pinf_ = fr_[0] = fr_[1] = sst_dev_ = upd_ = shist_ = scol_ = nullptr;
+  pcap_ = sout_cap_ = upd_cap_ = scol_cap_ = 0;
+  fcap_ = 0;
+}
+
+// The frontier from the whole table: the kSelK best pairs by (count desc, key asc) among those
+// >= min_freq (all of them when few), their slots flagged; the threshold = the last one taken
+// (or, when every pair of the counts' top buckets was taken, the lowest count of those buckets).
+bool WordLoop::sel_rebuild(uint64_t min_freq) {
+  constexpr uint32_t kSelK = 4096;
+  const double t0 = now_seconds();
+  hipStream_t s = S(stream_);
+  WL_OK(hipMemsetAsync(shist_, 0, kSelBuckets * sizeof(uint32_t), s));
+  k_sel_hist<<<1024, 512, 0, s>>>(pkey_, pcnt_, pcap_, min_freq, shist_);
+  WL_OK(hipGetLastError());
+  std::vector<uint32_t> hist(kSelBuckets);
+  WL_OK(hipMemcpyAsync(hist.data(), shist_, kSelBuckets * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  WL_OK(hipStreamSynchronize(s));
+  uint64_t acc = 0;
+  uint32_t bstar = kSelBuckets;
+  for (uint32_t b = kSelBuckets; b-- > 0;) {
+    if (!hist[b]) continue;
+    acc += hist[b];
+    bstar = b;
+    if (acc >= kSelK) break;
+  }
+  uint32_t st[kSelStats] = {};
+  WL_OK(hipMemcpyAsync(st, sst_dev_, sizeof(st), hipMemcpyDeviceToHost, s));
+  WL_OK(hipMemsetAsync(pinf_, 0, pcap_ * sizeof(uint32_t), s));
+  WL_OK(hipStreamSynchronize(s));
+  u64 thr[2] = {~0ull, 0ull};
+  uint32_t nf = 0;
+  if (acc > 0) {
+    if (acc > scol_cap_) {
+      if (scol_) WL_OK(hipFree(scol_));
+      scol_cap_ = std::max<uint64_t>(2 * acc, 1 << 16);
+      scol_ = wl_alloc<uint32_t>(scol_cap_ + 1, &bytes_);
+    }
+    uint32_t* ncol = scol_ + scol_cap_;
+    WL_OK(hipMemsetAsync(ncol, 0, sizeof(uint32_t), s));
+    k_sel_collect<<<1024, 512, 0, s>>>(pkey_, pcnt_, pcap_, min_freq, bstar, scol_, ncol, scol_cap_);
+    WL_OK(hipGetLastError());
+    uint32_t nc = 0;
+    WL_OK(hipMemcpyAsync(&nc, ncol, sizeof(nc), hipMemcpyDeviceToHost, s));
+    WL_OK(hipStreamSynchronize(s));
+    if (nc != acc) fatal("tiebreak=device: the frontier's collect disagrees with its histogram");
+    if (nc <= kSelK) {  // every pair of the top buckets: the threshold is their lowest count
+      nf = nc;
+      k_sel_pick<<<64, 256, 0, s>>>(scol_, nullptr, nf, fr_[0], pinf_);
+      WL_OK(hipGetLastError());
+      thr[0] = std::max<u64>(sel_bucket_lo(bstar), min_freq);
+      thr[1] = ~0ull;
+    } else {  // the top kSelK in (count desc, key asc) order: sort by key, then stably by count
+      size_t acc2 = 0;
+      u64* key = wl_alloc<u64>(nc, &acc2);
+      u64* key2 = wl_alloc<u64>(nc, &acc2);
+      u64* negc = wl_alloc<u64>(nc, &acc2);
+      u64* negc2 = wl_alloc<u64>(nc, &acc2);
+      uint32_t* idx = wl_alloc<uint32_t>(nc, &acc2);
+      uint32_t* idx2 = wl_alloc<uint32_t>(nc, &acc2);
+      k_sel_gather<<<256, 256, 0, s>>>(scol_, nc, pkey_, pcnt_, key, negc, idx);
+      WL_OK(hipGetLastError());
+      size_t tb = 0, tb2 = 0;
+      WL_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, idx, idx2, (int)nc, 0, 64, s));
+      WL_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, negc, negc2, idx, idx2, (int)nc, 0, 64, s));
+      void* tmp = wl_alloc<uint8_t>(std::max(tb, tb2), &acc2);
+      WL_OK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, key2, idx, idx2, (int)nc, 0, 64, s));
+      // counts in key order, then a stable sort by ~count
+      k_sel_gather<<<256, 256, 0, s>>>(scol_, nc, pkey_, pcnt_, key, negc, idx);  // key/negc of slot order
+      WL_OK(hipGetLastError());
+      std::vector<uint32_t> order(nc);
+      std::vector<u64> kc(nc), nn(nc);
+      WL_OK(hipMemcpyAsync(order.data(), idx2, nc * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      WL_OK(hipMemcpyAsync(nn.data(), negc, nc * sizeof(u64), hipMemcpyDeviceToHost, s));
+      WL_OK(hipMemcpyAsync(kc.data(), key, nc * sizeof(u64), hipMemcpyDeviceToHost, s));
+      WL_OK(hipStreamSynchronize(s));
+      // (host) ~count in key order, sorted stably on the device
+      std::vector<u64> nk(nc);
+      for (uint32_t i = 0; i < nc; ++i) nk[i] = nn[order[i]];
+      WL_OK(hipMemcpyAsync(negc, nk.data(), nc * sizeof(u64), hipMemcpyHostToDevice, s));
+      WL_OK(hipMemcpyAsync(idx, order.data(), nc * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+      WL_OK(hipcub::DeviceRadixSort::SortPairs(tmp, tb2, negc, negc2, idx, idx2, (int)nc, 0, 64, s));
+      nf = kSelK;
+      k_sel_pick<<<64, 256, 0, s>>>(scol_, idx2, nf, fr_[0], pinf_);
+      WL_OK(hipGetLastError());
+      uint32_t last = 0;
+      WL_OK(hipMemcpyAsync(&last, idx2 + (nf - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      WL_OK(hipStreamSynchronize(s));
+      thr[0] = ~nn[last];
+      thr[1] = kc[last];
+      for (void* q : {(void*)key, (void*)key2, (void*)negc, (void*)negc2, (void*)idx, (void*)idx2, tmp}) WL_OK(hipFree(q));
+    }
+  }
+  st[kSelNF] = nf;
+  st[kSelBuf] = 0;
+  st[kSelStatus] = 0;
+  WL_OK(hipMemcpyAsync(sst_dev_, st, sizeof(st), hipMemcpyHostToDevice, s));
+  WL_OK(hipMemcpyAsync(thr_, thr, sizeof(thr), hipMemcpyHostToDevice, s));
+  WL_OK(hipStreamSynchronize(s));
+  sst_.rebuilds += 1;
+  sst_.rebuild_ms += 1e3 * (now_seconds() - t0);
+  sst_.frontier_max = std::max<uint64_t>(sst_.frontier_max, nf);
+  return nf > 0;
+}
+
+int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32_t n_max, uint64_t min_freq,
+                         std::vector<SelectedMerge>* out) {
+  out->clear();
+  if (!ready_ || !posted_.empty()) return -1;
+  WL_OK(hipSetDevice(ordinal_));
+  stop();
+  if (n_max == 0) return 0;
+  reserve(X0 + (int32_t)n_max);
+  hipStream_t s = S(stream_);
+  // the table: room for the initial pairs and ~256 new pairs a merge, at most a quarter full
+  uint64_t want = 1 << 16;
+  while (want < 4 * ((uint64_t)pairs.size() + 256ull * n_max)) want <<= 1;
+  if (want > pcap_) {
+    for (void* q : {(void*)pkey_, (void*)pcnt_, (void*)pinf_})
+      if (q) WL_OK(hipFree(q));
+    pcap_ = want;
+    pkey_ = wl_alloc<u64>(pcap_, &bytes_);
+    pcnt_ = wl_alloc<u64>(pcap_, &bytes_);
+    pinf_ = wl_alloc<uint32_t>(pcap_, &bytes_);
+  }
+  if (!fr_[0]) {
+    fcap_ = 16384;
+    fr_[0] = wl_alloc<uint32_t>(fcap_, &bytes_);
+    fr_[1] = wl_alloc<uint32_t>(fcap_, &bytes_);
+    sst_dev_ = wl_alloc<uint32_t>(kSelWords, &bytes_);
+    thr_ = wl_alloc<u64>(2, &bytes_);
+    shist_ = wl_alloc<uint32_t>(kSelBuckets, &bytes_);
+  }
+  if (2ull * n_max > sout_cap_) {
+    if (sout_) WL_OK(hipFree(sout_));
+    sout_cap_ = 2ull * n_max;
+    sout_ = wl_alloc<u64>(sout_cap_, &bytes_);
+  }
+  const uint64_t need_upd = 4ull * ((uint64_t)cap_ + 1) + 64;  // records of one merge
+  if (need_upd > upd_cap_) {
+    if (upd_) WL_OK(hipFree(upd_));
+    upd_cap_ = need_upd;
+    upd_ = wl_alloc<uint32_t>(upd_cap_, &bytes_);
+  }
+  WL_OK(hipMemsetAsync(pkey_, 0xFF, pcap_ * sizeof(u64), s));
+  WL_OK(hipMemsetAsync(pcnt_, 0, pcap_ * sizeof(u64), s));
+  WL_OK(hipMemsetAsync(sst_dev_, 0, kSelWords * sizeof(uint32_t), s));
+  SelParams q{};
+  q.pkey = pkey_;
+  q.pcnt = pcnt_;
+  q.inf = pinf_;
+  q.pmask = pcap_ - 1;
+  q.fr[0] = fr_[0];
+  q.fr[1] = fr_[1];
+  q.fcap = fcap_;
+  q.st = sst_dev_;
+  q.thr = thr_;
+  q.out = sout_;
+  q.upd = upd_;
+  q.X0 = X0;
+  q.n_max = n_max;
+  q.min_freq = min_freq;
+  q.fill_max = (uint32_t)std::min<uint64_t>(3 * pcap_ / 4, 0xFFFFFFF0ull);
+  if (!pairs.empty()) {
+    size_t acc = 0;
+    PairCount* dp = wl_alloc<PairCount>(pairs.size(), &acc);
+    WL_OK(hipMemcpyAsync(dp, pairs.data(), pairs.size() * sizeof(PairCount), hipMemcpyHostToDevice, s));
+    k_sel_insert<<<512, 256, 0, s>>>(dp, pairs.size(), q);
+    WL_OK(hipGetLastError());
+    WL_OK(hipStreamSynchronize(s));
+    WL_OK(hipFree(dp));
+  }
+  sst_.table_slots = pcap_;
+  uint32_t m = 0;
+  if (sel_rebuild(min_freq)) {
+    WlParams p{};
+    p.wtok = wtok_;
+    p.weight = weight_;
+    p.pool = reinterpret_cast<WEnt*>(pool_);
+    p.pool_cap = pool_cap_;
+    p.dkey = dkey_;
+    p.dval = dval_;
+    p.dir_mask = dir_cap_ - 1;
+    p.lst = lst_;
+    p.lseq = lseq_;
+    p.id_cap = id_cap_;
+    p.dsum = dsum_;
+    p.dft = dft_;
+    p.dlist = dlist_;
+    p.dstate = dstate_;
+    p.cap = cap_;
+    p.unk = unk_;
+    p.sel = q;
+    dirty_ = true;
+    for (;;) {
+      p.seq0 = seq_ + 1;
+      WL_OK(hipEventRecord((hipEvent_t)ev_[0], s));
+      k_word_loop<true><<<1, kWlThreads, 0, s>>>(p);
+      WL_OK(hipGetLastError());
+      WL_OK(hipEventRecord((hipEvent_t)ev_[1], s));
+      WL_OK(hipStreamSynchronize(s));
+      float ms = 0;
+      WL_OK(hipEventElapsedTime(&ms, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]));
+      sst_.kernel_ms += ms;
+      sst_.launches += 1;
+      uint32_t st[kSelWords];
+      WL_OK(hipMemcpy(st, sst_dev_, sizeof(st), hipMemcpyDeviceToHost));
+      uint32_t ds[8];
+      WL_OK(hipMemcpy(ds, dstate_, sizeof(ds), hipMemcpyDeviceToHost));
+      if (ds[kStError]) {
+        std::fprintf(stderr, "[ERROR]\t k_word_loop<true>: error code %u\n", ds[kStError]);
+        fatal("tiebreak=device merge loop failed");
+      }
+      m = st[kSelM];
+      const uint32_t status = st[kSelStatus];
+      if (status == kSelDone) break;
+      if (status == kSelFull) fatal("tiebreak=device: the pair table is full (more new pairs than sized for)");
+      if (status != kSelRebuild) fatal("tiebreak=device: the merge loop ended without a status");
+      if (!sel_rebuild(min_freq)) break;
+    }
+    uint32_t st[kSelWords];
+    WL_OK(hipMemcpy(st, sst_dev_, sizeof(st), hipMemcpyDeviceToHost));
+    const u64* t64 = reinterpret_cast<const u64*>(st + kSelStats);
+    sst_.select_us += 1e-2 * (double)t64[0];
+    sst_.merge_us += 1e-2 * (double)t64[1];
+    sst_.listed += t64[2];
+    sst_.changed += t64[3];
+    sst_.occurrences += t64[4];
+    sst_.new_pairs += t64[5];
+    sst_.table_pairs = st[kSelIns];
+  }
+  sst_.merges += m;
+  std::vector<u64> o(2 * (size_t)m);
+  if (m) WL_OK(hipMemcpy(o.data(), sout_, o.size() * sizeof(u64), hipMemcpyDeviceToHost));
+  out->resize(m);
+  for (uint32_t i = 0; i < m; ++i)
+    (*out)[i] = SelectedMerge{(int32_t)(uint32_t)(o[2 * i] >> 32), (int32_t)(uint32_t)o[2 * i], o[2 * i + 1]};
+  return (int)m;
 }
 
 uint64_t WordLoop::pool_used() const {

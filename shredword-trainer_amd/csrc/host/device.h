@@ -79,6 +79,9 @@ class Device : public Backend {
   // K2+K3 for a chain of merges (ab[2i], ab[2i+1]) -> X0 + i: one k_merge launch applies them in
   // order per tile and reduces each merge's neighbour deltas separately.
   void merge_chain(const int32_t* ab, int n, int32_t X0) override;
+  // tiebreak=device on the indexed loop (WordLoop::run_select).
+  int device_select(const std::vector<PairCount>& pairs, int32_t X0, int n, uint64_t min_freq,
+                    std::vector<SelectedMerge>* out) override;
   // Multi-GPU: every launch's compacted records are all-gathered (fixed buckets of
   // `bucket_records` records per rank, RCCL over xGMI, queued behind k_merge on the stream);
   // collect() then returns the concatenation of all ranks' records, which the host combines

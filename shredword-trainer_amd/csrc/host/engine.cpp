@@ -196,9 +196,75 @@ int Engine::merge_batch(Backend& be, int batch) {
   return done;
 }
 
+// tiebreak=device: K1, then every merge selected and applied on the device.
+int Engine::train_device(Backend& be, double t0) {
+  sel_.reset(unk_, min_freq_);  // bpe_init; the heap stays empty (the device selects)
+  std::vector<PairCount> pairs;
+  be.count_pairs(unk_, &pairs);
+  times_.init_s += now_seconds() - t0;
+  const int target = (int)target_vocab_ - kBaseVocab;
+  int n = 0;
+  std::vector<SelectedMerge> sm;
+  const int32_t X0 = kBaseVocab + (int32_t)merge_a_.size();
+  // verify_argmax = k: the device selects k merges at a time from a table rebuilt from a fresh
+  // K1 count; the first merge of each chunk must be that count's maximum (ties: the smaller key)
+  const int chunk = verify_every_ > 0 ? verify_every_ : target;
+  while (n < target) {
+    if (n > 0) {
+      pairs.clear();
+      be.count_pairs(unk_, &pairs);
+    }
+    const int want = std::min(chunk, target - n);
+    std::vector<SelectedMerge> part;
+    const int got = be.device_select(pairs, X0 + n, want, min_freq_, &part);
+    if (got < 0) {
+      std::fprintf(stderr, "[ERROR]\t tiebreak=device needs the device's indexed merge loop (types layout, one GPU, "
+                   "index on)\n");
+      return -1;
+    }
+    if (verify_every_ > 0 && got > 0) {
+      uint64_t mc = 0, mk = ~0ull;
+      for (const PairCount& p : pairs) {
+        const uint64_t k = pack_pair(p.a, p.b);
+        if (p.count > mc || (p.count == mc && k < mk)) {
+          mc = p.count;
+          mk = k;
+        }
+      }
+      ++verify_checks_;
+      if (part[0].freq != mc || pack_pair(part[0].a, part[0].b) != mk) {
+        if (!verify_fail_)
+          std::fprintf(stderr, "[ERROR]\t tiebreak=device check at merge %d: selected (%d,%d) freq=%llu, fresh K1 max "
+                       "(%d,%d) freq=%llu\n", n, part[0].a, part[0].b, (unsigned long long)part[0].freq,
+                       pair_first(mk), (int32_t)(uint32_t)mk, (unsigned long long)mc);
+        ++verify_fail_;
+      }
+    }
+    sm.insert(sm.end(), part.begin(), part.end());
+    n += got;
+    if (got < want) break;
+  }
+  {
+    for (int i = 0; i < n; ++i) {
+      if (log_ >= 2)
+        std::printf("[MERGE]\t Merging (%d,%d) freq=%llu -> new_id=%d (merge %zu)\n", sm[i].a, sm[i].b,
+                    (unsigned long long)sm[i].freq, X0 + i, merge_a_.size() + 1);
+      if (trace_) std::fprintf(trace_, "M %d %d %llu %d\n", sm[i].a, sm[i].b, (unsigned long long)sm[i].freq, X0 + i);
+      merge_a_.push_back(sm[i].a);
+      merge_b_.push_back(sm[i].b);
+    }
+  }
+  be.quiesce();
+  if (trace_) std::fflush(trace_);
+  times_.train_s += now_seconds() - t0;
+  if (log_ >= 1) std::printf("[INFO]\t Training completed (tiebreak=device). Performed %d merges\n", n);
+  return n;
+}
+
 int Engine::train(Backend& be) {
   const double t0 = now_seconds();
   if (log_ >= 1) std::printf("[INFO]\t Starting BPE training (target vocab size: %zu)\n", target_vocab_);
+  if (tiebreak_device_) return train_device(be, t0);
   sel_.reset(unk_, min_freq_);  // bpe_init (bpe.cpp:98-108)
   mtrace_on_ = std::getenv("SHREDWORD_ENGINE_TRACE") != nullptr;
   if (const char* e = std::getenv("SHREDWORD_SIM_SELECT")) sel_.set_simulate_pops(std::atoi(e) != 0);

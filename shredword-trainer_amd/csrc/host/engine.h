@@ -42,6 +42,14 @@ class Backend {
   virtual void reserve_ids(int32_t max_id) {}
   // K6: final weighted token histogram over ids [0, T) (all ranks).
   virtual void token_freq(size_t T, std::vector<uint64_t>* freq) = 0;
+  // tiebreak=device (K5 as the selector): merges X0 .. X0 + n - 1 chosen AND applied on the
+  // device from its own pair table (`pairs`: the current K1 counts), each the pair of largest
+  // count, ties to the smaller key, while that count is >= min_freq; no host round trip per
+  // merge.  Returns the merges done (out: in order), -1 when the backend has no such loop.
+  virtual int device_select(const std::vector<PairCount>& pairs, int32_t X0, int n, uint64_t min_freq,
+                            std::vector<SelectedMerge>* out) {
+    return -1;
+  }
   // K5 check (debug): a fresh K1 over the current corpus reduced to the largest pair count
   // (*max_freq) and the count of (a, b) (*ab_freq).  Default: reduced on the host.
   virtual void pair_max(int32_t unk_id, int32_t a, int32_t b, uint64_t* max_freq, uint64_t* ab_freq) {
@@ -103,6 +111,11 @@ class Engine {
   // checked against a device recount of the corpus (Backend::pair_max): it must be the largest
   // pair count and (a, b)'s own count.  Mismatches are counted and the first is printed.
   void set_verify(int every) { verify_every_ = every < 0 ? 0 : every; }
+  // Merge selection of train(): the reference's heap replay (exact, default) or, opt-in, the
+  // device's own argmax (Backend::device_select): NOT bit-exact with the reference (ties go to
+  // the smaller pair key), every merge still the most frequent pair of the corpus at its step.
+  void set_tiebreak_device(bool on) { tiebreak_device_ = on; }
+  bool tiebreak_device() const { return tiebreak_device_; }
   uint64_t verify_checks() const { return verify_checks_; }
   uint64_t verify_failures() const { return verify_fail_; }
   void finish_speculation(Backend& be);  // rolls back unconfirmed guesses (before any other access)
@@ -137,6 +150,8 @@ class Engine {
   std::vector<int32_t> chain_ab_;
   uint64_t spec_hits_ = 0, spec_misses_ = 0, launches_ = 0;
   int verify_every_ = 0;
+  bool tiebreak_device_ = false;
+  int train_device(Backend& be, double t0);
   bool correct_ = true;
   uint64_t corrections_ = 0;
   uint64_t verify_checks_ = 0, verify_fail_ = 0;

@@ -95,6 +95,12 @@ struct PairCount {
   uint64_t ft;  // first touch (word rank << 32) | position: the reference bimap creation order
 };
 
+// tiebreak=device (opt-in, not the reference's order): a merge the device selected itself.
+struct SelectedMerge {
+  int32_t a, b;
+  uint64_t freq;
+};
+
 class Selector {
  public:
   // bpe_init's fresh pair map and heap (bpe.cpp:103-106).

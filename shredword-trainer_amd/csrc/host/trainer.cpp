@@ -132,6 +132,10 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
     else if (val == "auto") t->dist_mode = -1;
     else return -1;
     t->device_stale = true;
+  } else if (key == "tiebreak") {  // merge selection: the reference's heap (exact) or the device's argmax
+    if (val == "exact") t->engine.set_tiebreak_device(false);
+    else if (val == "device") t->engine.set_tiebreak_device(true);
+    else return -1;
   } else if (key == "verify_argmax") {
     const int n = std::atoi(val.c_str());
     if (n < 0) return -1;
@@ -224,6 +228,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   t->engine.set_verify(env_int("SHREDWORD_VERIFY_ARGMAX", 0));
   if (const char* v = std::getenv("SHREDWORD_DIST")) set_option(t, "dist", v);
   if (const char* v = std::getenv("SHREDWORD_RESIDENT")) set_option(t, "resident", v);
+  if (const char* v = std::getenv("SHREDWORD_TIEBREAK")) set_option(t, "tiebreak", v);
   if (t->engine.log() >= 1) std::printf("[INFO]\t BPE trainer initialized. Heap initialized successfully.\n");
   return t;
 }
@@ -475,6 +480,16 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
       s->index_records = w.records;
       s->index_switch_merge = t->dev->switch_merge();
       s->index_switch_ms = t->dev->switch_ms();
+      const SelectStats& q = wl->select_stats();
+      s->sel_merges = q.merges;
+      s->sel_launches = q.launches;
+      s->sel_rebuilds = q.rebuilds;
+      s->sel_kernel_ms = q.kernel_ms;
+      s->sel_rebuild_ms = q.rebuild_ms;
+      s->sel_select_us = q.select_us;
+      s->sel_merge_us = q.merge_us;
+      s->sel_table_pairs = q.table_pairs;
+      s->sel_table_slots = q.table_slots;
     }
   }
   {

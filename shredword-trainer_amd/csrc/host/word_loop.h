@@ -62,6 +62,14 @@ struct WordLoopStats {
   uint64_t records = 0;           // Σ delta records handed to the host
 };
 
+struct SelectStats {
+  uint64_t merges = 0, launches = 0, rebuilds = 0;
+  double kernel_ms = 0, rebuild_ms = 0;  // launches of k_word_loop<true>; frontier rebuilds (host wall)
+  double select_us = 0, merge_us = 0;    // device time: selecting, merging + table update (s_memrealtime)
+  uint64_t listed = 0, changed = 0, occurrences = 0, new_pairs = 0;
+  uint64_t table_slots = 0, table_pairs = 0, frontier_max = 0;
+};
+
 class WordLoop {
  public:
   static constexpr int kSlots = 4;  // merges in flight: the current one and up to 3 guesses
@@ -99,6 +107,14 @@ class WordLoop {
   void rollback(int32_t X);
   size_t in_flight() const { return posted_.size(); }
   uint32_t id_room() const { return cap_; }  // merges may post ids X with X + 2 <= id_room()
+  // tiebreak=device: merges X0 .. X0 + n_max - 1 selected and applied on the device, with no
+  // host round trip per merge (k_word_loop<true>).  `pairs`: the current words' pair counts (K1,
+  // pairs holding unk excluded).  Each merge takes the pair of largest count, ties to the smaller
+  // key ((u32)a << 32 | (u32)b), while that count is >= min_freq.  Returns the merges done (out:
+  // in order), or -1 when the loop is not usable.  The words are merged in place as by post_merge.
+  int run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32_t n_max, uint64_t min_freq,
+                 std::vector<SelectedMerge>* out);
+  const SelectStats& select_stats() const { return sst_; }
   // Ends the persistent launch (nothing may be in flight).
   void stop();
   bool running() const { return running_; }
@@ -117,6 +133,9 @@ class WordLoop {
   const WordLoopStats& stats() const { return st_; }
   void clear_stats() {
     st_ = WordLoopStats();
+    const uint64_t slots = sst_.table_slots;
+    sst_ = SelectStats();
+    sst_.table_slots = slots;
     trace_.clear();
   }
   // Per collected merge while timing is on, kTraceFields u32 each: X, listed words, scanned
@@ -205,6 +224,25 @@ class WordLoop {
   uint32_t seq_ = 0;
   uint32_t idle_polls_ = 1u << 22;  // ~10 s without a command: the launch ends itself (relaunched on demand)
   std::vector<Post> posted_;
+  // tiebreak=device: pair table, frontier, state (see word_loop.hip SelParams)
+  void sel_free();
+  bool sel_rebuild(uint64_t min_freq);  // false: no pair at or above min_freq is left
+  unsigned long long* pkey_ = nullptr;
+  unsigned long long* pcnt_ = nullptr;
+  uint32_t* pinf_ = nullptr;
+  uint64_t pcap_ = 0;
+  uint32_t* fr_[2] = {nullptr, nullptr};
+  uint32_t fcap_ = 0;
+  uint32_t* sst_dev_ = nullptr;
+  unsigned long long* thr_ = nullptr;
+  unsigned long long* sout_ = nullptr;
+  uint64_t sout_cap_ = 0;
+  uint32_t* upd_ = nullptr;
+  uint64_t upd_cap_ = 0;
+  uint32_t* shist_ = nullptr;
+  uint32_t* scol_ = nullptr;
+  uint64_t scol_cap_ = 0;
+  SelectStats sst_;
   void* ev_[2] = {};
   WordLoopStats st_;
   std::vector<uint32_t> trace_;

@@ -77,7 +77,10 @@ class ShredStats(Structure):
                 ("resident_aborts", c_uint64), ("verify_checks", c_uint64), ("verify_failures", c_uint64),
                 ("resident_merges", c_uint64), ("resident_bytes", c_double), ("resident_kernel_ms", c_double),
                 ("index_run_ints_read", c_uint64), ("index_run_ints_written", c_uint64),
-                ("index_records", c_uint64), ("resident_k3_bytes", c_double)]
+                ("index_records", c_uint64), ("resident_k3_bytes", c_double),
+                ("sel_merges", c_uint64), ("sel_launches", c_uint64), ("sel_rebuilds", c_uint64),
+                ("sel_kernel_ms", c_double), ("sel_rebuild_ms", c_double), ("sel_select_us", c_double),
+                ("sel_merge_us", c_double), ("sel_table_pairs", c_uint64), ("sel_table_slots", c_uint64)]
 
 
 Trainer = c_void_p

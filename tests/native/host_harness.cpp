@@ -270,12 +270,49 @@ class EmuBackend : public Backend {
     }
   }
 
+  // tiebreak=device, restated on the CPU: the same pair table semantics as k_word_loop<true>
+  // (count desc, key asc; each merge's records fold into the counts, the merged pair drops to 0).
+  int device_select(const std::vector<PairCount>& pairs, int32_t X0, int n, uint64_t min_freq,
+                    std::vector<SelectedMerge>* out) override {
+    std::unordered_map<uint64_t, uint64_t> cnt;
+    for (const PairCount& p : pairs) cnt[pack_pair(p.a, p.b)] += p.count;
+    const int32_t unk = unk_;
+    out->clear();
+    for (int m = 0; m < n; ++m) {
+      uint64_t bc = 0, bk = ~0ull;
+      for (const auto& kv : cnt)
+        if (kv.second >= min_freq && (kv.second > bc || (kv.second == bc && kv.first < bk))) {
+          bc = kv.second;
+          bk = kv.first;
+        }
+      if (bc == 0) break;
+      const int32_t a = pair_first(bk), b = (int32_t)(uint32_t)bk, X = X0 + m;
+      merge_one(a, b, X);
+      const DeltaRecord* recs = nullptr;
+      const size_t nr = collect(X, &recs);
+      for (size_t i = 0; i < nr; ++i) {
+        const uint32_t sl = recs[i].key >> 2, cat = recs[i].key & 3u;
+        const int32_t id = sl == 0 ? unk : (int32_t)(sl - 1);
+        if (id == unk) continue;
+        const int32_t f = cat < 2 ? id : (cat == 2 ? b : X), g = cat == 0 ? a : (cat == 1 ? X : id);
+        if (f == a && g == b) continue;
+        uint64_t& v = cnt[pack_pair(f, g)];
+        v += (cat & 1u) ? recs[i].sum : (uint64_t)(-(int64_t)recs[i].sum);
+      }
+      cnt[bk] = 0;
+      out->push_back({a, b, bc});
+    }
+    return (int)out->size();
+  }
+  void set_unk(int32_t u) { unk_ = u; }
+
   const TiledStream& stream() const { return ts_; }
 
  private:
   const WordTable& wt_;
   Layout layout_;
   uint32_t cap_;
+  int32_t unk_ = 0;
   TiledStream ts_;
   TileIndex index_;
   uint64_t visited_ = 0;
@@ -337,6 +374,7 @@ void* hh_open(const char* path, uint64_t vocab, int32_t unk, float cov, uint64_t
   size_t b = 0, e = 0;
   shard_range(h->wt, lay, rank, world, &b, &e);
   h->be.reset(new EmuBackend(h->wt, lay, b, e, slot_cap(vocab, unk)));
+  h->be->set_unk(unk);
   h->engine.configure(vocab, unk, mpf);
   h->engine.set_log(0);
   h->vocab = vocab;
@@ -372,9 +410,12 @@ int hh_load(void* p, const char* path) {
   h->be.reset();
   h->wt = std::move(wt);
   h->be.reset(new EmuBackend(h->wt, Layout::kTypes, 0, h->wt.num_words(), slot_cap(h->vocab, h->unk)));
+  h->be->set_unk(h->unk);
   h->engine.reload();
   return 0;
 }
+
+void hh_set_tiebreak_device(void* p, int on) { ((Harness*)p)->engine.set_tiebreak_device(on != 0); }
 
 void hh_count(void* p) {
   Harness* h = (Harness*)p;
@@ -417,6 +458,7 @@ void* hh_open_sharded(const char* path, uint64_t vocab, int32_t unk, float cov, 
     return nullptr;
   }
   h->be.reset(new EmuBackend(h->wt, Layout::kTypes, 0, h->wt.num_words(), slot_cap(vocab, unk)));
+  h->be->set_unk(unk);
   h->engine.configure(vocab, unk, mpf);
   h->engine.set_log(0);
   return h;

@@ -152,3 +152,35 @@ def test_host_logic_call_sequences(name, hh, seq_case, tmp_path):
     assert returns == case["returns"]
     assert trace == case["trace"]
     assert outputs == case["outputs"]
+
+
+TIEBREAK_CASES = ["small_v300", "adv_unk0", "adv_unk3_cov09", "ascii1m_unk7_cov09", "ascii1m_v3000_mpf2",
+                  "utf8_2m_v2000_mpf50", "ascii1m_unkm1_mpf2"]
+
+
+@pytest.mark.parametrize("name", TIEBREAK_CASES)
+def test_tiebreak_device_host_logic_matches_oracle_rule(name, hh, case_corpus, oracle_bin, tmp_path):
+    """tiebreak=device (opt-in, not the reference's order): the Engine's device-selection path over
+    the emulated kernels (EmuBackend::device_select: the pair-table rule of k_word_loop<true>)
+    against the oracle's restatement of the same rule (bpe_oracle --tiebreak-device 0: largest
+    count, ties to the smaller key, every count the reference's): the same merges and files."""
+    import subprocess
+    case, corpus = case_corpus(name)
+    cfg = case["config"]
+    h = hostharness.open_case(hh, corpus, cfg, "types")
+    try:
+        hh.hh_set_tiebreak_device(h, 1)
+        trace = str(tmp_path / "t.txt")
+        merges = hh.hh_train(h, trace.encode())
+        m, v = str(tmp_path / "h.model"), str(tmp_path / "h.vocab")
+        hh.hh_save(h, m.encode(), v.encode(), 1)
+    finally:
+        hh.hh_close(h)
+    om, ov, ot = (str(tmp_path / f"o.{k}") for k in ("model", "vocab", "trace"))
+    subprocess.run([oracle_bin, corpus, str(cfg["vocab_size"]), str(cfg["unk_id"]), repr(cfg["character_coverage"]),
+                    str(cfg["min_pair_freq"]), om, ov, "--trace", ot, "--tiebreak-device", "0"], check=True,
+                   stderr=subprocess.DEVNULL)
+    assert open(trace).read() == open(ot).read()
+    assert open(m, "rb").read() == open(om, "rb").read()
+    assert open(v, "rb").read() == open(ov, "rb").read()
+    assert merges == os.path.getsize(om) // 12
