@@ -182,7 +182,7 @@ def fullsize_case(cfg_name):
         return None
 
 
-def cpu_baseline_finish(h, cfg_name, target_merges, gpu_merges, timeout=600):
+def cpu_baseline_finish(h, cfg_name, target_merges, gpu_merges, timeout=600, corpus_bytes=None):
     """merges/s of the capped CPU run.  When it stopped early, the full train() time is
     extrapolated along the measured cost curve of the committed full-size run of the same
     corpus and config (the oracle's cumulative train seconds every 256 merges, measured in the
@@ -210,6 +210,7 @@ def cpu_baseline_finish(h, cfg_name, target_merges, gpu_merges, timeout=600):
                    f"started after the timed GPU steps (it overlaps only the untimed K1/encode/HBM legs); "
                    f"value = merges/s of this measured prefix"),
         "capped_merges": merges, "capped_train_s": train_s, "load_s": load_s,
+        "load_GBps": (corpus_bytes / load_s / 1e9) if corpus_bytes and load_s > 0 else None,
         "calibration": calibration_note(),
     }
     case = fullsize_case(cfg_name)
@@ -610,6 +611,10 @@ def main():
     cfg = dict(CONFIGS[args.config], name=args.config)
     if args.bytes:
         cfg["bytes"] = args.bytes
+    # the committed full-size oracle run of this corpus (tests/golden/fullsize/<case>): the config's
+    # own size, or e.g. c5_10g for --config c5 --bytes 10000000000
+    case_name = args.config if not args.bytes else (
+        f"{args.config}_{args.bytes // 10**9}g" if args.bytes % 10**9 == 0 else None)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -657,6 +662,11 @@ def main():
     path = corpus_path(cfg, args.config)
     gen_s = ensure_corpus(cfg, path) if local == 0 else 0.0
     barrier()
+    # C4's corpus is 8 shards of one logical corpus: on one GPU the load counts the 8 byte ranges
+    # in turn and merges their word lists, as 8 ranks of a sharded load would (corpus.cpp)
+    sim_shards = cfg.get("shards") if world == 1 else None
+    if sim_shards:
+        os.environ.setdefault("SHREDWORD_LOAD_SIM_SHARDS", str(sim_shards))
 
     pinned = None if args.no_pin else pin_host_loop(local)
     from shredword import dist as sdist
@@ -826,8 +836,8 @@ def main():
                                if k1["avg_launch_us"] > 0 else None)
         if args.tiebreak == "device":
             result["tiebreak_device"] = tiebreak_report(st, merges, elapsed, args, os.path.join(tmpd, f"bench_r{rank}"))
-        case = fullsize_case(args.config)
-        if case and not args.bytes and args.tiebreak == "exact":
+        case = fullsize_case(case_name) if case_name else None
+        if case and case["recipe"]["bytes"] == cfg["bytes"] and args.tiebreak == "exact":
             result["config"]["corpus_md5_expected"] = case["corpus_md5"]
             result["config"]["unique_bytes"] = case["unique_bytes"]
             # size-independent parity at full size: the bench's own .model/.vocab against the
@@ -837,7 +847,8 @@ def main():
             vm = hashlib.md5(open(os.path.join(tmpd, f"bench_r{rank}.vocab"), "rb").read()).hexdigest()
             result["parity_fullsize"] = {"model_md5_equal": mm == case["model_md5"],
                                          "vocab_md5_equal": vm == case["vocab_md5"],
-                                         "reference": f"tests/golden/fullsize/{args.config}/case.json"}
+                                         "merges_equal": per_step_merges == case["merges"],
+                                         "reference": f"tests/golden/fullsize/{case_name}/case.json"}
         if pair_count is not None:
             result["pair_count"] = pair_count
             if pair_count.get("achieved"):
@@ -862,7 +873,8 @@ def main():
             try:
                 if "error" in cpu_h:
                     raise RuntimeError(cpu_h["error"])
-                result["cpu_baseline"] = cpu_baseline_finish(cpu_h, args.config, cfg["vocab"] - 256, per_step_merges)
+                result["cpu_baseline"] = cpu_baseline_finish(cpu_h, case_name or args.config, cfg["vocab"] - 256,
+                                                             per_step_merges, corpus_bytes=cfg["bytes"])
             except Exception as e:  # the GPU number stands on its own
                 result["cpu_baseline"] = {"value": None, "error": repr(e)}
             if isinstance(encode, dict) and "ms" in encode:

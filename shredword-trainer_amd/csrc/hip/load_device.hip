@@ -20,12 +20,16 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../host/corpus.h"
@@ -62,6 +66,7 @@ constexpr u64 kTableProbes = 512;
 constexpr bool kLoadWideDefault = true;  // the wide shape (C3: PMC 87.8 -> 77.9 GB); SHREDWORD_LOAD_WIDE=0/1 overrides
 
 __device__ __forceinline__ bool delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }
+__device__ __forceinline__ uint32_t has_zero(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
 
 // One 32-byte HBM slot per distinct word (a probe and its atomics touch one cache line).
 struct Slot {
@@ -77,7 +82,7 @@ struct Table {
   Slot* slot;
   u64 mask;         // capacity - 1
   uint32_t* nkeys;
-  uint32_t* flags;  // [0] table too full, [1] key collision
+  uint32_t* flags;  // [0] table too full, [1] key collision, [2] a NUL byte in the text
 };
 
 // kmask keeps all 64 bits (tests narrow it, SHREDWORD_LOAD_KEY_BITS, to force key collisions).
@@ -166,7 +171,8 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
   const u64 t0 = (u64)blockIdx.x * tiles_per_wg;
   const u64 t1 = t0 + tiles_per_wg < ntiles ? t0 + tiles_per_wg : ntiles;
   const u64 range = t0 * kTileBytes;  // LDS first offsets are relative to it (< 2^32: host-checked)
-  __shared__ uint32_t s_full;
+  __shared__ uint32_t s_full, s_nul;
+  if (tid == 0) s_nul = 0;
   for (u64 tile = t0; tile < t1; ++tile) {
     const u64 base = tile * kTileBytes;
     if (tid == 0) s_full = __hip_atomic_load(&t.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -177,6 +183,11 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
     for (int j = 0; j < kTileBytes / 16 / kLoadThreads; ++j) {
       const int q = j * kLoadThreads + tid;  // 16-B piece q of the tile
       const int4 v = g[q];
+      // a NUL byte anywhere (the reference's fgets/strlen cuts lines there: those files take the
+      // host path; bytes past the corpus are the ' ' padding)
+      const uint32_t z = has_zero((uint32_t)v.x) | has_zero((uint32_t)v.y) | has_zero((uint32_t)v.z) |
+                         has_zero((uint32_t)v.w);
+      if (z && base + (u64)q * 16 < n) s_nul = 1u;
       uint32_t* dst = s_tile32 + (q / (kChunkBytes / 16)) * (kTileStride / 4) + (q % (kChunkBytes / 16)) * 4;
       dst[0] = (uint32_t)v.x;
       dst[1] = (uint32_t)v.y;
@@ -249,6 +260,7 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
     }
   }
   __syncthreads();
+  if (tid == 0 && s_nul) atomicOr(&t.flags[2], 1u);
   for (int i = tid; i < kLdsSlots; i += kLoadThreads) {
     if (!s_key[i]) continue;
     const u64 first = range + s_first[i];
@@ -281,6 +293,20 @@ __global__ void k_word_gather(Table t, const uint32_t* slot, uint32_t W, WordRec
   }
 }
 
+// rank r's length, for the offsets of the packed spellings
+__global__ void k_word_lens(const WordRec* rec, uint32_t W, u64* len) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < W; r += gridDim.x * blockDim.x) len[r] = rec[r].len;
+}
+// The spellings packed in rank order (the host word table's byte array): a wave per 64 words, a
+// lane per word.
+__global__ void k_word_spell(const uint8_t* d, const WordRec* rec, const u64* off, uint32_t W, uint8_t* out) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < W; r += gridDim.x * blockDim.x) {
+    const uint8_t* src = d + rec[r].first;
+    uint8_t* dst = out + off[r];
+    for (uint32_t k = 0; k < rec[r].len; ++k) dst[k] = src[k];
+  }
+}
+
 struct DevBuf {
   void* p = nullptr;
   DevBuf() = default;
@@ -297,35 +323,158 @@ static double wall() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec>* out, std::string* why,
-                     bool staged) {
-  out->clear();
-  const bool report = std::getenv("SHREDWORD_LOAD_REPORT") != nullptr;
-  const double t0 = wall();
+// The count of text already in HBM (db[0, n), ' ' padding after it): records in reference word
+// order, and (spell) the spellings packed in that order.  *nul: the text holds a NUL byte (the
+// records are then not made).
+static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool report, double t0, double t1,
+                            std::vector<WordRec>* out, std::vector<uint8_t>* spell, bool* nul, std::string* why) {
+  // table capacity: a power of two >= 1 M and >= n / 8192 (grown 4x while it is over 3/4 full):
+  // a small table keeps the slots the spills touch in L2 / MALL
+  u64 cap = 1ull << 20;
+  while (cap < (u64)(n / 8192) && cap < (1ull << 29)) cap <<= 1;
+  if (const char* e = std::getenv("SHREDWORD_LOAD_TABLE_SLOTS")) {  // tests: a table that must grow
+    const u64 want = std::strtoull(e, nullptr, 10);
+    if (want >= 1024) {
+      cap = 1024;
+      while (cap < want && cap < (1ull << 29)) cap <<= 1;
+    }
+  }
+  u64 kmask = ~0ull;
+  if (const char* e = std::getenv("SHREDWORD_LOAD_KEY_BITS")) {
+    const int bits = std::atoi(e);
+    if (bits > 0 && bits < 64) kmask = (1ull << bits) - 1;
+  }
+  const char* wenv = std::getenv("SHREDWORD_LOAD_WIDE");
+  const bool wide = wenv ? std::atoi(wenv) != 0 : kLoadWideDefault;
+  const u64 kTileBytes = (u64)kChunkBytes * (wide ? kWideThreads : kNarrowThreads);
+  const u64 ntiles = (n + kTileBytes - 1) / kTileBytes;
+  u64 grid = std::min<u64>(ntiles, (u64)cus * (wide ? 1 : 2));
+  u64 per = (ntiles + grid - 1) / grid;
+  while (per * (u64)kTileBytes >= (1ull << 32)) {  // LDS first offsets are 32-bit range-relative
+    grid *= 2;
+    per = (ntiles + grid - 1) / grid;
+  }
+  grid = (ntiles + per - 1) / per;
+  if (nul) *nul = false;
+  for (int attempt = 0; attempt < 6; ++attempt) {
+    const u64 seed = 0x51ED270B27A1F4A3ull * (u64)(attempt + 1);
+    DevBuf bslot, bmeta;
+    LOAD_OK(hipMalloc(&bslot.p, cap * sizeof(Slot)));
+    LOAD_OK(hipMalloc(&bmeta.p, 64));
+    LOAD_OK(hipMemsetAsync(bslot.p, 0, cap * sizeof(Slot), st));
+    LOAD_OK(hipMemsetAsync(bmeta.p, 0, 64, st));
+    Table t;
+    t.slot = (Slot*)bslot.p;
+    t.mask = cap - 1;
+    t.nkeys = (uint32_t*)bmeta.p;
+    t.flags = (uint32_t*)bmeta.p + 4;
+    if (wide)
+      k_word_count<kWideThreads, kWideSlots><<<(unsigned)grid, kWideThreads, 0, st>>>(db, n, t, seed, kmask, per);
+    else
+      k_word_count<kNarrowThreads, kNarrowSlots><<<(unsigned)grid, kNarrowThreads, 0, st>>>(db, n, t, seed, kmask, per);
+    LOAD_OK(hipGetLastError());
+    uint32_t meta[16];
+    LOAD_OK(hipMemcpyAsync(meta, bmeta.p, 64, hipMemcpyDeviceToHost, st));
+    LOAD_OK(hipStreamSynchronize(st));
+    const double t2 = wall();
+    const uint32_t W = meta[0];
+    if (meta[6]) {  // a NUL byte: the reference reads such lines only up to it (host path)
+      if (nul) *nul = true;
+      if (why) *why = "the text holds NUL bytes";
+      return false;
+    }
+    if (meta[4]) {  // too full: a bigger table
+      if (cap >= (1ull << 29)) break;
+      cap <<= 2;
+      continue;
+    }
+    if (meta[5]) continue;  // a 64-bit key collision: another seed
+    // reference word order: (djb2 & 4095, first offset); the keys are distinct
+    DevBuf bk, bs, bk2, bs2, bn, btmp, brec;
+    LOAD_OK(hipMalloc(&bk.p, (size_t)W * 8 + 8));
+    LOAD_OK(hipMalloc(&bs.p, (size_t)W * 4 + 4));
+    LOAD_OK(hipMalloc(&bk2.p, (size_t)W * 8 + 8));
+    LOAD_OK(hipMalloc(&bs2.p, (size_t)W * 4 + 4));
+    LOAD_OK(hipMalloc(&bn.p, 4));
+    LOAD_OK(hipMemsetAsync(bn.p, 0, 4, st));
+    k_word_compact<<<cus * 4, 256, 0, st>>>(t, (u64*)bk.p, (uint32_t*)bs.p, (uint32_t*)bn.p);
+    LOAD_OK(hipGetLastError());
+    size_t tmp_bytes = 0, tb2 = 0;
+    LOAD_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (u64*)bk.p, (u64*)bk2.p, (uint32_t*)bs.p,
+                                               (uint32_t*)bs2.p, (int)W, 0, 64, st));
+    LOAD_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, (u64*)bk.p, (u64*)bk2.p, (int)W + 1, st));
+    tmp_bytes = std::max(tmp_bytes, tb2);
+    LOAD_OK(hipMalloc(&btmp.p, tmp_bytes + 16));
+    LOAD_OK(hipcub::DeviceRadixSort::SortPairs(btmp.p, tmp_bytes, (u64*)bk.p, (u64*)bk2.p, (uint32_t*)bs.p,
+                                               (uint32_t*)bs2.p, (int)W, 0, 64, st));
+    LOAD_OK(hipMalloc(&brec.p, (size_t)W * sizeof(WordRec) + sizeof(WordRec)));
+    k_word_gather<<<cus * 4, 256, 0, st>>>(t, (const uint32_t*)bs2.p, W, (WordRec*)brec.p);
+    LOAD_OK(hipGetLastError());
+    out->resize(W);
+    if (W) LOAD_OK(hipMemcpyAsync(out->data(), brec.p, (size_t)W * sizeof(WordRec), hipMemcpyDeviceToHost, st));
+    if (spell) {  // the spellings in rank order: lengths -> offsets (bk: lengths, bk2: offsets) -> bytes
+      LOAD_OK(hipMemsetAsync(bk.p, 0, (size_t)W * 8 + 8, st));
+      k_word_lens<<<cus * 4, 256, 0, st>>>((const WordRec*)brec.p, W, (u64*)bk.p);
+      LOAD_OK(hipGetLastError());
+      LOAD_OK(hipcub::DeviceScan::ExclusiveSum(btmp.p, tb2, (u64*)bk.p, (u64*)bk2.p, (int)W + 1, st));
+      u64 S = 0;
+      LOAD_OK(hipMemcpyAsync(&S, (u64*)bk2.p + W, 8, hipMemcpyDeviceToHost, st));
+      LOAD_OK(hipStreamSynchronize(st));
+      DevBuf bsp;
+      LOAD_OK(hipMalloc(&bsp.p, S + 16));
+      k_word_spell<<<cus * 4, 256, 0, st>>>(db, (const WordRec*)brec.p, (const u64*)bk2.p, W, (uint8_t*)bsp.p);
+      LOAD_OK(hipGetLastError());
+      spell->resize(S);
+      if (S) LOAD_OK(hipMemcpyAsync(spell->data(), bsp.p, S, hipMemcpyDeviceToHost, st));
+      LOAD_OK(hipStreamSynchronize(st));
+    }
+    LOAD_OK(hipStreamSynchronize(st));
+    if (report)
+      std::fprintf(stderr, "[LOAD] %zu bytes: upload %.1f ms, count %.1f ms, order+gather%s %.1f ms, %u words\n", n,
+                   1e3 * (t1 - t0), 1e3 * (t2 - t1), spell ? "+spellings" : "", 1e3 * (wall() - t2), W);
+    return true;
+  }
+  if (why) *why = "the device word table did not converge";
+  return false;
+}
+
+static bool device_setup(int device, hipStream_t* st, int* cus, std::string* why) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
     if (why) *why = "no HIP device";
     return false;
   }
+  LOAD_OK(hipSetDevice(device));
+  LOAD_OK(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+  hipDeviceProp_t prop;
+  LOAD_OK(hipGetDeviceProperties(&prop, device));
+  *cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  return true;
+}
+
+struct StreamGuard {
+  hipStream_t s = nullptr;
+  ~StreamGuard() {
+    if (!s) return;
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+  }
+};
+
+bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec>* out, std::string* why,
+                     bool staged) {
+  out->clear();
+  const bool report = std::getenv("SHREDWORD_LOAD_REPORT") != nullptr;
+  const double t0 = wall();
   if (n == 0) return true;
   if (n >= (1ull << 52)) {
     if (why) *why = "corpus larger than 2^52 bytes";
     return false;
   }
-  LOAD_OK(hipSetDevice(device));
-  hipStream_t st;
-  LOAD_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  struct StreamGuard {
-    hipStream_t s;
-    ~StreamGuard() {
-      (void)hipStreamSynchronize(s);
-      (void)hipStreamDestroy(s);
-    }
-  } sg{st};
-  hipDeviceProp_t prop;
-  LOAD_OK(hipGetDeviceProperties(&prop, device));
-  const int cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-
+  StreamGuard sg;
+  int cus = 256;
+  if (!device_setup(device, &sg.s, &cus, why)) return false;
+  hipStream_t st = sg.s;
   if (report) std::fprintf(stderr, "[LOAD] range of %zu bytes at %p: device setup %.1f ms\n", n, (const void*)d,
                            1e3 * (wall() - t0));
   DevBuf dd;
@@ -364,92 +513,90 @@ bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec
     LOAD_OK(hipMemcpyAsync(db, d, n, hipMemcpyHostToDevice, st));
   }
   if (report) LOAD_OK(hipStreamSynchronize(st));
-  const double t1 = wall();
+  return count_on_device(db, n, st, cus, report, t0, wall(), out, nullptr, nullptr, why);
+}
 
-  // table capacity: a power of two >= 1 M and >= n / 8192 (grown 4x while it is over 3/4 full):
-  // a small table keeps the slots the spills touch in L2 / MALL
-  u64 cap = 1ull << 20;
-  while (cap < (u64)(n / 8192) && cap < (1ull << 29)) cap <<= 1;
-  if (const char* e = std::getenv("SHREDWORD_LOAD_TABLE_SLOTS")) {  // tests: a table that must grow
-    const u64 want = std::strtoull(e, nullptr, 10);
-    if (want >= 1024) {
-      cap = 1024;
-      while (cap < want && cap < (1ull << 29)) cap <<= 1;
-    }
+bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<WordRec>* out,
+                    std::vector<uint8_t>* spell, bool* nul, std::string* why) {
+  out->clear();
+  spell->clear();
+  *nul = false;
+  const bool report = std::getenv("SHREDWORD_LOAD_REPORT") != nullptr;
+  const double t0 = wall();
+  if (n == 0) return true;
+  if (n >= (1ull << 52)) {
+    if (why) *why = "corpus larger than 2^52 bytes";
+    return false;
   }
-  u64 kmask = ~0ull;
-  if (const char* e = std::getenv("SHREDWORD_LOAD_KEY_BITS")) {
-    const int bits = std::atoi(e);
-    if (bits > 0 && bits < 64) kmask = (1ull << bits) - 1;
+  StreamGuard sg;
+  int cus = 256;
+  if (!device_setup(device, &sg.s, &cus, why)) return false;
+  hipStream_t st = sg.s;
+  DevBuf dd;
+  LOAD_OK(hipMalloc(&dd.p, n + kPadBytes));
+  uint8_t* db = static_cast<uint8_t*>(dd.p);
+  LOAD_OK(hipMemsetAsync(db + n, ' ', kPadBytes, st));
+  LOAD_OK(hipStreamSynchronize(st));
+  // The file straight into HBM: T reader threads, each with its own stream and two pinned
+  // buffers, pread() chunk c (c = t, t + T, ...) into one buffer while the other's DMA runs.  No
+  // mapping of the file: the page-ins of an mmap (one fault per 4 KiB page) and the runtime's
+  // pageable staging are what bound the mapped upload.
+  size_t chunk = (size_t)32 << 20;
+  if (const char* e = std::getenv("SHREDWORD_LOAD_CHUNK_MB")) chunk = std::max<size_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+  const size_t nchunks = (n + chunk - 1) / chunk;
+  int T = 8;
+  if (const char* e = std::getenv("SHREDWORD_LOAD_READERS")) T = std::max(1, std::atoi(e));
+  T = (int)std::min<size_t>((size_t)T, nchunks);
+  std::vector<std::thread> pool;
+  std::atomic<int> failed{0};
+  std::atomic<uint64_t> read_ns{0};
+  for (int ti = 0; ti < T; ++ti)
+    pool.emplace_back([&, ti] {
+      hipStream_t s = nullptr;
+      void* pin[2] = {nullptr, nullptr};
+      hipEvent_t ev[2] = {nullptr, nullptr};
+      bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+      for (int k = 0; k < 2 && ok; ++k)
+        ok = hipHostMalloc(&pin[k], chunk, hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) == hipSuccess;
+      int k = 0, used[2] = {0, 0};
+      for (size_t c = (size_t)ti; ok && c < nchunks && !failed.load(std::memory_order_relaxed); c += (size_t)T, k ^= 1) {
+        if (used[k]) ok = hipEventSynchronize(ev[k]) == hipSuccess;  // buffer k's previous DMA is done
+        const size_t off = c * chunk, len = std::min(chunk, n - off);
+        const double tr = wall();
+        size_t got = 0;
+        while (ok && got < len) {
+          const ssize_t r = ::pread(fd, (uint8_t*)pin[k] + got, len - got, (off_t)(base + off + got));
+          if (r <= 0) ok = false;
+          else got += (size_t)r;
+        }
+        read_ns.fetch_add((uint64_t)(1e9 * (wall() - tr)), std::memory_order_relaxed);
+        ok = ok && hipMemcpyAsync(db + off, pin[k], len, hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipEventRecord(ev[k], s) == hipSuccess;
+        used[k] = 1;
+      }
+      if (s) ok = hipStreamSynchronize(s) == hipSuccess && ok;
+      for (int j = 0; j < 2; ++j) {
+        if (ev[j]) (void)hipEventDestroy(ev[j]);
+        if (pin[j]) (void)hipHostFree(pin[j]);
+      }
+      if (s) (void)hipStreamDestroy(s);
+      if (!ok) failed.store(1);
+    });
+  for (auto& th : pool) th.join();
+  if (failed.load()) {
+    if (why) *why = "reading / uploading the file failed";
+    return false;
   }
-  const char* wenv = std::getenv("SHREDWORD_LOAD_WIDE");
-  const bool wide = wenv ? std::atoi(wenv) != 0 : kLoadWideDefault;
-  const u64 kTileBytes = (u64)kChunkBytes * (wide ? kWideThreads : kNarrowThreads);
-  const u64 ntiles = (n + kTileBytes - 1) / kTileBytes;
-  u64 grid = std::min<u64>(ntiles, (u64)cus * (wide ? 1 : 2));
-  u64 per = (ntiles + grid - 1) / grid;
-  while (per * (u64)kTileBytes >= (1ull << 32)) {  // LDS first offsets are 32-bit range-relative
-    grid *= 2;
-    per = (ntiles + grid - 1) / grid;
-  }
-  grid = (ntiles + per - 1) / per;
-  for (int attempt = 0; attempt < 6; ++attempt) {
-    const u64 seed = 0x51ED270B27A1F4A3ull * (u64)(attempt + 1);
-    DevBuf bslot, bmeta;
-    LOAD_OK(hipMalloc(&bslot.p, cap * sizeof(Slot)));
-    LOAD_OK(hipMalloc(&bmeta.p, 64));
-    LOAD_OK(hipMemsetAsync(bslot.p, 0, cap * sizeof(Slot), st));
-    LOAD_OK(hipMemsetAsync(bmeta.p, 0, 64, st));
-    Table t;
-    t.slot = (Slot*)bslot.p;
-    t.mask = cap - 1;
-    t.nkeys = (uint32_t*)bmeta.p;
-    t.flags = (uint32_t*)bmeta.p + 4;
-    if (wide)
-      k_word_count<kWideThreads, kWideSlots><<<(unsigned)grid, kWideThreads, 0, st>>>(db, n, t, seed, kmask, per);
-    else
-      k_word_count<kNarrowThreads, kNarrowSlots><<<(unsigned)grid, kNarrowThreads, 0, st>>>(db, n, t, seed, kmask, per);
-    LOAD_OK(hipGetLastError());
-    uint32_t meta[16];
-    LOAD_OK(hipMemcpyAsync(meta, bmeta.p, 64, hipMemcpyDeviceToHost, st));
-    LOAD_OK(hipStreamSynchronize(st));
-    const double t2 = wall();
-    const uint32_t W = meta[0];
-    if (meta[4]) {  // too full: a bigger table
-      if (cap >= (1ull << 29)) break;
-      cap <<= 2;
-      continue;
-    }
-    if (meta[5]) continue;  // a 64-bit key collision: another seed
-    // reference word order: (djb2 & 4095, first offset); the keys are distinct
-    DevBuf bk, bs, bk2, bs2, bn, btmp, brec;
-    LOAD_OK(hipMalloc(&bk.p, (size_t)W * 8 + 8));
-    LOAD_OK(hipMalloc(&bs.p, (size_t)W * 4 + 4));
-    LOAD_OK(hipMalloc(&bk2.p, (size_t)W * 8 + 8));
-    LOAD_OK(hipMalloc(&bs2.p, (size_t)W * 4 + 4));
-    LOAD_OK(hipMalloc(&bn.p, 4));
-    LOAD_OK(hipMemsetAsync(bn.p, 0, 4, st));
-    k_word_compact<<<cus * 4, 256, 0, st>>>(t, (u64*)bk.p, (uint32_t*)bs.p, (uint32_t*)bn.p);
-    LOAD_OK(hipGetLastError());
-    size_t tmp_bytes = 0;
-    LOAD_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (u64*)bk.p, (u64*)bk2.p, (uint32_t*)bs.p,
-                                               (uint32_t*)bs2.p, (int)W, 0, 64, st));
-    LOAD_OK(hipMalloc(&btmp.p, tmp_bytes + 16));
-    LOAD_OK(hipcub::DeviceRadixSort::SortPairs(btmp.p, tmp_bytes, (u64*)bk.p, (u64*)bk2.p, (uint32_t*)bs.p,
-                                               (uint32_t*)bs2.p, (int)W, 0, 64, st));
-    LOAD_OK(hipMalloc(&brec.p, (size_t)W * sizeof(WordRec) + sizeof(WordRec)));
-    k_word_gather<<<cus * 4, 256, 0, st>>>(t, (const uint32_t*)bs2.p, W, (WordRec*)brec.p);
-    LOAD_OK(hipGetLastError());
-    out->resize(W);
-    if (W) LOAD_OK(hipMemcpyAsync(out->data(), brec.p, (size_t)W * sizeof(WordRec), hipMemcpyDeviceToHost, st));
-    LOAD_OK(hipStreamSynchronize(st));
-    if (report)
-      std::fprintf(stderr, "[LOAD] %zu bytes: upload %.1f ms, count %.1f ms, order+gather %.1f ms, %u words\n", n,
-                   1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (wall() - t2), W);
-    return true;
-  }
-  if (why) *why = "the device word table did not converge";
-  return false;
+  const double t1 = wall();
+  if (report)
+    std::fprintf(stderr, "[LOAD] phase file_to_hbm %.1f ms (%d readers, %zu MiB chunks, pread %.1f ms summed over "
+                 "readers): %.1f GB/s\n", 1e3 * (t1 - t0), T, chunk >> 20, 1e-6 * (double)read_ns.load(),
+                 (double)n / (t1 - t0) / 1e9);
+  if (!count_on_device(db, n, st, cus, report, t0, t1, out, spell, nul, why)) return false;
+  if (base)
+    for (WordRec& w : *out) w.first += base;  // file offsets
+  return true;
 }
 
 }  // namespace shred

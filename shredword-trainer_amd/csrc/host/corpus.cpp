@@ -87,10 +87,14 @@ inline uint64_t word_hash(const uint8_t* p, uint32_t len) {
 
 struct Entry {
   uint64_t hash;
-  uint64_t first;  // file offset of the first occurrence (also where the spelling lives)
+  uint64_t first;  // file offset of the first occurrence
   uint64_t count;
+  uint64_t sp;     // where the spelling lives in the bytes the entry is read against (the file, or
+                   // the spellings a sharded load gathered)
   uint32_t len;
+  uint32_t pad;
 };
+static_assert(sizeof(Entry) == 40, "the sharded load ships entries as bytes");
 
 constexpr int kPartBits = 6;
 constexpr int kParts = 1 << kPartBits;
@@ -112,22 +116,22 @@ struct Counter {
     slots.swap(s);
     mask = ns - 1;
   }
-  // Adds `cnt` occurrences of the word at d[off, off+len) first seen at `first`.
-  void add(const uint8_t* d, uint64_t hash, uint64_t off, uint32_t len, uint64_t cnt, uint64_t first) {
+  // Adds `cnt` occurrences of the word spelled at d[sp, sp+len), first seen at file offset `first`.
+  void add(const uint8_t* d, uint64_t hash, uint64_t sp, uint32_t len, uint64_t cnt, uint64_t first) {
     if (2 * (ents.size() + 1) > slots.size()) grow();
     uint64_t j = hash & mask;
     for (;;) {
       uint32_t s = slots[j];
       if (!s) break;
       Entry& e = ents[s - 1];
-      if (e.hash == hash && e.len == len && std::memcmp(d + e.first, d + off, len) == 0) {
+      if (e.hash == hash && e.len == len && std::memcmp(d + e.sp, d + sp, len) == 0) {
         e.count += cnt;
         if (first < e.first) e.first = first;  // spelling is identical, keep the earliest
         return;
       }
       j = (j + 1) & mask;
     }
-    ents.push_back({hash, first, cnt, len});
+    ents.push_back({hash, first, cnt, sp, len, 0});
     slots[j] = (uint32_t)ents.size();
   }
   const Entry* find(const uint8_t* d, uint64_t hash, uint64_t off, uint32_t len) const {
@@ -136,7 +140,7 @@ struct Counter {
       uint32_t s = slots[j];
       if (!s) return nullptr;
       const Entry& e = ents[s - 1];
-      if (e.hash == hash && e.len == len && std::memcmp(d + e.first, d + off, len) == 0) return &e;
+      if (e.hash == hash && e.len == len && std::memcmp(d + e.sp, d + off, len) == 0) return &e;
       j = (j + 1) & mask;
     }
   }
@@ -170,8 +174,9 @@ void scan_words(const uint8_t* d, Range r, F&& f) {
 
 // The word table from the distinct words in reference word order (rank order): spellings,
 // counts, the coverage cut and the symbols (bpe.cpp:156-172, histogram.cpp:7-53).
+// spell: the spellings already packed in rank order (the device gathered them), else from d.
 void finish_table(const uint8_t* d, const std::vector<WordRec>& recs, const LoadOptions& opt, int threads,
-                  WordTable* out) {
+                  WordTable* out, std::vector<uint8_t>* spell = nullptr) {
   const size_t W = recs.size();
   if (W > (size_t)kMaxRank) fatal("corpus has more than 2^30 distinct words");
   WordTable& wt = *out;
@@ -185,11 +190,16 @@ void finish_table(const uint8_t* d, const std::vector<WordRec>& recs, const Load
     S += recs[r].len;
   }
   wt.offset[W] = S;
-  wt.bytes.resize(S);
-  parallel_for(threads, (W + 4095) / 4096, [&](size_t blk, int) {
-    size_t r1 = std::min(W, (blk + 1) * 4096);
-    for (size_t r = blk * 4096; r < r1; ++r) std::memcpy(wt.bytes.data() + wt.offset[r], d + recs[r].first, recs[r].len);
-  });
+  if (spell) {
+    if (spell->size() != S) fatal("device spellings disagree with the word lengths");
+    wt.bytes.swap(*spell);
+  } else {
+    wt.bytes.resize(S);
+    parallel_for(threads, (W + 4095) / 4096, [&](size_t blk, int) {
+      size_t r1 = std::min(W, (blk + 1) * 4096);
+      for (size_t r = blk * 4096; r < r1; ++r) std::memcpy(wt.bytes.data() + wt.offset[r], d + recs[r].first, recs[r].len);
+    });
+  }
   uint64_t occ = 0;
   for (uint64_t c : wt.count) occ += c;
   wt.total_occurrences = occ;
@@ -244,7 +254,7 @@ std::vector<Counter> count_pieces(const uint8_t* d, const std::vector<Range>& pi
   parallel_for(threads, kParts, [&](size_t part, int) {
     Counter& m = merged[part];
     for (int t = 0; t < threads; ++t)
-      for (const Entry& e : local[t][part].ents) m.add(d, e.hash, e.first, e.len, e.count, e.first);
+      for (const Entry& e : local[t][part].ents) m.add(d, e.hash, e.sp, e.len, e.count, e.first);
   });
   return merged;
 }
@@ -252,6 +262,7 @@ std::vector<Counter> count_pieces(const uint8_t* d, const std::vector<Range>& pi
 struct OrderKey { uint64_t order; uint32_t part, idx; };
 
 // Reference word order (djb2 & 4095, first occurrence) over the merged counters, then the table.
+// d: the bytes the entries' spellings live in (Entry::sp).
 void order_and_finish(const uint8_t* d, const std::vector<Counter>& merged, const LoadOptions& opt, int threads,
                       WordTable* out, std::vector<OrderKey>* keys_out) {
   std::vector<size_t> part_base(kParts + 1, 0);
@@ -264,18 +275,28 @@ void order_and_finish(const uint8_t* d, const std::vector<Counter>& merged, cons
     for (uint32_t i = 0; i < merged[p].ents.size(); ++i) {
       const Entry& e = merged[p].ents[i];
       uint64_t h = 5381;
-      for (uint32_t k = 0; k < e.len; ++k) h = h * 33 + d[e.first + k];
+      for (uint32_t k = 0; k < e.len; ++k) h = h * 33 + d[e.sp + k];
       if (e.first >= (1ull << 52)) fatal("corpus larger than 2^52 bytes");
       keys[part_base[p] + i] = {((h & 4095) << 52) | e.first, (uint32_t)p, i};
     }
   });
   std::sort(keys.begin(), keys.end(), [](const OrderKey& a, const OrderKey& b) { return a.order < b.order; });
   std::vector<WordRec> recs(W);
+  std::vector<uint64_t> at(W + 1, 0);
   for (size_t r = 0; r < W; ++r) {
     const Entry& e = merged[keys[r].part].ents[keys[r].idx];
     recs[r] = WordRec{e.first, e.count, e.len, 0};
+    at[r + 1] = at[r] + e.len;
   }
-  finish_table(d, recs, opt, threads, out);
+  std::vector<uint8_t> spell(at[W]);
+  parallel_for(threads, (W + 4095) / 4096, [&](size_t blk, int) {
+    const size_t r1 = std::min(W, (blk + 1) * 4096);
+    for (size_t r = blk * 4096; r < r1; ++r) {
+      const Entry& e = merged[keys[r].part].ents[keys[r].idx];
+      std::memcpy(spell.data() + at[r], d + e.sp, e.len);
+    }
+  });
+  finish_table(nullptr, recs, opt, threads, out, &spell);
 }
 
 // First position >= x after a delimiter (0 and n stay): the words starting before it end before it.
@@ -285,28 +306,43 @@ uint64_t shard_cut(const uint8_t* d, uint64_t n, uint64_t x) {
   return x;
 }
 
-// The distinct words starting in rank r's byte range (of W), with their hashes and global offsets.
-std::vector<Entry> shard_entries(const uint8_t* d, size_t n, const LoadOptions& opt, uint64_t r, uint64_t W,
-                                 int threads, bool* on_gpu) {
+// The distinct words starting in rank r's byte range (of W): entries with their hashes and file
+// offsets, their spellings packed in *blob (Entry::sp indexes it), and whether the range holds a
+// NUL byte (*nul; the load then falls back to the host's line semantics on every rank).
+std::vector<Entry> shard_entries(const uint8_t* d, size_t n, int fd, const LoadOptions& opt, uint64_t r, uint64_t W,
+                                 int threads, bool* on_gpu, std::vector<uint8_t>* blob, bool* nul) {
   const uint64_t b = shard_cut(d, n, (uint64_t)((unsigned __int128)n * r / W));
   const uint64_t e = shard_cut(d, n, (uint64_t)((unsigned __int128)n * (r + 1) / W));
   std::vector<Entry> mine;
+  blob->clear();
   *on_gpu = false;
+  *nul = false;
   if (opt.gpu_device >= 0 && e > b && e - b >= opt.gpu_min_bytes) {
     std::vector<WordRec> recs;
     std::string why;
-    // any range short of the whole mapping goes through pinned buffers (the runtime's pageable
-    // copy of a part of a mapping is slow: load_device.hip)
-    if (gpu_count_words(opt.gpu_device, d + b, e - b, &recs, &why, /*staged=*/b > 0 || e < n)) {
+    // the range straight from the file (reader threads + pinned buffers), the spellings from the
+    // device; without a file (in-memory bytes), from the mapping through pinned buffers
+    const bool ok = fd >= 0 ? gpu_count_file(opt.gpu_device, fd, b, e - b, &recs, blob, nul, &why)
+                            : gpu_count_words(opt.gpu_device, d + b, e - b, &recs, &why, /*staged=*/b > 0 || e < n);
+    if (*nul) return mine;
+    if (ok) {
       *on_gpu = true;
       const double th = now_seconds();
+      std::vector<uint64_t> at(recs.size() + 1, 0);
+      for (size_t i = 0; i < recs.size(); ++i) {
+        if (fd < 0) recs[i].first += b;
+        at[i + 1] = at[i] + recs[i].len;
+      }
+      if (fd < 0) {
+        blob->resize(at[recs.size()]);
+        for (size_t i = 0; i < recs.size(); ++i) std::memcpy(blob->data() + at[i], d + recs[i].first, recs[i].len);
+      }
       mine.resize(recs.size());
       parallel_for(threads, (recs.size() + 4095) / 4096, [&](size_t blk, int) {
         const size_t i1 = std::min(recs.size(), (blk + 1) * 4096);
-        for (size_t i = blk * 4096; i < i1; ++i) {
-          const uint64_t f = b + recs[i].first;
-          mine[i] = Entry{word_hash(d + f, recs[i].len), f, recs[i].count, recs[i].len};
-        }
+        for (size_t i = blk * 4096; i < i1; ++i)
+          mine[i] = Entry{word_hash(blob->data() + at[i], recs[i].len), recs[i].first, recs[i].count, at[i],
+                          recs[i].len, 0};
       });
       if (std::getenv("SHREDWORD_LOAD_REPORT"))
         std::fprintf(stderr, "[LOAD] range %llu/%llu: %zu word hashes %.1f ms\n", (unsigned long long)r,
@@ -316,17 +352,30 @@ std::vector<Entry> shard_entries(const uint8_t* d, size_t n, const LoadOptions& 
     std::fprintf(stderr, "[WARNING]\t GPU word count unavailable (%s): counting on the host\n", why.c_str());
   }
   if (e > b) {
+    if (std::memchr(d + b, 0, e - b)) {
+      *nul = true;
+      return mine;
+    }
     const uint64_t target = std::max<uint64_t>(1 << 20, (e - b) / (uint64_t)(threads * 8) + 1);
     std::vector<uint64_t> pw;
     std::vector<Counter> c = count_pieces(d, split_pieces(d, {{b, e}}, target), threads, &pw);
-    for (const Counter& k : c) mine.insert(mine.end(), k.ents.begin(), k.ents.end());
+    uint64_t at = 0;
+    for (const Counter& k : c)
+      for (const Entry& x : k.ents) {
+        mine.push_back(x);
+        mine.back().sp = at;
+        at += x.len;
+      }
+    blob->resize(at);
+    for (const Entry& x : mine) std::memcpy(blob->data() + x.sp, d + x.first, x.len);
   }
   return mine;
 }
 
 // Every rank's word list merged (counts summed, first occurrence min; equal hashes must spell
-// the same word: Counter::add compares the bytes), then the table in reference order.
-void merge_entries(const uint8_t* d, const Entry* all, size_t total, const LoadOptions& opt, int threads,
+// the same word: Counter::add compares the bytes), then the table in reference order.  `blob`
+// holds every entry's spelling (Entry::sp).
+void merge_entries(const uint8_t* blob, const Entry* all, size_t total, const LoadOptions& opt, int threads,
                    WordTable* out) {
   // 64-bit indices: Σ over ranks of distinct words per rank can pass 2^32 even when the merged
   // table stays small
@@ -334,57 +383,114 @@ void merge_entries(const uint8_t* d, const Entry* all, size_t total, const LoadO
   for (size_t i = 0; i < total; ++i) by_part[all[i].hash >> (64 - kPartBits)].push_back((uint64_t)i);
   std::vector<Counter> merged(kParts);
   parallel_for(threads, kParts, [&](size_t p, int) {
-    for (uint64_t i : by_part[p]) merged[p].add(d, all[i].hash, all[i].first, all[i].len, all[i].count, all[i].first);
+    for (uint64_t i : by_part[p]) merged[p].add(blob, all[i].hash, all[i].sp, all[i].len, all[i].count, all[i].first);
   });
   std::vector<OrderKey> keys;
-  order_and_finish(d, merged, opt, threads, out, &keys);
+  order_and_finish(blob, merged, opt, threads, out, &keys);
+}
+
+// A rank's words as one gather buffer: [u64 entries][u64 blob bytes][u64 nul][entries][blob].
+void pack_shard(const std::vector<Entry>& ents, const std::vector<uint8_t>& blob, bool nul, std::vector<uint8_t>* out) {
+  const uint64_t h[3] = {ents.size(), blob.size(), nul ? 1ull : 0ull};
+  out->resize(sizeof(h) + ents.size() * sizeof(Entry) + blob.size());
+  std::memcpy(out->data(), h, sizeof(h));
+  if (!ents.empty()) std::memcpy(out->data() + sizeof(h), ents.data(), ents.size() * sizeof(Entry));
+  if (!blob.empty()) std::memcpy(out->data() + sizeof(h) + ents.size() * sizeof(Entry), blob.data(), blob.size());
+}
+
+// Appends one rank's buffer to (all, blob), its spellings' offsets moved past the blob so far.
+// False for a malformed buffer; *used = its size.
+bool unpack_shard(const uint8_t* p, size_t avail, std::vector<Entry>* all, std::vector<uint8_t>* blob, bool* nul,
+                  size_t* used) {
+  uint64_t h[3];
+  if (avail < sizeof(h)) return false;
+  std::memcpy(h, p, sizeof(h));
+  const size_t need = sizeof(h) + h[0] * sizeof(Entry) + h[1];
+  if (h[0] > avail / sizeof(Entry) || h[1] > avail || need > avail) return false;
+  const uint64_t base = blob->size();
+  const size_t e0 = all->size();
+  all->resize(e0 + h[0]);
+  if (h[0]) std::memcpy(all->data() + e0, p + sizeof(h), h[0] * sizeof(Entry));
+  for (size_t i = e0; i < all->size(); ++i) (*all)[i].sp += base;
+  blob->insert(blob->end(), p + sizeof(h) + h[0] * sizeof(Entry), p + need);
+  *nul = *nul || h[2] != 0;
+  *used = need;
+  return true;
 }
 
 // The sharded load (LoadOptions::shard_world > 1): this rank's words, then every rank's merged.
 // SHREDWORD_LOAD_SIM_SHARDS=k (tests, one process): the k ranges counted in turn, merged the same way.
-bool load_sharded(const uint8_t* d, size_t n, const LoadOptions& opt, int threads, WordTable* out, int sim,
-                  std::string* err) {
-  bool on_gpu = false;
+// Returns 0, -1 on a failed gather (*err), or 1 when some range holds a NUL byte (the caller loads
+// without sharding: the reference's line semantics need the whole file in order).
+int load_sharded(const uint8_t* d, size_t n, int fd, const LoadOptions& opt, int threads, WordTable* out, int sim,
+                 std::string* err) {
+  bool on_gpu = false, nul = false;
+  std::vector<Entry> all;
+  std::vector<uint8_t> blob;
   if (sim > 1) {
-    std::vector<Entry> all;
-    for (int r = 0; r < sim; ++r) {
-      bool g = false;
-      std::vector<Entry> m = shard_entries(d, n, opt, (uint64_t)r, (uint64_t)sim, threads, &g);
+    for (int r = 0; r < sim && !nul; ++r) {
+      bool g = false, z = false;
+      std::vector<uint8_t> b;
+      std::vector<Entry> m = shard_entries(d, n, fd, opt, (uint64_t)r, (uint64_t)sim, threads, &g, &b, &z);
       on_gpu = on_gpu || g;
-      all.insert(all.end(), m.begin(), m.end());
+      nul = nul || z;
+      std::vector<uint8_t> buf;
+      pack_shard(m, b, z, &buf);
+      size_t used = 0;
+      unpack_shard(buf.data(), buf.size(), &all, &blob, &nul, &used);
     }
-    merge_entries(d, all.data(), all.size(), opt, threads, out);
   } else {
-    std::vector<Entry> mine = shard_entries(d, n, opt, (uint64_t)opt.shard_rank, (uint64_t)opt.shard_world, threads,
-                                            &on_gpu);
+    std::vector<uint8_t> b;
+    bool z = false;
+    std::vector<Entry> mine = shard_entries(d, n, fd, opt, (uint64_t)opt.shard_rank, (uint64_t)opt.shard_world, threads,
+                                            &on_gpu, &b, &z);
+    std::vector<uint8_t> buf;
+    pack_shard(mine, b, z, &buf);
     size_t got = 0;
-    const Entry* all = (const Entry*)opt.gather(opt.gather_ctx, mine.data(), mine.size() * sizeof(Entry), &got);
+    const uint8_t* g = (const uint8_t*)opt.gather(opt.gather_ctx, buf.data(), buf.size(), &got);
     // A failed gather (the caller's callback raised, a peer left) must not become an empty
     // table: every rank would then train on nothing without an error.
-    if (!all || got % sizeof(Entry) != 0 || got < mine.size() * sizeof(Entry)) {
+    bool ok = g != nullptr && got >= buf.size();
+    size_t pos = 0, ranks = 0;
+    while (ok && pos < got) {
+      size_t used = 0;
+      ok = unpack_shard(g + pos, got - pos, &all, &blob, &nul, &used);
+      pos += used;
+      ++ranks;
+    }
+    if (!ok || ranks != (size_t)opt.shard_world) {
       if (err)
         *err = "sharded load: the word-list all-gather failed (" + std::to_string(got) + " bytes returned for " +
-               std::to_string(mine.size() * sizeof(Entry)) + " sent)";
-      return false;
+               std::to_string(buf.size()) + " sent)";
+      return -1;
     }
-    merge_entries(d, all, got / sizeof(Entry), opt, threads, out);
   }
+  if (nul) return 1;
+  merge_entries(blob.data(), all.data(), all.size(), opt, threads, out);
   out->counted_on_gpu = on_gpu;
-  return true;
+  return 0;
 }
 
 }  // namespace
 
-int load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordTable* out, std::string* err) {
+int load_corpus_bytes(const uint8_t* d, size_t n, const LoadOptions& opt, WordTable* out, std::string* err, int fd) {
   int threads = opt.threads > 0 ? opt.threads : (int)std::thread::hardware_concurrency();
   threads = std::max(1, std::min(threads, 32));
   const char* sim_env = std::getenv("SHREDWORD_LOAD_SIM_SHARDS");
   const int sim = sim_env ? std::atoi(sim_env) : 0;
-  if (((opt.shard_world > 1 && opt.gather) || sim > 1) && !opt.want_stream && n > 0 && !std::memchr(d, 0, n))
-    return load_sharded(d, n, opt, threads, out, sim, err) ? 0 : -1;
+  if (((opt.shard_world > 1 && opt.gather) || sim > 1) && !opt.want_stream && n > 0) {
+    const int r = load_sharded(d, n, fd, opt, threads, out, sim, err);
+    if (r <= 0) return r;
+    // a NUL byte in some rank's range: every rank loads the whole file the reference's way
+  }
   // the device count (types layout, NUL-free files: every line is read whole, so the words are
   // the maximal runs of non-delimiters of the whole file)
-  if (opt.gpu_device >= 0 && !opt.want_stream && n >= opt.gpu_min_bytes && !std::memchr(d, 0, n)) {
+  const bool report = std::getenv("SHREDWORD_LOAD_REPORT") != nullptr;
+  const double tz = now_seconds();
+  const bool nul_free = opt.gpu_device >= 0 && !opt.want_stream && n >= opt.gpu_min_bytes && !std::memchr(d, 0, n);
+  if (report && opt.gpu_device >= 0) std::fprintf(stderr, "[LOAD] phase nul_scan %.1f ms (host memchr, page-in)\n",
+                                                   1e3 * (now_seconds() - tz));
+  if (nul_free) {
     std::vector<WordRec> recs;
     std::string why;
     const double t0 = now_seconds();
@@ -449,15 +555,42 @@ int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::s
     ::close(fd);
     return load_corpus_bytes(nullptr, 0, opt, out, err);
   }
+  // The device path reads the file itself (no mapping): the whole-file count of a types-layout
+  // load.  A NUL byte sends the file to the host's fgets/strlen path below.
+  LoadOptions o2 = opt;
+  const char* sim_env = std::getenv("SHREDWORD_LOAD_SIM_SHARDS");
+  const bool sharded = (opt.shard_world > 1 && opt.gather) || (sim_env && std::atoi(sim_env) > 1);
+  if (opt.gpu_device >= 0 && !opt.want_stream && !sharded && n >= opt.gpu_min_bytes) {
+    std::vector<WordRec> recs;
+    std::vector<uint8_t> spell;
+    std::string why;
+    bool nul = false;
+    const double t0 = now_seconds();
+    if (gpu_count_file(opt.gpu_device, fd, 0, n, &recs, &spell, &nul, &why)) {
+      ::close(fd);
+      const double t1 = now_seconds();
+      int threads = opt.threads > 0 ? opt.threads : (int)std::thread::hardware_concurrency();
+      threads = std::max(1, std::min(threads, 32));
+      finish_table(nullptr, recs, opt, threads, out, &spell);
+      out->counted_on_gpu = true;
+      if (std::getenv("SHREDWORD_LOAD_REPORT"))
+        std::fprintf(stderr, "[LOAD] phase device_count %.1f ms (file -> HBM, count, order, spellings), host_table "
+                     "%.1f ms (coverage, symbols)\n", 1e3 * (t1 - t0), 1e3 * (now_seconds() - t1));
+      return 0;
+    }
+    if (!nul) std::fprintf(stderr, "[WARNING]\t GPU word count unavailable (%s): counting on the host\n", why.c_str());
+    o2.gpu_device = -1;  // the host path (NUL bytes: the reference's line semantics)
+  }
   void* m = ::mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
-  ::close(fd);
   if (m == MAP_FAILED) {
+    ::close(fd);
     if (err) *err = std::string("Couldn't map file: ") + path;
     return -1;
   }
   ::madvise(m, n, MADV_SEQUENTIAL);
-  const int rc = load_corpus_bytes((const uint8_t*)m, n, opt, out, err);
+  const int rc = load_corpus_bytes((const uint8_t*)m, n, o2, out, err, sharded ? fd : -1);
   ::munmap(m, n);
+  ::close(fd);
   return rc;
 }
 

@@ -73,11 +73,22 @@ struct WordRec {
 bool gpu_count_words(int device, const uint8_t* d, size_t n, std::vector<WordRec>* out, std::string* why,
                      bool staged = false);
 
+// The same count read straight from an open file (no mapping): reader threads pread() into
+// pinned buffers and DMA each chunk to HBM; the device also gathers the spellings in rank order
+// (*spell: the word table's byte array).  *nul: the file holds a NUL byte (false is returned; the
+// caller takes the host's fgets/strlen path).
+// [base, base + n) of the file (a sharded load's byte range): records carry file offsets.
+bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<WordRec>* out,
+                    std::vector<uint8_t>* spell, bool* nul, std::string* why);
+
 // Returns 0 on success, -1 if the file cannot be opened/mapped (message in *err).
 int load_corpus(const char* path, const LoadOptions& opt, WordTable* out, std::string* err);
 
 // Builds a WordTable from in-memory text (same rules); used by tests and tools.
 // 0, or -1 with *err set (a sharded load whose word-list all-gather failed).
-int load_corpus_bytes(const uint8_t* data, size_t n, const LoadOptions& opt, WordTable* out, std::string* err = nullptr);
+// fd >= 0: the same bytes as an open file (the device count of a sharded load reads its range
+// from it instead of the mapping).
+int load_corpus_bytes(const uint8_t* data, size_t n, const LoadOptions& opt, WordTable* out, std::string* err = nullptr,
+                      int fd = -1);
 
 }  // namespace shred

@@ -193,13 +193,18 @@ bool ensure_device(Trainer* t, const char* caller) {
     const bool xshard = dist_active() && t->dist_exchange();  // replicate: every rank holds the whole table
     const int rank = xshard ? dist_state().rank : 0, world = xshard ? dist_state().world : 1;
     shard_range(t->wt, t->layout, rank, world, &begin, &end);
+    const double tp = now_seconds();
     TiledStream ts;
     pack_tiles(t->wt, t->layout, begin, end, &ts);
     int32_t max_id = 0;
     for (int c = 0; c < 256; ++c)
       if (t->wt.keep[c]) max_id = c;
+    const double tu = now_seconds();
     t->dev->upload(ts, t->layout, t->wt.count, max_id);
     t->device_stale = false;
+    if (std::getenv("SHREDWORD_LOAD_REPORT"))
+      std::fprintf(stderr, "[LOAD] phase pack_tiles %.1f ms, device upload %.1f ms (tiles + word runs + index + "
+                   "resident plan)\n", 1e3 * (tu - tp), 1e3 * (now_seconds() - tu));
   }
   return true;
 }
@@ -275,6 +280,7 @@ int bpe_load_corpus(Trainer* t, const char* path) {
     std::fprintf(stderr, "[ERROR]\t %s\n", err.c_str());
     return -1;
   }
+  const double t_table = now_seconds();
   t->wt = std::move(wt);  // last load wins (bpe.cpp:176-178)
   t->loaded = true;
   t->device_stale = true;
@@ -285,6 +291,10 @@ int bpe_load_corpus(Trainer* t, const char* path) {
   std::string why;
   if (Device::available(&why) && !ensure_device(t, "bpe_load_corpus")) return -1;
   t->load_s = now_seconds() - t0;
+  if (std::getenv("SHREDWORD_LOAD_REPORT"))
+    std::fprintf(stderr, "[LOAD] phase word_table %.1f ms (file -> distinct words, order, coverage, symbols), "
+                 "device_table %.1f ms (tiles, upload, resident plan, word runs + index), total %.1f ms\n",
+                 1e3 * (t_table - t0), 1e3 * (t->load_s - (t_table - t0)), 1e3 * t->load_s);
   return 0;
 }
 

@@ -578,4 +578,10 @@ bool gpu_count_words(int, const uint8_t*, size_t, std::vector<WordRec>*, std::st
   if (why) *why = "host harness: no device";
   return false;
 }
+bool gpu_count_file(int, int, uint64_t, size_t, std::vector<WordRec>*, std::vector<uint8_t>*, bool* nul,
+                    std::string* why) {
+  *nul = false;
+  if (why) *why = "host harness: no device";
+  return false;
+}
 }  // namespace shred

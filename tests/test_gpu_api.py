@@ -696,3 +696,45 @@ def test_plain_ctypes_then_torch_exits_cleanly(then, tmp_path):
                           env=dict(os.environ, SHREDWORD_LOG="0"))
     assert proc.returncode == 0, (proc.returncode, proc.stderr[-2000:])
     assert proc.stdout.strip().startswith("ok")
+
+
+@pytest.mark.parametrize("readers,chunk_mb", [(8, 32), (3, 1)])
+def test_file_streamed_to_hbm_matches_host(readers, chunk_mb, tmp_path, monkeypatch):
+    """load_corpus reads the file straight into HBM (gpu_count_file: reader threads, pread into
+    pinned buffers, one DMA per chunk; the spellings come back from the device): the same table
+    and training bytes as the host count, with chunks of 1 MiB over 3 readers as well."""
+    monkeypatch.setenv("SHREDWORD_GPU_LOAD_MIN", "1")
+    monkeypatch.setenv("SHREDWORD_LOAD_READERS", str(readers))
+    monkeypatch.setenv("SHREDWORD_LOAD_CHUNK_MB", str(chunk_mb))
+    corpus = str(tmp_path / "u.txt")
+    corpora.gen_synthetic(corpus, 5_500_000, 78, "mixed")
+    outs = []
+    for gpu in (0, 1):
+        t = _trainer(vocab_size=2000, unk_id=0, character_coverage=0.9995, min_pair_freq=2)
+        t.set_option("gpu_load", gpu)
+        t.load_corpus(corpus)
+        outs.append(_train_bytes(t, tmp_path, f"s{gpu}"))
+        assert t.stats()["load_on_gpu"] == gpu
+        t.destroy()
+    assert outs[0] == outs[1]
+
+
+def test_nul_byte_file_takes_the_host_path(tmp_path, monkeypatch):
+    """A NUL byte deep inside a file (the reference's fgets/strlen drop the rest of that line):
+    the device count notices it and the host path counts; files equal the host-only load's."""
+    monkeypatch.setenv("SHREDWORD_GPU_LOAD_MIN", "1")
+    corpus = str(tmp_path / "n.txt")
+    corpora.gen_synthetic(corpus, 3_000_000, 79, "utf8")
+    data = bytearray(open(corpus, "rb").read())
+    at = data.index(b"\n", 2_000_000) + 5
+    data[at] = 0
+    open(corpus, "wb").write(bytes(data))
+    outs = []
+    for gpu in (1, 0):
+        t = _trainer(vocab_size=1500, unk_id=0, min_pair_freq=2)
+        t.set_option("gpu_load", gpu)
+        t.load_corpus(corpus)
+        assert t.stats()["load_on_gpu"] == 0
+        outs.append(_train_bytes(t, tmp_path, f"n{gpu}"))
+        t.destroy()
+    assert outs[0] == outs[1]

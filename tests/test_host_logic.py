@@ -184,3 +184,15 @@ def test_tiebreak_device_host_logic_matches_oracle_rule(name, hh, case_corpus, o
     assert open(m, "rb").read() == open(om, "rb").read()
     assert open(v, "rb").read() == open(ov, "rb").read()
     assert merges == os.path.getsize(om) // 12
+
+
+@pytest.mark.parametrize("name", ["adv_unk0", "adv_cov05", "utf8_2m_v2000_mpf50"])
+def test_sharded_load_ranges_match_reference(name, hh, case_corpus, tmp_path, monkeypatch):
+    """The sharded load's word lists (3 byte ranges counted in turn, shipped with their spellings and
+    merged) give the reference's files; a range holding a NUL byte (the adversarial corpora) sends
+    every rank to the whole-file fgets/strlen path instead."""
+    monkeypatch.setenv("SHREDWORD_LOAD_SIM_SHARDS", "3")
+    case, corpus = case_corpus(name)
+    merges, model, vocab, trace = _run(hh, case, corpus, tmp_path, "types")
+    assert merges == case["merges"]
+    assert model == case["model_bytes"] and vocab == case["vocab_bytes"]
