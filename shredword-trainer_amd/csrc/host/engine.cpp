@@ -121,7 +121,9 @@ bool Engine::merge_one(Backend& be, int remaining) {
   // overlap: the next merges' guesses run while this one is consumed (up to the backend's depth;
   // each guess shares no token with this merge or the guesses before it)
   if (spec && chain == 1) {
-    const size_t depth = (size_t)std::max(1, be.overlap_depth());
+    // early guess: one guess (X+1) in flight before the collect; the one after it (X+2) is made
+    // once X is applied (below).  Otherwise the backend's depth, all guessed here.
+    const size_t depth = early_guess_ ? 1 : (size_t)std::max(1, be.overlap_depth());
     while (pending_.size() < depth && (int)pending_.size() + 1 < remaining && be.can_overlap()) {
       used_.assign({a, b});
       for (const Guess& p : pending_) {
@@ -161,6 +163,21 @@ bool Engine::merge_one(Backend& be, int remaining) {
     }
   }
   sel_.apply_finish(a, b, X);
+  // Early guess: with X applied, the guess for X+2 is made now, on the heap the coming selects
+  // will pop (the guess for X+1 and every pair sharing its tokens counted as changing), and posted
+  // at once, so the device has X+2 queued before it finishes X+1.  The selects of X+1 happen after
+  // the post (the heap replay is off the device's path); a wrong guess for X+1 undoes both.
+  if (early_guess_ && spec && chain == 1 && pending_.size() == 1 && pending_.front().X == X + 1 && remaining > 2 &&
+      be.can_overlap()) {
+    const Guess g1 = pending_.front();
+    used_.assign({g1.a, g1.b});
+    Guess g{0, 0, X + 2};
+    if (sel_.predict_avoid(used_.data(), used_.size(), pred_window_, &g.a, &g.b)) {
+      pending_.push_back(g);
+      ++launches_;
+      be.merge_scan(g.a, g.b, g.X);
+    }
+  }
   times_.launch_s += t2 - t1;
   times_.wait_s += t3 - t2;
   if (launched) {

@@ -106,6 +106,9 @@ class Engine {
   // Late correction of the guess in flight once the current merge's records are known (default
   // on; SHREDWORD_CORRECT=0 turns it off).
   void set_correction(bool on) { correct_ = on; }
+  // Early guess (default on; SHREDWORD_EARLY_GUESS=0 or option early_guess=0 turns it off): the
+  // guess for X+2 is posted right after X is applied, before the select of X+1 (see merge_one).
+  void set_early_guess(bool on) { early_guess_ = on; }
   uint64_t corrections() const { return corrections_; }
   // K5 argmax verifier (debug): every `every` merges (0 = off), the selected pair's frequency is
   // checked against a device recount of the corpus (Backend::pair_max): it must be the largest
@@ -153,6 +156,7 @@ class Engine {
   bool tiebreak_device_ = false;
   int train_device(Backend& be, double t0);
   bool correct_ = true;
+  bool early_guess_ = true;
   uint64_t corrections_ = 0;
   uint64_t verify_checks_ = 0, verify_fail_ = 0;
   size_t probe_k_ = 0, probe_window_ = 256;

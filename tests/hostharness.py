@@ -35,6 +35,7 @@ def load():
     lib.hh_load.restype = ctypes.c_int
     lib.hh_count.argtypes = [ctypes.c_void_p]
     lib.hh_set_tiebreak_device.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.hh_set_early_guess.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.hh_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     lib.hh_trace_line.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     lib.hh_save.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]

@@ -415,6 +415,7 @@ int hh_load(void* p, const char* path) {
   return 0;
 }
 
+void hh_set_early_guess(void* p, int on) { ((Harness*)p)->engine.set_early_guess(on != 0); }
 void hh_set_tiebreak_device(void* p, int on) { ((Harness*)p)->engine.set_tiebreak_device(on != 0); }
 
 void hh_count(void* p) {
