@@ -393,24 +393,33 @@ __global__ __launch_bounds__(kThreads) void k_cache_encode(const uint8_t* __rest
   sl[1] = pack_payload(off, (u64)L, (u64)m);
 }
 
+// Per occurrence: its word's cached ids, written straight to the output at the chunk's place.
+// The chunk's place is its exclusive sum over the chunks before it, found by a decoupled
+// look-back: chunks are taken in ticket order (a block never waits for one that has not started),
+// each publishes its id count, then walks back over the predecessors' published counts until one
+// that also published its inclusive sum (status 2), and publishes its own.  The states are 8-B
+// agent atomics on both sides (cross-XCD coherent).  No staging copy of the ids.
+constexpr u64 kLbValue = (1ull << 62) - 1;
 __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restrict__ text, u64 n,
                                                           const u64* __restrict__ slot, u64 cmask,
-                                                          const int32_t* __restrict__ arena, int32_t* __restrict__ pad,
-                                                          uint32_t* __restrict__ bstart, u64* __restrict__ bcnt,
-                                                          u64* __restrict__ misc) {
+                                                          const int32_t* __restrict__ arena, int32_t* __restrict__ out,
+                                                          u64 out_cap, u64* __restrict__ bcnt, u64* __restrict__ lb,
+                                                          u64 nb, u64* __restrict__ misc) {
   __shared__ uint32_t s_text[kStageBytes / 4];
   __shared__ uint32_t s_list[kSpanWords * kThreads];  // this chunk's words: arena offsets, column per thread
   __shared__ uint32_t s_inc[kThreads];
-  __shared__ uint32_t s_start;
+  __shared__ u64 s_chunk, s_prefix;
   const int tid = threadIdx.x;
-  const u64 chunk = blockIdx.x;
-  if (tid == 0) s_start = 0xFFFFFFFFu;
+  if (tid == 0) {
+    s_chunk = __hip_atomic_fetch_add(lb + nb, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ticket
+  }
+  __syncthreads();
+  const u64 chunk = s_chunk;
   const TextView tv = stage_chunk(text, n, chunk, s_text);  // synchronises
   const u64 cbase = chunk * kChunk;
   const u64 base = cbase + (u64)tid * kSpan;
-  uint32_t cnt = 0, nw = 0, first = 0xFFFFFFFFu;
+  uint32_t cnt = 0, nw = 0;
   for_each_word(tv, n, base, [&](u64 s, u64 L, int) {
-    if (first == 0xFFFFFFFFu) first = (uint32_t)(s - cbase);
     if (L > (u64)kEncMaxWord) return;  // flagged by k_cache_insert
     const u64 h = word_hash(tv, s, (uint32_t)L);
     u64 pay = 0, i = (h >> 17) & cmask;
@@ -444,7 +453,6 @@ __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restr
     ++nw;
     cnt += m;
   });
-  if (first != 0xFFFFFFFFu) atomicMin(&s_start, first);
   // block-inclusive scan of the per-thread id counts
   s_inc[tid] = cnt;
   __syncthreads();
@@ -454,8 +462,33 @@ __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restr
     s_inc[tid] += v;
     __syncthreads();
   }
-  const uint32_t start = s_start == 0xFFFFFFFFu ? 0u : s_start;
-  int32_t* dst = pad + cbase + start + (s_inc[tid] - cnt);
+  if (tid == 0) {
+    const u64 agg = s_inc[kThreads - 1];
+    u64 prefix = 0;
+    if (chunk == 0) {
+      __hip_atomic_exchange(lb, (2ull << 62) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_exchange(lb + chunk, (1ull << 62) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (u64 j = chunk - 1;;) {
+        const u64 v = __hip_atomic_fetch_add(lb + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 status = v >> 62;
+        if (status == 0) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix += v & kLbValue;
+        if (status == 2 || j == 0) break;
+        --j;
+      }
+      __hip_atomic_exchange(lb + chunk, (2ull << 62) | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_prefix = prefix;
+    bcnt[chunk] = agg;
+    if (prefix + agg > out_cap) flag(misc, 16);  // the output is too small: nothing of this chunk is written
+  }
+  __syncthreads();
+  if (s_prefix + s_inc[kThreads - 1] > out_cap) return;
+  int32_t* dst = out + s_prefix + (s_inc[tid] - cnt);
   for (uint32_t w = 0; w < nw; ++w) {
     const uint32_t e = s_list[w * kThreads + tid];
     if (e & 0x80000000u) {  // inline ids: the slot line the lookup just read
@@ -472,22 +505,6 @@ __global__ __launch_bounds__(kThreads) void k_cache_words(const uint8_t* __restr
     for (uint32_t k = 0; k < m; ++k) dst[k] = src[k];
     dst += m;
   }
-  if (tid == 0) {
-    bcnt[chunk] = s_inc[kThreads - 1];
-    bstart[chunk] = start;
-  }
-}
-
-// Block b's run pad[b * kChunk + bstart[b], + count) -> out at its exclusive block sum.
-__global__ __launch_bounds__(kThreads) void k_block_emit(const int32_t* __restrict__ pad,
-                                                         const uint32_t* __restrict__ bstart,
-                                                         const u64* __restrict__ bcnt, const u64* __restrict__ binc,
-                                                         int32_t* __restrict__ out) {
-  const u64 b = blockIdx.x;
-  const u64 total = bcnt[b];
-  const int32_t* src = pad + b * kChunk + bstart[b];
-  int32_t* dst = out + (binc[b] - total);
-  for (u64 i = threadIdx.x; i < total; i += kThreads) dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(kThreads) void k_encode_emit(const int32_t* __restrict__ pad, const uint32_t* __restrict__ tcnt,
@@ -613,7 +630,7 @@ bool EncodeDevice::reserve(size_t n, std::string* why) {
     return false;
   }
   if (hipMalloc(&pad_, cap * 4) != hipSuccess || hipMalloc(&rank_, cap * 4) != hipSuccess ||
-      hipMalloc(&tcnt_, nb * kThreads * 4) != hipSuccess || hipMalloc(&bcnt_, 2 * nb * 8) != hipSuccess ||
+      hipMalloc(&tcnt_, nb * kThreads * 4) != hipSuccess || hipMalloc(&bcnt_, (3 * nb + 1) * 8) != hipSuccess ||
       hipcub::DeviceScan::InclusiveSum(nullptr, scan_tmp_bytes_, bcnt_, bcnt_ + nb, (int)nb) != hipSuccess ||
       hipMalloc(&scan_tmp_, scan_tmp_bytes_ ? scan_tmp_bytes_ : 16) != hipSuccess) {
     *why = "scratch allocation failed";
@@ -667,8 +684,10 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
       enck<<<dim3((unsigned)(cc / kThreads)), dim3(kThreads), 0, st>>>(text, n, byte_map_, table_, mask_, cslot_, cc,
                                                                        rank_, arena_cap, pad_, misc_);
       ENC_OK(hipGetLastError());
-      k_cache_words<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, cslot_, cc - 1, rank_, pad_, tcnt_, bcnt_,
-                                                                   misc_);
+      // look-back states and the ticket (bcnt_[2 nb, 3 nb], zero = "not published")
+      ENC_OK(hipMemsetAsync(bcnt_ + 2 * nb, 0, (nb + 1) * 8, st));
+      k_cache_words<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(text, n, cslot_, cc - 1, rank_, out, (u64)cap, bcnt_,
+                                                                   bcnt_ + 2 * nb, nb, misc_);
     } else {
       const bool aligned = (reinterpret_cast<uintptr_t>(text) & 15) == 0;
       auto kern = aligned ? (packed_ ? k_encode_words<true, true> : k_encode_words<true, false>)
@@ -684,6 +703,7 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
     ENC_OK(hipStreamSynchronize(st));
     const uint64_t fl = host_misc_[1];
     if (fl & 1) return -3;
+    if (fl & 16) return -2;  // the output capacity (the cached path writes it directly)
     if (!(fl & 14)) break;
     if (fl == 2 && cc < ccap_) {  // only a probe window overflowed: a bigger table
       cc = std::min(ccap_, cc * 4);
@@ -699,9 +719,7 @@ int64_t EncodeDevice::encode(const uint8_t* text, size_t n, int32_t* out, size_t
   const u64 total = host_misc_[0];
   if (total > cap) return -2;
   ENC_OK(hipEventRecord(ev[2], st));
-  if (total && cached)
-    k_block_emit<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(pad_, tcnt_, bcnt_, bcnt_ + nb, out);
-  else if (total)
+  if (total && !cached)  // the cached path wrote the ids in place (k_cache_words)
     k_encode_emit<<<dim3((unsigned)nb), dim3(kThreads), 0, st>>>(pad_, tcnt_, bcnt_ + nb, out);
   ENC_OK(hipGetLastError());
   ENC_OK(hipEventRecord(ev[3], st));
