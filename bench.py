@@ -414,10 +414,10 @@ def encode_leg(model, vocab, unk, path, reps, device=0, cfg_name="c3"):
     del text, out
     torch.cuda.empty_cache()
     per = {k: pmc_traffic(cfg_name, "types", k) for k in
-           ("k_cache_insert", "k_cache_encode<true>", "k_cache_words", "k_block_emit")}
+           ("k_cache_insert", "k_cache_encode<true>", "k_cache_words")}
     traffic = sum(v or 0.0 for v in per.values())
-    return {"kernel": ("k_cache_insert + k_cache_encode + k_cache_words + hipCUB scan + k_block_emit "
-                       "(word cache; median of reps, HIP events)"),
+    return {"kernel": ("k_cache_insert + k_cache_encode + k_cache_words (ids written in place after a decoupled "
+                       "look-back over chunk sums; word cache; median of reps, HIP events)"),
             "traffic_by_kernel": per, "traffic_x_algorithmic": (traffic / alg) if traffic else None,
             "traffic_bytes": traffic or None,
             "text_bytes": n, "ids": nids, "ms": ms, "text_GBps": n / (ms * 1e-3) / 1e9,
