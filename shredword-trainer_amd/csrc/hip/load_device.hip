@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -82,7 +83,8 @@ struct Table {
   Slot* slot;
   u64 mask;         // capacity - 1
   uint32_t* nkeys;
-  uint32_t* flags;  // [0] table too full, [1] key collision, [2] a NUL byte in the text
+  uint32_t* flags;  // [0] table too full, [1] key collision, [2] a NUL byte in the text, [3] a word
+                    // past a segment's landed bytes
 };
 
 // kmask keeps all 64 bits (tests narrow it, SHREDWORD_LOAD_KEY_BITS, to force key collisions).
@@ -151,7 +153,7 @@ __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 
 // (djb2 & 4095) is computed at the flush, from the slot's first occurrence.
 template <int kLoadThreads, int kLdsSlots>
 __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u64 n, Table t, u64 seed, u64 kmask,
-                                                             u64 tiles_per_wg) {
+                                                             u64 tiles_per_wg, u64 tile0, u64 tile1, u64 safe_end) {
   constexpr int kTileBytes = kChunkBytes * kLoadThreads;
   __shared__ u64 s_key[kLdsSlots];
   __shared__ uint32_t s_first[kLdsSlots];
@@ -167,9 +169,10 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
     s_cnt[i] = 0;
     s_len[i] = 0;
   }
-  const u64 ntiles = (n + kTileBytes - 1) / kTileBytes;
-  const u64 t0 = (u64)blockIdx.x * tiles_per_wg;
-  const u64 t1 = t0 + tiles_per_wg < ntiles ? t0 + tiles_per_wg : ntiles;
+  // tiles [tile0, tile1) of the text (a segment counted while later ones are still uploading:
+  // bytes at or past safe_end may not have landed yet)
+  const u64 t0 = tile0 + (u64)blockIdx.x * tiles_per_wg;
+  const u64 t1 = t0 + tiles_per_wg < tile1 ? t0 + tiles_per_wg : tile1;
   const u64 range = t0 * kTileBytes;  // LDS first offsets are relative to it (< 2^32: host-checked)
   __shared__ uint32_t s_full, s_nul;
   if (tid == 0) s_nul = 0;
@@ -207,6 +210,10 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
       uint32_t w[kSpell / 4] = {0, 0, 0, 0};  // the leading bytes, packed
       uint32_t len = 0;
       for (;; ++len) {
+        if (base + p + len >= safe_end) {  // a word running past the landed bytes: count again later
+          atomicOr(&t.flags[3], 1u);
+          break;
+        }
         const uint32_t c = tile_byte<kTileBytes>(s_tile, d, base, p + len);
         if (delim(c)) break;
         h = (h ^ c) * 0x100000001B3ull;
@@ -323,13 +330,43 @@ static double wall() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// The count of text already in HBM (db[0, n), ' ' padding after it): records in reference word
-// order, and (spell) the spellings packed in that order.  *nul: the text holds a NUL byte (the
-// records are then not made).
-static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool report, double t0, double t1,
-                            std::vector<WordRec>* out, std::vector<uint8_t>* spell, bool* nul, std::string* why) {
-  // table capacity: a power of two >= 1 M and >= n / 8192 (grown 4x while it is over 3/4 full):
-  // a small table keeps the slots the spills touch in L2 / MALL
+// The count kernel's geometry for n bytes: workgroup shape, tiles per workgroup.
+struct CountShape {
+  bool wide;
+  u64 tile_bytes, ntiles, per;
+};
+static CountShape count_shape(size_t n, int cus) {
+  const char* wenv = std::getenv("SHREDWORD_LOAD_WIDE");
+  CountShape c;
+  c.wide = wenv ? std::atoi(wenv) != 0 : kLoadWideDefault;
+  c.tile_bytes = (u64)kChunkBytes * (c.wide ? kWideThreads : kNarrowThreads);
+  c.ntiles = (n + c.tile_bytes - 1) / c.tile_bytes;
+  u64 grid = std::min<u64>(std::max<u64>(c.ntiles, 1), (u64)cus * (c.wide ? 1 : 2));
+  c.per = (c.ntiles + grid - 1) / grid;
+  while (c.per * c.tile_bytes >= (1ull << 32)) {  // LDS first offsets are 32-bit range-relative
+    grid *= 2;
+    c.per = (c.ntiles + grid - 1) / grid;
+  }
+  if (c.per == 0) c.per = 1;
+  return c;
+}
+// k_word_count over tiles [tile0, tile1).
+// per: tiles per workgroup (0: the whole-text shape's).
+static void count_launch(const CountShape& c, const uint8_t* db, size_t n, const Table& t, u64 seed, u64 kmask,
+                         u64 tile0, u64 tile1, u64 safe_end, hipStream_t st, u64 per = 0) {
+  if (tile1 <= tile0) return;
+  if (!per) per = c.per;
+  const u64 grid = (tile1 - tile0 + per - 1) / per;
+  if (c.wide)
+    k_word_count<kWideThreads, kWideSlots><<<(unsigned)grid, kWideThreads, 0, st>>>(db, n, t, seed, kmask, per, tile0,
+                                                                                    tile1, safe_end);
+  else
+    k_word_count<kNarrowThreads, kNarrowSlots><<<(unsigned)grid, kNarrowThreads, 0, st>>>(db, n, t, seed, kmask, per,
+                                                                                          tile0, tile1, safe_end);
+}
+static u64 count_table_slots(size_t n) {
+  // a power of two >= 1 M and >= n / 8192 (grown 4x while it is over 3/4 full): a small table
+  // keeps the slots the spills touch in L2 / MALL
   u64 cap = 1ull << 20;
   while (cap < (u64)(n / 8192) && cap < (1ull << 29)) cap <<= 1;
   if (const char* e = std::getenv("SHREDWORD_LOAD_TABLE_SLOTS")) {  // tests: a table that must grow
@@ -339,42 +376,67 @@ static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool
       while (cap < want && cap < (1ull << 29)) cap <<= 1;
     }
   }
+  return cap;
+}
+static u64 count_key_mask() {
   u64 kmask = ~0ull;
   if (const char* e = std::getenv("SHREDWORD_LOAD_KEY_BITS")) {
     const int bits = std::atoi(e);
     if (bits > 0 && bits < 64) kmask = (1ull << bits) - 1;
   }
-  const char* wenv = std::getenv("SHREDWORD_LOAD_WIDE");
-  const bool wide = wenv ? std::atoi(wenv) != 0 : kLoadWideDefault;
-  const u64 kTileBytes = (u64)kChunkBytes * (wide ? kWideThreads : kNarrowThreads);
-  const u64 ntiles = (n + kTileBytes - 1) / kTileBytes;
-  u64 grid = std::min<u64>(ntiles, (u64)cus * (wide ? 1 : 2));
-  u64 per = (ntiles + grid - 1) / grid;
-  while (per * (u64)kTileBytes >= (1ull << 32)) {  // LDS first offsets are 32-bit range-relative
-    grid *= 2;
-    per = (ntiles + grid - 1) / grid;
-  }
-  grid = (ntiles + per - 1) / per;
+  return kmask;
+}
+static u64 count_seed(int attempt) { return 0x51ED270B27A1F4A3ull * (u64)(attempt + 1); }
+
+// A count's device table (slots + meta) that outlives one attempt (the segmented count of
+// gpu_count_file hands its table to count_on_device).
+struct CountTable {
+  DevBuf slot, meta;
+  u64 cap = 0;
+  Table t{};
+};
+static bool count_table_alloc(CountTable* ct, u64 cap, hipStream_t st, std::string* why) {
+  if (ct->slot.p) (void)hipFree(ct->slot.p);
+  if (ct->meta.p) (void)hipFree(ct->meta.p);
+  ct->slot.p = ct->meta.p = nullptr;
+  LOAD_OK(hipMalloc(&ct->slot.p, cap * sizeof(Slot)));
+  LOAD_OK(hipMalloc(&ct->meta.p, 64));
+  LOAD_OK(hipMemsetAsync(ct->slot.p, 0, cap * sizeof(Slot), st));
+  LOAD_OK(hipMemsetAsync(ct->meta.p, 0, 64, st));
+  ct->cap = cap;
+  ct->t.slot = (Slot*)ct->slot.p;
+  ct->t.mask = cap - 1;
+  ct->t.nkeys = (uint32_t*)ct->meta.p;
+  ct->t.flags = (uint32_t*)ct->meta.p + 4;
+  return true;
+}
+
+// The count of text already in HBM (db[0, n), ' ' padding after it): records in reference word
+// order, and (spell) the spellings packed in that order.  *nul: the text holds a NUL byte (the
+// records are then not made).  pre: a table already counted (attempt 0, seed 0) or nullptr.
+static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool report, double t0, double t1,
+                            std::vector<WordRec>* out, std::vector<uint8_t>* spell, bool* nul, std::string* why,
+                            CountTable* pre = nullptr) {
+  u64 cap = count_table_slots(n);
+  const u64 kmask = count_key_mask();
+  const CountShape shape = count_shape(n, cus);
   if (nul) *nul = false;
+  CountTable own;
   for (int attempt = 0; attempt < 6; ++attempt) {
-    const u64 seed = 0x51ED270B27A1F4A3ull * (u64)(attempt + 1);
-    DevBuf bslot, bmeta;
-    LOAD_OK(hipMalloc(&bslot.p, cap * sizeof(Slot)));
-    LOAD_OK(hipMalloc(&bmeta.p, 64));
-    LOAD_OK(hipMemsetAsync(bslot.p, 0, cap * sizeof(Slot), st));
-    LOAD_OK(hipMemsetAsync(bmeta.p, 0, 64, st));
-    Table t;
-    t.slot = (Slot*)bslot.p;
-    t.mask = cap - 1;
-    t.nkeys = (uint32_t*)bmeta.p;
-    t.flags = (uint32_t*)bmeta.p + 4;
-    if (wide)
-      k_word_count<kWideThreads, kWideSlots><<<(unsigned)grid, kWideThreads, 0, st>>>(db, n, t, seed, kmask, per);
-    else
-      k_word_count<kNarrowThreads, kNarrowSlots><<<(unsigned)grid, kNarrowThreads, 0, st>>>(db, n, t, seed, kmask, per);
-    LOAD_OK(hipGetLastError());
+    const u64 seed = count_seed(attempt);
+    CountTable* ct = nullptr;
+    if (attempt == 0 && pre) {
+      ct = pre;
+      cap = pre->cap;
+    } else {
+      if (!count_table_alloc(&own, cap, st, why)) return false;
+      ct = &own;
+      count_launch(shape, db, n, ct->t, seed, kmask, 0, shape.ntiles, ~0ull, st);
+      LOAD_OK(hipGetLastError());
+    }
+    const Table& t = ct->t;
     uint32_t meta[16];
-    LOAD_OK(hipMemcpyAsync(meta, bmeta.p, 64, hipMemcpyDeviceToHost, st));
+    LOAD_OK(hipMemcpyAsync(meta, ct->meta.p, 64, hipMemcpyDeviceToHost, st));
     LOAD_OK(hipStreamSynchronize(st));
     const double t2 = wall();
     const uint32_t W = meta[0];
@@ -388,7 +450,7 @@ static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool
       cap <<= 2;
       continue;
     }
-    if (meta[5]) continue;  // a 64-bit key collision: another seed
+    if (meta[5] || meta[7]) continue;  // a 64-bit key collision (another seed), or a segment's word past its bytes
     // reference word order: (djb2 & 4095, first offset); the keys are distinct
     DevBuf bk, bs, bk2, bs2, bn, btmp, brec;
     LOAD_OK(hipMalloc(&bk.p, (size_t)W * 8 + 8));
@@ -430,8 +492,9 @@ static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool
     }
     LOAD_OK(hipStreamSynchronize(st));
     if (report)
-      std::fprintf(stderr, "[LOAD] %zu bytes: upload %.1f ms, count %.1f ms, order+gather%s %.1f ms, %u words\n", n,
-                   1e3 * (t1 - t0), 1e3 * (t2 - t1), spell ? "+spellings" : "", 1e3 * (wall() - t2), W);
+      std::fprintf(stderr, "[LOAD] %zu bytes: upload %.1f ms, count %.1f ms%s, order+gather%s %.1f ms, %u words\n", n,
+                   1e3 * (t1 - t0), 1e3 * (t2 - t1), attempt == 0 && pre ? " (past the overlapped upload)" : "",
+                   spell ? "+spellings" : "", 1e3 * (wall() - t2), W);
     return true;
   }
   if (why) *why = "the device word table did not converge";
@@ -540,13 +603,34 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   // The file straight into HBM: T reader threads, each with its own stream and two pinned
   // buffers, pread() chunk c (c = t, t + T, ...) into one buffer while the other's DMA runs.  No
   // mapping of the file: the page-ins of an mmap (one fault per 4 KiB page) and the runtime's
-  // pageable staging are what bound the mapped upload.
+  // pageable staging are what bound the mapped upload.  Overlap: the count runs on segments
+  // (whole tiles) as they land -- segment k once every chunk up to the end of segment k + 1 is
+  // in HBM (a word may run into the next segment; one running further is flagged and the whole
+  // count is repeated after the upload).
   size_t chunk = (size_t)32 << 20;
   if (const char* e = std::getenv("SHREDWORD_LOAD_CHUNK_MB")) chunk = std::max<size_t>(1, std::strtoull(e, nullptr, 10)) << 20;
   const size_t nchunks = (n + chunk - 1) / chunk;
   int T = 8;
   if (const char* e = std::getenv("SHREDWORD_LOAD_READERS")) T = std::max(1, std::atoi(e));
   T = (int)std::min<size_t>((size_t)T, nchunks);
+  const CountShape shape = count_shape(n, cus);
+  u64 seg_bytes = (u64)2 << 30;
+  if (const char* e = std::getenv("SHREDWORD_LOAD_SEGMENT_MB")) seg_bytes = std::max<u64>(1, std::strtoull(e, nullptr, 10)) << 20;
+  const char* oenv = std::getenv("SHREDWORD_LOAD_OVERLAP");
+  const u64 seg_tiles = std::max<u64>(1, seg_bytes / shape.tile_bytes);
+  const u64 nseg = (shape.ntiles + seg_tiles - 1) / seg_tiles;
+  const bool overlap = !(oenv && oenv[0] == '0') && nseg > 1;
+  std::vector<hipEvent_t> ev(nchunks, nullptr);
+  for (size_t c = 0; c < nchunks; ++c) LOAD_OK(hipEventCreateWithFlags(&ev[c], hipEventDisableTiming));
+  struct EventsGuard {
+    std::vector<hipEvent_t>& v;
+    ~EventsGuard() {
+      for (hipEvent_t e : v)
+        if (e) (void)hipEventDestroy(e);
+    }
+  } eg{ev};
+  std::unique_ptr<std::atomic<int>[]> recorded(new std::atomic<int>[nchunks]);
+  for (size_t c = 0; c < nchunks; ++c) recorded[c].store(0);
   std::vector<std::thread> pool;
   std::atomic<int> failed{0};
   std::atomic<uint64_t> read_ns{0};
@@ -554,35 +638,63 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
     pool.emplace_back([&, ti] {
       hipStream_t s = nullptr;
       void* pin[2] = {nullptr, nullptr};
-      hipEvent_t ev[2] = {nullptr, nullptr};
       bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
-      for (int k = 0; k < 2 && ok; ++k)
-        ok = hipHostMalloc(&pin[k], chunk, hipHostMallocDefault) == hipSuccess &&
-             hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) == hipSuccess;
-      int k = 0, used[2] = {0, 0};
-      for (size_t c = (size_t)ti; ok && c < nchunks && !failed.load(std::memory_order_relaxed); c += (size_t)T, k ^= 1) {
-        if (used[k]) ok = hipEventSynchronize(ev[k]) == hipSuccess;  // buffer k's previous DMA is done
-        const size_t off = c * chunk, len = std::min(chunk, n - off);
-        const double tr = wall();
-        size_t got = 0;
-        while (ok && got < len) {
-          const ssize_t r = ::pread(fd, (uint8_t*)pin[k] + got, len - got, (off_t)(base + off + got));
-          if (r <= 0) ok = false;
-          else got += (size_t)r;
+      for (int k = 0; k < 2 && ok; ++k) ok = hipHostMalloc(&pin[k], chunk, hipHostMallocDefault) == hipSuccess;
+      int k = 0;
+      size_t last[2] = {SIZE_MAX, SIZE_MAX};
+      for (size_t c = (size_t)ti; c < nchunks; c += (size_t)T, k ^= 1) {
+        if (ok && !failed.load(std::memory_order_relaxed)) {
+          if (last[k] != SIZE_MAX) ok = hipEventSynchronize(ev[last[k]]) == hipSuccess;  // buffer k is free again
+          const size_t off = c * chunk, len = std::min(chunk, n - off);
+          const double tr = wall();
+          size_t got = 0;
+          while (ok && got < len) {
+            const ssize_t r = ::pread(fd, (uint8_t*)pin[k] + got, len - got, (off_t)(base + off + got));
+            if (r <= 0) ok = false;
+            else got += (size_t)r;
+          }
+          read_ns.fetch_add((uint64_t)(1e9 * (wall() - tr)), std::memory_order_relaxed);
+          ok = ok && hipMemcpyAsync(db + off, pin[k], len, hipMemcpyHostToDevice, s) == hipSuccess &&
+               hipEventRecord(ev[c], s) == hipSuccess;
+          last[k] = c;
         }
-        read_ns.fetch_add((uint64_t)(1e9 * (wall() - tr)), std::memory_order_relaxed);
-        ok = ok && hipMemcpyAsync(db + off, pin[k], len, hipMemcpyHostToDevice, s) == hipSuccess &&
-             hipEventRecord(ev[k], s) == hipSuccess;
-        used[k] = 1;
+        if (!ok) failed.store(1);
+        recorded[c].store(ok ? 1 : 2, std::memory_order_release);  // 2: failed (the counter stops)
       }
       if (s) ok = hipStreamSynchronize(s) == hipSuccess && ok;
-      for (int j = 0; j < 2; ++j) {
-        if (ev[j]) (void)hipEventDestroy(ev[j]);
+      for (int j = 0; j < 2; ++j)
         if (pin[j]) (void)hipHostFree(pin[j]);
-      }
       if (s) (void)hipStreamDestroy(s);
       if (!ok) failed.store(1);
     });
+  // the segmented count on this thread's stream, behind the chunks' events
+  CountTable pre;
+  bool pre_ok = false;
+  if (overlap) {
+    pre_ok = count_table_alloc(&pre, count_table_slots(n), st, why);
+    size_t waited = 0;  // chunks [0, waited) are behind an event wait on st
+    for (u64 k = 0; pre_ok && k < nseg; ++k) {
+      const u64 tile0 = k * seg_tiles, tile1 = std::min(shape.ntiles, tile0 + seg_tiles);
+      const u64 reach = std::min<u64>(n, std::min(shape.ntiles, tile1 + seg_tiles) * shape.tile_bytes);
+      const size_t need = k + 1 == nseg ? nchunks : (size_t)((reach + chunk - 1) / chunk);
+      for (; waited < need; ++waited) {
+        int r;
+        while ((r = recorded[waited].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        if (r != 1) {
+          pre_ok = false;
+          break;
+        }
+        if (hipStreamWaitEvent(st, ev[waited], 0) != hipSuccess) pre_ok = false;
+      }
+      if (!pre_ok) break;
+      const u64 safe_end = k + 1 == nseg ? ~0ull : (u64)need * chunk;
+      // a segment over the whole chip (a workgroup per CU: shape.per would leave most idle)
+      const u64 per_seg = std::max<u64>(1, (tile1 - tile0 + (u64)cus * (shape.wide ? 1 : 2) - 1) /
+                                               ((u64)cus * (shape.wide ? 1 : 2)));
+      count_launch(shape, db, n, pre.t, count_seed(0), count_key_mask(), tile0, tile1, safe_end, st, per_seg);
+      if (hipGetLastError() != hipSuccess) pre_ok = false;
+    }
+  }
   for (auto& th : pool) th.join();
   if (failed.load()) {
     if (why) *why = "reading / uploading the file failed";
@@ -591,9 +703,9 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   const double t1 = wall();
   if (report)
     std::fprintf(stderr, "[LOAD] phase file_to_hbm %.1f ms (%d readers, %zu MiB chunks, pread %.1f ms summed over "
-                 "readers): %.1f GB/s\n", 1e3 * (t1 - t0), T, chunk >> 20, 1e-6 * (double)read_ns.load(),
-                 (double)n / (t1 - t0) / 1e9);
-  if (!count_on_device(db, n, st, cus, report, t0, t1, out, spell, nul, why)) return false;
+                 "readers): %.1f GB/s%s\n", 1e3 * (t1 - t0), T, chunk >> 20, 1e-6 * (double)read_ns.load(),
+                 (double)n / (t1 - t0) / 1e9, overlap ? "; the count ran on segments meanwhile" : "");
+  if (!count_on_device(db, n, st, cus, report, t0, t1, out, spell, nul, why, pre_ok ? &pre : nullptr)) return false;
   if (base)
     for (WordRec& w : *out) w.first += base;  // file offsets
   return true;
