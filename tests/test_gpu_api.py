@@ -698,16 +698,27 @@ def test_plain_ctypes_then_torch_exits_cleanly(then, tmp_path):
     assert proc.stdout.strip().startswith("ok")
 
 
-@pytest.mark.parametrize("readers,chunk_mb", [(8, 32), (3, 1)])
-def test_file_streamed_to_hbm_matches_host(readers, chunk_mb, tmp_path, monkeypatch):
+@pytest.mark.parametrize("readers,chunk_mb,seg_mb,long_word", [(8, 32, 2048, False), (3, 1, 1, False),
+                                                                (2, 1, 1, True), (4, 1, 0, False)])
+def test_file_streamed_to_hbm_matches_host(readers, chunk_mb, seg_mb, long_word, tmp_path, monkeypatch):
     """load_corpus reads the file straight into HBM (gpu_count_file: reader threads, pread into
-    pinned buffers, one DMA per chunk; the spellings come back from the device): the same table
-    and training bytes as the host count, with chunks of 1 MiB over 3 readers as well."""
+    pinned buffers, one DMA per chunk; the spellings come back from the device), counting 1 MiB
+    segments while later chunks still upload (seg_mb 0: no overlap): the same table and training
+    bytes as the host count -- also with a 2.5 MB word that runs past a segment's landed bytes
+    (the count is then repeated after the upload)."""
     monkeypatch.setenv("SHREDWORD_GPU_LOAD_MIN", "1")
     monkeypatch.setenv("SHREDWORD_LOAD_READERS", str(readers))
     monkeypatch.setenv("SHREDWORD_LOAD_CHUNK_MB", str(chunk_mb))
+    if seg_mb:
+        monkeypatch.setenv("SHREDWORD_LOAD_SEGMENT_MB", str(seg_mb))
+    else:
+        monkeypatch.setenv("SHREDWORD_LOAD_OVERLAP", "0")
     corpus = str(tmp_path / "u.txt")
     corpora.gen_synthetic(corpus, 5_500_000, 78, "mixed")
+    if long_word:
+        data = open(corpus, "rb").read()
+        at = data.index(b"\n", 900_000) + 1
+        open(corpus, "wb").write(data[:at] + b"ab" * 1_250_000 + b"\n" + data[at:])
     outs = []
     for gpu in (0, 1):
         t = _trainer(vocab_size=2000, unk_id=0, character_coverage=0.9995, min_pair_freq=2)
