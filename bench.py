@@ -528,9 +528,11 @@ def tiebreak_report(st, merges, elapsed, args, out_prefix):
         pos = end + 1
     n = max(1, st["sel_merges"])
     return {
-        "mode": "device: every merge selected on the GPU inside k_word_loop<true> (pair table + frontier argmax, "
-                "ties to the smaller pair key); NOT the reference's merge order",
-        "merges_per_s": merges / elapsed, "sel_merges": st["sel_merges"], "launches": st["sel_launches"],
+        "mode": "device: merges selected by the largest pair count, ties to the smaller pair key -- the early ones "
+                "on the host from exact counts while the whole-chip resident loop merges, then every merge on the GPU "
+                "inside k_word_loop<true> (pair table + frontier argmax); NOT the reference's merge order",
+        "merges_per_s": merges / elapsed, "sel_merges": st["sel_merges"], "host_phase_merges": st["sel_host_merges"],
+        "launches": st["sel_launches"],
         "rebuilds": st["sel_rebuilds"], "rebuild_ms": st["sel_rebuild_ms"], "kernel_ms": st["sel_kernel_ms"],
         "device_select_us_per_merge": st["sel_select_us"] / n, "device_merge_us_per_merge": st["sel_merge_us"] / n,
         "table_pairs": st["sel_table_pairs"], "table_slots": st["sel_table_slots"],

@@ -202,6 +202,8 @@ typedef struct ShredStats {
   double sel_merge_us;         /* device: Σ time merging and updating the pair table */
   uint64_t sel_table_pairs;    /* pairs in the device pair table at the end */
   uint64_t sel_table_slots;    /* its capacity */
+  uint64_t sel_host_merges;    /* tiebreak=device: early merges selected on the host by the same rule
+                                  (exact counts) while the whole-chip resident loop runs them */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -3360,6 +3360,12 @@ int Device::device_select(const std::vector<PairCount>& pairs, int32_t X0, int n
   HIP_OK(hipSetDevice(ordinal_));
   park();
   if (!wl_ || !wl_->ready() || exchange_ || layout_ != Layout::kTypes || !index_on_) return -1;
+  if (switch_pending_ || hybrid_resident_phase()) {  // the resident phase ends here (its tiles are current)
+    switch_pending_ = false;
+    idx_phase_ = true;
+    switch_x_ = X0;
+    words_stale_ = true;
+  }
   if (words_stale_) index_refresh();  // the words from the tiles (a tile-path merge, or a reset)
   const int r = wl_->run_select(pairs, X0, (uint32_t)std::max(n, 0), min_freq, out);
   if (r > 0) {

@@ -445,6 +445,10 @@ static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool
       if (why) *why = "the text holds NUL bytes";
       return false;
     }
+    if (report && (meta[4] || meta[5] || meta[7]))
+      std::fprintf(stderr, "[LOAD] count attempt %d over %zu bytes repeated:%s%s%s (%.1f ms)\n", attempt, n,
+                   meta[4] ? " table too full" : "", meta[5] ? " key collision" : "",
+                   meta[7] ? " a word past a segment's landed bytes" : "", 1e3 * (t2 - t1));
     if (meta[4]) {  // too full: a bigger table
       if (cap >= (1ull << 29)) break;
       cap <<= 2;

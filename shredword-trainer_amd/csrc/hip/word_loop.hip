@@ -1175,6 +1175,7 @@ WordLoop::WordLoop(int ordinal, void* stream, int32_t unk_id) : ordinal_(ordinal
   // the idle bound (polls without a command before the launch ends itself); tests shrink it to
   // race the time-out against the posts
   if (const char* e = std::getenv("SHREDWORD_WL_IDLE_POLLS")) idle_polls_ = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char* e = std::getenv("SHREDWORD_SELECT_REPORT")) sel_report_ = std::atoi(e) != 0;
   for (auto& e : ev_) {
     hipEvent_t ev;
     WL_OK(hipEventCreate(&ev));
@@ -1878,6 +1879,10 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
         std::fprintf(stderr, "[ERROR]\t k_word_loop<true>: error code %u\n", ds[kStError]);
         fatal("tiebreak=device merge loop failed");
       }
+      if (sel_report_)
+        std::fprintf(stderr, "[SELECT] launch %llu: merges %u..%u in %.3f ms (%.2f us/merge), status %u, table %u\n",
+                     (unsigned long long)sst_.launches, m, st[kSelM], ms,
+                     st[kSelM] > m ? 1e3 * ms / (st[kSelM] - m) : 0.0, st[kSelStatus], st[kSelIns]);
       m = st[kSelM];
       const uint32_t status = st[kSelStatus];
       if (status == kSelDone) break;

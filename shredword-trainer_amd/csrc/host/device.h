@@ -82,6 +82,8 @@ class Device : public Backend {
   // tiebreak=device on the indexed loop (WordLoop::run_select).
   int device_select(const std::vector<PairCount>& pairs, int32_t X0, int n, uint64_t min_freq,
                     std::vector<SelectedMerge>* out) override;
+  // The early merges run on the whole-chip resident loop (host-selected) until the hybrid switch.
+  bool device_select_now() const override { return !hybrid_resident_phase() || switch_pending_; }
   // Multi-GPU: every launch's compacted records are all-gathered (fixed buckets of
   // `bucket_records` records per rank, RCCL over xGMI, queued behind k_merge on the stream);
   // collect() then returns the concatenation of all ranks' records, which the host combines

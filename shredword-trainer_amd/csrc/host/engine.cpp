@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <string>
+#include <unordered_map>
 
 #include "common.h"
 
@@ -223,11 +224,102 @@ int Engine::train_device(Backend& be, double t0) {
   int n = 0;
   std::vector<SelectedMerge> sm;
   const int32_t X0 = kBaseVocab + (int32_t)merge_a_.size();
+  bool exhausted = false;
+  if (target > 0 && !be.device_select_now()) {
+    // The early merges, while the backend's whole-chip loop serves them better than the one
+    // workgroup of the device selector: the same rule (largest count, ties to the smaller key)
+    // over exact host counts kept by each merge's delta records, then the device takes over
+    // with those counts as its table.
+    be.reserve_ids(X0 + target);
+    std::unordered_map<uint64_t, uint64_t> cnt;
+    cnt.reserve(2 * pairs.size() + 1024);
+    // lazy max-heap on (count, ~key): an entry is live while its count is the pair's count
+    std::vector<std::pair<uint64_t, uint64_t>> heap;
+    heap.reserve(pairs.size());
+    for (const PairCount& p : pairs) {
+      const uint64_t k = pack_pair(p.a, p.b);
+      cnt[k] = p.count;
+      if (p.count >= min_freq_ && p.count > 0) heap.push_back({p.count, ~k});
+    }
+    std::make_heap(heap.begin(), heap.end());
+    while (n < target && !be.device_select_now()) {
+      uint64_t best = 0, bk = 0;
+      bool found = false;
+      while (!heap.empty()) {
+        std::pop_heap(heap.begin(), heap.end());
+        const auto top = heap.back();
+        heap.pop_back();
+        const uint64_t k = ~top.second;
+        const auto it = cnt.find(k);
+        if (it == cnt.end() || it->second != top.first) continue;  // stale
+        best = top.first;
+        bk = k;
+        found = true;
+        break;
+      }
+      if (!found) {
+        exhausted = true;
+        break;
+      }
+      const int32_t a = pair_first(bk), b = pair_second(bk), X = X0 + n;
+      be.merge_scan(a, b, X);
+      const DeltaRecord* recs = nullptr;
+      const size_t nr = be.collect(X, &recs);
+      for (size_t i = 0; i < nr; ++i) {
+        const uint32_t cat = recs[i].key & 3u, slot = recs[i].key >> 2;
+        const int32_t id = slot == 0 ? unk_ : (int32_t)(slot - 1);
+        int32_t f, s;
+        switch (cat) {
+          case kOldLeft: f = id; s = a; break;
+          case kNewLeft: f = id; s = X; break;
+          case kOldRight: f = b; s = id; break;
+          default: f = X; s = id; break;
+        }
+        if ((f == a && s == b) || f == unk_ || s == unk_) continue;
+        uint64_t& v = cnt[pack_pair(f, s)];
+        if (cat == kOldLeft || cat == kOldRight)
+          v = v >= recs[i].sum ? v - recs[i].sum : 0;
+        else
+          v += recs[i].sum;
+        if (v >= min_freq_ && v > 0) {
+          heap.push_back({v, ~pack_pair(f, s)});
+          std::push_heap(heap.begin(), heap.end());
+        }
+      }
+      cnt[bk] = 0;
+      sm.push_back(SelectedMerge{a, b, best});
+      ++n;
+    }
+    pairs.clear();
+    for (const auto& kv : cnt)
+      if (kv.second) pairs.push_back(PairCount{pair_first(kv.first), pair_second(kv.first), kv.second, 0});
+    std::sort(pairs.begin(), pairs.end(), [](const PairCount& x, const PairCount& y) {
+      return pack_pair(x.a, x.b) < pack_pair(y.a, y.b);
+    });
+    host_phase_merges_ += (uint64_t)n;
+    if (verify_every_ > 0 && n > 0 && !exhausted) {  // the host counts must be the corpus's
+      std::vector<PairCount> fresh;
+      be.count_pairs(unk_, &fresh);
+      std::sort(fresh.begin(), fresh.end(), [](const PairCount& x, const PairCount& y) {
+        return pack_pair(x.a, x.b) < pack_pair(y.a, y.b);
+      });
+      bool same = fresh.size() == pairs.size();
+      for (size_t i = 0; same && i < fresh.size(); ++i)
+        same = fresh[i].a == pairs[i].a && fresh[i].b == pairs[i].b && fresh[i].count == pairs[i].count;
+      ++verify_checks_;
+      if (!same) {
+        if (!verify_fail_)
+          std::fprintf(stderr, "[ERROR]\t tiebreak=device: the host counts after %d merges differ from a fresh K1\n", n);
+        ++verify_fail_;
+      }
+    }
+  }
   // verify_argmax = k: the device selects k merges at a time from a table rebuilt from a fresh
   // K1 count; the first merge of each chunk must be that count's maximum (ties: the smaller key)
   const int chunk = verify_every_ > 0 ? verify_every_ : target;
-  while (n < target) {
-    if (n > 0) {
+  const int n_host = n;
+  while (n < target && !exhausted) {
+    if (n > n_host) {
       pairs.clear();
       be.count_pairs(unk_, &pairs);
     }

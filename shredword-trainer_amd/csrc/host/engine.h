@@ -50,6 +50,10 @@ class Backend {
                             std::vector<SelectedMerge>* out) {
     return -1;
   }
+  // False while the backend's own loop serves merges better than device_select (the device's
+  // whole-chip resident phase, before its switch to the indexed loop): train() in
+  // tiebreak=device selects those merges on the host by the same rule (exact counts).
+  virtual bool device_select_now() const { return true; }
   // K5 check (debug): a fresh K1 over the current corpus reduced to the largest pair count
   // (*max_freq) and the count of (a, b) (*ab_freq).  Default: reduced on the host.
   virtual void pair_max(int32_t unk_id, int32_t a, int32_t b, uint64_t* max_freq, uint64_t* ab_freq) {
@@ -121,6 +125,7 @@ class Engine {
   bool tiebreak_device() const { return tiebreak_device_; }
   uint64_t verify_checks() const { return verify_checks_; }
   uint64_t verify_failures() const { return verify_fail_; }
+  uint64_t host_phase_merges() const { return host_phase_merges_; }  // tiebreak=device, selected on the host
   void finish_speculation(Backend& be);  // rolls back unconfirmed guesses (before any other access)
   uint64_t spec_hits() const { return spec_hits_; }
   uint64_t spec_misses() const { return spec_misses_; }
@@ -159,6 +164,7 @@ class Engine {
   bool early_guess_ = true;
   uint64_t corrections_ = 0;
   uint64_t verify_checks_ = 0, verify_fail_ = 0;
+  uint64_t host_phase_merges_ = 0;
   size_t probe_k_ = 0, probe_window_ = 256;
   std::vector<std::vector<int32_t>> chain_log_;
   // SHREDWORD_ENGINE_TRACE=<path>: per merge (hit, select, launch, wait, apply µs, records),

@@ -512,6 +512,7 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
   s->num_symbols = t->wt.num_symbols();
   s->num_occurrences = t->wt.total_occurrences;
   s->num_merges = t->engine.num_merges();
+  s->sel_host_merges = t->engine.host_phase_merges();
   s->heap_size = t->engine.selector().heap_size();
   const Selector::Counters& c = t->engine.selector().counters();
   s->heap_pops = c.pops;

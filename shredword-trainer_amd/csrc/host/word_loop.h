@@ -223,6 +223,7 @@ class WordLoop {
   void* status_dev_ = nullptr;
   uint32_t seq_ = 0;
   uint32_t idle_polls_ = 1u << 22;  // ~10 s without a command: the launch ends itself (relaunched on demand)
+  bool sel_report_ = false;         // SHREDWORD_SELECT_REPORT=1: one stderr line per k_word_loop<true> launch
   std::vector<Post> posted_;
   // tiebreak=device: pair table, frontier, state (see word_loop.hip SelParams)
   void sel_free();

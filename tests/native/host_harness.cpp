@@ -251,8 +251,14 @@ class EmuBackend : public Backend {
     }
     recs_ = std::move(pd.recs);
     *recs = recs_.data();
+    if (phase_left_ > 0) --phase_left_;
     return recs_.size();
   }
+
+  // The device's resident phase, emulated: the first `k` merges of each tiebreak=device train()
+  // are selected on the host (Engine::train_device) before device_select takes over.
+  void set_device_phase(int k) { phase_ = phase_left_ = k < 0 ? 0 : k; }
+  bool device_select_now() const override { return phase_left_ == 0; }
 
   void token_freq(size_t T, std::vector<uint64_t>* freq) override {
     freq->assign(T, 0);
@@ -274,6 +280,7 @@ class EmuBackend : public Backend {
   // (count desc, key asc; each merge's records fold into the counts, the merged pair drops to 0).
   int device_select(const std::vector<PairCount>& pairs, int32_t X0, int n, uint64_t min_freq,
                     std::vector<SelectedMerge>* out) override {
+    phase_left_ = phase_;  // the next train() starts with its host phase again
     std::unordered_map<uint64_t, uint64_t> cnt;
     for (const PairCount& p : pairs) cnt[pack_pair(p.a, p.b)] += p.count;
     const int32_t unk = unk_;
@@ -313,6 +320,7 @@ class EmuBackend : public Backend {
   Layout layout_;
   uint32_t cap_;
   int32_t unk_ = 0;
+  int phase_ = 0, phase_left_ = 0;
   TiledStream ts_;
   TileIndex index_;
   uint64_t visited_ = 0;
@@ -417,6 +425,11 @@ int hh_load(void* p, const char* path) {
 
 void hh_set_early_guess(void* p, int on) { ((Harness*)p)->engine.set_early_guess(on != 0); }
 void hh_set_tiebreak_device(void* p, int on) { ((Harness*)p)->engine.set_tiebreak_device(on != 0); }
+void hh_set_device_phase(void* p, int k) {
+  Harness* h = (Harness*)p;
+  if (h->be) h->be->set_device_phase(k);
+}
+uint64_t hh_host_phase_merges(void* p) { return ((Harness*)p)->engine.host_phase_merges(); }
 
 void hh_count(void* p) {
   Harness* h = (Harness*)p;

@@ -64,7 +64,7 @@ def test_tiebreak_device_matches_its_cpu_rule(name, case_corpus, tmp_path):
     assert trace == ot
     assert model == om
     assert vocab == ov
-    assert st["sel_merges"] == n and (n == 0 or st["sel_launches"] >= 1)
+    assert st["sel_merges"] + st["sel_host_merges"] == n and (st["sel_merges"] == 0 or st["sel_launches"] >= 1)
     assert st["heap_size"] == 0  # the host heap took no part
 
 

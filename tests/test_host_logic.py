@@ -158,20 +158,25 @@ TIEBREAK_CASES = ["small_v300", "adv_unk0", "adv_unk3_cov09", "ascii1m_unk7_cov0
                   "utf8_2m_v2000_mpf50", "ascii1m_unkm1_mpf2"]
 
 
+@pytest.mark.parametrize("phase", [0, 7, 100000])
 @pytest.mark.parametrize("name", TIEBREAK_CASES)
-def test_tiebreak_device_host_logic_matches_oracle_rule(name, hh, case_corpus, oracle_bin, tmp_path):
+def test_tiebreak_device_host_logic_matches_oracle_rule(name, phase, hh, case_corpus, oracle_bin, tmp_path):
     """tiebreak=device (opt-in, not the reference's order): the Engine's device-selection path over
     the emulated kernels (EmuBackend::device_select: the pair-table rule of k_word_loop<true>)
     against the oracle's restatement of the same rule (bpe_oracle --tiebreak-device 0: largest
-    count, ties to the smaller key, every count the reference's): the same merges and files."""
+    count, ties to the smaller key, every count the reference's): the same merges and files.
+    `phase`: the first merges selected on the host by the same rule (the device's resident phase,
+    Engine::train_device) -- none, 7, or every merge."""
     import subprocess
     case, corpus = case_corpus(name)
     cfg = case["config"]
     h = hostharness.open_case(hh, corpus, cfg, "types")
     try:
         hh.hh_set_tiebreak_device(h, 1)
+        hh.hh_set_device_phase(h, phase)
         trace = str(tmp_path / "t.txt")
         merges = hh.hh_train(h, trace.encode())
+        assert hh.hh_host_phase_merges(h) == min(phase, merges)
         m, v = str(tmp_path / "h.model"), str(tmp_path / "h.vocab")
         hh.hh_save(h, m.encode(), v.encode(), 1)
     finally:
