@@ -3365,6 +3365,7 @@ int Device::device_select(const std::vector<PairCount>& pairs, int32_t X0, int n
     idx_phase_ = true;
     switch_x_ = X0;
     words_stale_ = true;
+    wl_->reserve(std::max(X0 + n, reserved_max_id_));  // as hybrid_switch: the id tables before the index
   }
   if (words_stale_) index_refresh();  // the words from the tiles (a tile-path merge, or a reset)
   const int r = wl_->run_select(pairs, X0, (uint32_t)std::max(n, 0), min_freq, out);

@@ -242,6 +242,7 @@ int Engine::train_device(Backend& be, double t0) {
       if (p.count >= min_freq_ && p.count > 0) heap.push_back({p.count, ~k});
     }
     std::make_heap(heap.begin(), heap.end());
+    std::unordered_map<uint64_t, int64_t> net;
     while (n < target && !be.device_select_now()) {
       uint64_t best = 0, bk = 0;
       bool found = false;
@@ -265,6 +266,10 @@ int Engine::train_device(Backend& be, double t0) {
       be.merge_scan(a, b, X);
       const DeltaRecord* recs = nullptr;
       const size_t nr = be.collect(X, &recs);
+      // one net delta per pair first: a pair can take both signs in one merge ((X, a) of
+      // "a b a b": -w as the second occurrence's left pair, +w as the first's right pair), and
+      // the records come in any order
+      net.clear();
       for (size_t i = 0; i < nr; ++i) {
         const uint32_t cat = recs[i].key & 3u, slot = recs[i].key >> 2;
         const int32_t id = slot == 0 ? unk_ : (int32_t)(slot - 1);
@@ -276,13 +281,15 @@ int Engine::train_device(Backend& be, double t0) {
           default: f = X; s = id; break;
         }
         if ((f == a && s == b) || f == unk_ || s == unk_) continue;
-        uint64_t& v = cnt[pack_pair(f, s)];
-        if (cat == kOldLeft || cat == kOldRight)
-          v = v >= recs[i].sum ? v - recs[i].sum : 0;
-        else
-          v += recs[i].sum;
+        const int64_t d = (cat == kOldLeft || cat == kOldRight) ? -(int64_t)recs[i].sum : (int64_t)recs[i].sum;
+        net[pack_pair(f, s)] += d;
+      }
+      for (const auto& kd : net) {
+        if (kd.second == 0) continue;
+        uint64_t& v = cnt[kd.first];
+        v = kd.second < 0 ? (v >= (uint64_t)(-kd.second) ? v - (uint64_t)(-kd.second) : 0) : v + (uint64_t)kd.second;
         if (v >= min_freq_ && v > 0) {
-          heap.push_back({v, ~pack_pair(f, s)});
+          heap.push_back({v, ~kd.first});
           std::push_heap(heap.begin(), heap.end());
         }
       }

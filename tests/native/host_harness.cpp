@@ -1,3 +1,4 @@
+#include <algorithm>
 // Test-only harness: the product's host code (corpus loader, tile packing, Engine, Selector)
 // driven by a CPU emulation of the device kernels, so the host logic and the multi-rank exchange
 // can be checked without a GPU.  NOT part of the product library (built into
@@ -250,6 +251,9 @@ class EmuBackend : public Backend {
       std::fflush(rec_);
     }
     recs_ = std::move(pd.recs);
+    // with a host phase set, the records come newest-first: the device's order is arbitrary
+    // (workgroups, spills), so the host side must not depend on it
+    if (phase_ > 0) std::reverse(recs_.begin(), recs_.end());
     *recs = recs_.data();
     if (phase_left_ > 0) --phase_left_;
     return recs_.size();
