@@ -120,6 +120,22 @@ constexpr int kSelM = 0, kSelNF = 1, kSelBuf = 2, kSelStatus = 3, kSelIns = 4, k
 constexpr int kSelWords = kSelStats + 2 * 6;  // st: 6 words, then 6 u64 statistics
 // exit status: merges done (target reached / below min_pair_freq), frontier to rebuild, table full
 constexpr uint32_t kSelDone = 1, kSelRebuild = 2, kSelFull = 3;
+// The frontier lives in LDS for the whole launch: each entry's count follows the table's (the
+// merge's records add to both; inf[slot] = LDS position + 1), so a select is an LDS scan.  A
+// rebuild picks kSelK entries; merges append, and past kSelF - kSelRoom the dead ones (below the
+// threshold, or merged) are compacted away in LDS.
+constexpr uint32_t kSelF = 1536, kSelK = 1024, kSelRoom = 384;
+constexpr uint32_t kInfReserved = 0xFFFFFFFFu;  // a slot being appended
+template <bool kOn>
+struct SelLds {  // k_word_loop<false>: none
+  u64 key[1], cnt[1];
+  uint32_t slot[1], n;
+};
+template <>
+struct SelLds<true> {
+  u64 key[kSelF], cnt[kSelF];
+  uint32_t slot[kSelF], n;
+};
 
 struct WlParams {
   int32_t* wtok;
@@ -195,8 +211,8 @@ __device__ __forceinline__ u64 sel_slot(const SelParams& q, u64 pk) {
 // One combined record of merge (a, b) -> X as a change of a pair's count (the reference's
 // FreqChangeMap entry, bpe.cpp:297-313, minus the pair merged and pairs holding unk).  New pairs
 // (categories 1 and 3: they hold X) are listed for the frontier.
-__device__ __forceinline__ void sel_apply(const SelParams& q, uint32_t* nnew, int32_t unk, uint32_t cap, uint32_t key,
-                                          u64 sum, int32_t a, int32_t b, int32_t X) {
+__device__ __forceinline__ void sel_apply(const SelParams& q, SelLds<true>& F, uint32_t* nnew, int32_t unk, uint32_t cap,
+                                          uint32_t key, u64 sum, int32_t a, int32_t b, int32_t X) {
   const uint32_t sl = key >> 2, cat = key & 3u;
   const int32_t id = sl == 0 ? unk : (int32_t)(sl - 1u);
   if (id == unk || sum == 0) return;
@@ -205,7 +221,10 @@ __device__ __forceinline__ void sel_apply(const SelParams& q, uint32_t* nnew, in
   if (f == a && g == b) return;
   const u64 h = sel_slot(q, pair_key(f, g));
   if (h == ~0ull) return;
-  atomicAdd(q.pcnt + h, (cat & 1u) ? sum : (u64)(-(int64_t)sum));
+  const u64 d = (cat & 1u) ? sum : (u64)(-(int64_t)sum);
+  atomicAdd(q.pcnt + h, d);
+  const uint32_t pos = ld_agent(q.inf + h) - 1u;  // in the frontier: its LDS count too
+  if (pos < kSelF) atomicAdd(reinterpret_cast<unsigned long long*>(&F.cnt[pos]), (unsigned long long)d);
   if (cat & 1u) q.upd[atomicAdd(nnew, 1u)] = (uint32_t)h;
   (void)cap;
 }
@@ -421,7 +440,7 @@ struct LoopS {
   u64 occ, t[2];
   u64 t_wait, t_idle, t_undo;  // s_memrealtime: this command's wait began; idle / undo since the last flag
   // tiebreak=device
-  uint32_t sm, snf, sbuf, snk, snew, status;
+  uint32_t sm, snk, snew, status, sel_pos, sover, scompact;
   u64 sel_slot;
   u64 bc[kWlThreads / 64], bk[kWlThreads / 64];
   uint32_t bs[kWlThreads / 64];
@@ -438,6 +457,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   __shared__ DeltaH s_h;
   __shared__ LoopS S;
   __shared__ u64 s_q[kQ];  // the listed entries that pass the filter, merged densely
+  __shared__ SelLds<kSelf> s_f;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t tid = threadIdx.x;
   int32_t* const mys = s_strip + tid;
@@ -449,52 +469,51 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   uint32_t expect = p.seq0;
   uint32_t exit_op = kOpStop;
   const MergeCtx mc{&S.nspill};
+  if constexpr (kSelf) {  // the rebuilt frontier into LDS, each slot told its position
+    const SelParams& q = p.sel;
+    const uint32_t nf = min(ld_agent(q.st + kSelNF), kSelK);
+    for (uint32_t i = tid; i < nf; i += kWlThreads) {
+      const uint32_t sl = ld_agent(q.fr[0] + i);
+      s_f.slot[i] = sl;
+      s_f.key[i] = ld_agent64(q.pkey + sl);
+      s_f.cnt[i] = ld_agent64(q.pcnt + sl);
+      __hip_atomic_store(q.inf + sl, i + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0) {
+      s_f.n = nf;
+      S.scompact = 0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
   for (;;) {
     if constexpr (kSelf) {
-      // ---- tiebreak=device: the best live frontier entry is the merge (count desc, key asc);
-      // the entries still at or above the threshold are kept in the other buffer
+      // ---- tiebreak=device: the best live frontier entry (count desc, key asc; at or above the
+      // threshold) is the merge, by a scan of the LDS frontier
       const SelParams& q = p.sel;
       if (tid == 0) {
         S.sm = ld_agent(q.st + kSelM);
-        S.snf = ld_agent(q.st + kSelNF);
-        S.sbuf = ld_agent(q.st + kSelBuf);
         S.snk = 0;
         S.status = 0;
         S.t_wait = __builtin_amdgcn_s_memrealtime();
       }
       __syncthreads();
-      const uint32_t nf = S.snf, buf = S.sbuf;
+      const uint32_t nf = min(s_f.n, kSelF);
       const u64 tc = q.thr[0], tk = q.thr[1];
-      const uint32_t* fi = q.fr[buf];
-      uint32_t* fo = q.fr[buf ^ 1u];
       u64 bc = 0, bk = kEmpty64;
-      uint32_t bs = kEmpty32;
-      for (uint32_t i0 = 0; i0 < nf; i0 += kWlThreads) {
-        const uint32_t i = i0 + tid;
-        bool keep = false;
-        u64 c = 0, k = kEmpty64;
-        uint32_t sl = 0;
-        if (i < nf) {
-          sl = ld_agent(fi + i);
-          c = ld_agent64(q.pcnt + sl);
-          k = ld_agent64(q.pkey + sl);
-          keep = sel_at_least(c, k, tc, tk);
-        }
-        if (keep && sel_better(c, k, bc, bk)) {
-          bc = c;
-          bk = k;
-          bs = sl;
-        }
-        const u64 bl = __ballot(keep);
-        if (bl) {
-          const int lead = __ffsll((long long)bl) - 1;
-          uint32_t base = 0;
-          if (lane == lead) base = atomicAdd(&S.snk, (uint32_t)__popcll(bl));
-          base = __shfl(base, lead, 64);
-          if (keep) fo[base + (uint32_t)__popcll(bl & ((1ull << lane) - 1ull))] = sl;
+      uint32_t bs = kEmpty32, live = 0;
+      for (uint32_t i = tid; i < nf; i += kWlThreads) {
+        const u64 c = s_f.cnt[i], k = s_f.key[i];
+        if (sel_at_least(c, k, tc, tk)) {
+          ++live;
+          if (sel_better(c, k, bc, bk)) {
+            bc = c;
+            bk = k;
+            bs = i;
+          }
         }
       }
+      if (__ballot(live != 0) && lane == 0) atomicAdd(&S.snk, 1u);
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) {
         const u64 c2 = __shfl_xor(bc, d, 64), k2 = __shfl_xor(bk, d, 64);
@@ -534,11 +553,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           S.cmd[5] = expect;
           S.cmd[6] = 0;  // no list given: the loop looks it up
           S.cmd[7] = 0;
-          S.sel_slot = bs;
+          S.sel_pos = bs;
+          S.sel_slot = s_f.slot[bs];
           q.out[2 * (u64)m] = bk;
           q.out[2 * (u64)m + 1] = bc;
-          q.st[kSelNF] = S.snk;  // the kept entries are the frontier now
-          q.st[kSelBuf] = buf ^ 1u;
         }
       }
     } else if (wid == 0) {
@@ -812,33 +830,96 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       __syncthreads();
       for (int i = tid; i < kDh; i += kWlThreads) {
         const uint32_t key = s_h.key[i];
-        if (key != kEmpty32) sel_apply(q, &S.snew, p.unk, p.cap, key, s_h.sum[i], a, b, X);
+        if (key != kEmpty32) sel_apply(q, s_f, &S.snew, p.unk, p.cap, key, s_h.sum[i], a, b, X);
       }
       const uint32_t nsp = S.nspill;
       for (uint32_t i = tid; i < nsp; i += kWlThreads) {
         const uint32_t key = p.dlist[i];
         const u64 sum = atomicExch(&p.dsum[key], 0ull);
         atomicExch(&p.dft[key], kEmpty64);
-        sel_apply(q, &S.snew, p.unk, p.cap, key, sum, a, b, X);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(q.pcnt + S.sel_slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const u64 tc = q.thr[0], tk = q.thr[1];
-      uint32_t* fo = q.fr[S.sbuf ^ 1u];
-      const uint32_t nnew = S.snew;
-      for (uint32_t i = tid; i < nnew; i += kWlThreads) {
-        const uint32_t sl = q.upd[i];
-        const u64 c = ld_agent64(q.pcnt + sl), k = ld_agent64(q.pkey + sl);
-        if (sel_at_least(c, k, tc, tk) && atomicCAS(q.inf + sl, 0u, 1u) == 0u) {
-          const uint32_t pos = atomicAdd(&S.snk, 1u);
-          if (pos < q.fcap) fo[pos] = sl;
-        }
+        sel_apply(q, s_f, &S.snew, p.unk, p.cap, key, sum, a, b, X);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        q.st[kSelNF] = S.snk < q.fcap ? S.snk : q.fcap;
+        __hip_atomic_store(q.pcnt + S.sel_slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_f.cnt[S.sel_pos] = 0;
+        S.sover = 0;
+      }
+      const u64 tc = q.thr[0], tk = q.thr[1];
+      const uint32_t nnew = S.snew;
+      for (uint32_t i = tid; i < nnew; i += kWlThreads) {
+        const uint32_t sl = q.upd[i];
+        const u64 c = ld_agent64(q.pcnt + sl), k = ld_agent64(q.pkey + sl);
+        if (sel_at_least(c, k, tc, tk) && atomicCAS(q.inf + sl, 0u, kInfReserved) == 0u) {
+          const uint32_t pos = atomicAdd(&s_f.n, 1u);
+          if (pos < kSelF) {
+            s_f.slot[pos] = sl;
+            s_f.key[pos] = k;
+            s_f.cnt[pos] = c;
+            __hip_atomic_store(q.inf + sl, pos + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            S.sover = 1;  // the frontier lost an entry: rebuild
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      // past kSelF - kSelRoom entries: the dead ones go (in place, order kept), the rest are told
+      // their new positions
+      if (!S.sover && s_f.n > kSelF - kSelRoom) {
+        constexpr int kPer = (int)((kSelF + kWlThreads - 1) / kWlThreads);
+        const uint32_t n0 = s_f.n;
+        u64 ck[kPer], kk[kPer];
+        uint32_t sk[kPer];
+        uint32_t mine = 0, keepm = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {  // thread t holds entries kPer*t .. kPer*t + kPer-1
+          const uint32_t i = (uint32_t)kPer * tid + (uint32_t)j;
+          ck[j] = 0;
+          kk[j] = kEmpty64;
+          sk[j] = 0;
+          if (i < n0) {
+            ck[j] = s_f.cnt[i];
+            kk[j] = s_f.key[i];
+            sk[j] = s_f.slot[i];
+            if (sel_at_least(ck[j], kk[j], tc, tk)) {
+              keepm |= 1u << j;
+              ++mine;
+            }
+          }
+        }
+        const uint32_t incl = wave_incl_add(mine);
+        if (lane == 63) S.bs[wid] = incl;  // wave totals
+        __syncthreads();
+        uint32_t base = incl - mine;
+        for (int w = 0; w < wid; ++w) base += S.bs[w];
+        uint32_t tot = 0;
+        for (int w = 0; w < kWlThreads / 64; ++w) tot += S.bs[w];
+        __syncthreads();  // every entry is in registers before any is moved
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const uint32_t i = (uint32_t)kPer * tid + (uint32_t)j;
+          if (i >= n0) continue;
+          if ((keepm >> j) & 1u) {
+            s_f.cnt[base] = ck[j];
+            s_f.key[base] = kk[j];
+            s_f.slot[base] = sk[j];
+            __hip_atomic_store(q.inf + sk[j], base + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ++base;
+          } else {
+            __hip_atomic_store(q.inf + sk[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          s_f.n = tot;
+          ++S.scompact;
+        }
+      }
+      if (tid == 0) {
+        q.st[kSelNF] = min(s_f.n, kSelF);
         q.st[kSelM] = S.sm + 1u;
         // statistics (st words 6..): select ticks, merge ticks (u64 each), listed / changed words,
         // occurrences (u64), new pairs
@@ -850,10 +931,11 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         t64[3] += nchg;
         t64[4] += S.occ;
         t64[5] += nnew;
-        // after a complete merge: a frontier past its capacity lost entries (rebuild), a table past
-        // its fill bound must grow (the host stops)
+        q.st[kSelBuf] = S.scompact;  // (statistic: LDS compactions of this launch)
+        // after a complete merge: a frontier that lost an entry needs a rebuild, a table past its
+        // fill bound must grow (the host stops)
         const uint32_t full = ld_agent(q.st + kSelIns) > q.fill_max || ld_agent(q.st + kSelErr) != 0;
-        S.status = full ? kSelFull : (S.snk > q.fcap ? kSelRebuild : 0u);
+        S.status = full ? kSelFull : (S.sover ? kSelRebuild : 0u);
       }
       __syncthreads();
       if (S.status) {
@@ -1675,7 +1757,6 @@ void WordLoop::sel_free() {
 // >= min_freq (all of them when few), their slots flagged; the threshold = the last one taken
 // (or, when every pair of the counts' top buckets was taken, the lowest count of those buckets).
 bool WordLoop::sel_rebuild(uint64_t min_freq) {
-  constexpr uint32_t kSelK = 4096;
   const double t0 = now_seconds();
   hipStream_t s = S(stream_);
   WL_OK(hipMemsetAsync(shist_, 0, kSelBuckets * sizeof(uint32_t), s));
@@ -1880,9 +1961,9 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
         fatal("tiebreak=device merge loop failed");
       }
       if (sel_report_)
-        std::fprintf(stderr, "[SELECT] launch %llu: merges %u..%u in %.3f ms (%.2f us/merge), status %u, table %u\n",
-                     (unsigned long long)sst_.launches, m, st[kSelM], ms,
-                     st[kSelM] > m ? 1e3 * ms / (st[kSelM] - m) : 0.0, st[kSelStatus], st[kSelIns]);
+        std::fprintf(stderr, "[SELECT] launch %llu: merges %u..%u in %.3f ms (%.2f us/merge), status %u, table %u, "
+                     "%u LDS compactions\n", (unsigned long long)sst_.launches, m, st[kSelM], ms,
+                     st[kSelM] > m ? 1e3 * ms / (st[kSelM] - m) : 0.0, st[kSelStatus], st[kSelIns], st[kSelBuf]);
       m = st[kSelM];
       const uint32_t status = st[kSelStatus];
       if (status == kSelDone) break;

@@ -263,6 +263,26 @@ int Engine::train_device(Backend& be, double t0) {
         break;
       }
       const int32_t a = pair_first(bk), b = pair_second(bk), X = X0 + n;
+      if (verify_every_ > 0 && n % verify_every_ == 0) {  // K5: the pick is a fresh K1's maximum
+        std::vector<PairCount> fresh;
+        be.count_pairs(unk_, &fresh);
+        uint64_t mc = 0, mk = ~0ull;
+        for (const PairCount& p : fresh) {
+          const uint64_t k = pack_pair(p.a, p.b);
+          if (p.count > mc || (p.count == mc && k < mk)) {
+            mc = p.count;
+            mk = k;
+          }
+        }
+        ++verify_checks_;
+        if (mc != best || mk != bk) {
+          if (!verify_fail_)
+            std::fprintf(stderr, "[ERROR]\t tiebreak=device check at merge %d (host phase): selected (%d,%d) freq=%llu, "
+                         "fresh K1 max (%d,%d) freq=%llu\n", n, a, b, (unsigned long long)best, pair_first(mk),
+                         pair_second(mk), (unsigned long long)mc);
+          ++verify_fail_;
+        }
+      }
       be.merge_scan(a, b, X);
       const DeltaRecord* recs = nullptr;
       const size_t nr = be.collect(X, &recs);
