@@ -20,6 +20,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -416,8 +417,8 @@ static bool count_table_alloc(CountTable* ct, u64 cap, hipStream_t st, std::stri
 // records are then not made).  pre: a table already counted (attempt 0, seed 0) or nullptr.
 static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool report, double t0, double t1,
                             std::vector<WordRec>* out, std::vector<uint8_t>* spell, bool* nul, std::string* why,
-                            CountTable* pre = nullptr) {
-  u64 cap = count_table_slots(n);
+                            CountTable* pre = nullptr, size_t table_n = 0) {
+  u64 cap = count_table_slots(std::max(n, table_n));
   const u64 kmask = count_key_mask();
   const CountShape shape = count_shape(n, cus);
   if (nul) *nul = false;
@@ -624,6 +625,14 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   const u64 seg_tiles = std::max<u64>(1, seg_bytes / shape.tile_bytes);
   const u64 nseg = (shape.ntiles + seg_tiles - 1) / seg_tiles;
   const bool overlap = !(oenv && oenv[0] == '0') && nseg > 1;
+  // A byte range of a larger file (a sharded load) holds about as many distinct words as the whole
+  // file (Heaps' law: a 5 GB half of C3 has all of its 1.25 M): its table is sized by the file,
+  // not by the range, or it overflows and the count runs twice.
+  size_t table_n = n;
+  {
+    struct stat sb;
+    if (fstat(fd, &sb) == 0 && sb.st_size > 0) table_n = std::max(n, (size_t)sb.st_size);
+  }
   std::vector<hipEvent_t> ev(nchunks, nullptr);
   for (size_t c = 0; c < nchunks; ++c) LOAD_OK(hipEventCreateWithFlags(&ev[c], hipEventDisableTiming));
   struct EventsGuard {
@@ -675,7 +684,7 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   CountTable pre;
   bool pre_ok = false;
   if (overlap) {
-    pre_ok = count_table_alloc(&pre, count_table_slots(n), st, why);
+    pre_ok = count_table_alloc(&pre, count_table_slots(table_n), st, why);
     size_t waited = 0;  // chunks [0, waited) are behind an event wait on st
     for (u64 k = 0; pre_ok && k < nseg; ++k) {
       const u64 tile0 = k * seg_tiles, tile1 = std::min(shape.ntiles, tile0 + seg_tiles);
@@ -709,7 +718,8 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
     std::fprintf(stderr, "[LOAD] phase file_to_hbm %.1f ms (%d readers, %zu MiB chunks, pread %.1f ms summed over "
                  "readers): %.1f GB/s%s\n", 1e3 * (t1 - t0), T, chunk >> 20, 1e-6 * (double)read_ns.load(),
                  (double)n / (t1 - t0) / 1e9, overlap ? "; the count ran on segments meanwhile" : "");
-  if (!count_on_device(db, n, st, cus, report, t0, t1, out, spell, nul, why, pre_ok ? &pre : nullptr)) return false;
+  if (!count_on_device(db, n, st, cus, report, t0, t1, out, spell, nul, why, pre_ok ? &pre : nullptr, table_n))
+    return false;
   if (base)
     for (WordRec& w : *out) w.first += base;  // file offsets
   return true;

@@ -90,7 +90,22 @@ def main():
     os.environ["SHREDWORD_BENCH_DIR"] = d
     path = bench.corpus_path(cfg, args.config)
     say(f"{args.config}: {cfg['bytes'] / 1e9:.0f} GB corpus in {d}")
-    gen_s = bench.ensure_corpus(cfg, path)
+    import threading
+    done = threading.Event()
+
+    def heartbeat():  # generation takes minutes: a line every 30 s keeps the run visibly alive
+        while not done.wait(30):
+            try:
+                say(f"generating: {os.path.getsize(path + '.part') / 1e9:.1f} GB written")
+            except OSError:
+                say("generating")
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    try:
+        gen_s = bench.ensure_corpus(cfg, path)
+    finally:
+        done.set()
+        hb.join()
     say(f"generated in {gen_s:.0f} s")
     env_shards = cfg.get("shards")
     if env_shards:
