@@ -117,7 +117,7 @@ struct SelParams {
 };
 // st words
 constexpr int kSelM = 0, kSelNF = 1, kSelBuf = 2, kSelStatus = 3, kSelIns = 4, kSelErr = 5, kSelStats = 6;
-constexpr int kSelWords = kSelStats + 2 * 6;  // st: 6 words, then 6 u64 statistics
+constexpr int kSelWords = kSelStats + 2 * 8;  // st: 6 words, then 8 u64 statistics
 // exit status: merges done (target reached / below min_pair_freq), frontier to rebuild, table full
 constexpr uint32_t kSelDone = 1, kSelRebuild = 2, kSelFull = 3;
 // The frontier lives in LDS for the whole launch: each entry's count follows the table's (the
@@ -819,6 +819,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       // ---- tiebreak=device: the records change the pair table; the pairs this merge created
       // that rank at or above the threshold join the frontier
       const SelParams& q = p.sel;
+      const u64 t_tab = __builtin_amdgcn_s_memrealtime();
       if (tid == 0) {
         if (X >= 0 && (uint32_t)X < p.id_cap) {
           p.lst[X] = (u64)top | ((u64)nchg << 32);
@@ -931,6 +932,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         t64[3] += nchg;
         t64[4] += S.occ;
         t64[5] += nnew;
+        t64[6] += now - t_tab;  // of t64[1]: the table and frontier update
+        t64[7] += S.scompact ? 1u : 0u;
         q.st[kSelBuf] = S.scompact;  // (statistic: LDS compactions of this launch)
         // after a complete merge: a frontier that lost an entry needs a rebuild, a table past its
         // fill bound must grow (the host stops)
@@ -1980,6 +1983,12 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
     sst_.changed += t64[3];
     sst_.occurrences += t64[4];
     sst_.new_pairs += t64[5];
+    sst_.table_us += 1e-2 * (double)t64[6];
+    if (sel_report_ && m)
+      std::fprintf(stderr, "[SELECT] %u merges: device select %.2f us, merge %.2f us (of it table + frontier %.2f us) "
+                   "per merge; %llu LDS compactions, %llu listed / %llu changed words\n", m, 1e-2 * (double)t64[0] / m,
+                   1e-2 * (double)t64[1] / m, 1e-2 * (double)t64[6] / m, (unsigned long long)t64[7],
+                   (unsigned long long)t64[2], (unsigned long long)t64[3]);
     sst_.table_pairs = st[kSelIns];
   }
   sst_.merges += m;

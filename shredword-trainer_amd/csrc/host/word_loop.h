@@ -66,6 +66,7 @@ struct SelectStats {
   uint64_t merges = 0, launches = 0, rebuilds = 0;
   double kernel_ms = 0, rebuild_ms = 0;  // launches of k_word_loop<true>; frontier rebuilds (host wall)
   double select_us = 0, merge_us = 0;    // device time: selecting, merging + table update (s_memrealtime)
+  double table_us = 0;                   // of merge_us: the pair table + frontier update
   uint64_t listed = 0, changed = 0, occurrences = 0, new_pairs = 0;
   uint64_t table_slots = 0, table_pairs = 0, frontier_max = 0;
 };
