@@ -122,9 +122,10 @@ constexpr int kSelWords = kSelStats + 2 * 8;  // st: 6 words, then 8 u64 statist
 constexpr uint32_t kSelDone = 1, kSelRebuild = 2, kSelFull = 3;
 // The frontier lives in LDS for the whole launch: each entry's count follows the table's (the
 // merge's records add to both; inf[slot] = LDS position + 1), so a select is an LDS scan.  A
-// rebuild picks kSelK entries; merges append, and past kSelF - kSelRoom the dead ones (below the
-// threshold, or merged) are compacted away in LDS.
-constexpr uint32_t kSelF = 1536, kSelK = 1024, kSelRoom = 384;
+// rebuild picks kSelK entries; merges append, and past kSelF - kSelSlack entries the dead ones
+// (below the threshold, or merged) are compacted away in LDS.  When more than kSelF - kSelRoom
+// stay live the launch ends for a rebuild (a compaction per merge would cost more).
+constexpr uint32_t kSelF = 1536, kSelK = 768, kSelRoom = 384, kSelSlack = 96;
 constexpr uint32_t kInfReserved = 0xFFFFFFFFu;  // a slot being appended
 template <bool kOn>
 struct SelLds {  // k_word_loop<false>: none
@@ -868,7 +869,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       __syncthreads();
       // past kSelF - kSelRoom entries: the dead ones go (in place, order kept), the rest are told
       // their new positions
-      if (!S.sover && s_f.n > kSelF - kSelRoom) {
+      if (!S.sover && s_f.n > kSelF - kSelSlack) {
         constexpr int kPer = (int)((kSelF + kWlThreads - 1) / kWlThreads);
         const uint32_t n0 = s_f.n;
         u64 ck[kPer], kk[kPer];
@@ -917,6 +918,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         if (tid == 0) {
           s_f.n = tot;
           ++S.scompact;
+          if (tot > kSelF - kSelRoom) S.sover = 1;  // mostly live: a rebuild, not a compaction per merge
         }
       }
       if (tid == 0) {
