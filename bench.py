@@ -306,9 +306,10 @@ def pmc_source(cfg_name, layout, kernel):
     return None
 
 
-def pmc_traffic(cfg_name, layout, kernel=None):
+def pmc_traffic(cfg_name, layout, kernel=None, all_launches=False):
     """Measured HBM bytes per launch of `kernel` (default k_merge) for this workload, from the
-    committed PMC summaries (profiles/*_<config>_<layout>*_pmc_traffic.json)."""
+    committed PMC summaries (profiles/*_<config>_<layout>*_pmc_traffic.json).  all_launches: the
+    sum over the profiled run's launches (the load's segmented count: one load = all of them)."""
     import glob
     if kernel is None:
         kernel = "k_merge<true>" if layout == "types" else "k_merge<false>"
@@ -317,7 +318,7 @@ def pmc_traffic(cfg_name, layout, kernel=None):
             k = json.load(open(path))["kernels"]
             ent = k.get(kernel)
             if ent:
-                return ent["hbm_bytes_per_launch"]
+                return ent["hbm_bytes_per_launch"] * (ent.get("launches", 1) if all_launches else 1)
         except (OSError, ValueError, KeyError):
             continue
     return None
@@ -818,7 +819,8 @@ def main():
                      "algorithmic_bytes": cfg["bytes"],
                      "load_s_max_over_ranks": load_s_max, "load_s_rank0": load_s,
                      "bytes_per_rank": cfg["bytes"] / world if one_job else cfg["bytes"],
-                     "traffic_bytes": pmc_traffic(args.config, args.layout, "k_word_count"),
+                     "traffic_bytes": pmc_traffic(args.config, args.layout, "k_word_count", all_launches=True),
+                     "traffic_source": pmc_source(args.config, args.layout, "k_word_count"),
                      "note": ("load_corpus: page-in + PCIe upload + device word count + host table; outside the timed "
                               "step" + ("; each rank counts its byte range, the word lists are all-gathered and "
                                         "merged on every rank" if one_job else ""))},
