@@ -3741,6 +3741,10 @@ size_t Device::collect(int32_t X, const DeltaRecord** recs) {
   return n;
 }
 
+bool Device::peek(int32_t X, const DeltaRecord** recs, size_t* n) {
+  return wl_ && wl_->in_flight() && wl_->peek(X, recs, n);
+}
+
 void Device::rollback(int32_t X) {
   HIP_OK(hipSetDevice(ordinal_));
   if (wl_ && wl_->in_flight()) {

@@ -1713,6 +1713,17 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   return n;
 }
 
+bool WordLoop::peek(int32_t X, const DeltaRecord** recs, size_t* n) const {
+  if (posted_.empty() || posted_.front().X != X) return false;
+  const Slot& sl = slot_[(uint32_t)X & (kSlots - 1)];
+  if (__atomic_load_n(sl.host_hdr + 1, __ATOMIC_ACQUIRE) != posted_.front().seq) return false;
+  const size_t k = sl.host_hdr[0];
+  if (k > sl.rec_cap) return false;  // collect() reports it
+  *recs = sl.host_recs;
+  *n = k;
+  return true;
+}
+
 void WordLoop::rollback(int32_t X) {
   while (!posted_.empty() && posted_.back().X >= X) {
     const Post pp = posted_.back();

@@ -98,6 +98,8 @@ class Device : public Backend {
   void set_exchange(const Exchange& x);
   // K4: merge X's records (host memory); the first collect of a chain waits for the launch.
   size_t collect(int32_t X, const DeltaRecord** recs) override;
+  // The indexed loop's finished merge X, without collecting it (Engine's apply helper).
+  bool peek(int32_t X, const DeltaRecord** recs, size_t* n) override;
   static constexpr int kChainMax = 8;
   int max_chain() const override {
     return speculate_ && !resident_eligible() && !index_eligible() ? kChainMax : 1;

@@ -32,8 +32,67 @@ void Engine::count_bigrams(Backend& be) {
                 sel_.heap_size(), (unsigned long long)min_freq_);
 }
 
+Engine::~Engine() { helper_stop(); }
+
+void Engine::helper_start() {
+  if (helper_ || !helper_on_) return;
+  helper_ = new Helper();
+  Helper* h = helper_;
+  const Selector* sel = &sel_;
+  h->th = std::thread([h, sel] {
+    unsigned idle = 0;
+    for (;;) {
+      const int st = h->state.load(std::memory_order_acquire);
+      if (st == 1) {
+        sel->prepare(h->a, h->b, h->X, h->recs, h->n, &h->out, h->pf, h->pfm);
+        h->state.store(2, std::memory_order_release);
+        idle = 0;
+      } else if (st == 3) {
+        return;
+      } else if (++idle < (1u << 20)) {
+        __builtin_ia32_pause();
+      } else {
+        std::this_thread::yield();
+      }
+    }
+  });
+}
+
+void Engine::helper_stop() {
+  if (!helper_) return;
+  helper_drain();
+  helper_->state.store(3, std::memory_order_release);
+  helper_->th.join();
+  delete helper_;
+  helper_ = nullptr;
+}
+
+void Engine::helper_drain() {
+  if (!helper_) return;
+  while (helper_->state.load(std::memory_order_acquire) == 1) __builtin_ia32_pause();
+  helper_->state.store(0, std::memory_order_relaxed);
+}
+
+void Engine::helper_offer(Backend& be) {
+  if (!helper_ || pending_.empty() || helper_->state.load(std::memory_order_acquire) != 0) return;
+  const Guess& g = pending_.front();
+  const DeltaRecord* recs = nullptr;
+  size_t n = 0;
+  if (!be.peek(g.X, &recs, &n)) return;
+  Helper* h = helper_;
+  h->a = g.a;
+  h->b = g.b;
+  h->X = g.X;
+  h->recs = recs;
+  h->n = n;
+  h->pf = sel_.table_base();
+  h->pfm = sel_.table_mask();
+  h->state.store(1, std::memory_order_release);
+}
+
 void Engine::finish_speculation(Backend& be) {
   if (pending_.empty()) return;
+  helper_drain();  // the helper may be reading a guess's records: done before they are undone
   be.rollback(pending_.front().X);
   pending_.clear();
   ++spec_misses_;
@@ -43,6 +102,7 @@ void Engine::finish_speculation(Backend& be) {
 // after the confirmed merges), so the next launch starts from the selected merge again.
 void Engine::verify_selection(Backend& be, int32_t a, int32_t b, uint64_t freq) {
   if (!pending_.empty()) {
+    helper_drain();
     be.rollback(pending_.front().X);
     pending_.clear();
   }
@@ -76,6 +136,9 @@ bool Engine::merge_one(Backend& be, int remaining) {
       sel_.set_truth(pc);
     }
   }
+  // the guess in flight for this merge, if the device has finished it: the helper combines and
+  // orders its records while the select below runs
+  if (exact) helper_offer(be);
   const double t0 = now_seconds();
   const bool ok = sel_.select(&a, &b, &freq);
   const double t1 = now_seconds();
@@ -140,9 +203,23 @@ bool Engine::merge_one(Backend& be, int remaining) {
   }
   const double t2 = now_seconds();
   const DeltaRecord* recs = nullptr;
-  const size_t n = be.collect(X, &recs);
+  bool adopted = false;
+  if (helper_) {
+    const int st = helper_->state.load(std::memory_order_acquire);
+    if (st != 0 && launched && helper_->X == X && helper_->a == a && helper_->b == b) {
+      while (helper_->state.load(std::memory_order_acquire) == 1) __builtin_ia32_pause();
+      be.collect(X, &recs);  // the flag is up: the helper read these records
+      sel_.adopt(&helper_->out);
+      helper_->state.store(0, std::memory_order_relaxed);
+      adopted = true;
+      ++helper_used_;
+    } else if (st != 0) {
+      helper_drain();
+    }
+  }
+  const size_t n = adopted ? 0 : be.collect(X, &recs);
   const double t3 = now_seconds();
-  sel_.apply_combine(a, b, X, recs, n);
+  if (!adopted) sel_.apply_combine(a, b, X, recs, n);
   // Late correction: with (a, b)'s changes known, a new pair holding X that is strictly more
   // frequent than the guess in flight (made before them; its own count is unchanged by this
   // merge) replaces it now, so the device undoes and redoes the guess while this merge is
@@ -155,6 +232,7 @@ bool Engine::merge_one(Backend& be, int remaining) {
     uint32_t gv = 0;
     sel_.lookup(g.a, g.b, &gf, &gv);
     if (sel_.predict_after(X, gf, &pa, &pb, &pf)) {
+      helper_drain();
       be.rollback(g.X);
       pending_.clear();
       pending_.push_back({pa, pb, X + 1});
@@ -179,6 +257,7 @@ bool Engine::merge_one(Backend& be, int remaining) {
       be.merge_scan(g.a, g.b, g.X);
     }
   }
+  if (spec) helper_offer(be);  // X+1's records, if they have landed
   times_.launch_s += t2 - t1;
   times_.wait_s += t3 - t2;
   if (launched) {
@@ -406,6 +485,7 @@ int Engine::train(Backend& be) {
   if (const char* e = std::getenv("SHREDWORD_SIM_SELECT")) sel_.set_simulate_pops(std::atoi(e) != 0);
   mtrace_.clear();
   count_bigrams(be);
+  helper_start();
   times_.init_s += now_seconds() - t0;
   int total = 0;
   const int target = (int)target_vocab_ - kBaseVocab;  // bpe.cpp:353
@@ -435,6 +515,7 @@ int Engine::train(Backend& be) {
     total += merged;
   }
   finish_speculation(be);
+  helper_stop();
   be.quiesce();
   if (trace_) std::fflush(trace_);
   times_.train_s += now_seconds() - t0;

@@ -4,9 +4,11 @@
 // product library (tests build a kernel-emulation backend of their own).
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <thread>
 #include <vector>
 
 #include "selector.h"
@@ -26,6 +28,9 @@ class Backend {
     merge_chain(ab, 1, X);
   }
   virtual size_t collect(int32_t X, const DeltaRecord** recs) = 0;
+  // Non-blocking look at the oldest outstanding merge X: true with its records once the device
+  // has finished it (they stay valid until X is collected or rolled back).  Default: never.
+  virtual bool peek(int32_t X, const DeltaRecord** recs, size_t* n) { return false; }
   // Longest chain the backend runs (1: one merge per pass, e.g. under a multi-GPU exchange).
   virtual int max_chain() const { return 1; }
   // True when a second launch may be issued before the first is collected (its merges run
@@ -113,6 +118,12 @@ class Engine {
   // Early guess (default on; SHREDWORD_EARLY_GUESS=0 or option early_guess=0 turns it off): the
   // guess for X+2 is posted right after X is applied, before the select of X+1 (see merge_one).
   void set_early_guess(bool on) { early_guess_ = on; }
+  // Apply helper (default on; SHREDWORD_APPLY_HELPER=0 or option apply_helper=0 turns it off): a
+  // second host thread combines and orders the records of the guess in flight (Selector::prepare)
+  // while this thread selects; a confirmed guess then only has its changes walked and pushed.
+  void set_apply_helper(bool on) { helper_on_ = on; }
+  uint64_t helper_used() const { return helper_used_; }
+  ~Engine();
   uint64_t corrections() const { return corrections_; }
   // K5 argmax verifier (debug): every `every` merges (0 = off), the selected pair's frequency is
   // checked against a device recount of the corpus (Backend::pair_max): it must be the largest
@@ -165,6 +176,24 @@ class Engine {
   uint64_t corrections_ = 0;
   uint64_t verify_checks_ = 0, verify_fail_ = 0;
   uint64_t host_phase_merges_ = 0;
+  // the apply helper: one job at a time (0 idle, 1 submitted, 2 done, 3 quit)
+  struct Helper {
+    std::thread th;
+    std::atomic<int> state{0};
+    int32_t a = 0, b = 0, X = 0;
+    const DeltaRecord* recs = nullptr;
+    size_t n = 0;
+    const void* pf = nullptr;
+    uint64_t pfm = 0;
+    Selector::Prepared out;
+  };
+  Helper* helper_ = nullptr;
+  bool helper_on_ = true;
+  uint64_t helper_used_ = 0;
+  void helper_start();
+  void helper_stop();
+  void helper_drain();                       // no job running (its result dropped)
+  void helper_offer(Backend& be);            // submits the oldest guess's records if they are ready
   size_t probe_k_ = 0, probe_window_ = 256;
   std::vector<std::vector<int32_t>> chain_log_;
   // SHREDWORD_ENGINE_TRACE=<path>: per merge (hit, select, launch, wait, apply µs, records),

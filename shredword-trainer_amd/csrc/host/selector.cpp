@@ -384,14 +384,22 @@ void Selector::apply(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, s
   apply_finish(a, b, X);
 }
 
-void Selector::apply_combine(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n) {
+void Selector::prepare(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n, Prepared* p,
+                       const void* prefetch_base, uint64_t prefetch_mask) const {
   const uint64_t c0 = __builtin_ia32_rdtsc();
+  p->a = a;
+  p->b = b;
+  p->X = X;
+  p->records = n;
   // 1. records -> FreqChange entries keyed exactly like the reference's pair_hash.
-  changes_.clear();
+  std::vector<Change>& changes = p->changes;
+  changes.clear();
   size_t cap = 64;
   while (cap < 2 * n + 2) cap <<= 1;
-  change_index_.assign(cap, 0);
+  p->index.assign(cap, 0);
+  uint32_t* index = p->index.data();
   const uint64_t cm = cap - 1;
+  const Info* pt = static_cast<const Info*>(prefetch_base);
   for (size_t i = 0; i < n; ++i) {
     const uint32_t cat = recs[i].key & 3u;
     const uint32_t slot = recs[i].key >> 2;
@@ -407,15 +415,15 @@ void Selector::apply_combine(int32_t a, int32_t b, int32_t X, const DeltaRecord*
     const int64_t d = (cat == kOldLeft || cat == kOldRight) ? -(int64_t)recs[i].sum : (int64_t)recs[i].sum;
     uint64_t j = mix64(hk) & cm;
     for (;;) {
-      uint32_t s = change_index_[j];
+      uint32_t s = index[j];
       if (!s) {
         // the pair's info line, requested now: the combine and the ordering hide its miss
-        __builtin_prefetch(&table_[mix64(pack_pair((int32_t)(hk >> 32), (int32_t)hk)) & mask_]);
-        changes_.push_back({hk, d, recs[i].ft});
-        change_index_[j] = (uint32_t)changes_.size();
+        if (pt) __builtin_prefetch(&pt[mix64(pack_pair((int32_t)(hk >> 32), (int32_t)hk)) & prefetch_mask]);
+        changes.push_back({hk, d, recs[i].ft});
+        index[j] = (uint32_t)changes.size();
         break;
       }
-      Change& c = changes_[s - 1];
+      Change& c = changes[s - 1];
       if (c.hk == hk) {
         c.delta += d;
         if (recs[i].ft < c.ft) c.ft = recs[i].ft;
@@ -424,16 +432,67 @@ void Selector::apply_combine(int32_t a, int32_t b, int32_t X, const DeltaRecord*
       j = (j + 1) & cm;
     }
   }
+  const uint64_t c1 = __builtin_ia32_rdtsc();
+  p->cyc_combine = c1 - c0;
+  // 2. reference application order: bucket (hk % 1024) ascending, latest first touch first.
+  //    Two stable 5-bit counting passes by bucket (the usual ~100 changes never pay for a
+  //    1024-entry prefix), then a sort by first touch inside each bucket.
+  static_assert(kDeltaBuckets == 1024, "two 5-bit passes");
+  const size_t nc = changes.size();
+  std::vector<Change>& staged = p->staged;
+  std::vector<Change>& ordered = p->ordered;
+  staged.resize(nc);
+  ordered.resize(nc);
+  {
+    uint32_t cnt[33] = {};
+    for (const Change& c : changes) cnt[(c.hk & 31u) + 1]++;
+    for (int k = 0; k < 32; ++k) cnt[k + 1] += cnt[k];
+    for (const Change& c : changes) staged[cnt[c.hk & 31u]++] = c;
+  }
+  {
+    uint32_t cnt[33] = {};
+    for (const Change& c : staged) cnt[((c.hk >> 5) & 31u) + 1]++;
+    for (int k = 0; k < 32; ++k) cnt[k + 1] += cnt[k];
+    for (const Change& c : staged) ordered[cnt[(c.hk >> 5) & 31u]++] = c;
+  }
+  // Inside a bucket, first touch descending (unique per change, so any sort gives the same
+  // order).  Buckets are not small: every (p, a) change lands in a's bucket and every (p, X)
+  // change in X's (the bucket is the second id's low bits), so each holds about a quarter of
+  // the merge's changes -- sorted, not insertion-sorted.
+  for (size_t i = 0; i < nc;) {
+    const uint64_t bk = ordered[i].hk % kDeltaBuckets;
+    size_t e = i + 1;
+    while (e < nc && ordered[e].hk % kDeltaBuckets == bk) ++e;
+    if (e - i > 1) std::sort(ordered.begin() + i, ordered.begin() + e, [](const Change& x, const Change& y) { return x.ft > y.ft; });
+    i = e;
+  }
+  p->cyc_order = __builtin_ia32_rdtsc() - c1;
+}
+
+void Selector::apply_combine(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n) {
+  prepare(a, b, X, recs, n, &own_, table_.data(), mask_);
   ctr_.records += n;
-  ctr_.changes += changes_.size();
-  ctr_.cyc_combine += __builtin_ia32_rdtsc() - c0;
+  ctr_.changes += own_.changes.size();
+  ctr_.cyc_combine += own_.cyc_combine;
+  ctr_.cyc_order += own_.cyc_order;
+}
+
+void Selector::adopt(Prepared* p) {
+  std::swap(own_, *p);
+  // the lines the other core requested are in the shared L3: bring them closer for the walk
+  for (const Change& c : own_.ordered)
+    __builtin_prefetch(&table_[mix64(pack_pair((int32_t)(c.hk >> 32), (int32_t)c.hk)) & mask_]);
+  ctr_.records += own_.records;
+  ctr_.changes += own_.changes.size();
+  ctr_.cyc_combine += own_.cyc_combine;
+  ctr_.cyc_order += own_.cyc_order;
 }
 
 bool Selector::predict_after(int32_t X, uint64_t above, int32_t* pa, int32_t* pb, uint64_t* pf) const {
   // Pairs holding X are new: their count after this merge is their combined delta, exactly.
   uint64_t best_f = above;
   bool found = false;
-  for (const Change& c : changes_) {
+  for (const Change& c : own_.changes) {
     const int32_t f = (int32_t)(uint32_t)(c.hk >> 32), s = (int32_t)(uint32_t)c.hk;
     if ((f != X && s != X) || f == unk_ || s == unk_ || c.delta <= 0) continue;
     const uint64_t v = (uint64_t)c.delta;
@@ -449,39 +508,8 @@ bool Selector::predict_after(int32_t X, uint64_t above, int32_t* pa, int32_t* pb
 }
 
 void Selector::apply_finish(int32_t a, int32_t b, int32_t X) {
-  const uint64_t c1 = __builtin_ia32_rdtsc();
-  // 2. reference application order: bucket (hk % 1024) ascending, latest first touch first.
-  //    Two stable 5-bit counting passes by bucket (the usual ~100 changes never pay for a
-  //    1024-entry prefix), then insertion sort inside the (almost always tiny) buckets.
-  static_assert(kDeltaBuckets == 1024, "two 5-bit passes");
-  const size_t nc = changes_.size();
-  staged_.resize(nc);
-  ordered_.resize(nc);
-  {
-    uint32_t cnt[33] = {};
-    for (const Change& c : changes_) cnt[(c.hk & 31u) + 1]++;
-    for (int k = 0; k < 32; ++k) cnt[k + 1] += cnt[k];
-    for (const Change& c : changes_) staged_[cnt[c.hk & 31u]++] = c;
-  }
-  {
-    uint32_t cnt[33] = {};
-    for (const Change& c : staged_) cnt[((c.hk >> 5) & 31u) + 1]++;
-    for (int k = 0; k < 32; ++k) cnt[k + 1] += cnt[k];
-    for (const Change& c : staged_) ordered_[cnt[(c.hk >> 5) & 31u]++] = c;
-  }
-  // Inside a bucket, first touch descending (unique per change, so any sort gives the same
-  // order).  Buckets are not small: every (p, a) change lands in a's bucket and every (p, X)
-  // change in X's (the bucket is the second id's low bits), so each holds about a quarter of
-  // the merge's changes -- sorted, not insertion-sorted.
-  for (size_t i = 0; i < nc;) {
-    const uint64_t bk = ordered_[i].hk % kDeltaBuckets;
-    size_t e = i + 1;
-    while (e < nc && ordered_[e].hk % kDeltaBuckets == bk) ++e;
-    if (e - i > 1) std::sort(ordered_.begin() + i, ordered_.begin() + e, [](const Change& x, const Change& y) { return x.ft > y.ft; });
-    i = e;
-  }
   const uint64_t c2 = __builtin_ia32_rdtsc();
-  ctr_.cyc_order += c2 - c1;
+  const std::vector<Change>& ordered_ = own_.ordered;
   // (the table lines this merge touches were requested by apply_combine)
   if (2 * (count_ + ordered_.size() + 1) > table_.size()) grow();
   // The pair-info updates first, then the heap pushes in the same order: the pushes read nothing

@@ -103,6 +103,29 @@ struct SelectedMerge {
 
 class Selector {
  public:
+  // One merge's records combined per pair and put in the reference's application order: the part
+  // of apply() that reads nothing of the selector's state, so another thread can make it while the
+  // selector selects (Engine's apply helper).
+  struct Change { uint64_t hk; int64_t delta; uint64_t ft; };
+  struct Prepared {
+    int32_t a = 0, b = 0, X = 0;
+    size_t records = 0;
+    std::vector<Change> changes, staged, ordered;
+    std::vector<uint32_t> index;
+    uint64_t cyc_combine = 0, cyc_order = 0;
+  };
+  // Thread-safe against every other member: reads only unk_ (fixed during a train()).
+  // prefetch_base / prefetch_mask: a snapshot of the pair table to prefetch the changed pairs'
+  // lines from (nullptr: none).
+  void prepare(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs, size_t n, Prepared* p,
+               const void* prefetch_base, uint64_t prefetch_mask) const;
+  // The table snapshot for prepare() on another thread.
+  const void* table_base() const { return table_.data(); }
+  uint64_t table_mask() const { return mask_; }
+  // A merge prepared elsewhere becomes the current one (as after apply_combine); p gets the old
+  // buffers back for reuse.
+  void adopt(Prepared* p);
+
   // bpe_init's fresh pair map and heap (bpe.cpp:103-106).
   void reset(int32_t unk_id, uint64_t min_pair_freq);
   // bpe_load_corpus: a fresh pair map (bpe.cpp:183); the heap and its entries stay.
@@ -189,7 +212,6 @@ class Selector {
   struct HeapNode { uint64_t fv; int32_t a, b; };
   static uint64_t node_freq(const HeapNode& n) { return n.fv >> 24; }
   static uint32_t node_version(const HeapNode& n) { return (uint32_t)(n.fv & 0xFFFFFFu); }
-  struct Change { uint64_t hk; int64_t delta; uint64_t ft; };
   static constexpr uint64_t kEmptyKey = 0x8000000080000000ull;
 
   Info& get(int32_t a, int32_t b);  // get-or-create (bimap_get)
@@ -216,10 +238,7 @@ class Selector {
   // its four grandchildren one 64-byte line, so a sift level touches one cache line (frequency
   // and payload together).  heap_[0] is padding.
   HugeVec<HeapNode> heap_;
-  std::vector<Change> changes_;
-  std::vector<uint32_t> change_index_;
-  std::vector<Change> staged_;  // apply: the first counting pass
-  std::vector<Change> ordered_;
+  Prepared own_;  // the current merge's changes (apply_combine / adopt -> apply_finish)
   std::vector<HeapNode> pushes_;  // apply: the pushes of one merge, in order
   bool simulate_select(const int32_t* used, size_t n_used, uint64_t floor, int32_t* pa, int32_t* pb) const;
   bool simulate_pops_ = true;

@@ -104,6 +104,8 @@ class WordLoop {
   void post_merge(int32_t a, int32_t b, int32_t X);
   // The records of the oldest posted merge, which must be X (waits for its flag).
   size_t collect(int32_t X, const DeltaRecord** recs);
+  // Non-blocking: X is the oldest posted merge and its flag is up (records as collect() gives them).
+  bool peek(int32_t X, const DeltaRecord** recs, size_t* n) const;
   // Undoes every posted merge with id >= X, newest first (queued; nothing waits).
   void rollback(int32_t X);
   size_t in_flight() const { return posted_.size(); }

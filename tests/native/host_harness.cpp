@@ -259,6 +259,16 @@ class EmuBackend : public Backend {
     return recs_.size();
   }
 
+  // The oldest outstanding merge's records before it is collected (the emulated kernels ran at
+  // launch time, so they are always ready): the Engine's apply helper reads them on its thread.
+  bool peek(int32_t X, const DeltaRecord** recs, size_t* n) override {
+    if (!peek_on_ || gather_ || queue_.empty() || queue_.front().X != X) return false;
+    *recs = queue_.front().recs.data();
+    *n = queue_.front().recs.size();
+    return true;
+  }
+  bool peek_on_ = std::getenv("HH_PEEK") ? std::atoi(std::getenv("HH_PEEK")) != 0 : true;
+
   // The device's resident phase, emulated: the first `k` merges of each tiebreak=device train()
   // are selected on the host (Engine::train_device) before device_select takes over.
   void set_device_phase(int k) { phase_ = phase_left_ = k < 0 ? 0 : k; }
@@ -434,6 +444,8 @@ void hh_set_device_phase(void* p, int k) {
   if (h->be) h->be->set_device_phase(k);
 }
 uint64_t hh_host_phase_merges(void* p) { return ((Harness*)p)->engine.host_phase_merges(); }
+uint64_t hh_helper_used(void* p) { return ((Harness*)p)->engine.helper_used(); }
+void hh_set_apply_helper(void* p, int on) { ((Harness*)p)->engine.set_apply_helper(on != 0); }
 
 void hh_count(void* p) {
   Harness* h = (Harness*)p;
