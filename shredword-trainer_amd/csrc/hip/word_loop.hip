@@ -52,6 +52,11 @@ constexpr int kStripV = 6;              // 16-B loads per word run: [length][23 
 constexpr int kStrip = 4 * kStripV;     // ints per lane in the LDS strip
 constexpr uint32_t kStripTok = kStrip - 1;
 constexpr int kB = 8;                   // pool entries per lane per scan round (one load batch)
+#ifdef SHRED_WL_NO_PREFETCH
+constexpr bool kWlPrefetch = false;     // (A/B builds) each word's run loaded in its own iteration
+#else
+constexpr bool kWlPrefetch = true;      // the next word's run loads while this one merges
+#endif
 constexpr int kQ = kWlThreads * kB + kWlThreads;  // LDS queue of filtered entries (a round + a remainder)
 constexpr uint32_t kRing = 64;          // command ring entries
 constexpr uint32_t kOpMerge = 1, kOpStop = 2, kOpTimeout = 3, kOpUnmerge = 4;
@@ -762,18 +767,33 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       __syncthreads();  // every thread has read qn before the next round queues more
       const bool last = base + (u64)kWlThreads * kB >= cnt;
       if (qn < (uint32_t)kWlThreads && !last) continue;
-      for (uint32_t qi = tid; qi < ((qn + kWlThreads - 1) / kWlThreads) * kWlThreads; qi += kWlThreads) {
+      // A lane's words one after another, the next word's run and weight loading while this one
+      // merges (the compiler's waits count the loads; big merges queue up to 9 words a lane)
+      const uint32_t qend = ((qn + kWlThreads - 1) / kWlThreads) * kWlThreads;
+      u64 e_n = kEmpty64, wc_n = 0;
+      Run x_n{};
+      if (kWlPrefetch && tid < qn) {
+        e_n = s_q[tid];
+        x_n = load_run(p.wtok + (uint32_t)(e_n >> 32));
+        wc_n = p.weight[(uint32_t)e_n];
+      }
+      for (uint32_t qi = tid; qi < qend; qi += kWlThreads) {
+        if (!kWlPrefetch && qi < qn) {
+          e_n = s_q[qi];
+          x_n = load_run(p.wtok + (uint32_t)(e_n >> 32));
+          wc_n = p.weight[(uint32_t)e_n];
+        }
+        const u64 e = e_n, wc = wc_n;
+        const Run x = x_n;
+        if (kWlPrefetch && qi + kWlThreads < qn) {
+          e_n = s_q[qi + kWlThreads];
+          x_n = load_run(p.wtok + (uint32_t)(e_n >> 32));
+          wc_n = p.weight[(uint32_t)e_n];
+        }
         uint32_t occ = 0;
-        u64 nsig = 0, e = kEmpty64;
+        u64 nsig = 0;
         if (qi < qn) {
-          e = s_q[qi];
-          const uint32_t w = (uint32_t)e;
           int32_t* r = p.wtok + (uint32_t)(e >> 32);
-          const Run x = load_run(r);
-          const u64 wc = p.weight[w];
-          // every load of the word lands here, once: a first use of wc later would wait (vmcnt
-          // counts stores too) for the stores issued by then
-          asm volatile("s_waitcnt vmcnt(0)" ::"v"(wc), "v"(x.v[0].x) : "memory");
           const uint32_t L = (uint32_t)x.v[0].x;
           uint32_t nl = L;
           if (qi == 0 && base == 0) S.st[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
