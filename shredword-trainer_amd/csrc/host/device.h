@@ -116,6 +116,9 @@ class Device : public Backend {
   // it); the launch path two launches.
   static constexpr int kResSlots = 4;
   int overlap_depth() const override { return resident_eligible() || index_eligible() ? spec_depth_ : 1; }
+  // k_resident and the indexed loop queue up to kResSlots / WordLoop::kSlots merges; the launch
+  // path's two launches hold one guess behind the current merge.
+  int max_guesses() const override { return resident_eligible() || index_eligible() ? kResSlots - 1 : 1; }
   void set_spec_depth(int d) { spec_depth_ = std::max(1, std::min(d, kResSlots - 1)); }
   uint32_t min_slot_cap() const {
     uint32_t c = UINT32_MAX;

@@ -247,7 +247,7 @@ bool Engine::merge_one(Backend& be, int remaining) {
   // at once, so the device has X+2 queued before it finishes X+1.  The selects of X+1 happen after
   // the post (the heap replay is off the device's path); a wrong guess for X+1 undoes both.
   if (early_guess_ && spec && chain == 1 && pending_.size() == 1 && pending_.front().X == X + 1 && remaining > 2 &&
-      be.can_overlap()) {
+      be.can_overlap() && be.max_guesses() >= 2) {
     const Guess g1 = pending_.front();
     used_.assign({g1.a, g1.b});
     Guess g{0, 0, X + 2};

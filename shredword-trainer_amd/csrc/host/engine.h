@@ -38,6 +38,8 @@ class Backend {
   virtual bool can_overlap() const { return false; }
   // How many guessed merges may be in flight behind the current one (overlap mode).
   virtual int overlap_depth() const { return 1; }
+  // How many guesses the backend can hold in flight at all (the early guess needs 2).
+  virtual int max_guesses() const { return 1; }
   // Undoes every launched merge with id >= X that was not collected, newest first (each
   // expands its X back into (a, b)), so the corpus is exactly as before those merges.
   virtual void rollback(int32_t X) {}

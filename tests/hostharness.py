@@ -41,6 +41,9 @@ def load():
     lib.hh_helper_used.argtypes = [ctypes.c_void_p]
     lib.hh_helper_used.restype = ctypes.c_uint64
     lib.hh_set_apply_helper.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.hh_set_verify.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.hh_verify_failures.argtypes = [ctypes.c_void_p]
+    lib.hh_verify_failures.restype = ctypes.c_uint64
     lib.hh_set_early_guess.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.hh_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     lib.hh_trace_line.argtypes = [ctypes.c_void_p, ctypes.c_char_p]

@@ -273,6 +273,7 @@ class EmuBackend : public Backend {
   // are selected on the host (Engine::train_device) before device_select takes over.
   void set_device_phase(int k) { phase_ = phase_left_ = k < 0 ? 0 : k; }
   bool device_select_now() const override { return phase_left_ == 0; }
+  int max_guesses() const override { return 3; }
 
   void token_freq(size_t T, std::vector<uint64_t>* freq) override {
     freq->assign(T, 0);
@@ -446,6 +447,8 @@ void hh_set_device_phase(void* p, int k) {
 uint64_t hh_host_phase_merges(void* p) { return ((Harness*)p)->engine.host_phase_merges(); }
 uint64_t hh_helper_used(void* p) { return ((Harness*)p)->engine.helper_used(); }
 void hh_set_apply_helper(void* p, int on) { ((Harness*)p)->engine.set_apply_helper(on != 0); }
+void hh_set_verify(void* p, int every) { ((Harness*)p)->engine.set_verify(every); }
+uint64_t hh_verify_failures(void* p) { return ((Harness*)p)->engine.verify_failures(); }
 
 void hh_count(void* p) {
   Harness* h = (Harness*)p;
