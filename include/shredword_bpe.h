@@ -204,6 +204,7 @@ typedef struct ShredStats {
   uint64_t sel_table_slots;    /* its capacity */
   uint64_t sel_host_merges;    /* tiebreak=device: early merges selected on the host by the same rule
                                   (exact counts) while the whole-chip resident loop runs them */
+  uint64_t sel_table_grows;    /* tiebreak=device: pair tables grown 4x between launches */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

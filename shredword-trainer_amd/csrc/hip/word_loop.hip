@@ -1255,6 +1255,16 @@ __global__ void k_sel_insert(const PairCount* pc, uint64_t n, SelParams q) {
   }
 }
 
+// The live pairs of a table (count > 0), for a bigger one.
+__global__ void k_sel_export(const u64* pkey, const u64* pcnt, u64 cap, PairCount* out, uint32_t* n) {
+  for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < cap; i += (u64)gridDim.x * blockDim.x) {
+    const u64 k = pkey[i], c = pcnt[i];
+    if (k == kEmpty64 || c == 0) continue;
+    const uint32_t j = atomicAdd(n, 1u);
+    out[j] = PairCount{(int32_t)(uint32_t)(k >> 32), (int32_t)(uint32_t)k, c, 0};
+  }
+}
+
 template <class T>
 T* wl_alloc(size_t n, size_t* acc) {
   void* p = nullptr;
@@ -1897,16 +1907,17 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
   if (n_max == 0) return 0;
   reserve(X0 + (int32_t)n_max);
   hipStream_t s = S(stream_);
-  // the table: room for the initial pairs and ~256 new pairs a merge, at most a quarter full
+  // the table: the initial pairs and ~32 new pairs a merge at most half full (C3 creates ≈ 42
+  // a merge on average; a table past 3/4 full is grown 4x between launches), small enough that
+  // the merge loop's probes mostly hit the MALL
   uint64_t want = 1 << 16;
-  while (want < 4 * ((uint64_t)pairs.size() + 256ull * n_max)) want <<= 1;
-  if (want > pcap_) {
-    for (void* q : {(void*)pkey_, (void*)pcnt_, (void*)pinf_})
-      if (q) WL_OK(hipFree(q));
-    pcap_ = want;
-    pkey_ = wl_alloc<u64>(pcap_, &bytes_);
-    pcnt_ = wl_alloc<u64>(pcap_, &bytes_);
-    pinf_ = wl_alloc<uint32_t>(pcap_, &bytes_);
+  while (want < 2 * ((uint64_t)pairs.size() + 32ull * n_max)) want <<= 1;
+  if (const char* e = std::getenv("SHREDWORD_SELECT_TABLE_SLOTS")) {  // tests: a table that must grow
+    const uint64_t t = std::strtoull(e, nullptr, 10);
+    if (t >= 1024) {  // never below what the initial pairs need (they must all fit)
+      want = 1024;
+      while (want < t || want < 2 * (uint64_t)pairs.size()) want <<= 1;
+    }
   }
   if (!fr_[0]) {
     fcap_ = 16384;
@@ -1927,33 +1938,49 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
     upd_cap_ = need_upd;
     upd_ = wl_alloc<uint32_t>(upd_cap_, &bytes_);
   }
-  WL_OK(hipMemsetAsync(pkey_, 0xFF, pcap_ * sizeof(u64), s));
-  WL_OK(hipMemsetAsync(pcnt_, 0, pcap_ * sizeof(u64), s));
   WL_OK(hipMemsetAsync(sst_dev_, 0, kSelWords * sizeof(uint32_t), s));
   SelParams q{};
-  q.pkey = pkey_;
-  q.pcnt = pcnt_;
-  q.inf = pinf_;
-  q.pmask = pcap_ - 1;
-  q.fr[0] = fr_[0];
-  q.fr[1] = fr_[1];
-  q.fcap = fcap_;
-  q.st = sst_dev_;
-  q.thr = thr_;
-  q.out = sout_;
-  q.upd = upd_;
-  q.X0 = X0;
-  q.n_max = n_max;
-  q.min_freq = min_freq;
-  q.fill_max = (uint32_t)std::min<uint64_t>(3 * pcap_ / 4, 0xFFFFFFF0ull);
-  if (!pairs.empty()) {
-    size_t acc = 0;
-    PairCount* dp = wl_alloc<PairCount>(pairs.size(), &acc);
-    WL_OK(hipMemcpyAsync(dp, pairs.data(), pairs.size() * sizeof(PairCount), hipMemcpyHostToDevice, s));
-    k_sel_insert<<<512, 256, 0, s>>>(dp, pairs.size(), q);
-    WL_OK(hipGetLastError());
+  auto table_from = [&](const PairCount* dp, size_t np, uint64_t cap) {  // a fresh table holding dp
+    if (cap != pcap_) {
+      for (void* t : {(void*)pkey_, (void*)pcnt_, (void*)pinf_})
+        if (t) WL_OK(hipFree(t));
+      pcap_ = cap;
+      pkey_ = wl_alloc<u64>(pcap_, &bytes_);
+      pcnt_ = wl_alloc<u64>(pcap_, &bytes_);
+      pinf_ = wl_alloc<uint32_t>(pcap_, &bytes_);
+    }
+    WL_OK(hipMemsetAsync(pkey_, 0xFF, pcap_ * sizeof(u64), s));
+    WL_OK(hipMemsetAsync(pcnt_, 0, pcap_ * sizeof(u64), s));
+    q.pkey = pkey_;
+    q.pcnt = pcnt_;
+    q.inf = pinf_;
+    q.pmask = pcap_ - 1;
+    q.fr[0] = fr_[0];
+    q.fr[1] = fr_[1];
+    q.fcap = fcap_;
+    q.st = sst_dev_;
+    q.thr = thr_;
+    q.out = sout_;
+    q.upd = upd_;
+    q.X0 = X0;
+    q.n_max = n_max;
+    q.min_freq = min_freq;
+    q.fill_max = (uint32_t)std::min<uint64_t>(3 * pcap_ / 4, 0xFFFFFFF0ull);
+    uint32_t zero = 0;
+    WL_OK(hipMemcpyAsync(sst_dev_ + kSelIns, &zero, sizeof(zero), hipMemcpyHostToDevice, s));
+    WL_OK(hipMemcpyAsync(sst_dev_ + kSelErr, &zero, sizeof(zero), hipMemcpyHostToDevice, s));
+    if (np) {
+      k_sel_insert<<<512, 256, 0, s>>>(dp, np, q);
+      WL_OK(hipGetLastError());
+    }
     WL_OK(hipStreamSynchronize(s));
-    WL_OK(hipFree(dp));
+  };
+  {
+    size_t acc = 0;
+    PairCount* dp = pairs.empty() ? nullptr : wl_alloc<PairCount>(pairs.size(), &acc);
+    if (dp) WL_OK(hipMemcpyAsync(dp, pairs.data(), pairs.size() * sizeof(PairCount), hipMemcpyHostToDevice, s));
+    table_from(dp, pairs.size(), want);
+    if (dp) WL_OK(hipFree(dp));
   }
   sst_.table_slots = pcap_;
   uint32_t m = 0;
@@ -2003,7 +2030,33 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
       m = st[kSelM];
       const uint32_t status = st[kSelStatus];
       if (status == kSelDone) break;
-      if (status == kSelFull) fatal("tiebreak=device: the pair table is full (more new pairs than sized for)");
+      if (status == kSelFull) {  // the table past 3/4 full (or a probe run past its bound): 4x, live pairs moved
+        size_t acc = 0;
+        PairCount* dp = wl_alloc<PairCount>(pcap_, &acc);
+        uint32_t* dn = wl_alloc<uint32_t>(1, &acc);
+        WL_OK(hipMemsetAsync(dn, 0, sizeof(uint32_t), s));
+        k_sel_export<<<1024, 256, 0, s>>>(pkey_, pcnt_, pcap_, dp, dn);
+        WL_OK(hipGetLastError());
+        uint32_t np = 0;
+        WL_OK(hipMemcpyAsync(&np, dn, sizeof(np), hipMemcpyDeviceToHost, s));
+        WL_OK(hipStreamSynchronize(s));
+        // the exported pairs must survive the old table's release: keep them in their own buffer
+        const uint64_t grown = 4 * pcap_;
+        u64* ok = pkey_;
+        u64* oc = pcnt_;
+        uint32_t* oi = pinf_;
+        pkey_ = pcnt_ = nullptr;
+        pinf_ = nullptr;
+        pcap_ = 0;
+        table_from(dp, np, grown);
+        for (void* t : {(void*)ok, (void*)oc, (void*)oi}) WL_OK(hipFree(t));
+        WL_OK(hipFree(dp));
+        WL_OK(hipFree(dn));
+        ++sst_.grows;
+        p.sel = q;
+        if (!sel_rebuild(min_freq)) break;
+        continue;
+      }
       if (status != kSelRebuild) fatal("tiebreak=device: the merge loop ended without a status");
       if (!sel_rebuild(min_freq)) break;
     }
@@ -2024,6 +2077,7 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
                    (unsigned long long)t64[2], (unsigned long long)t64[3]);
     sst_.table_pairs = st[kSelIns];
   }
+  sst_.table_slots = pcap_;
   sst_.merges += m;
   std::vector<u64> o(2 * (size_t)m);
   if (m) WL_OK(hipMemcpy(o.data(), sout_, o.size() * sizeof(u64), hipMemcpyDeviceToHost));

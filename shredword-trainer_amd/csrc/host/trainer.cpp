@@ -506,6 +506,7 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
       s->sel_merge_us = q.merge_us;
       s->sel_table_pairs = q.table_pairs;
       s->sel_table_slots = q.table_slots;
+      s->sel_table_grows = q.grows;
     }
   }
   {

@@ -69,6 +69,7 @@ struct SelectStats {
   double table_us = 0;                   // of merge_us: the pair table + frontier update
   uint64_t listed = 0, changed = 0, occurrences = 0, new_pairs = 0;
   uint64_t table_slots = 0, table_pairs = 0, frontier_max = 0;
+  uint64_t grows = 0;  // pair tables grown 4x (past 3/4 full) between launches
 };
 
 class WordLoop {

@@ -123,3 +123,15 @@ def test_tiebreak_device_deep_run(case_corpus, tmp_path):
     assert freqs[-1] >= case["config"]["min_pair_freq"]
     assert _symbols(vocab, model) == _symbols(case["vocab_bytes"], case["model_bytes"])
     assert st["sel_rebuilds"] >= 1 and st["sel_table_pairs"] < st["sel_table_slots"]
+
+
+@pytest.mark.parametrize("name", ["ascii1m_v3000_mpf2", "mixed2m_v4000"])
+def test_tiebreak_device_pair_table_grows(name, case_corpus, tmp_path, monkeypatch):
+    """A pair table sized below what the run needs (SHREDWORD_SELECT_TABLE_SLOTS) is grown 4x
+    between launches with its live pairs moved: the same files as the default size."""
+    case, corpus = case_corpus(name)
+    n1, m1, v1, t1, st1 = _train(case, corpus, tmp_path, "big")
+    monkeypatch.setenv("SHREDWORD_SELECT_TABLE_SLOTS", "1024")
+    n2, m2, v2, t2, st2 = _train(case, corpus, tmp_path, "small")
+    assert (n1, m1, v1, t1) == (n2, m2, v2, t2)
+    assert st2["sel_table_grows"] >= 1 and st1["sel_table_grows"] == 0
