@@ -1907,11 +1907,11 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
   if (n_max == 0) return 0;
   reserve(X0 + (int32_t)n_max);
   hipStream_t s = S(stream_);
-  // the table: the initial pairs and ~32 new pairs a merge at most half full (C3 creates ≈ 42
-  // a merge on average; a table past 3/4 full is grown 4x between launches), small enough that
-  // the merge loop's probes mostly hit the MALL
+  // the table: room for the initial pairs and ~256 new pairs a merge, at most a quarter full
+  // (short probe runs: a table sized for the MALL, half full at C3's end, made the update slower,
+  // 6.9 -> 8.2 µs a merge); past 3/4 full it is grown 4x between launches
   uint64_t want = 1 << 16;
-  while (want < 2 * ((uint64_t)pairs.size() + 32ull * n_max)) want <<= 1;
+  while (want < 4 * ((uint64_t)pairs.size() + 256ull * n_max)) want <<= 1;
   if (const char* e = std::getenv("SHREDWORD_SELECT_TABLE_SLOTS")) {  // tests: a table that must grow
     const uint64_t t = std::strtoull(e, nullptr, 10);
     if (t >= 1024) {  // never below what the initial pairs need (they must all fit)
