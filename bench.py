@@ -27,8 +27,9 @@ N GPUs: ``--gpus N`` with N > 1 launches N ranks itself (torch.distributed.run, 
 GPU, rank r on device r) unless WORLD_SIZE is already set (the driver's own torchrun).
 ``--dist`` picks what the ranks do:
 * ``replicate`` (the default for N > 1): ONE training.  The load is sharded (rank r counts byte
-  range r of the corpus on its GPU, the word lists are all-gathered over RCCL and merged) and the
-  merge loop runs on every rank.  The merge loop is a serial chain of dependent merges (merge
+  range r of the corpus on its GPU, the word lists are all-gathered over torch.distributed's RCCL
+  -- an nccl group; ``--load-gather rccl`` uses the library's own communicator instead -- and
+  merged) and the merge loop runs on every rank.  The merge loop is a serial chain of dependent merges (merge
   m+1's selection needs merge m's exact frequency changes), so ``value`` (merges
   of the one training / max-over-ranks train() time) does not grow with N; ``load`` reports
   the part that does shard (max-over-ranks load_corpus time) and ``end_to_end_s`` = load + one
@@ -585,6 +586,10 @@ def main():
     ap.add_argument("--dist", default="replicate", choices=["replicas", "replicate", "exchange"],
                     help="N > 1: one training with a sharded load (replicate, the default) or a per-merge RCCL "
                          "exchange (exchange), or N independent jobs (replicas); see the module docstring")
+    ap.add_argument("--load-gather", default="torch", choices=["torch", "rccl"],
+                    help="N > 1 replicate, a GPU per rank: the sharded load's word-list all-gather over "
+                         "torch.distributed's RCCL (an nccl group, default) or the library's own RCCL "
+                         "communicator (dist_allgather_bytes)")
     ap.add_argument("--tiebreak", default="exact", choices=["exact", "device"],
                     help="merge selection: exact (the reference's heap replay, bit-exact files; default) or device "
                          "(opt-in K5 mode: every merge selected on the GPU, ties to the smaller pair key)")
@@ -680,17 +685,24 @@ def main():
     if one_job and share and args.dist == "exchange":
         raise SystemExit("bench: --dist exchange needs one GPU per rank (RCCL per merge); use --dist replicate")
     gather_via = None
-    if one_job and not share:
+    # replicate on a GPU per rank: the load's gather over torch.distributed's RCCL (an nccl group
+    # beside the gloo one) unless --load-gather rccl asks for the library's own communicator;
+    # exchange needs the library's communicator (a collective per merge)
+    torch_gather = one_job and not share and args.dist == "replicate" and args.load_gather == "torch"
+    if one_job and not share and not torch_gather:
         sdist.init_from_env(device=dev)
         gather_via = "RCCL all-gather over xGMI (dist_allgather_bytes)"
-    rccl_ranks = lib.shred_dist_ranks() if one_job and not share else 0
+    rccl_ranks = lib.shred_dist_ranks() if one_job and not share and not torch_gather else 0
 
     t = BPETrainer(vocab_size=cfg["vocab"], unk_id=cfg["unk"], character_coverage=cfg["cov"], min_pair_freq=cfg["mpf"])
     t.set_option("log", 0)
     t.set_option("device", dev)
     t.set_option("layout", args.layout)
     t.set_option("tiebreak", args.tiebreak)
-    if one_job and not share:
+    if torch_gather:
+        t.set_load_gather(rank, world, sdist.host_load_gather(dist.new_group(backend="nccl")))
+        gather_via = "torch.distributed all_gather_object over an nccl (RCCL, xGMI) group"
+    elif one_job and not share:
         t.set_option("dist", args.dist)
     elif one_job:
         t.set_load_gather(rank, world, sdist.host_load_gather())

@@ -38,9 +38,10 @@ def finalize():
 
 
 def host_load_gather(group=None):
-    """A shred_gather_fn over torch.distributed's host collectives (gloo): the sharded load's
-    word-list all-gather without RCCL (BPETrainer.set_load_gather).  The returned callback keeps
-    its last result alive until its next call, as the C ABI requires."""
+    """A shred_gather_fn over torch.distributed (BPETrainer.set_load_gather): the sharded load's
+    word-list all-gather on `group` -- gloo when ranks share a GPU, an nccl group (torch's RCCL over
+    xGMI) when each rank has its own, the bench's default for replicate.  The returned callback
+    keeps its last result alive until its next call, as the C ABI requires."""
     import torch.distributed as dist
 
     from .cbase import GATHER_FN
