@@ -99,15 +99,15 @@ struct WEnt {
 };
 
 // tiebreak=device (K5 as the selector, WordLoop::run_select): the loop picks its own merges from
-// a pair table on the device.  Table: open addressing on the pair key, count beside it (pairs
-// holding unk are never in it).  Frontier: the slots of every pair ranked at or above a threshold
+// a pair table on the device.  Table: open addressing on the pair key, 16 B a slot -- the key,
+// then a word holding the count (low 48 bits) and the slot's frontier position + 1 (high 16
+// bits, 0: not in the frontier), so one atomicAdd on the word both counts and tells where the
+// LDS copy is (pairs holding unk are never in it).  Frontier: the slots of every pair ranked at or above a threshold
 // (count desc, key asc) plus stale ones; each merge takes the best live frontier entry, and pairs
 // a merge creates above the threshold join it (only new pairs ever gain: every other count only
 // falls).  An empty frontier sends the launch back to the host, which rebuilds it whole-chip.
 struct SelParams {
-  u64* pkey;          // pair key, kEmpty64 = empty slot
-  u64* pcnt;          // its count in the corpus
-  uint32_t* inf;      // per slot: 1 while in the frontier
+  u64* tab;           // slot h: tab[2h] pair key (kEmpty64 = empty), tab[2h + 1] count | pos + 1 << 48
   u64 pmask;
   uint32_t* fr[2];    // frontier buffers (slots); st[kSelBuf] says which is current
   uint32_t fcap;
@@ -131,7 +131,8 @@ constexpr uint32_t kSelDone = 1, kSelRebuild = 2, kSelFull = 3;
 // (below the threshold, or merged) are compacted away in LDS.  When more than kSelF - kSelRoom
 // stay live the launch ends for a rebuild (a compaction per merge would cost more).
 constexpr uint32_t kSelF = 1536, kSelK = 768, kSelRoom = 384, kSelSlack = 96;
-constexpr uint32_t kInfReserved = 0xFFFFFFFFu;  // a slot being appended
+constexpr u64 kCntMask = (1ull << 48) - 1;  // the count in a slot's count word; pos + 1 above it
+constexpr int kPosShift = 48;
 template <bool kOn>
 struct SelLds {  // k_word_loop<false>: none
   u64 key[1], cnt[1];
@@ -195,41 +196,47 @@ __device__ __forceinline__ u64 ld_agent64(const u64* p) {
 __device__ __forceinline__ bool sel_better(u64 c, u64 k, u64 c2, u64 k2) { return c > c2 || (c == c2 && k < k2); }
 __device__ __forceinline__ bool sel_at_least(u64 c, u64 k, u64 tc, u64 tk) { return c > tc || (c == tc && k <= tk); }
 // The table slot of pair key pk, inserted when absent (~0 when the table is past its probe bound).
-__device__ __forceinline__ u64 sel_slot(const SelParams& q, u64 pk) {
+// ins / err: counters of inserts and probe overflows (LDS in the loop, global in k_sel_insert).
+__device__ __forceinline__ u64 sel_slot(const SelParams& q, u64 pk, uint32_t* ins, uint32_t* err) {
   u64 h = mix64(pk) & q.pmask;
 #pragma unroll 1
   for (uint32_t probe = 0; probe < 4096u; ++probe) {
-    const u64 cur = ld_agent64(q.pkey + h);
+    const u64 cur = ld_agent64(q.tab + 2 * h);
     if (cur == pk) return h;
     if (cur == kEmpty64) {
-      const u64 prev = atomicCAS(q.pkey + h, kEmpty64, pk);
+      const u64 prev = atomicCAS(q.tab + 2 * h, kEmpty64, pk);
       if (prev == kEmpty64) {
-        atomicAdd(q.st + kSelIns, 1u);
+        atomicAdd(ins, 1u);
         return h;
       }
       if (prev == pk) return h;
     }
     h = (h + 1) & q.pmask;
   }
-  atomicMax(q.st + kSelErr, 1u);
+  atomicMax(err, 1u);
   return ~0ull;
 }
 // One combined record of merge (a, b) -> X as a change of a pair's count (the reference's
 // FreqChangeMap entry, bpe.cpp:297-313, minus the pair merged and pairs holding unk).  New pairs
 // (categories 1 and 3: they hold X) are listed for the frontier.
-__device__ __forceinline__ void sel_apply(const SelParams& q, SelLds<true>& F, uint32_t* nnew, int32_t unk, uint32_t cap,
-                                          uint32_t key, u64 sum, int32_t a, int32_t b, int32_t X) {
+__device__ __forceinline__ void sel_apply(const SelParams& q, SelLds<true>& F, uint32_t* nnew, uint32_t* ins, uint32_t* err,
+                                          int32_t unk, uint32_t cap, uint32_t key, u64 sum, int32_t a, int32_t b,
+                                          int32_t X) {
   const uint32_t sl = key >> 2, cat = key & 3u;
   const int32_t id = sl == 0 ? unk : (int32_t)(sl - 1u);
   if (id == unk || sum == 0) return;
   const int32_t f = cat < 2u ? id : (cat == 2u ? b : X);
   const int32_t g = cat == 0u ? a : (cat == 1u ? X : id);
   if (f == a && g == b) return;
-  const u64 h = sel_slot(q, pair_key(f, g));
+  const u64 h = sel_slot(q, pair_key(f, g), ins, err);
   if (h == ~0ull) return;
   const u64 d = (cat & 1u) ? sum : (u64)(-(int64_t)sum);
-  atomicAdd(q.pcnt + h, d);
-  const uint32_t pos = ld_agent(q.inf + h) - 1u;  // in the frontier: its LDS count too
+  // the count word's old value says where the LDS copy is.  A pair in the frontier holds no X, so
+  // it only falls and never below 0: its position bits are intact.  A new pair (holding X) is not
+  // in the frontier yet; a decrement landing before its increment may borrow through the
+  // position bits (reading as 0xFFFF, "not in the frontier") and the increment carries them back.
+  const u64 old = atomicAdd(q.tab + 2 * h + 1, d);
+  const uint32_t pos = (uint32_t)(old >> kPosShift) - 1u;
   if (pos < kSelF) atomicAdd(reinterpret_cast<unsigned long long*>(&F.cnt[pos]), (unsigned long long)d);
   if (cat & 1u) q.upd[atomicAdd(nnew, 1u)] = (uint32_t)h;
   (void)cap;
@@ -446,7 +453,7 @@ struct LoopS {
   u64 occ, t[2];
   u64 t_wait, t_idle, t_undo;  // s_memrealtime: this command's wait began; idle / undo since the last flag
   // tiebreak=device
-  uint32_t sm, snk, snew, status, sel_pos, sover, scompact;
+  uint32_t sm, snk, snew, status, sel_pos, sover, scompact, sins, serr;
   u64 sel_slot;
   u64 bc[kWlThreads / 64], bk[kWlThreads / 64];
   uint32_t bs[kWlThreads / 64];
@@ -480,14 +487,18 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     const uint32_t nf = min(ld_agent(q.st + kSelNF), kSelK);
     for (uint32_t i = tid; i < nf; i += kWlThreads) {
       const uint32_t sl = ld_agent(q.fr[0] + i);
+      const u64 c = ld_agent64(q.tab + 2 * (u64)sl + 1) & kCntMask;
       s_f.slot[i] = sl;
-      s_f.key[i] = ld_agent64(q.pkey + sl);
-      s_f.cnt[i] = ld_agent64(q.pcnt + sl);
-      __hip_atomic_store(q.inf + sl, i + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_f.key[i] = ld_agent64(q.tab + 2 * (u64)sl);
+      s_f.cnt[i] = c;
+      __hip_atomic_store(q.tab + 2 * (u64)sl + 1, c | ((u64)(i + 1u) << kPosShift), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid == 0) {
       s_f.n = nf;
       S.scompact = 0;
+      S.sins = ld_agent(q.st + kSelIns);  // the table's inserts so far (the host's and earlier launches')
+      S.serr = 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -510,7 +521,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       uint32_t bs = kEmpty32, live = 0;
       for (uint32_t i = tid; i < nf; i += kWlThreads) {
         const u64 c = s_f.cnt[i], k = s_f.key[i];
-        if (sel_at_least(c, k, tc, tk)) {
+        if (k != kEmpty64 && sel_at_least(c, k, tc, tk)) {
           ++live;
           if (sel_better(c, k, bc, bk)) {
             bc = c;
@@ -852,19 +863,20 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       __syncthreads();
       for (int i = tid; i < kDh; i += kWlThreads) {
         const uint32_t key = s_h.key[i];
-        if (key != kEmpty32) sel_apply(q, s_f, &S.snew, p.unk, p.cap, key, s_h.sum[i], a, b, X);
+        if (key != kEmpty32) sel_apply(q, s_f, &S.snew, &S.sins, &S.serr, p.unk, p.cap, key, s_h.sum[i], a, b, X);
       }
       const uint32_t nsp = S.nspill;
       for (uint32_t i = tid; i < nsp; i += kWlThreads) {
         const uint32_t key = p.dlist[i];
         const u64 sum = atomicExch(&p.dsum[key], 0ull);
         atomicExch(&p.dft[key], kEmpty64);
-        sel_apply(q, s_f, &S.snew, p.unk, p.cap, key, sum, a, b, X);
+        sel_apply(q, s_f, &S.snew, &S.sins, &S.serr, p.unk, p.cap, key, sum, a, b, X);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) {
-        __hip_atomic_store(q.pcnt + S.sel_slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) {  // the merged pair: count 0 (it never occurs again), still at its LDS position
+        __hip_atomic_store(q.tab + 2 * S.sel_slot + 1, (u64)(S.sel_pos + 1u) << kPosShift, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
         s_f.cnt[S.sel_pos] = 0;
         S.sover = 0;
       }
@@ -872,14 +884,17 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       const uint32_t nnew = S.snew;
       for (uint32_t i = tid; i < nnew; i += kWlThreads) {
         const uint32_t sl = q.upd[i];
-        const u64 c = ld_agent64(q.pcnt + sl), k = ld_agent64(q.pkey + sl);
-        if (sel_at_least(c, k, tc, tk) && atomicCAS(q.inf + sl, 0u, kInfReserved) == 0u) {
+        const u64 k = ld_agent64(q.tab + 2 * (u64)sl), cv = ld_agent64(q.tab + 2 * (u64)sl + 1);
+        const u64 c = cv & kCntMask;
+        if ((cv >> kPosShift) == 0 && sel_at_least(c, k, tc, tk)) {
+          // a place first, then the claim (a pair listed twice claims once; the loser's place
+          // stays a dead entry)
           const uint32_t pos = atomicAdd(&s_f.n, 1u);
           if (pos < kSelF) {
+            const bool won = atomicCAS(q.tab + 2 * (u64)sl + 1, cv, c | ((u64)(pos + 1u) << kPosShift)) == cv;
             s_f.slot[pos] = sl;
-            s_f.key[pos] = k;
-            s_f.cnt[pos] = c;
-            __hip_atomic_store(q.inf + sl, pos + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_f.key[pos] = won ? k : kEmpty64;
+            s_f.cnt[pos] = won ? c : 0;
           } else {
             S.sover = 1;  // the frontier lost an entry: rebuild
           }
@@ -905,7 +920,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
             ck[j] = s_f.cnt[i];
             kk[j] = s_f.key[i];
             sk[j] = s_f.slot[i];
-            if (sel_at_least(ck[j], kk[j], tc, tk)) {
+            if (kk[j] != kEmpty64 && sel_at_least(ck[j], kk[j], tc, tk)) {
               keepm |= 1u << j;
               ++mine;
             }
@@ -927,10 +942,11 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
             s_f.cnt[base] = ck[j];
             s_f.key[base] = kk[j];
             s_f.slot[base] = sk[j];
-            __hip_atomic_store(q.inf + sk[j], base + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(q.tab + 2 * (u64)sk[j] + 1, ck[j] | ((u64)(base + 1u) << kPosShift), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
             ++base;
-          } else {
-            __hip_atomic_store(q.inf + sk[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else if (kk[j] != kEmpty64) {  // (a dead place of a lost claim owns no slot)
+            __hip_atomic_store(q.tab + 2 * (u64)sk[j] + 1, ck[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -959,7 +975,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         q.st[kSelBuf] = S.scompact;  // (statistic: LDS compactions of this launch)
         // after a complete merge: a frontier that lost an entry needs a rebuild, a table past its
         // fill bound must grow (the host stops)
-        const uint32_t full = ld_agent(q.st + kSelIns) > q.fill_max || ld_agent(q.st + kSelErr) != 0;
+        const uint32_t full = S.sins > q.fill_max || S.serr != 0;
         S.status = full ? kSelFull : (S.sover ? kSelRebuild : 0u);
       }
       __syncthreads();
@@ -1037,6 +1053,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   if (tid == 0) {
     p.dstate[kStPoolTop] = S.pool_top;
     if constexpr (kSelf) {
+      p.sel.st[kSelIns] = S.sins;
+      p.sel.st[kSelErr] = S.serr;
       p.sel.st[kSelStatus] = exit_op;
       __threadfence_system();
       return;
@@ -1193,13 +1211,14 @@ inline u64 sel_bucket_lo(uint32_t b) {
   return (u64)(256u + mant) << (lg - 8u);
 }
 
-__global__ void k_sel_hist(const u64* pkey, const u64* pcnt, u64 n, u64 minf, uint32_t* hist) {
+__global__ void k_sel_hist(u64* tab, u64 n, u64 minf, uint32_t* hist) {
   __shared__ uint32_t h[kSelLds];
   for (uint32_t i = threadIdx.x; i < kSelLds; i += blockDim.x) h[i] = 0;
   __syncthreads();
   for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-    const u64 c = pcnt[i];
-    if (pkey[i] == kEmpty64 || c < minf) continue;
+    const u64 cv = tab[2 * i + 1], c = cv & kCntMask;
+    if (cv >> kPosShift) tab[2 * i + 1] = c;  // the last launch's frontier positions are void now
+    if (tab[2 * i] == kEmpty64 || c < minf) continue;
     const uint32_t b = sel_bucket(c);
     if (b < kSelLds) atomicAdd(&h[b], 1u);
     else atomicAdd(&hist[b], 1u);
@@ -1209,15 +1228,15 @@ __global__ void k_sel_hist(const u64* pkey, const u64* pcnt, u64 n, u64 minf, ui
     if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-__global__ void k_sel_collect(const u64* pkey, const u64* pcnt, u64 n, u64 minf, uint32_t bstar, uint32_t* out,
-                              uint32_t* nout, u64 cap) {
+__global__ void k_sel_collect(const u64* tab, u64 n, u64 minf, uint32_t bstar, uint32_t* out, uint32_t* nout,
+                              u64 cap) {
   const int lane = threadIdx.x & 63;
   for (u64 i0 = blockIdx.x * (u64)blockDim.x; i0 < n; i0 += (u64)gridDim.x * blockDim.x) {
     const u64 i = i0 + threadIdx.x;
     bool take = false;
     if (i < n) {
-      const u64 c = pcnt[i];
-      take = pkey[i] != kEmpty64 && c >= minf && sel_bucket(c) >= bstar;
+      const u64 c = tab[2 * i + 1] & kCntMask;
+      take = tab[2 * i] != kEmpty64 && c >= minf && sel_bucket(c) >= bstar;
     }
     const u64 bl = __ballot(take);
     if (!bl) continue;
@@ -1230,35 +1249,39 @@ __global__ void k_sel_collect(const u64* pkey, const u64* pcnt, u64 n, u64 minf,
   }
 }
 
-__global__ void k_sel_gather(const uint32_t* slots, uint32_t n, const u64* pkey, const u64* pcnt, u64* key,
-                             u64* negc, uint32_t* idx) {
+__global__ void k_sel_gather(const uint32_t* slots, uint32_t n, const u64* tab, u64* key, u64* negc, uint32_t* idx) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    key[i] = pkey[slots[i]];
-    negc[i] = ~pcnt[slots[i]];
+    key[i] = tab[2 * (u64)slots[i]];
+    negc[i] = ~(tab[2 * (u64)slots[i] + 1] & kCntMask);
     idx[i] = i;
   }
 }
 
 // idx: the sorted order; the first n of the collected slots in that order -> the frontier
-__global__ void k_sel_pick(const uint32_t* slots, const uint32_t* idx, uint32_t n, uint32_t* fr, uint32_t* inf) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t s = slots[idx ? idx[i] : i];
-    fr[i] = s;
-    inf[s] = 1u;
-  }
+__global__ void k_sel_pick(const uint32_t* slots, const uint32_t* idx, uint32_t n, uint32_t* fr) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    fr[i] = slots[idx ? idx[i] : i];
 }
 
 __global__ void k_sel_insert(const PairCount* pc, uint64_t n, SelParams q) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const u64 h = sel_slot(q, pair_key(pc[i].a, pc[i].b));
-    if (h != ~0ull) q.pcnt[h] = pc[i].count;
+    const u64 h = sel_slot(q, pair_key(pc[i].a, pc[i].b), q.st + kSelIns, q.st + kSelErr);
+    if (h != ~0ull) q.tab[2 * h + 1] = pc[i].count & kCntMask;
+  }
+}
+
+// An empty table: every key kEmpty64, every count word 0.
+__global__ void k_sel_clear(u64* tab, u64 n) {
+  for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    tab[2 * i] = kEmpty64;
+    tab[2 * i + 1] = 0;
   }
 }
 
 // The live pairs of a table (count > 0), for a bigger one.
-__global__ void k_sel_export(const u64* pkey, const u64* pcnt, u64 cap, PairCount* out, uint32_t* n) {
+__global__ void k_sel_export(const u64* tab, u64 cap, PairCount* out, uint32_t* n) {
   for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < cap; i += (u64)gridDim.x * blockDim.x) {
-    const u64 k = pkey[i], c = pcnt[i];
+    const u64 k = tab[2 * i], c = tab[2 * i + 1] & kCntMask;
     if (k == kEmpty64 || c == 0) continue;
     const uint32_t j = atomicAdd(n, 1u);
     out[j] = PairCount{(int32_t)(uint32_t)(k >> 32), (int32_t)(uint32_t)k, c, 0};
@@ -1790,11 +1813,11 @@ void WordLoop::stop() {
 // tiebreak=device
 
 void WordLoop::sel_free() {
-  void* ptrs[] = {pkey_, pcnt_, pinf_, fr_[0], fr_[1], sst_dev_, thr_, sout_, upd_, shist_, scol_};
+  void* ptrs[] = {ptab_, fr_[0], fr_[1], sst_dev_, thr_, sout_, upd_, shist_, scol_};
   for (void* q : ptrs)
     if (q) WL_OK(hipFree(q));
-  pkey_ = pcnt_ = thr_ = sout_ = nullptr;
-  pinf_ = fr_[0] = fr_[1] = sst_dev_ = upd_ = shist_ = scol_ = nullptr;
+  ptab_ = thr_ = sout_ = nullptr;
+  fr_[0] = fr_[1] = sst_dev_ = upd_ = shist_ = scol_ = nullptr;
   pcap_ = sout_cap_ = upd_cap_ = scol_cap_ = 0;
   fcap_ = 0;
 }
@@ -1806,7 +1829,7 @@ bool WordLoop::sel_rebuild(uint64_t min_freq) {
   const double t0 = now_seconds();
   hipStream_t s = S(stream_);
   WL_OK(hipMemsetAsync(shist_, 0, kSelBuckets * sizeof(uint32_t), s));
-  k_sel_hist<<<1024, 512, 0, s>>>(pkey_, pcnt_, pcap_, min_freq, shist_);
+  k_sel_hist<<<1024, 512, 0, s>>>(ptab_, pcap_, min_freq, shist_);
   WL_OK(hipGetLastError());
   std::vector<uint32_t> hist(kSelBuckets);
   WL_OK(hipMemcpyAsync(hist.data(), shist_, kSelBuckets * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -1821,7 +1844,6 @@ bool WordLoop::sel_rebuild(uint64_t min_freq) {
   }
   uint32_t st[kSelStats] = {};
   WL_OK(hipMemcpyAsync(st, sst_dev_, sizeof(st), hipMemcpyDeviceToHost, s));
-  WL_OK(hipMemsetAsync(pinf_, 0, pcap_ * sizeof(uint32_t), s));
   WL_OK(hipStreamSynchronize(s));
   u64 thr[2] = {~0ull, 0ull};
   uint32_t nf = 0;
@@ -1833,7 +1855,7 @@ bool WordLoop::sel_rebuild(uint64_t min_freq) {
     }
     uint32_t* ncol = scol_ + scol_cap_;
     WL_OK(hipMemsetAsync(ncol, 0, sizeof(uint32_t), s));
-    k_sel_collect<<<1024, 512, 0, s>>>(pkey_, pcnt_, pcap_, min_freq, bstar, scol_, ncol, scol_cap_);
+    k_sel_collect<<<1024, 512, 0, s>>>(ptab_, pcap_, min_freq, bstar, scol_, ncol, scol_cap_);
     WL_OK(hipGetLastError());
     uint32_t nc = 0;
     WL_OK(hipMemcpyAsync(&nc, ncol, sizeof(nc), hipMemcpyDeviceToHost, s));
@@ -1841,7 +1863,7 @@ bool WordLoop::sel_rebuild(uint64_t min_freq) {
     if (nc != acc) fatal("tiebreak=device: the frontier's collect disagrees with its histogram");
     if (nc <= kSelK) {  // every pair of the top buckets: the threshold is their lowest count
       nf = nc;
-      k_sel_pick<<<64, 256, 0, s>>>(scol_, nullptr, nf, fr_[0], pinf_);
+      k_sel_pick<<<64, 256, 0, s>>>(scol_, nullptr, nf, fr_[0]);
       WL_OK(hipGetLastError());
       thr[0] = std::max<u64>(sel_bucket_lo(bstar), min_freq);
       thr[1] = ~0ull;
@@ -1853,7 +1875,7 @@ bool WordLoop::sel_rebuild(uint64_t min_freq) {
       u64* negc2 = wl_alloc<u64>(nc, &acc2);
       uint32_t* idx = wl_alloc<uint32_t>(nc, &acc2);
       uint32_t* idx2 = wl_alloc<uint32_t>(nc, &acc2);
-      k_sel_gather<<<256, 256, 0, s>>>(scol_, nc, pkey_, pcnt_, key, negc, idx);
+      k_sel_gather<<<256, 256, 0, s>>>(scol_, nc, ptab_, key, negc, idx);
       WL_OK(hipGetLastError());
       size_t tb = 0, tb2 = 0;
       WL_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, idx, idx2, (int)nc, 0, 64, s));
@@ -1861,7 +1883,7 @@ bool WordLoop::sel_rebuild(uint64_t min_freq) {
       void* tmp = wl_alloc<uint8_t>(std::max(tb, tb2), &acc2);
       WL_OK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, key2, idx, idx2, (int)nc, 0, 64, s));
       // counts in key order, then a stable sort by ~count
-      k_sel_gather<<<256, 256, 0, s>>>(scol_, nc, pkey_, pcnt_, key, negc, idx);  // key/negc of slot order
+      k_sel_gather<<<256, 256, 0, s>>>(scol_, nc, ptab_, key, negc, idx);  // key/negc of slot order
       WL_OK(hipGetLastError());
       std::vector<uint32_t> order(nc);
       std::vector<u64> kc(nc), nn(nc);
@@ -1876,7 +1898,7 @@ bool WordLoop::sel_rebuild(uint64_t min_freq) {
       WL_OK(hipMemcpyAsync(idx, order.data(), nc * sizeof(uint32_t), hipMemcpyHostToDevice, s));
       WL_OK(hipcub::DeviceRadixSort::SortPairs(tmp, tb2, negc, negc2, idx, idx2, (int)nc, 0, 64, s));
       nf = kSelK;
-      k_sel_pick<<<64, 256, 0, s>>>(scol_, idx2, nf, fr_[0], pinf_);
+      k_sel_pick<<<64, 256, 0, s>>>(scol_, idx2, nf, fr_[0]);
       WL_OK(hipGetLastError());
       uint32_t last = 0;
       WL_OK(hipMemcpyAsync(&last, idx2 + (nf - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -1942,18 +1964,13 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
   SelParams q{};
   auto table_from = [&](const PairCount* dp, size_t np, uint64_t cap) {  // a fresh table holding dp
     if (cap != pcap_) {
-      for (void* t : {(void*)pkey_, (void*)pcnt_, (void*)pinf_})
-        if (t) WL_OK(hipFree(t));
+      if (ptab_) WL_OK(hipFree(ptab_));
       pcap_ = cap;
-      pkey_ = wl_alloc<u64>(pcap_, &bytes_);
-      pcnt_ = wl_alloc<u64>(pcap_, &bytes_);
-      pinf_ = wl_alloc<uint32_t>(pcap_, &bytes_);
+      ptab_ = wl_alloc<u64>(2 * pcap_, &bytes_);
     }
-    WL_OK(hipMemsetAsync(pkey_, 0xFF, pcap_ * sizeof(u64), s));
-    WL_OK(hipMemsetAsync(pcnt_, 0, pcap_ * sizeof(u64), s));
-    q.pkey = pkey_;
-    q.pcnt = pcnt_;
-    q.inf = pinf_;
+    k_sel_clear<<<1024, 256, 0, s>>>(ptab_, pcap_);
+    WL_OK(hipGetLastError());
+    q.tab = ptab_;
     q.pmask = pcap_ - 1;
     q.fr[0] = fr_[0];
     q.fr[1] = fr_[1];
@@ -2035,21 +2052,18 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
         PairCount* dp = wl_alloc<PairCount>(pcap_, &acc);
         uint32_t* dn = wl_alloc<uint32_t>(1, &acc);
         WL_OK(hipMemsetAsync(dn, 0, sizeof(uint32_t), s));
-        k_sel_export<<<1024, 256, 0, s>>>(pkey_, pcnt_, pcap_, dp, dn);
+        k_sel_export<<<1024, 256, 0, s>>>(ptab_, pcap_, dp, dn);
         WL_OK(hipGetLastError());
         uint32_t np = 0;
         WL_OK(hipMemcpyAsync(&np, dn, sizeof(np), hipMemcpyDeviceToHost, s));
         WL_OK(hipStreamSynchronize(s));
         // the exported pairs must survive the old table's release: keep them in their own buffer
         const uint64_t grown = 4 * pcap_;
-        u64* ok = pkey_;
-        u64* oc = pcnt_;
-        uint32_t* oi = pinf_;
-        pkey_ = pcnt_ = nullptr;
-        pinf_ = nullptr;
+        u64* old = ptab_;
+        ptab_ = nullptr;
         pcap_ = 0;
         table_from(dp, np, grown);
-        for (void* t : {(void*)ok, (void*)oc, (void*)oi}) WL_OK(hipFree(t));
+        WL_OK(hipFree(old));
         WL_OK(hipFree(dp));
         WL_OK(hipFree(dn));
         ++sst_.grows;

@@ -232,9 +232,7 @@ class WordLoop {
   // tiebreak=device: pair table, frontier, state (see word_loop.hip SelParams)
   void sel_free();
   bool sel_rebuild(uint64_t min_freq);  // false: no pair at or above min_freq is left
-  unsigned long long* pkey_ = nullptr;
-  unsigned long long* pcnt_ = nullptr;
-  uint32_t* pinf_ = nullptr;
+  unsigned long long* ptab_ = nullptr;  // tiebreak=device pair table: 16-B slots (key, count | pos)
   uint64_t pcap_ = 0;
   uint32_t* fr_[2] = {nullptr, nullptr};
   uint32_t fcap_ = 0;
