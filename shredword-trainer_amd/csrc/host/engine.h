@@ -120,7 +120,7 @@ class Engine {
   // Early guess (default on; SHREDWORD_EARLY_GUESS=0 or option early_guess=0 turns it off): the
   // guess for X+2 is posted right after X is applied, before the select of X+1 (see merge_one).
   void set_early_guess(bool on) { early_guess_ = on; }
-  // Apply helper (default on; SHREDWORD_APPLY_HELPER=0 or option apply_helper=0 turns it off): a
+  // Apply helper (opt-in; SHREDWORD_APPLY_HELPER=1 or option apply_helper=1): a
   // second host thread combines and orders the records of the guess in flight (Selector::prepare)
   // while this thread selects; a confirmed guess then only has its changes walked and pushed.
   void set_apply_helper(bool on) { helper_on_ = on; }
@@ -190,7 +190,7 @@ class Engine {
     Selector::Prepared out;
   };
   Helper* helper_ = nullptr;
-  bool helper_on_ = true;
+  bool helper_on_ = false;  // C3 +0.7%, C4 80 GB -20% (profiles/r04_c4_80g_option_ab.json): off by default
   uint64_t helper_used_ = 0;
   void helper_start();
   void helper_stop();

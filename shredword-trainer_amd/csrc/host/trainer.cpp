@@ -234,7 +234,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   t->engine.set_speculation(env_int("SHREDWORD_SPECULATE", 1) != 0);
   t->engine.set_correction(env_int("SHREDWORD_CORRECT", 1) != 0);
   t->engine.set_early_guess(env_int("SHREDWORD_EARLY_GUESS", 1) != 0);
-  t->engine.set_apply_helper(env_int("SHREDWORD_APPLY_HELPER", 1) != 0);
+  t->engine.set_apply_helper(env_int("SHREDWORD_APPLY_HELPER", 0) != 0);
   if (const char* v = std::getenv("SHREDWORD_CHAIN")) set_option(t, "chain", v);
   t->engine.set_verify(env_int("SHREDWORD_VERIFY_ARGMAX", 0));
   if (const char* v = std::getenv("SHREDWORD_DIST")) set_option(t, "dist", v);
