@@ -246,8 +246,10 @@ bool Engine::merge_one(Backend& be, int remaining) {
   // will pop (the guess for X+1 and every pair sharing its tokens counted as changing), and posted
   // at once, so the device has X+2 queued before it finishes X+1.  The selects of X+1 happen after
   // the post (the heap replay is off the device's path); a wrong guess for X+1 undoes both.
+  // (merges with many records are device-heavy: a wrong second guess then wastes a long merge and
+  // its undo on the device; early_max_records bounds where the early guess is made)
   if (early_guess_ && spec && chain == 1 && pending_.size() == 1 && pending_.front().X == X + 1 && remaining > 2 &&
-      be.can_overlap() && be.max_guesses() >= 2) {
+      be.can_overlap() && be.max_guesses() >= 2 && (uint64_t)sel_.last_records() <= early_max_records_) {
     const Guess g1 = pending_.front();
     used_.assign({g1.a, g1.b});
     Guess g{0, 0, X + 2};

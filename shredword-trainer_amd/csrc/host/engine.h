@@ -120,6 +120,8 @@ class Engine {
   // Early guess (default on; SHREDWORD_EARLY_GUESS=0 or option early_guess=0 turns it off): the
   // guess for X+2 is posted right after X is applied, before the select of X+1 (see merge_one).
   void set_early_guess(bool on) { early_guess_ = on; }
+  // ... only after merges with at most this many delta records (default: always).
+  void set_early_max_records(uint64_t n) { early_max_records_ = n; }
   // Apply helper (opt-in; SHREDWORD_APPLY_HELPER=1 or option apply_helper=1): a
   // second host thread combines and orders the records of the guess in flight (Selector::prepare)
   // while this thread selects; a confirmed guess then only has its changes walked and pushed.
@@ -175,6 +177,7 @@ class Engine {
   int train_device(Backend& be, double t0);
   bool correct_ = true;
   bool early_guess_ = true;
+  uint64_t early_max_records_ = ~0ull;
   uint64_t corrections_ = 0;
   uint64_t verify_checks_ = 0, verify_fail_ = 0;
   uint64_t host_phase_merges_ = 0;

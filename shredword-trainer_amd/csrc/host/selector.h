@@ -185,6 +185,7 @@ class Selector {
     uint64_t cyc_combine = 0, cyc_order = 0, cyc_walk = 0, cyc_push = 0;  // TSC cycles inside apply()
   };
   const Counters& counters() const { return ctr_; }
+  size_t last_records() const { return own_.records; }  // the current merge's delta records
 
  private:
   // One flat open-addressing table: a lookup touches one cache line.  kEmptyKey is the packed

@@ -94,6 +94,8 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
     t->engine.set_speculation(std::atoi(val.c_str()) != 0);
   } else if (key == "early_guess") {
     t->engine.set_early_guess(std::atoi(val.c_str()) != 0);
+  } else if (key == "early_max_records") {
+    t->engine.set_early_max_records(std::strtoull(val.c_str(), nullptr, 10));
   } else if (key == "apply_helper") {
     t->engine.set_apply_helper(std::atoi(val.c_str()) != 0);
   } else if (key == "exchange" || key == "exchange_bucket") {
@@ -235,6 +237,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   t->engine.set_correction(env_int("SHREDWORD_CORRECT", 1) != 0);
   t->engine.set_early_guess(env_int("SHREDWORD_EARLY_GUESS", 1) != 0);
   t->engine.set_apply_helper(env_int("SHREDWORD_APPLY_HELPER", 0) != 0);
+  if (const char* e = std::getenv("SHREDWORD_EARLY_MAX_RECORDS")) t->engine.set_early_max_records(std::strtoull(e, nullptr, 10));
   if (const char* v = std::getenv("SHREDWORD_CHAIN")) set_option(t, "chain", v);
   t->engine.set_verify(env_int("SHREDWORD_VERIFY_ARGMAX", 0));
   if (const char* v = std::getenv("SHREDWORD_DIST")) set_option(t, "dist", v);

@@ -54,7 +54,7 @@ def main():
     say(f"loaded in {time.time() - t0:.1f} s")
     res = {"config": args.config, "corpus_bytes": cfg["bytes"], "runs": []}
     tmpd = os.environ.get("TMPDIR", "/tmp")
-    defaults = {"early_guess": "1", "apply_helper": "1", "switch_occ": "4000"}
+    defaults = {"early_guess": "1", "apply_helper": "0", "switch_occ": "4000", "early_max_records": str(2**63)}
     for setting in args.set:
         opts = dict(defaults)
         if setting != "-":
