@@ -235,7 +235,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   if (const char* v = std::getenv("SHREDWORD_TRACE")) set_option(t, "trace", v);
   t->engine.set_speculation(env_int("SHREDWORD_SPECULATE", 1) != 0);
   t->engine.set_correction(env_int("SHREDWORD_CORRECT", 1) != 0);
-  t->engine.set_early_guess(env_int("SHREDWORD_EARLY_GUESS", 1) != 0);
+  t->engine.set_early_guess(env_int("SHREDWORD_EARLY_GUESS", 0) != 0);
   t->engine.set_apply_helper(env_int("SHREDWORD_APPLY_HELPER", 0) != 0);
   if (const char* e = std::getenv("SHREDWORD_EARLY_MAX_RECORDS")) t->engine.set_early_max_records(std::strtoull(e, nullptr, 10));
   if (const char* v = std::getenv("SHREDWORD_CHAIN")) set_option(t, "chain", v);

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None, index=1, spec_depth=None, speculate=None,
-           hybrid=None, switch_occ=None, verify=None):
+           hybrid=None, switch_occ=None, verify=None, **opts):
     from shredword.trainer import BPETrainer
 
     cfg = case["config"]
@@ -34,6 +34,8 @@ def _train(case, corpus, tmp_path, layout="types", resident=1, stats=None, index
         t.set_option("speculate", speculate)
     if verify is not None:
         t.set_option("verify_argmax", verify)
+    for k, v in opts.items():
+        t.set_option(k, v)
     t.load_corpus(corpus)
     merges = t.train()
     model, vocab = str(tmp_path / "g.model"), str(tmp_path / "g.vocab")
@@ -222,3 +224,15 @@ def test_sharded_load_two_processes_on_gpu(name, case_corpus, tmp_path):
     for r in range(2):
         assert open(tmp_path / f"r{r}.model", "rb").read() == case["model_bytes"]
         assert open(tmp_path / f"r{r}.vocab", "rb").read() == case["vocab_bytes"]
+
+
+@pytest.mark.parametrize("path", ["hybrid", "index", "resident"])
+@pytest.mark.parametrize("name", ["adv_cov05", "ascii1m_v3000_mpf2", "mixed2m_v4000", "utf8_4m_v8192_mpf5",
+                                  "utf8_24m_v32000_mpf2"])
+def test_opt_in_host_pipelining_matches_reference(name, path, case_corpus, tmp_path):
+    """The opt-in host pipelining (early_guess: two guesses in flight; apply_helper: a second host
+    thread combining the guessed merge's records) on the merge paths: the reference's bytes."""
+    case, corpus = case_corpus(name)
+    kw = {"hybrid": {}, "index": {"hybrid": 0}, "resident": {"index": 0}}[path]
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, stats=st, early_guess=1, apply_helper=1, **kw))

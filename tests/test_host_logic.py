@@ -205,14 +205,16 @@ def test_sharded_load_ranges_match_reference(name, hh, case_corpus, tmp_path, mo
 
 @pytest.mark.parametrize("name", ["ascii1m_v3000_mpf2", "utf8_4m_v8192_mpf5", "mixed2m_v4000", "adv_unk3_cov09"])
 def test_apply_helper_gives_the_reference_bytes(name, hh, case_corpus, tmp_path):
-    """The apply helper (a second host thread combining and ordering the guessed merge's records
-    while the selector selects) on and off: both the reference's trace and files, and the helper
-    actually took merges when on."""
+    """The opt-in host pipelining -- the apply helper (a second host thread combining and ordering
+    the guessed merge's records while the selector selects) and the early guess (two guesses in
+    flight) -- on and off: both the reference's trace and files, and the helper actually took
+    merges when on."""
     case, corpus = case_corpus(name)
     for on in (1, 0):
         h = hostharness.open_case(hh, corpus, case["config"], "types")
         try:
             hh.hh_set_apply_helper(h, on)
+            hh.hh_set_early_guess(h, on)
             trace = str(tmp_path / f"t{on}.txt")
             merges = hh.hh_train(h, trace.encode())
             used = hh.hh_helper_used(h)
