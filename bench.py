@@ -49,6 +49,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -148,6 +149,37 @@ def pin_host_loop(local_rank):
     except OSError:
         return None
     return dom
+
+
+def pin_exclusive(dom):
+    """The host loop (this thread) alone on one core of its L3 domain: the thread on the domain's
+    second core, every other thread of the process (HIP runtime, torch, loaders) moved off that
+    core and its SMT sibling.  Threads this one starts later inherit its one-CPU mask, so call it
+    after the load.  Returns the CPU, or None when the domain is too small."""
+    if not dom or len(dom) < 4:
+        return None
+    cpu = sorted(dom)[1]
+    sib = {cpu}
+    try:
+        with open(f"/sys/devices/system/cpu/cpu{cpu}/topology/thread_siblings_list") as f:
+            for part in f.read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                sib.update(range(int(lo), int(hi or lo) + 1))
+    except OSError:
+        pass
+    others = set(range(os.cpu_count() or 1)) - sib  # (the kernel intersects it with the cpuset)
+    me = threading.get_native_id()
+    try:
+        for tid in os.listdir("/proc/self/task"):
+            if int(tid) != me and others:
+                try:
+                    os.sched_setaffinity(int(tid), others)
+                except OSError:
+                    pass
+        os.sched_setaffinity(0, {cpu})
+    except OSError:
+        return None
+    return cpu
 
 
 def cpu_baseline_start(cfg, path, seconds):
@@ -726,6 +758,7 @@ def main():
             raise RuntimeError("bpe_train failed")
         return n
 
+    excl = pin_exclusive(pinned) if (pinned and os.environ.get("SHREDWORD_PIN_EXCLUSIVE", "0") == "1") else None
     for _ in range(args.warmup):
         train_step()
     t.set_option("timing", 1)
@@ -740,6 +773,8 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - start
+    if excl is not None:
+        os.sched_setaffinity(0, set(pinned))  # the later legs and the CPU baseline on the domain again
     all_merges = merges
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64)
@@ -836,7 +871,9 @@ def main():
                      "note": ("load_corpus: page-in + PCIe upload + device word count + host table; outside the timed "
                               "step" + ("; each rank counts its byte range, the word lists are all-gathered and "
                                         "merged on every rank" if one_job else ""))},
-            "host_cpus": (f"pinned to the L3 domain {pinned[0]}-{pinned[-1]} ({len(pinned)} CPUs)" if pinned
+            "host_cpus": (f"pinned to the L3 domain {pinned[0]}-{pinned[-1]} ({len(pinned)} CPUs)"
+                          + (f"; the host loop alone on CPU {excl} (no other thread on its core)" if excl is not None else "")
+                          if pinned
                           else "not pinned"),
             "host_breakdown_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
             "init_s_last_step": st["init_seconds"],
