@@ -151,6 +151,28 @@ def pin_host_loop(local_rank):
     return dom
 
 
+def host_thp():
+    """Transparent huge pages of this process (the selector's heap and pair table ask for them:
+    a select walks the heap's levels, one TLB entry per 2 MiB instead of per 4 KiB) and the
+    kernel's THP settings."""
+    out = {}
+    try:
+        with open("/proc/self/smaps_rollup") as f:
+            for line in f:
+                if line.startswith(("AnonHugePages:", "Anonymous:")):
+                    k, v = line.split(":", 1)
+                    out[k.strip() + "_kB"] = int(v.split()[0])
+    except OSError:
+        pass
+    for name in ("enabled", "defrag"):
+        try:
+            with open(f"/sys/kernel/mm/transparent_hugepage/{name}") as f:
+                out[name] = f.read().strip()
+        except OSError:
+            pass
+    return out
+
+
 def pin_exclusive(dom):
     """The host loop (this thread) alone on one core of its L3 domain: the thread on the domain's
     second core, every other thread of the process (HIP runtime, torch, loaders) moved off that
@@ -871,6 +893,7 @@ def main():
                      "note": ("load_corpus: page-in + PCIe upload + device word count + host table; outside the timed "
                               "step" + ("; each rank counts its byte range, the word lists are all-gathered and "
                                         "merged on every rank" if one_job else ""))},
+            "host_thp": host_thp(),
             "host_cpus": (f"pinned to the L3 domain {pinned[0]}-{pinned[-1]} ({len(pinned)} CPUs)"
                           + (f"; the host loop alone on CPU {excl} (no other thread on its core)" if excl is not None else "")
                           if pinned
