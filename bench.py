@@ -795,6 +795,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - start
+    thp = host_thp()  # while the trainer's selector tables are still mapped
     if excl is not None:
         os.sched_setaffinity(0, set(pinned))  # the later legs and the CPU baseline on the domain again
     all_merges = merges
@@ -893,7 +894,7 @@ def main():
                      "note": ("load_corpus: page-in + PCIe upload + device word count + host table; outside the timed "
                               "step" + ("; each rank counts its byte range, the word lists are all-gathered and "
                                         "merged on every rank" if one_job else ""))},
-            "host_thp": host_thp(),
+            "host_thp": thp,
             "host_cpus": (f"pinned to the L3 domain {pinned[0]}-{pinned[-1]} ({len(pinned)} CPUs)"
                           + (f"; the host loop alone on CPU {excl} (no other thread on its core)" if excl is not None else "")
                           if pinned
