@@ -128,10 +128,32 @@ def l3_domain(cpu):
     return [cpu]
 
 
-def pin_host_loop(local_rank):
+def gpu_numa_cpus(dev):
+    """The CPUs of the NUMA node the GPU `dev` hangs off (sysfs of its PCI function), or None."""
+    try:
+        import torch
+        pr = torch.cuda.get_device_properties(dev)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read().strip())
+        if node < 0:
+            return None
+        cpus = set()
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            for part in f.read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                cpus.update(range(int(lo), int(hi or lo) + 1))
+        return cpus
+    except Exception:  # noqa: BLE001 (no sysfs entry, no torch property: keep the plain choice)
+        return None
+
+
+def pin_host_loop(local_rank, dev=None):
     """Keeps this rank's threads on one last-level-cache domain (the host replay's heap and pair
     table live in that cache; a migration to another CCD starts cold).  Rank r takes the (r+1)-th
-    domain of the allowed CPUs; the last CPU stays free for the CPU baseline."""
+    domain of the allowed CPUs; the last CPU stays free for the CPU baseline.  With
+    SHREDWORD_PIN_NUMA=1 the domains come from the NUMA node of the rank's GPU (the records and
+    commands cross PCIe to pinned host memory every merge)."""
     allowed = sorted(os.sched_getaffinity(0))
     if len(allowed) < 4:
         return None
@@ -142,8 +164,19 @@ def pin_host_loop(local_rank):
         d = [x for x in l3_domain(c) if x != allowed[-1]]
         seen.update(d)
         domains.append(d)
+    near = gpu_numa_cpus(dev) if (dev is not None and os.environ.get("SHREDWORD_PIN_NUMA", "0") == "1") else None
+    if near:
+        local = [d for d in domains if set(d) <= near]
+        if local:
+            # ranks on the same node take its domains in turn; past CPU 0's domain when possible
+            start = 1 if len(local) > 1 and 0 in local[0] else 0
+            return _pin(local[(start + local_rank) % len(local)])
     # the domain of CPU 0 takes most of the OS's interrupts and housekeeping: start past it
     dom = domains[(local_rank + 1) % len(domains)] if len(domains) > 1 else domains[0]
+    return _pin(dom)
+
+
+def _pin(dom):
     try:
         os.sched_setaffinity(0, set(dom))
     except OSError:
@@ -730,7 +763,7 @@ def main():
     if sim_shards:
         os.environ.setdefault("SHREDWORD_LOAD_SIM_SHARDS", str(sim_shards))
 
-    pinned = None if args.no_pin else pin_host_loop(local)
+    pinned = None if args.no_pin else pin_host_loop(local, dev)
     from shredword import dist as sdist
     from shredword.cbase import lib
     from shredword.trainer import BPETrainer
