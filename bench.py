@@ -151,9 +151,10 @@ def gpu_numa_cpus(dev):
 def pin_host_loop(local_rank, dev=None):
     """Keeps this rank's threads on one last-level-cache domain (the host replay's heap and pair
     table live in that cache; a migration to another CCD starts cold).  Rank r takes the (r+1)-th
-    domain of the allowed CPUs; the last CPU stays free for the CPU baseline.  With
-    SHREDWORD_PIN_NUMA=1 the domains come from the NUMA node of the rank's GPU (the records and
-    commands cross PCIe to pinned host memory every merge)."""
+    domain of the allowed CPUs; the last CPU stays free for the CPU baseline.  The domains come
+    from the NUMA node of the rank's GPU (the records and commands cross PCIe to pinned host memory
+    every merge: C3 A/B on one box 54.8-55.6 k on the far socket, 56.1-56.3 k on the GPU's;
+    SHREDWORD_PIN_NUMA=0 for the plain choice)."""
     allowed = sorted(os.sched_getaffinity(0))
     if len(allowed) < 4:
         return None
@@ -164,7 +165,7 @@ def pin_host_loop(local_rank, dev=None):
         d = [x for x in l3_domain(c) if x != allowed[-1]]
         seen.update(d)
         domains.append(d)
-    near = gpu_numa_cpus(dev) if (dev is not None and os.environ.get("SHREDWORD_PIN_NUMA", "0") == "1") else None
+    near = gpu_numa_cpus(dev) if (dev is not None and os.environ.get("SHREDWORD_PIN_NUMA", "1") == "1") else None
     if near:
         local = [d for d in domains if set(d) <= near]
         if local:
