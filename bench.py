@@ -788,8 +788,14 @@ def main():
     t.set_option("layout", args.layout)
     t.set_option("tiebreak", args.tiebreak)
     if torch_gather:
-        t.set_load_gather(rank, world, sdist.host_load_gather(dist.new_group(backend="nccl")))
-        gather_via = "torch.distributed all_gather_object over an nccl (RCCL, xGMI) group"
+        try:
+            ggroup = dist.new_group(backend="nccl")
+            gather_via = "torch.distributed all_gather_object over an nccl (RCCL, xGMI) group"
+        except Exception as e:  # noqa: BLE001
+            print(f"[WARNING]\t nccl group unavailable ({e!r}); the load gathers over gloo", file=sys.stderr)
+            ggroup = None
+            gather_via = "torch.distributed all_gather_object over the gloo group (nccl unavailable)"
+        t.set_load_gather(rank, world, sdist.host_load_gather(ggroup, fallback=dist.group.WORLD))
     elif one_job and not share:
         t.set_option("dist", args.dist)
     elif one_job:

@@ -37,10 +37,11 @@ def finalize():
     lib.shred_dist_finalize()
 
 
-def host_load_gather(group=None):
+def host_load_gather(group=None, fallback=None):
     """A shred_gather_fn over torch.distributed (BPETrainer.set_load_gather): the sharded load's
     word-list all-gather on `group` -- gloo when ranks share a GPU, an nccl group (torch's RCCL over
-    xGMI) when each rank has its own, the bench's default for replicate.  The returned callback
+    xGMI) when each rank has its own, the bench's default for replicate; `fallback` (e.g. the
+    default gloo group) is used when the collective on `group` raises.  The returned callback
     keeps its last result alive until its next call, as the C ABI requires."""
     import torch.distributed as dist
 
@@ -53,7 +54,15 @@ def host_load_gather(group=None):
         try:
             mine = ctypes.string_at(send, nbytes) if nbytes else b""
             parts = [None] * dist.get_world_size(group)
-            dist.all_gather_object(parts, mine, group=group)
+            try:
+                dist.all_gather_object(parts, mine, group=group)
+            except Exception as e:  # noqa: BLE001 (e.g. the nccl group failed to come up on every rank)
+                if fallback is None:
+                    raise
+                import sys
+                print(f"[WARNING]\t host_load_gather: {e!r}; gathering over the fallback group", file=sys.stderr)
+                parts = [None] * dist.get_world_size(fallback)
+                dist.all_gather_object(parts, mine, group=fallback)
             blob = b"".join(parts)
             keep["buf"] = ctypes.create_string_buffer(blob, max(1, len(blob)))
             out_bytes[0] = len(blob)
