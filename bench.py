@@ -773,10 +773,14 @@ def main():
     if one_job and share and args.dist == "exchange":
         raise SystemExit("bench: --dist exchange needs one GPU per rank (RCCL per merge); use --dist replicate")
     gather_via = None
+    gather_state = {}
     # replicate on a GPU per rank: the load's gather over torch.distributed's RCCL (an nccl group
     # beside the gloo one) unless --load-gather rccl asks for the library's own communicator;
     # exchange needs the library's communicator (a collective per merge)
-    torch_gather = one_job and not share and args.dist == "replicate" and args.load_gather == "torch"
+    # (SHREDWORD_BENCH_NCCL_GATHER=1 takes that path even on a shared card: a rehearsal of the
+    # gloo fallback, since RCCL refuses the group there)
+    force_nccl = os.environ.get("SHREDWORD_BENCH_NCCL_GATHER", "0") == "1"
+    torch_gather = one_job and (not share or force_nccl) and args.dist == "replicate" and args.load_gather == "torch"
     if one_job and not share and not torch_gather:
         sdist.init_from_env(device=dev)
         gather_via = "RCCL all-gather over xGMI (dist_allgather_bytes)"
@@ -795,7 +799,9 @@ def main():
             print(f"[WARNING]\t nccl group unavailable ({e!r}); the load gathers over gloo", file=sys.stderr)
             ggroup = None
             gather_via = "torch.distributed all_gather_object over the gloo group (nccl unavailable)"
-        t.set_load_gather(rank, world, sdist.host_load_gather(ggroup, fallback=dist.group.WORLD))
+        t.set_load_gather(rank, world, sdist.host_load_gather(ggroup, fallback=dist.group.WORLD, state=gather_state))
+        if share and args.layout == "types":
+            t.set_option("resident", 0)
     elif one_job and not share:
         t.set_option("dist", args.dist)
     elif one_job:
@@ -808,6 +814,9 @@ def main():
     t.load_corpus(path)
     load_s = time.time() - t0
     load_s_max = load_s
+    if gather_state.get("fell_back"):
+        gather_via = ("torch.distributed all_gather_object over the gloo group (the nccl gather raised: "
+                      + gather_state["fell_back"].splitlines()[-1][:160] + ")")
     if dist is not None:
         tl = torch.tensor([load_s], dtype=torch.float64)
         dist.all_reduce(tl, op=dist.ReduceOp.MAX)

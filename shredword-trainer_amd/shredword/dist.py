@@ -37,11 +37,12 @@ def finalize():
     lib.shred_dist_finalize()
 
 
-def host_load_gather(group=None, fallback=None):
+def host_load_gather(group=None, fallback=None, state=None):
     """A shred_gather_fn over torch.distributed (BPETrainer.set_load_gather): the sharded load's
     word-list all-gather on `group` -- gloo when ranks share a GPU, an nccl group (torch's RCCL over
     xGMI) when each rank has its own, the bench's default for replicate; `fallback` (e.g. the
-    default gloo group) is used when the collective on `group` raises.  The returned callback
+    default gloo group) is used when the collective on `group` raises (state["fell_back"] = the
+    error, when a dict is given).  The returned callback
     keeps its last result alive until its next call, as the C ABI requires."""
     import torch.distributed as dist
 
@@ -53,14 +54,20 @@ def host_load_gather(group=None, fallback=None):
         # which reads as "no words"): report a NULL result and the library fails load_corpus.
         try:
             mine = ctypes.string_at(send, nbytes) if nbytes else b""
-            parts = [None] * dist.get_world_size(group)
             try:
+                if keep.get("fell_back"):
+                    raise RuntimeError("an earlier gather on this group raised")
+                parts = [None] * dist.get_world_size(group)
                 dist.all_gather_object(parts, mine, group=group)
             except Exception as e:  # noqa: BLE001 (e.g. the nccl group failed to come up on every rank)
                 if fallback is None:
                     raise
-                import sys
-                print(f"[WARNING]\t host_load_gather: {e!r}; gathering over the fallback group", file=sys.stderr)
+                if not keep.get("fell_back"):
+                    import sys
+                    print(f"[WARNING]\t host_load_gather: {e!r}; gathering over the fallback group", file=sys.stderr)
+                    keep["fell_back"] = True
+                    if state is not None:
+                        state["fell_back"] = str(e) or repr(e)
                 parts = [None] * dist.get_world_size(fallback)
                 dist.all_gather_object(parts, mine, group=fallback)
             blob = b"".join(parts)

@@ -26,11 +26,16 @@ def main():
     t.set_option("log", 0)
     if os.environ.get("TRAIN") == "1":
         t.set_option("resident", 0)  # ranks share one GPU here: the whole-chip loop would not be co-resident
-    t.set_load_gather(rank, world, sdist.host_load_gather())
+    state = {}
+    if os.environ.get("BROKEN_GROUP") == "1":  # a group whose gather raises on every rank: the fallback carries it
+        t.set_load_gather(rank, world, sdist.host_load_gather(object(), fallback=dist.group.WORLD, state=state))
+    else:
+        t.set_load_gather(rank, world, sdist.host_load_gather())
     t.load_corpus(corpus)
     st = t.stats()
     info = {"rank": rank, "num_words": st["num_words"], "num_symbols": st["num_symbols"],
-            "num_occurrences": st["num_occurrences"], "load_on_gpu": st["load_on_gpu"]}
+            "num_occurrences": st["num_occurrences"], "load_on_gpu": st["load_on_gpu"],
+            "fell_back": bool(state.get("fell_back"))}
     if os.environ.get("TRAIN") == "1":
         info["merges"] = t._train(t.trainer)
         t._save(t.trainer, os.path.join(outdir, f"r{rank}.model").encode(),

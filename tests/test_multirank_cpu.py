@@ -132,3 +132,16 @@ def test_product_sharded_load_over_host_gather(world, case_corpus, tmp_path):
     many = _run_product_ranks(corpus, case["config"], world, tmp_path)
     keys = ("num_words", "num_symbols", "num_occurrences")
     assert all(tuple(i[k] for k in keys) == tuple(one[0][k] for k in keys) for i in many)
+
+
+def test_product_sharded_load_gather_fallback(case_corpus, tmp_path):
+    """host_load_gather(group, fallback=WORLD): when the collective on `group` raises on every rank
+    (bench: the nccl group on a box where RCCL refuses it), the word lists go over the fallback
+    group and the merged table is unchanged."""
+    case, corpus = case_corpus("utf8_4m_v8192_mpf5")
+    (tmp_path / "one").mkdir()
+    one = _run_product_ranks(corpus, case["config"], 1, tmp_path / "one")
+    many = _run_product_ranks(corpus, case["config"], 2, tmp_path, env={"BROKEN_GROUP": "1"})
+    keys = ("num_words", "num_symbols", "num_occurrences")
+    assert all(i["fell_back"] for i in many)
+    assert all(tuple(i[k] for k in keys) == tuple(one[0][k] for k in keys) for i in many)
