@@ -127,6 +127,9 @@ class Engine {
   // second host thread combines and orders the records of the guess in flight (Selector::prepare)
   // while this thread selects; a confirmed guess then only has its changes walked and pushed.
   void set_apply_helper(bool on) { helper_on_ = on; }
+  // Heap slots the overlap guess (Selector::predict_avoid) may look at (default 256;
+  // SHREDWORD_PRED_WINDOW overrides).
+  void set_pred_window(size_t n) { pred_window_ = n ? n : 1; }
   uint64_t helper_used() const { return helper_used_; }
   ~Engine();
   uint64_t corrections() const { return corrections_; }

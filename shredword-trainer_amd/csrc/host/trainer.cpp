@@ -238,6 +238,7 @@ Trainer* create_trainer(const BPEConfig* config) {
   t->engine.set_early_guess(env_int("SHREDWORD_EARLY_GUESS", 0) != 0);
   t->engine.set_apply_helper(env_int("SHREDWORD_APPLY_HELPER", 0) != 0);
   if (const char* e = std::getenv("SHREDWORD_EARLY_MAX_RECORDS")) t->engine.set_early_max_records(std::strtoull(e, nullptr, 10));
+  if (const char* e = std::getenv("SHREDWORD_PRED_WINDOW")) t->engine.set_pred_window(std::strtoull(e, nullptr, 10));
   if (const char* v = std::getenv("SHREDWORD_CHAIN")) set_option(t, "chain", v);
   t->engine.set_verify(env_int("SHREDWORD_VERIFY_ARGMAX", 0));
   if (const char* v = std::getenv("SHREDWORD_DIST")) set_option(t, "dist", v);
