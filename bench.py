@@ -73,6 +73,25 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
+def size_label(nbytes: int) -> str:
+    for unit, div in (("GB", 10**9), ("MB", 10**6), ("kB", 10**3)):
+        if nbytes >= div:
+            v = nbytes / div
+            return f"{v:g} {unit}"
+    return f"{nbytes} B"
+
+
+def workload_label(name: str, cfg: dict, default_bytes: int) -> str:
+    """config.workload: the named config's description, or, when --bytes changed the corpus size,
+    the parameters actually run (a 10 GB run was labelled "100 GB")."""
+    if cfg["bytes"] == default_bytes:
+        return cfg["desc"]
+    script = {"ascii": "ASCII", "utf8": "UTF-8", "mixed": "mixed-script"}[cfg["script"]]
+    return (f"{name.upper()} parameters at {size_label(cfg['bytes'])}: BPE vocab_size={cfg['vocab']} "
+            f"min_pair_freq={cfg['mpf']} coverage={cfg['cov']} on a {size_label(cfg['bytes'])} synthetic {script} "
+            f"corpus (seed {cfg['seed']}; the {name.upper()} config itself is {size_label(default_bytes)})")
+
+
 def log(msg):
     print(msg, file=sys.stderr, flush=True)
 
@@ -913,7 +932,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic (committed deterministic generator, SURVEY.md §8 d2)",
             "config": {
-                "workload": cfg["desc"],
+                "workload": workload_label(args.config, cfg, CONFIGS[args.config]["bytes"]),
                 "corpus_bytes": cfg["bytes"], "seed": cfg["seed"], "script": cfg["script"],
                 "vocab_size": cfg["vocab"], "min_pair_freq": cfg["mpf"], "character_coverage": cfg["cov"],
                 "unk_id": cfg["unk"], "layout": args.layout,

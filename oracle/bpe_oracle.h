@@ -53,6 +53,11 @@ void or_set_tiebreak(OrTrainer* t, int mode, long after);
  * "B batch done heap_size top_freq" per batch (bpe.cpp:369).  NULL disables. */
 void or_set_trace(OrTrainer* t, const char* path);
 void or_set_progress(OrTrainer* t, long every);  /* > 0: PROGRESS lines on stderr every `every` merges */
+/* n > 1: each merge's recount and merge scan split over n threads (word ranges); same output. */
+void or_set_threads(OrTrainer* t, int n);
+/* The last or_load's bytes read and number of distinct byte values. */
+uint64_t or_load_bytes(const OrTrainer* t);
+int or_load_unique_bytes(const OrTrainer* t);
 
 /* Introspection for unit tests. */
 size_t or_num_words(const OrTrainer* t);

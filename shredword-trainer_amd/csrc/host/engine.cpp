@@ -22,11 +22,36 @@ void Engine::forget_merges() {
   sel_.reset(unk_, min_freq_);
 }
 
+void Engine::refresh_selector(Backend& be) {
+  if (!selector_stale_) return;
+  selector_stale_ = false;
+  sel_.reset(unk_, min_freq_);
+  std::vector<PairCount> pairs;
+  be.count_pairs(unk_, &pairs);
+  sel_.add_counts(std::move(pairs));
+}
+
+void Engine::check_exact(Backend& be) {
+  if (!verify_exact_ || !sel_.exact() || selector_stale_) return;
+  std::vector<PairCount> fresh;
+  be.count_pairs(unk_, &fresh);
+  ++exact_checks_;
+  const size_t bad = sel_.exact_mismatches(fresh);
+  if (bad) {
+    if (!exact_fail_)
+      std::fprintf(stderr, "[ERROR]\t exactness check after %zu merges: %zu pair counts differ from a fresh K1\n",
+                   merge_a_.size(), bad);
+    ++exact_fail_;
+  }
+}
+
 void Engine::count_bigrams(Backend& be) {
+  refresh_selector(be);
   std::vector<PairCount> pairs;
   be.count_pairs(unk_, &pairs);
   const size_t unique = pairs.size();
   sel_.add_counts(std::move(pairs));
+  check_exact(be);
   if (log_ >= 1)
     std::printf("[INFO]\t Counted %zu unique pairs\n[INFO]\t Added %zu pairs to heap (freq >= %llu)\n", unique,
                 sel_.heap_size(), (unsigned long long)min_freq_);
@@ -93,7 +118,7 @@ void Engine::helper_offer(Backend& be) {
 void Engine::finish_speculation(Backend& be) {
   if (pending_.empty()) return;
   helper_drain();  // the helper may be reading a guess's records: done before they are undone
-  be.rollback(pending_.front().X);
+  be.undo_guesses(pending_.front().X);
   pending_.clear();
   ++spec_misses_;
 }
@@ -103,7 +128,7 @@ void Engine::finish_speculation(Backend& be) {
 void Engine::verify_selection(Backend& be, int32_t a, int32_t b, uint64_t freq) {
   if (!pending_.empty()) {
     helper_drain();
-    be.rollback(pending_.front().X);
+    be.undo_guesses(pending_.front().X);
     pending_.clear();
   }
   uint64_t mx = 0, fab = 0;
@@ -165,6 +190,7 @@ bool Engine::merge_one(Backend& be, int remaining) {
     const Guess& g = pending_.front();
     if (g.X == X && g.a == a && g.b == b) {
       launched = true;
+      if (g.posted) be.guess_confirmed();
       pending_.erase(pending_.begin());
       ++spec_hits_;
     } else {
@@ -194,11 +220,11 @@ bool Engine::merge_one(Backend& be, int remaining) {
         used_.push_back(p.a);
         used_.push_back(p.b);
       }
-      Guess g{0, 0, X + 1 + (int32_t)pending_.size()};
+      Guess g{0, 0, X + 1 + (int32_t)pending_.size(), true};
       if (!sel_.predict_avoid(used_.data(), used_.size(), pred_window_, &g.a, &g.b)) break;
       pending_.push_back(g);
       ++launches_;
-      be.merge_scan(g.a, g.b, g.X);
+      be.post_guess(g.a, g.b, g.X);
     }
   }
   const double t2 = now_seconds();
@@ -233,12 +259,12 @@ bool Engine::merge_one(Backend& be, int remaining) {
     sel_.lookup(g.a, g.b, &gf, &gv);
     if (sel_.predict_after(X, gf, &pa, &pb, &pf)) {
       helper_drain();
-      be.rollback(g.X);
+      be.undo_guesses(g.X);
       pending_.clear();
-      pending_.push_back({pa, pb, X + 1});
+      pending_.push_back({pa, pb, X + 1, true});
       ++launches_;
       ++corrections_;
-      be.merge_scan(pa, pb, X + 1);
+      be.post_guess(pa, pb, X + 1);
     }
   }
   sel_.apply_finish(a, b, X);
@@ -252,11 +278,11 @@ bool Engine::merge_one(Backend& be, int remaining) {
       be.can_overlap() && be.max_guesses() >= 2 && (uint64_t)sel_.last_records() <= early_max_records_) {
     const Guess g1 = pending_.front();
     used_.assign({g1.a, g1.b});
-    Guess g{0, 0, X + 2};
+    Guess g{0, 0, X + 2, true};
     if (sel_.predict_avoid(used_.data(), used_.size(), pred_window_, &g.a, &g.b)) {
       pending_.push_back(g);
       ++launches_;
-      be.merge_scan(g.a, g.b, g.X);
+      be.post_guess(g.a, g.b, g.X);
     }
   }
   if (spec) helper_offer(be);  // X+1's records, if they have landed
@@ -278,6 +304,7 @@ bool Engine::merge_one(Backend& be, int remaining) {
 }
 
 int Engine::merge_batch(Backend& be, int batch) {
+  refresh_selector(be);
   if (sel_.heap_empty()) {
     if (log_ >= 2) std::printf("[INFO]\t Heap is empty, no more merges possible\n");
     return 0;
@@ -292,6 +319,7 @@ int Engine::merge_batch(Backend& be, int batch) {
   }
   finish_speculation(be);
   be.quiesce();
+  check_exact(be);
   return done;
 }
 
@@ -472,6 +500,9 @@ int Engine::train_device(Backend& be, double t0) {
     }
   }
   be.quiesce();
+  // the host Selector never saw these merges: a later bpe_merge_batch / bpe_count_bigrams first
+  // rebuilds it from a fresh K1 of the merged corpus, as bpe_init would
+  selector_stale_ = true;
   if (trace_) std::fflush(trace_);
   times_.train_s += now_seconds() - t0;
   if (log_ >= 1) std::printf("[INFO]\t Training completed (tiebreak=device). Performed %d merges\n", n);
@@ -482,6 +513,7 @@ int Engine::train(Backend& be) {
   const double t0 = now_seconds();
   if (log_ >= 1) std::printf("[INFO]\t Starting BPE training (target vocab size: %zu)\n", target_vocab_);
   if (tiebreak_device_) return train_device(be, t0);
+  selector_stale_ = false;
   sel_.reset(unk_, min_freq_);  // bpe_init (bpe.cpp:98-108)
   mtrace_on_ = std::getenv("SHREDWORD_ENGINE_TRACE") != nullptr;
   if (const char* e = std::getenv("SHREDWORD_SIM_SELECT")) sel_.set_simulate_pops(std::atoi(e) != 0);
@@ -521,6 +553,7 @@ int Engine::train(Backend& be) {
   be.quiesce();
   if (trace_) std::fflush(trace_);
   times_.train_s += now_seconds() - t0;
+  check_exact(be);
   if (log_ >= 1) std::printf("[INFO]\t Training completed. Performed %d merges\n", total);
   if (const char* tp = std::getenv("SHREDWORD_ENGINE_TRACE")) {
     if (FILE* f = std::fopen(tp, "w")) {

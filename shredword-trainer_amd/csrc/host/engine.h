@@ -11,6 +11,7 @@
 #include <thread>
 #include <vector>
 
+#include "common.h"
 #include "selector.h"
 
 namespace shred {
@@ -27,6 +28,23 @@ class Backend {
     const int32_t ab[2] = {a, b};
     merge_chain(ab, 1, X);
   }
+  // A guess: merge X posted before the merges ahead of it are confirmed.  The backend holds at
+  // most max_guesses() unconfirmed guesses; one more is refused (fatal), never run: a backend
+  // past its depth would miscount (the launch path with two guesses).
+  void post_guess(int32_t a, int32_t b, int32_t X) {
+    if (guesses_ >= max_guesses()) fatal("post_guess: more unconfirmed guesses than the backend holds");
+    ++guesses_;
+    merge_scan(a, b, X);
+  }
+  void guess_confirmed() {
+    if (guesses_ > 0) --guesses_;
+  }
+  // Undoes every unconfirmed guess (rollback from the oldest, X).
+  void undo_guesses(int32_t X) {
+    rollback(X);
+    guesses_ = 0;
+  }
+  int guesses_in_flight() const { return guesses_; }
   virtual size_t collect(int32_t X, const DeltaRecord** recs) = 0;
   // Non-blocking look at the oldest outstanding merge X: true with its records once the device
   // has finished it (they stay valid until X is collected or rolled back).  Default: never.
@@ -72,6 +90,9 @@ class Backend {
       if (p.a == a && p.b == b) *ab_freq = p.count;
     }
   }
+
+ private:
+  int guesses_ = 0;
 };
 
 struct EngineTimes {
@@ -84,7 +105,10 @@ struct EngineTimes {
 class Engine {
  public:
   void configure(size_t target_vocab_size, int32_t unk_id, uint64_t min_pair_freq);
-  void reset_selection() { sel_.reset(unk_, min_freq_); }
+  void reset_selection() {
+    selector_stale_ = false;
+    sel_.reset(unk_, min_freq_);
+  }
   // bpe_load_corpus: the pair map starts fresh, the heap and the merges stay (bpe.cpp:176-183).
   void reload() { sel_.reset_info(); }
   void forget_merges();
@@ -143,6 +167,11 @@ class Engine {
   void set_tiebreak_device(bool on) { tiebreak_device_ = on; }
   bool tiebreak_device() const { return tiebreak_device_; }
   uint64_t verify_checks() const { return verify_checks_; }
+  // Debug: after every count / batch / train, while the selector claims its pair
+  // info is the corpus's exact count, compare it with a fresh K1 (Selector::exact_mismatches).
+  void set_verify_exact(bool on) { verify_exact_ = on; }
+  uint64_t exact_checks() const { return exact_checks_; }
+  uint64_t exact_failures() const { return exact_fail_; }
   uint64_t verify_failures() const { return verify_fail_; }
   uint64_t host_phase_merges() const { return host_phase_merges_; }  // tiebreak=device, selected on the host
   void finish_speculation(Backend& be);  // rolls back unconfirmed guesses (before any other access)
@@ -171,6 +200,7 @@ class Engine {
   size_t pred_window_ = 256;
   struct Guess {
     int32_t a, b, X;
+    bool posted = false;  // its own launch (Backend::post_guess), not the tail of a chain
   };
   std::vector<Guess> pending_;  // launched guesses awaiting confirmation, oldest first
   std::vector<int32_t> used_;
@@ -179,6 +209,11 @@ class Engine {
   int verify_every_ = 0;
   bool tiebreak_device_ = false;
   int train_device(Backend& be, double t0);
+  bool verify_exact_ = false;
+  uint64_t exact_checks_ = 0, exact_fail_ = 0;
+  void check_exact(Backend& be);
+  bool selector_stale_ = false;         // tiebreak=device trained: the heap does not hold the corpus
+  void refresh_selector(Backend& be);   // ... rebuilt from a fresh K1 before the next batch / count
   bool correct_ = true;
   bool early_guess_ = false;
   uint64_t early_max_records_ = ~0ull;

@@ -105,6 +105,24 @@ const Selector::Info* Selector::find(uint64_t key) const {
   }
 }
 
+size_t Selector::exact_mismatches(const std::vector<PairCount>& fresh) const {
+  size_t bad = 0, seen = 0;
+  for (const PairCount& p : fresh) {
+    if (p.a == unk_ || p.b == unk_) continue;
+    const Info* in = find(pack_pair(p.a, p.b));
+    bad += !in || in->freq() != p.count;
+    ++seen;
+  }
+  size_t live = 0;  // infos with a count, unk pairs aside: exactly the fresh count's pairs
+  for (size_t j = 0; j < table_.size(); ++j) {
+    const Info& in = table_[j];
+    if (in.key == kEmptyKey || in.freq() == 0) continue;
+    if (pair_first(in.key) == unk_ || pair_second(in.key) == unk_) continue;
+    ++live;
+  }
+  return bad + (live > seen ? live - seen : 0);
+}
+
 bool Selector::lookup(int32_t a, int32_t b, uint64_t* freq, uint32_t* version) const {
   const Info* in = find(pack_pair(a, b));
   *freq = in ? in->freq() : 0;

@@ -168,6 +168,9 @@ class Selector {
   // True while every pair's info equals its count in the corpus (recompute_freq is then
   // info.freq).  Otherwise select() needs the truth table.
   bool exact() const { return exact_; }
+  // Debug check of exact(): the number of pairs, unk pairs aside, whose info differs
+  // from `fresh` (a fresh K1 of the corpus), counting pairs present on one side only.
+  size_t exact_mismatches(const std::vector<PairCount>& fresh) const;
   bool truth_live() const { return truth_live_; }
   // The corpus's pair counts now (a fresh K1): recompute_freq's values until the corpus changes;
   // each applied merge then updates them by its exact deltas.

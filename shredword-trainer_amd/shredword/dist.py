@@ -41,33 +41,49 @@ def host_load_gather(group=None, fallback=None, state=None):
     """A shred_gather_fn over torch.distributed (BPETrainer.set_load_gather): the sharded load's
     word-list all-gather on `group` -- gloo when ranks share a GPU, an nccl group (torch's RCCL over
     xGMI) when each rank has its own, the bench's default for replicate; `fallback` (e.g. the
-    default gloo group) is used when the collective on `group` raises (state["fell_back"] = the
-    error, when a dict is given).  The returned callback
+    default gloo group) is used when the collective on `group` raises on ANY rank: after every
+    attempt the ranks agree over `fallback` (all_reduce MAX of a failure flag) and fall back all
+    together, for the rest of the load (state["fell_back"] = the error, when a dict is given).
+    The returned callback
     keeps its last result alive until its next call, as the C ABI requires."""
     import torch.distributed as dist
 
     from .cbase import GATHER_FN
     keep = {}
 
+    def agree_failed(failed):
+        """Every rank's verdict on the attempt, over the fallback group: the gather falls back only
+        all together (all_gather_object is two collectives; a rank that fell back alone would wait in
+        a gloo gather the others never join)."""
+        import torch
+        flag = torch.tensor([1 if failed else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=fallback)
+        return bool(flag.item())
+
     def gather(_ctx, send, nbytes, out_bytes):
         # An exception must not cross the C boundary (ctypes would print it and return 0 bytes,
         # which reads as "no words"): report a NULL result and the library fails load_corpus.
         try:
             mine = ctypes.string_at(send, nbytes) if nbytes else b""
-            try:
-                if keep.get("fell_back"):
-                    raise RuntimeError("an earlier gather on this group raised")
-                parts = [None] * dist.get_world_size(group)
-                dist.all_gather_object(parts, mine, group=group)
-            except Exception as e:  # noqa: BLE001 (e.g. the nccl group failed to come up on every rank)
-                if fallback is None:
-                    raise
-                if not keep.get("fell_back"):
+            parts = None
+            if not keep.get("fell_back"):
+                err = None
+                try:
+                    parts = [None] * dist.get_world_size(group)
+                    dist.all_gather_object(parts, mine, group=group)
+                except Exception as e:  # noqa: BLE001 (e.g. the nccl group failed to come up)
+                    if fallback is None:
+                        raise
+                    err = e
+                if fallback is not None and agree_failed(err is not None):
                     import sys
-                    print(f"[WARNING]\t host_load_gather: {e!r}; gathering over the fallback group", file=sys.stderr)
+                    why = (str(err) or repr(err)) if err is not None else "the gather raised on another rank"
+                    print(f"[WARNING]\t host_load_gather: {why}; every rank gathers over the fallback group",
+                          file=sys.stderr)
                     keep["fell_back"] = True
                     if state is not None:
-                        state["fell_back"] = str(e) or repr(e)
+                        state["fell_back"] = why
+            if keep.get("fell_back"):
                 parts = [None] * dist.get_world_size(fallback)
                 dist.all_gather_object(parts, mine, group=fallback)
             blob = b"".join(parts)

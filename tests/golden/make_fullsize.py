@@ -15,6 +15,12 @@ by every golden in tests/golden/*/ (tests/test_oracle.py), including the referen
 
 Corpora are regenerated from the recipe (bin/gen_corpus) and their md5 is checked.  Usage:
     python tests/golden/make_fullsize.py c2 [c3 ...]       (minutes for c2, ~1 h for c3)
+
+The two largest configs (C4 80 GB, C5 100 GB; VERDICT r04 missing 1) never touch the disk: the
+generator streams through ``tee`` (md5sum on the side) into the oracle's streaming reader
+(``bpe_oracle /dev/stdin``, read once in order, fgets semantics unchanged), and the oracle's two
+O(S) scans per merge run on ``--threads`` host threads (same output: tests/test_oracle.py).
+    python tests/golden/make_fullsize.py --threads 4 c5
 """
 from __future__ import annotations
 
@@ -45,7 +51,12 @@ CASES = {
     # C4's parameters (vocab 32000, min_pair_freq 2000, seed 4) on one 10 GB shard-sized corpus:
     # the GPU test loads it as 8 byte ranges (the sharded load of C4) and must match this run
     "c4_10g": (10_000_000_000, 4, "utf8", (32000, 0, 0.995, 2000)),
+    # the full-size C4 and C5 corpora of bench.py CONFIGS, streamed (no file)
+    "c4": (80_000_000_000, 4, "utf8", (32000, 0, 0.995, 2000)),
+    "c5": (100_000_000_000, 5, "mixed", (64000, 0, 0.9995, 2000)),
 }
+STREAM_FROM = 20_000_000_000   # corpora this large are streamed, not written
+GEN = os.path.join(REPO, "shredword-trainer_amd", "bin", "gen_corpus")
 
 
 def corpus_file(name: str, nbytes: int, seed: int, script: str) -> str:
@@ -83,20 +94,49 @@ def md5_bytes(b: bytes) -> str:
     return hashlib.md5(b).hexdigest()
 
 
-def make(name: str) -> None:
+def run_streamed(name, nbytes, seed, script, oracle_args, tmp, threads, gen_threads):
+    """gen_corpus -> tee (md5sum) -> bpe_oracle /dev/stdin.  Returns (stderr text, corpus md5)."""
+    md5_path = tmp + ".md5"
+    if os.path.exists(md5_path):
+        os.unlink(md5_path)
+    err_path = tmp + ".err"
+    cmd = (f"set -o pipefail; {GEN} --bytes {nbytes} --seed {seed} --script {script} --out /dev/stdout "
+           f"--threads {gen_threads} | tee >(md5sum > {md5_path}) | {ORACLE_EXE} /dev/stdin "
+           + " ".join(oracle_args) + f" --threads {threads} 2> {err_path}")
+    subprocess.run(["bash", "-c", cmd], check=True)
+    for _ in range(600):   # the md5sum process substitution may end just after the pipeline
+        if os.path.exists(md5_path) and os.path.getsize(md5_path) >= 32:
+            break
+        time.sleep(1)
+    md5 = open(md5_path).read().split()[0]
+    err = open(err_path).read()
+    os.unlink(md5_path)
+    return err, md5
+
+
+def make(name: str, threads: int = 1, gen_threads: int = 3) -> None:
     nbytes, seed, script, (vocab, unk, cov, mpf) = CASES[name]
-    path = corpus_file(name, nbytes, seed, script)
-    md5, nbyte = corpus_stats(path)
     d = os.path.join(OUT, name)
     os.makedirs(d, exist_ok=True)
     tmp = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"fullsize_{name}")
+    oracle_args = [str(vocab), str(unk), repr(cov), str(mpf), tmp + ".model", tmp + ".vocab",
+                   "--trace", tmp + ".trace", "--progress", "256"]
     t0 = time.time()
-    proc = subprocess.run([ORACLE_EXE, path, str(vocab), str(unk), repr(cov), str(mpf), tmp + ".model",
-                           tmp + ".vocab", "--trace", tmp + ".trace", "--progress", "256"],
-                          stderr=subprocess.PIPE, check=True)
+    streamed = nbytes >= STREAM_FROM
+    if streamed:
+        err, md5 = run_streamed(name, nbytes, seed, script, oracle_args, tmp, threads, gen_threads)
+        nbyte = None
+    else:
+        path = corpus_file(name, nbytes, seed, script)
+        md5, nbyte = corpus_stats(path)
+        proc = subprocess.run([ORACLE_EXE, path] + oracle_args + ["--threads", str(threads)],
+                              stderr=subprocess.PIPE, check=True)
+        err = proc.stderr.decode()
     wall = time.time() - t0
-    err = proc.stderr.decode()
     fields = dict(kv.split("=") for kv in err.split("TIMING", 1)[1].split())
+    if nbyte is None:
+        nbyte = int(fields["unique_bytes"])
+    assert int(fields["bytes"]) == nbytes, (fields["bytes"], nbytes)
     # measured cost curve: cumulative train seconds after every 256 merges (bench.py extrapolates
     # its capped CPU baseline along this curve)
     curve = [[int(l.split()[1]), float(l.split()[2])] for l in err.splitlines() if l.startswith("PROGRESS ")]
@@ -114,8 +154,8 @@ def make(name: str) -> None:
         "merges": int(fields["merges"]),
         "model_md5": md5_bytes(model), "vocab_md5": md5_bytes(vocabb), "vocab_bytes": len(vocabb),
         "oracle": {"exe": "oracle/_build/bpe_oracle", "load_s": float(fields["load"]),
-                   "train_s": float(fields["train"]), "wall_s": wall,
-                   "cpu": cpu_model(), "progress": curve},
+                   "train_s": float(fields["train"]), "wall_s": wall, "threads": threads,
+                   "streamed": streamed, "cpu": cpu_model(), "progress": curve},
     }
     with open(os.path.join(d, "case.json"), "w") as f:
         json.dump(case, f, indent=1)
@@ -126,5 +166,11 @@ def make(name: str) -> None:
 
 
 if __name__ == "__main__":
-    for n in sys.argv[1:] or ["c2"]:
-        make(n)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("names", nargs="*", default=["c2"])
+    ap.add_argument("--threads", type=int, default=1, help="oracle scan threads (same output)")
+    ap.add_argument("--gen-threads", type=int, default=3)
+    a = ap.parse_args()
+    for n in a.names:
+        make(n, a.threads, a.gen_threads)

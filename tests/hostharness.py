@@ -45,6 +45,13 @@ def load():
     lib.hh_verify_failures.argtypes = [ctypes.c_void_p]
     lib.hh_verify_failures.restype = ctypes.c_uint64
     lib.hh_set_early_guess.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.hh_set_verify_exact.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    for fn in ("hh_exact_checks", "hh_exact_failures"):
+        getattr(lib, fn).argtypes = [ctypes.c_void_p]
+        getattr(lib, fn).restype = ctypes.c_uint64
+    lib.hh_set_max_guesses.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.hh_post_guesses.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.c_int32]
+    lib.hh_post_guesses.restype = ctypes.c_int
     lib.hh_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     lib.hh_trace_line.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     lib.hh_save.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]

@@ -273,7 +273,8 @@ class EmuBackend : public Backend {
   // are selected on the host (Engine::train_device) before device_select takes over.
   void set_device_phase(int k) { phase_ = phase_left_ = k < 0 ? 0 : k; }
   bool device_select_now() const override { return phase_left_ == 0; }
-  int max_guesses() const override { return 3; }
+  int max_guesses() const override { return max_guesses_; }
+  int max_guesses_ = 3;   // hh_set_max_guesses: the launch path's 1
 
   void token_freq(size_t T, std::vector<uint64_t>* freq) override {
     freq->assign(T, 0);
@@ -439,6 +440,24 @@ int hh_load(void* p, const char* path) {
 }
 
 void hh_set_early_guess(void* p, int on) { ((Harness*)p)->engine.set_early_guess(on != 0); }
+void hh_set_verify_exact(void* p, int on) { ((Harness*)p)->engine.set_verify_exact(on != 0); }
+uint64_t hh_exact_checks(void* p) { return ((Harness*)p)->engine.exact_checks(); }
+uint64_t hh_exact_failures(void* p) { return ((Harness*)p)->engine.exact_failures(); }
+void hh_set_max_guesses(void* p, int n) {
+  Harness* h = (Harness*)p;
+  if (h->be) h->be->max_guesses_ = n;
+}
+// Posts n guesses straight through Backend::post_guess (pairs (a_i, b_i), ids X0 + i), then
+// undoes them; returns the guesses that were in flight.  Past max_guesses the post is fatal.
+int hh_post_guesses(void* p, const int32_t* ab, int n, int32_t X0) {
+  Harness* h = (Harness*)p;
+  if (!h->be) return -1;
+  h->be->reserve_ids(X0 + n);
+  for (int i = 0; i < n; ++i) h->be->post_guess(ab[2 * i], ab[2 * i + 1], X0 + i);
+  const int in_flight = h->be->guesses_in_flight();
+  h->be->undo_guesses(X0);
+  return in_flight;
+}
 void hh_set_tiebreak_device(void* p, int on) { ((Harness*)p)->engine.set_tiebreak_device(on != 0); }
 void hh_set_device_phase(void* p, int k) {
   Harness* h = (Harness*)p;

@@ -29,6 +29,12 @@ def main():
     state = {}
     if os.environ.get("BROKEN_GROUP") == "1":  # a group whose gather raises on every rank: the fallback carries it
         t.set_load_gather(rank, world, sdist.host_load_gather(object(), fallback=dist.group.WORLD, state=state))
+    elif os.environ.get("BROKEN_GROUP") == "last":
+        # only the last rank's gather raises; the others' "succeeds" on a group without it (a
+        # partial list): every rank must still fall back together and build the whole table
+        alone = dist.new_group(list(range(world - 1)))
+        grp = object() if rank == world - 1 else alone
+        t.set_load_gather(rank, world, sdist.host_load_gather(grp, fallback=dist.group.WORLD, state=state))
     else:
         t.set_load_gather(rank, world, sdist.host_load_gather())
     t.load_corpus(corpus)

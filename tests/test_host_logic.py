@@ -117,6 +117,7 @@ def run_script_harness(hh, case, ops, tmp_path):
     h = hh.hh_create(cfg["vocab_size"], cfg["unk_id"], cfg["character_coverage"], cfg["min_pair_freq"])
     trace = str(tmp_path / "seq_trace.txt")
     hh.hh_set_trace(h, trace.encode())
+    hh.hh_set_verify_exact(h, 1)  # the selector's exact() claim checked against a fresh K1 after every op
     outputs, returns = [], []
     try:
         for op in ops:
@@ -137,6 +138,7 @@ def run_script_harness(hh, case, ops, tmp_path):
                 outputs.append((open(m, "rb").read(), open(v, "rb").read()))
             returns.append([op[0], str(ret)])
             hh.hh_trace_line(h, f"S {op[0]} {ret}\n".encode())
+        assert hh.hh_exact_failures(h) == 0, "the selector claimed exact counts that a fresh K1 contradicts"
     finally:
         hh.hh_close(h)
     return open(trace).read(), outputs, returns
@@ -226,3 +228,64 @@ def test_apply_helper_gives_the_reference_bytes(name, hh, case_corpus, tmp_path)
         assert open(trace).read() == case["trace"]
         assert open(m, "rb").read() == case["model_bytes"] and open(v, "rb").read() == case["vocab_bytes"]
         assert (used > merges // 2) if on else used == 0
+
+
+_POST_GUESSES = r"""
+import ctypes, sys
+sys.path.insert(0, {tests!r})
+import hostharness
+lib = hostharness.load()
+h = hostharness.open_case(lib, {corpus!r}, {cfg!r})
+lib.hh_init(h)
+lib.hh_set_max_guesses(h, {max_guesses})
+ab = (ctypes.c_int32 * 4)(116, 104, 101, 32)
+print("IN_FLIGHT", lib.hh_post_guesses(h, ab, 2, 256), flush=True)
+"""
+
+
+@pytest.mark.parametrize("max_guesses", [1, 2])
+def test_backend_refuses_a_guess_past_its_depth(max_guesses, case_corpus, tmp_path):
+    """a backend that holds one guess (the launch path) must refuse a second
+    unconfirmed one with a fatal error instead of running it (the stream layout miscounted with
+    two).  Two guesses through Backend::post_guess: refused at max_guesses 1, held at 2."""
+    import subprocess
+    import sys
+    case, corpus = case_corpus("small_v300")
+    code = _POST_GUESSES.format(tests=os.path.dirname(os.path.abspath(__file__)), corpus=corpus,
+                                cfg=case["config"], max_guesses=max_guesses)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    if max_guesses == 1:
+        assert p.returncode != 0
+        assert "more unconfirmed guesses than the backend holds" in p.stderr
+        assert "IN_FLIGHT" not in p.stdout
+    else:
+        assert p.returncode == 0, p.stderr
+        assert "IN_FLIGHT 2" in p.stdout
+
+
+def test_batch_after_tiebreak_device_train_rebuilds_the_heap(hh, case_corpus, tmp_path):
+    """train() under tiebreak=device selects on the device and never fills the host
+    heap; a bpe_merge_batch after it must still merge (the heap is rebuilt from a fresh K1 of the
+    merged corpus, as bpe_init would build it), not return 0.  Same files as an explicit
+    bpe_init before the batch."""
+    case, corpus = case_corpus("utf8_2m_v2000_mpf50")
+    cfg = dict(case["config"], vocab_size=1000)
+    out = []
+    for explicit_init in (False, True):
+        h = hostharness.open_case(hh, corpus, cfg, "types")
+        try:
+            hh.hh_set_tiebreak_device(h, 1)
+            hh.hh_set_device_phase(h, 0)
+            first = hh.hh_train(h, None)
+            assert first == 1000 - 256
+            if explicit_init:
+                hh.hh_init(h)
+            got = hh.hh_merge_batch(h, 25)
+            m, v = str(tmp_path / f"m{int(explicit_init)}"), str(tmp_path / f"v{int(explicit_init)}")
+            hh.hh_save(h, m.encode(), v.encode(), 1)
+            out.append((got, open(m, "rb").read(), open(v, "rb").read()))
+        finally:
+            hh.hh_close(h)
+    assert out[0][0] == 25
+    assert out[0] == out[1]
+    assert len(out[0][1]) == 12 * (1000 - 256 + 25)

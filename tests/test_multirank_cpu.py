@@ -145,3 +145,16 @@ def test_product_sharded_load_gather_fallback(case_corpus, tmp_path):
     keys = ("num_words", "num_symbols", "num_occurrences")
     assert all(i["fell_back"] for i in many)
     assert all(tuple(i[k] for k in keys) == tuple(one[0][k] for k in keys) for i in many)
+
+
+def test_product_sharded_load_gather_fallback_one_rank_fails(case_corpus, tmp_path):
+    """the gather raises on ONE rank only (the others' collective returns): the ranks
+    agree on a failure flag after the attempt and fall back together, so no rank waits in a gloo
+    gather the others skip and every rank builds the single-rank table."""
+    case, corpus = case_corpus("utf8_4m_v8192_mpf5")
+    (tmp_path / "one").mkdir()
+    one = _run_product_ranks(corpus, case["config"], 1, tmp_path / "one")
+    many = _run_product_ranks(corpus, case["config"], 2, tmp_path, env={"BROKEN_GROUP": "last"})
+    keys = ("num_words", "num_symbols", "num_occurrences")
+    assert all(i["fell_back"] for i in many)
+    assert all(tuple(i[k] for k in keys) == tuple(one[0][k] for k in keys) for i in many)
