@@ -598,6 +598,14 @@ def merge_loop_report(st, merges, elapsed, args):
             "words_scanned_per_merge": st["index_scanned"] / idx_n,
             "words_changed_per_merge": st["index_changed"] / idx_n,
             "occurrences_per_merge": st["index_occurrences"] / idx_n,
+            "k4_on_device": {"merges_finalized": st["index_finalized"],
+                             "device_records_out_us_per_merge": st["index_dev_out_us"] / idx_n,
+                             "device_finalize_us_per_finalized_merge": st["index_dev_fin_us"] / max(1, st["index_finalized"]),
+                             "raw_records_per_finalized_merge": st["index_fin_records"] / max(1, st["index_finalized"]),
+                             "raw_records_per_merge": st["index_raw_records"] / idx_n,
+                             "changes_or_records_to_host_per_merge": st["index_records"] / idx_n,
+                             "note": "finalize_changes: records combined per pair key and ordered (bucket, first "
+                                     "touch desc) on the device; the host only walks them"},
             "device_lookup_us_per_merge": st["index_dev_lookup_us"] / idx_n,
             "device_scan_us_per_merge": st["index_dev_scan_us"] / idx_n,
             "host_post_to_flag_us_per_merge": st["index_wait_us"] / idx_n,

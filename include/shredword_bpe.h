@@ -205,6 +205,12 @@ typedef struct ShredStats {
   uint64_t sel_host_merges;    /* tiebreak=device: early merges selected on the host by the same rule
                                   (exact counts) while the whole-chip resident loop runs them */
   uint64_t sel_table_grows;    /* tiebreak=device: pair tables grown 4x between launches */
+  /* K4 on the device (k_word_loop finalize_changes, round 5) */
+  uint64_t index_raw_records;  /* k_word_loop: Σ delta records before the device's combine */
+  uint64_t index_finalized;    /* k_word_loop: merges whose records left as ordered changes */
+  double index_dev_out_us;     /* k_word_loop: Σ device time handing the records out (raw or finalized) */
+  double index_dev_fin_us;     /*   of which: the finalized merges */
+  uint64_t index_fin_records;  /*   their raw records */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -2994,6 +2994,7 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
   }
   if (layout == Layout::kTypes && !exchange_ && index_on_) {
     if (!wl_) wl_ = new WordLoop(ordinal_, stream_, unk_);
+    if (fin_ >= 0) wl_->set_finalize((uint32_t)fin_);
     if (!wl_->upload(ts, weight_)) {
       delete wl_;
       wl_ = nullptr;
@@ -3718,8 +3719,10 @@ void Device::finish_launch(ChainRun& run_) {
 
 size_t Device::collect(int32_t X, const DeltaRecord** recs) {
   HIP_OK(hipSetDevice(ordinal_));
+  last_changes_ = false;
   if (wl_ && wl_->in_flight()) {
     const size_t n = wl_->collect(X, recs);
+    last_changes_ = wl_->last_changes();
     records_total_ += n;
     records_max_ = std::max<uint64_t>(records_max_, n);
     return n;

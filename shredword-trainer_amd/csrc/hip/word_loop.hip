@@ -58,6 +58,7 @@ constexpr bool kWlPrefetch = false;     // (A/B builds) each word's run loaded i
 constexpr bool kWlPrefetch = true;      // the next word's run loads while this one merges
 #endif
 constexpr int kQ = kWlThreads * kB + kWlThreads;  // LDS queue of filtered entries (a round + a remainder)
+constexpr uint32_t kDeltaBucketsDev = 1024;  // the reference's FREQ_CHANGE_BUCKETS (bpe.cpp:16)
 constexpr uint32_t kRing = 64;          // command ring entries
 constexpr uint32_t kOpMerge = 1, kOpStop = 2, kOpTimeout = 3, kOpUnmerge = 4;
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
@@ -165,6 +166,7 @@ struct WlParams {
   uint32_t* status;  // host-visible: [0] exit op
   uint32_t seq0;
   uint32_t idle_polls;
+  uint32_t fin_max;  // K4 on the device: merges with at most this many records leave as ordered changes (0: off)
   WlSlotDev sl[WordLoop::kSlots];
   SelParams sel;  // k_word_loop<true> only
 };
@@ -251,6 +253,7 @@ struct DeltaH {
 // The merge's shared state in LDS.
 struct MergeCtx {
   uint32_t* nspill;  // delta keys spilled past the LDS hash
+  uint32_t* nkeys;   // delta keys in the LDS hash
 };
 
 // One neighbour delta (reference freq_change_add, bpe.cpp:274-290): Σ weight and min first touch
@@ -262,6 +265,7 @@ __device__ __forceinline__ void delta_add(DeltaH& h, const WlParams& p, const Me
   for (int probe = 0; probe < 32; ++probe) {
     const uint32_t prev = atomicCAS(&h.key[s], kEmpty32, key);
     if (prev == kEmpty32 || prev == key) {
+      if (prev == kEmpty32) atomicAdd(c.nkeys, 1u);
       atomicAdd(&h.sum[s], w);
       atomicMin(&h.ft[s], ft);
       return;
@@ -444,7 +448,7 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
 // The loop's state in LDS.
 struct LoopS {
   uint32_t cmd[8];
-  uint32_t nout, nchg, pool_top, err, scan, filter, nspill, qn;
+  uint32_t nout, nchg, pool_top, err, scan, filter, nspill, qn, nkeys, nfin;
   uint32_t rd, wr;  // run ints read (length + tokens of every scanned word) / written back (changed words)
   u64 lst_x;        // the words-of list written for X (offset | (count + 1) << 32), for the host
   uint32_t st[4];
@@ -458,6 +462,199 @@ struct LoopS {
   u64 bc[kWlThreads / 64], bk[kWlThreads / 64];
   uint32_t bs[kWlThreads / 64];
 };
+
+
+// K4 on the device (reference FreqChangeMap, bpe.cpp:9-50, applied at :297-313):
+// the merge's n records (LDS hash + spilled keys) leave as the reference's changes, in the order
+// the reference applies them, so the host only walks them.  Per record the pair (first, second)
+// and its signed delta; records of one pair key combined (Σ delta, min first touch); the merged
+// pair (a, b) dropped (the host skips it); order: bucket key % 1024 ascending, then first touch
+// descending (the bucket chains' head insertion).  The key is the reference's
+// ((u64)(i64)first << 32) | (u64)(i64)second, sign extension included (a negative second id
+// makes every such key equal, as in the reference).  First touches are unique per record, so the
+// min-first-touch record of a key leads it and a bucket's order is a rank by first touch.
+// LDS (the merge's arrays are free by now): records in q (hk, delta, ft, then a bucket-sorted ft
+// copy; kFinMax each), the combine table in the strip (hk, min ft, Σ delta; 2 kFinMax slots), the
+// 1024 bucket counters in h.key.  Returns the changes written (host records, in order).
+constexpr uint32_t kFinMax = 1024;
+constexpr uint32_t kFinTab = 2 * kFinMax;
+// the combine table's empty key: (INT32_MAX, INT32_MAX) is no pair's key (ids are < 2^30), while
+// ~0 is one: (f, s) with a negative second id (unk = -1) sign-extends to all ones
+constexpr u64 kFinEmpty = 0x7FFFFFFF7FFFFFFFull;
+static_assert(4 * kFinMax <= (uint32_t)kQ, "record arrays in the queue");
+static_assert(3 * kFinTab * 8 <= (uint32_t)(kStrip * kWlThreads * 4), "combine table in the strip");
+static_assert(kDeltaBucketsDev * 4 <= kDh * 4, "bucket counters in the hash keys");
+
+__device__ __forceinline__ void fin_record(u64* q, uint32_t r, uint32_t key, u64 sum, u64 ft, int32_t unk, int32_t a,
+                                           int32_t b, int32_t X) {
+  const uint32_t sl = key >> 2, cat = key & 3u;
+  const int32_t id = sl == 0 ? unk : (int32_t)(sl - 1u);
+  const int32_t f = cat < 2u ? id : (cat == 2u ? b : X);
+  const int32_t g = cat == 0u ? a : (cat == 1u ? X : id);
+  q[r] = ((u64)(int64_t)f << 32) | (u64)(int64_t)g;
+  q[kFinMax + r] = (cat & 1u) ? sum : (u64)(-(int64_t)sum);
+  q[2 * kFinMax + r] = ft;
+}
+
+// The merge's records (LDS hash slots, then the spilled keys) as (hk, delta, ft) in q[0, n).
+__device__ __forceinline__ void fin_gather(const WlParams& p, DeltaH& h, LoopS& S, u64* q, int32_t a, int32_t b,
+                                           int32_t X) {
+  const uint32_t tid = threadIdx.x;
+  for (int i = tid; i < kDh; i += kWlThreads) {
+    const uint32_t key = h.key[i];
+    if (key != kEmpty32) fin_record(q, atomicAdd(&S.nout, 1u), key, h.sum[i], h.ft[i], p.unk, a, b, X);
+  }
+  const uint32_t nsp = S.nspill;
+  for (uint32_t i = tid; i < nsp; i += kWlThreads) {
+    const uint32_t key = p.dlist[i];
+    const u64 sum = atomicExch(&p.dsum[key], 0ull);
+    const u64 ft = atomicExch(&p.dft[key], kEmpty64);
+    fin_record(q, atomicAdd(&S.nout, 1u), key, sum, ft, p.unk, a, b, X);
+  }
+}
+
+__device__ __forceinline__ u64 rl64(u64 x, uint32_t j) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)j);
+  return ((u64)hi << 32) | lo;
+}
+
+// finalize_changes for n <= 64 records, by one wave alone (no barrier, no LDS atomics): lane i
+// holds record i; the combine and the ranks are scalar loops over the records (readlane
+// broadcasts).  Same output as finalize_changes.  Returns the changes written.
+__device__ uint32_t finalize_wave(const u64* q, const WlSlotDev& sd, int32_t a, int32_t b, uint32_t n) {
+  const int lane = threadIdx.x & 63;
+  const bool mine = (uint32_t)lane < n;
+  const u64 hk = mine ? q[lane] : kFinEmpty;
+  const u64 d = mine ? q[kFinMax + lane] : 0ull;
+  const u64 ft = mine ? q[2 * kFinMax + lane] : kEmpty64;
+  const u64 kab = ((u64)(int64_t)a << 32) | (u64)(int64_t)b;
+  // records of one key: Σ delta, the min first touch leads
+  u64 sum = 0;
+  bool lead = mine && hk != kab;
+#pragma unroll 1
+  for (uint32_t j = 0; j < n; ++j) {
+    const u64 hj = rl64(hk, j), fj = rl64(ft, j), dj = rl64(d, j);
+    const bool same = hj == hk;
+    sum += same ? dj : 0ull;
+    lead = lead && !(same && fj < ft);
+  }
+  // place = leaders before this one: bucket ascending, then first touch descending
+  const u64 lm = __ballot(lead);
+  const uint32_t bk = (uint32_t)hk & (kDeltaBucketsDev - 1);
+  uint32_t r = 0;
+#pragma unroll 1
+  for (u64 rest = lm; rest; rest &= rest - 1) {
+    const uint32_t j = (uint32_t)__builtin_ctzll(rest);
+    const uint32_t bj = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hk, (int)j) & (kDeltaBucketsDev - 1);
+    const u64 fj = rl64(ft, j);
+    r += (bj < bk || (bj == bk && fj > ft)) ? 1u : 0u;
+  }
+  if (lead) {
+    u64* dst = reinterpret_cast<u64*>(sd.recs + r);
+    dst[0] = hk;
+    dst[1] = sum;
+    dst[2] = ft;
+  }
+  return (uint32_t)__popcll(lm);
+}
+
+__device__ uint32_t finalize_changes(const WlParams& p, DeltaH& h, LoopS& S, u64* q, u64* tab, const WlSlotDev& sd,
+                                     int32_t a, int32_t b, int32_t X, uint32_t n) {
+  const uint32_t tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  u64* const fhk = q;
+  u64* const fd = q + kFinMax;
+  u64* const fft = q + 2 * kFinMax;
+  u64* const mft = q + 3 * kFinMax;
+  u64* const thk = tab;
+  u64* const tft = tab + kFinTab;
+  u64* const td = tab + 2 * kFinTab;
+  uint32_t* const cnt = h.key;
+  // 1. records -> (hk, delta, ft) in LDS; combine table cleared
+  fin_gather(p, h, S, q, a, b, X);
+  for (uint32_t i = tid; i < kFinTab; i += kWlThreads) {
+    thk[i] = kFinEmpty;
+    tft[i] = kEmpty64;
+    td[i] = 0;
+  }
+  __syncthreads();
+  // 2. combine per key: Σ delta and min first touch in the table
+  constexpr int kPer = (int)(kFinMax / kWlThreads);
+  uint32_t slot[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint32_t i = tid + (uint32_t)j * kWlThreads;
+    slot[j] = 0;
+    if (i < n) {
+      const u64 hk = fhk[i];
+      uint32_t t = (uint32_t)mix64(hk) & (kFinTab - 1);
+#pragma unroll 1
+      for (;;) {
+        const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&thk[t]), kFinEmpty, hk);
+        if (prev == kFinEmpty || prev == hk) break;
+        t = (t + 1) & (kFinTab - 1);
+      }
+      slot[j] = t;
+      atomicMin(reinterpret_cast<unsigned long long*>(&tft[t]), fft[i]);
+      atomicAdd(reinterpret_cast<unsigned long long*>(&td[t]), fd[i]);
+    }
+  }
+  for (uint32_t i = tid; i < kDeltaBucketsDev; i += kWlThreads) cnt[i] = 0;
+  __syncthreads();
+  // 3. a key's leader (its min first touch) takes a place in its bucket
+  const u64 kab = ((u64)(int64_t)a << 32) | (u64)(int64_t)b;
+  uint32_t li[kPer];
+  bool lead[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint32_t i = tid + (uint32_t)j * kWlThreads;
+    lead[j] = i < n && tft[slot[j]] == fft[i] && fhk[i] != kab;
+    li[j] = lead[j] ? atomicAdd(&cnt[fhk[i] & (kDeltaBucketsDev - 1)], 1u) : 0u;
+  }
+  __syncthreads();
+  // 4. bucket bases: exclusive scan of the 1024 counters, two a thread
+  static_assert(kDeltaBucketsDev == 2 * kWlThreads, "two counters a thread");
+  {
+    const uint32_t c0 = cnt[2 * tid], c1 = cnt[2 * tid + 1];
+    const uint32_t incl = wave_incl_add(c0 + c1);
+    if (lane == 63) S.bs[wid] = incl;
+    __syncthreads();
+    uint32_t base = incl - c0 - c1, tot = 0;
+    for (int w = 0; w < kWlThreads / 64; ++w) {
+      if (w < wid) base += S.bs[w];
+      tot += S.bs[w];
+    }
+    cnt[2 * tid] = base;
+    cnt[2 * tid + 1] = base + c0;
+    if (tid == 0) S.nfin = tot;
+  }
+  __syncthreads();
+  // 5. each bucket's first touches side by side
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint32_t i = tid + (uint32_t)j * kWlThreads;
+    if (lead[j]) mft[cnt[fhk[i] & (kDeltaBucketsDev - 1)] + li[j]] = fft[i];
+  }
+  __syncthreads();
+  // 6. place = bucket base + the bucket's members with a later first touch
+  const uint32_t m = S.nfin;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (!lead[j]) continue;
+    const uint32_t i = tid + (uint32_t)j * kWlThreads;
+    const uint32_t bk = (uint32_t)(fhk[i] & (kDeltaBucketsDev - 1));
+    const uint32_t beg = cnt[bk], end = bk + 1 < kDeltaBucketsDev ? cnt[bk + 1] : m;
+    const u64 ft = fft[i];
+    uint32_t r = 0;
+    for (uint32_t k = beg; k < end; ++k) r += mft[k] > ft ? 1u : 0u;
+    u64* dst = reinterpret_cast<u64*>(sd.recs + beg + r);
+    dst[0] = fhk[i];
+    dst[1] = td[slot[j]];
+    dst[2] = ft;
+  }
+  return m;
+}
 
 }  // namespace
 
@@ -481,7 +678,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   }
   uint32_t expect = p.seq0;
   uint32_t exit_op = kOpStop;
-  const MergeCtx mc{&S.nspill};
+  const MergeCtx mc{&S.nspill, &S.nkeys};
   if constexpr (kSelf) {  // the rebuilt frontier into LDS, each slot told its position
     const SelParams& q = p.sel;
     const uint32_t nf = min(ld_agent(q.st + kSelNF), kSelK);
@@ -695,6 +892,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.rd = 0;
         S.wr = 0;
         S.nspill = 0;
+        S.nkeys = 0;
         S.filter = need != 0;
         S.occ = 0;
         S.err = 0;
@@ -997,7 +1195,21 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.lst_x = (u64)top | ((u64)(nchg + 1u) << 32);  // for the host: offset, count + 1
       }
     }
-    {
+    const uint32_t nrec = S.nkeys + S.nspill;
+    const bool fin = p.fin_max != 0 && nrec <= p.fin_max && nrec <= kFinMax;
+    const u64 t_fin = __builtin_amdgcn_s_memrealtime();
+    if (fin && nrec <= 64u) {  // one wave combines and orders them
+      fin_gather(p, s_h, S, s_q, a, b, X);
+      __syncthreads();
+      if (wid == 0) {
+        const uint32_t m = finalize_wave(s_q, sd, a, b, nrec);
+        if (lane == 0) S.nfin = m;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (fin) {
+      finalize_changes(p, s_h, S, s_q, reinterpret_cast<u64*>(s_strip), sd, a, b, X, nrec);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
       for (int i = tid; i < kDh; i += kWlThreads) {
         const uint32_t key = s_h.key[i];
         if (key == kEmpty32) continue;
@@ -1022,7 +1234,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     }
     __syncthreads();
     if (tid == 0) {
-      sd.hdr[0] = S.nout;
+      sd.hdr[0] = fin ? S.nfin : S.nout;
+      sd.hdr[22] = fin ? 1u : 0u;  // 1: ordered changes (finalize_changes), else raw records
+      sd.hdr[23] = nrec;
+      sd.hdr[30] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_fin);  // records out: gather (+ finalize)
       sd.hdr[2] = (uint32_t)cnt;
       sd.hdr[3] = S.nchg;
       u64* h64 = reinterpret_cast<u64*>(sd.hdr);
@@ -1315,6 +1530,7 @@ WordLoop::WordLoop(int ordinal, void* stream, int32_t unk_id) : ordinal_(ordinal
   // the idle bound (polls without a command before the launch ends itself); tests shrink it to
   // race the time-out against the posts
   if (const char* e = std::getenv("SHREDWORD_WL_IDLE_POLLS")) idle_polls_ = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char* e = std::getenv("SHREDWORD_WL_FINALIZE")) fin_max_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_SELECT_REPORT")) sel_report_ = std::atoi(e) != 0;
   for (auto& e : ev_) {
     hipEvent_t ev;
@@ -1652,6 +1868,7 @@ void WordLoop::launch(uint32_t seq0) {
   p.status = static_cast<uint32_t*>(status_dev_);
   p.seq0 = seq0;
   p.idle_polls = idle_polls_;
+  p.fin_max = fin_max_;
   for (int k = 0; k < kSlots; ++k) {
     p.sl[k].recs = static_cast<DeltaRecord*>(slot_[k].dev_recs);
     p.sl[k].hdr = static_cast<uint32_t*>(slot_[k].dev_hdr);
@@ -1744,6 +1961,14 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   st_.run_ints_read += h[14];
   st_.run_ints_written += h[15];
   st_.records += h[0];
+  st_.raw_records += h[22] ? h[23] : h[0];
+  st_.finalized += h[22] ? 1u : 0u;
+  st_.dev_out_us += 1e-2 * (double)h[30];
+  if (h[22]) {
+    st_.dev_fin_us += 1e-2 * (double)h[30];
+    st_.fin_records += h[23];
+  }
+  last_changes_ = h[22] != 0;
   st_.changed += h[3];
   st_.occurrences += h64[2];
   st_.dev_us += 1e-2 * (double)h64[3];  // s_memrealtime: 100 MHz
@@ -1770,6 +1995,7 @@ bool WordLoop::peek(int32_t X, const DeltaRecord** recs, size_t* n) const {
   if (posted_.empty() || posted_.front().X != X) return false;
   const Slot& sl = slot_[(uint32_t)X & (kSlots - 1)];
   if (__atomic_load_n(sl.host_hdr + 1, __ATOMIC_ACQUIRE) != posted_.front().seq) return false;
+  if (sl.host_hdr[22]) return false;  // ordered changes already: nothing for the apply helper to prepare
   const size_t k = sl.host_hdr[0];
   if (k > sl.rec_cap) return false;  // collect() reports it
   *recs = sl.host_recs;

@@ -98,6 +98,7 @@ class Device : public Backend {
   void set_exchange(const Exchange& x);
   // K4: merge X's records (host memory); the first collect of a chain waits for the launch.
   size_t collect(int32_t X, const DeltaRecord** recs) override;
+  bool records_are_changes() const override { return last_changes_; }
   // The indexed loop's finished merge X, without collecting it (Engine's apply helper).
   bool peek(int32_t X, const DeltaRecord** recs, size_t* n) override;
   static constexpr int kChainMax = 8;
@@ -155,6 +156,15 @@ class Device : public Backend {
     hybrid_ = on;
   }
   void set_switch_occurrences(uint64_t n) { switch_occ_ = n; }
+  // The indexed loop's K4 on the device for merges of at most n records (0: off; -1 leaves the
+  // loop's default); takes effect at the loop's next launch.
+  void set_finalize(int64_t n) {
+    fin_ = n;
+    if (wl_ && n >= 0) {
+      index_sync();
+      wl_->set_finalize((uint32_t)n);
+    }
+  }
   int64_t switch_merge() const { return switch_x_; }
   double switch_ms() const { return switch_ms_; }
   const WordLoop* word_loop() const { return wl_; }
@@ -331,6 +341,8 @@ class Device : public Backend {
   int32_t max_id_seen_ = 0;
   int32_t max_id0_ = 0;  // max id at upload (reset_tokens restores it)
   bool speculate_ = true;
+  bool last_changes_ = false;  // the last collect() gave ordered changes (the indexed loop's K4)
+  int64_t fin_ = -1;           // set_finalize (-1: the loop's default)
   uint64_t rollbacks_ = 0;
 
   void* merge_params_ = nullptr;        // MergeParams kernel arguments (with the inline tile list)

@@ -245,7 +245,12 @@ bool Engine::merge_one(Backend& be, int remaining) {
   }
   const size_t n = adopted ? 0 : be.collect(X, &recs);
   const double t3 = now_seconds();
-  if (!adopted) sel_.apply_combine(a, b, X, recs, n);
+  if (!adopted) {
+    if (be.records_are_changes())
+      sel_.apply_changes(a, b, X, reinterpret_cast<const Selector::Change*>(recs), n);
+    else
+      sel_.apply_combine(a, b, X, recs, n);
+  }
   // Late correction: with (a, b)'s changes known, a new pair holding X that is strictly more
   // frequent than the guess in flight (made before them; its own count is unchanged by this
   // merge) replaces it now, so the device undoes and redoes the guess while this merge is
@@ -399,7 +404,15 @@ int Engine::train_device(Backend& be, double t0) {
       // "a b a b": -w as the second occurrence's left pair, +w as the first's right pair), and
       // the records come in any order
       net.clear();
-      for (size_t i = 0; i < nr; ++i) {
+      if (be.records_are_changes()) {  // already one change per pair key (reference keys: the pair's own
+        const auto* ch = reinterpret_cast<const Selector::Change*>(recs);  // ids, as neither is unk here)
+        for (size_t i = 0; i < nr; ++i) {
+          const int32_t f = (int32_t)(uint32_t)(ch[i].hk >> 32), s = (int32_t)(uint32_t)ch[i].hk;
+          if ((f == a && s == b) || f == unk_ || s == unk_) continue;
+          net[pack_pair(f, s)] += ch[i].delta;
+        }
+      }
+      for (size_t i = 0; i < nr && !be.records_are_changes(); ++i) {
         const uint32_t cat = recs[i].key & 3u, slot = recs[i].key >> 2;
         const int32_t id = slot == 0 ? unk_ : (int32_t)(slot - 1);
         int32_t f, s;

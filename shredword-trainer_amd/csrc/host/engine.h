@@ -46,6 +46,9 @@ class Backend {
   }
   int guesses_in_flight() const { return guesses_; }
   virtual size_t collect(int32_t X, const DeltaRecord** recs) = 0;
+  // True when the last collect() handed out Selector::Change entries (combined per pair key, in
+  // the reference's application order: K4 done on the device) instead of raw delta records.
+  virtual bool records_are_changes() const { return false; }
   // Non-blocking look at the oldest outstanding merge X: true with its records once the device
   // has finished it (they stay valid until X is collected or rolled back).  Default: never.
   virtual bool peek(int32_t X, const DeltaRecord** recs, size_t* n) { return false; }

@@ -495,6 +495,20 @@ void Selector::apply_combine(int32_t a, int32_t b, int32_t X, const DeltaRecord*
   ctr_.cyc_order += own_.cyc_order;
 }
 
+void Selector::apply_changes(int32_t a, int32_t b, int32_t X, const Change* c, size_t n) {
+  own_.a = a;
+  own_.b = b;
+  own_.X = X;
+  own_.records = n;
+  own_.ordered.assign(c, c + n);
+  own_.cyc_combine = own_.cyc_order = 0;
+  // the walk's info lines, requested together so their misses overlap
+  for (size_t i = 0; i < n; ++i)
+    __builtin_prefetch(&table_[mix64(pack_pair((int32_t)(c[i].hk >> 32), (int32_t)c[i].hk)) & mask_]);
+  ctr_.records += n;
+  ctr_.changes += n;
+}
+
 void Selector::adopt(Prepared* p) {
   std::swap(own_, *p);
   // the lines the other core requested are in the shared L3: bring them closer for the walk
@@ -510,7 +524,7 @@ bool Selector::predict_after(int32_t X, uint64_t above, int32_t* pa, int32_t* pb
   // Pairs holding X are new: their count after this merge is their combined delta, exactly.
   uint64_t best_f = above;
   bool found = false;
-  for (const Change& c : own_.changes) {
+  for (const Change& c : own_.ordered) {
     const int32_t f = (int32_t)(uint32_t)(c.hk >> 32), s = (int32_t)(uint32_t)c.hk;
     if ((f != X && s != X) || f == unk_ || s == unk_ || c.delta <= 0) continue;
     const uint64_t v = (uint64_t)c.delta;

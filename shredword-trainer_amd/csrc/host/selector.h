@@ -114,6 +114,10 @@ class Selector {
     std::vector<uint32_t> index;
     uint64_t cyc_combine = 0, cyc_order = 0;
   };
+  // K4 done on the device (word_loop.hip finalize_changes): the merge's changes already combined
+  // per pair key and in the reference's application order (bucket ascending, first touch
+  // descending); the next apply_finish walks them as they are.
+  void apply_changes(int32_t a, int32_t b, int32_t X, const Change* c, size_t n);
   // Thread-safe against every other member: reads only unk_ (fixed during a train()).
   // prefetch_base / prefetch_mask: a snapshot of the pair table to prefetch the changed pairs'
   // lines from (nullptr: none).

@@ -47,6 +47,7 @@ struct Trainer {
   int hybrid = -1;               // resident first, indexed after: -1 default (on), 0 off, 1 on
   int64_t switch_occ = -1;       // hybrid switch: occurrences of a resident merge below which (-1 default)
   int spec_depth = 0;            // resident guesses in flight (0: env SHREDWORD_SPEC_DEPTH or default)
+  int64_t finalize = -1;         // indexed loop: K4 on the device up to this many records (-1 default, 0 off)
   bool gpu_load = true;          // count the corpus words on the device (types layout)
   double load_s = 0;
   // shred_set_load_gather: a sharded load over the caller's all-gather (no RCCL)
@@ -125,6 +126,11 @@ int set_option(Trainer* t, const std::string& key, const std::string& val) {
     if (n < 0) return -1;
     t->switch_occ = n;
     if (t->dev) t->dev->set_switch_occurrences((uint64_t)n);
+  } else if (key == "finalize") {  // K4 on the device (ordered changes) for merges of <= n records
+    const long long n = std::atoll(val.c_str());
+    if (n < 0) return -1;
+    t->finalize = n;
+    if (t->dev) t->dev->set_finalize((uint32_t)n);
   } else if (key == "spec_depth") {
     const int d = std::atoi(val.c_str());
     if (d < 1 || d > Device::kResSlots - 1) return -1;
@@ -174,6 +180,7 @@ bool ensure_device(Trainer* t, const char* caller) {
     if (t->index >= 0) t->dev->set_index(t->index != 0);
     if (t->hybrid >= 0) t->dev->set_hybrid(t->hybrid != 0);
     if (t->switch_occ >= 0) t->dev->set_switch_occurrences((uint64_t)t->switch_occ);
+    if (t->finalize >= 0) t->dev->set_finalize((uint32_t)t->finalize);
     t->dev->set_spec_depth(t->spec_depth ? t->spec_depth : env_int("SHREDWORD_SPEC_DEPTH", 1));
     if ((dist_active() && t->dist_exchange()) || t->local_exchange) {
       Device::Exchange x;
@@ -498,6 +505,11 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
       s->index_run_ints_read = w.run_ints_read;
       s->index_run_ints_written = w.run_ints_written;
       s->index_records = w.records;
+      s->index_raw_records = w.raw_records;
+      s->index_finalized = w.finalized;
+      s->index_dev_out_us = w.dev_out_us;
+      s->index_dev_fin_us = w.dev_fin_us;
+      s->index_fin_records = w.fin_records;
       s->index_switch_merge = t->dev->switch_merge();
       s->index_switch_ms = t->dev->switch_ms();
       const SelectStats& q = wl->select_stats();

@@ -60,6 +60,11 @@ struct WordLoopStats {
   uint64_t run_ints_read = 0;     // Σ ints of the scanned words' runs (length + tokens)
   uint64_t run_ints_written = 0;  // Σ ints of the changed words' runs written back
   uint64_t records = 0;           // Σ delta records handed to the host
+  uint64_t raw_records = 0;       // Σ delta records of the merges (before the device's combine)
+  uint64_t finalized = 0;         // merges whose records left as ordered changes
+  double dev_out_us = 0;          // Σ device time handing the records out (raw, or gathered + finalized)
+  double dev_fin_us = 0;          //   of which: the merges whose records were finalized
+  uint64_t fin_records = 0;       //   their raw records
 };
 
 struct SelectStats {
@@ -103,8 +108,14 @@ class WordLoop {
 
   // Queues merge (a, b) -> X (the persistent launch starts on the first post).
   void post_merge(int32_t a, int32_t b, int32_t X);
-  // The records of the oldest posted merge, which must be X (waits for its flag).
+  // The records of the oldest posted merge, which must be X (waits for its flag).  When
+  // last_changes() is true afterwards they are Selector::Change entries instead (K4 on the device:
+  // combined per pair key, in the reference's application order; word_loop.hip finalize_changes).
   size_t collect(int32_t X, const DeltaRecord** recs);
+  bool last_changes() const { return last_changes_; }
+  // K4 on the device for merges of at most n records (0: off; SHREDWORD_WL_FINALIZE overrides).
+  void set_finalize(uint32_t n) { fin_max_ = n; }
+  uint32_t finalize_max() const { return fin_max_; }
   // Non-blocking: X is the oldest posted merge and its flag is up (records as collect() gives them).
   bool peek(int32_t X, const DeltaRecord** recs, size_t* n) const;
   // Undoes every posted merge with id >= X, newest first (queued; nothing waits).
@@ -228,6 +239,10 @@ class WordLoop {
   uint32_t seq_ = 0;
   uint32_t idle_polls_ = 1u << 22;  // ~10 s without a command: the launch ends itself (relaunched on demand)
   bool sel_report_ = false;         // SHREDWORD_SELECT_REPORT=1: one stderr line per k_word_loop<true> launch
+  // K4 on the device up to this many records (<= 64: one wave; up to kFinMax: the workgroup).  Off
+  // by default: measured on C3 it costs the device more than it saves the host
+  uint32_t fin_max_ = 0;
+  bool last_changes_ = false;
   std::vector<Post> posted_;
   // tiebreak=device: pair table, frontier, state (see word_loop.hip SelParams)
   void sel_free();

@@ -254,10 +254,51 @@ class EmuBackend : public Backend {
     // with a host phase set, the records come newest-first: the device's order is arbitrary
     // (workgroups, spills), so the host side must not depend on it
     if (phase_ > 0) std::reverse(recs_.begin(), recs_.end());
-    *recs = recs_.data();
     if (phase_left_ > 0) --phase_left_;
+    changes_out_ = fin_ && !gather_;
+    if (changes_out_) {  // K4 as the device's finalize_changes gives it, restated the reference's way
+      to_changes(pd.a, pd.b, X);
+      *recs = reinterpret_cast<const DeltaRecord*>(chg_.data());
+      return chg_.size();
+    }
+    *recs = recs_.data();
     return recs_.size();
   }
+  bool records_are_changes() const override { return changes_out_; }
+  // The reference's FreqChangeMap (bpe.cpp:9-50) fed the records' events in scan order (first
+  // touch ascending): 1024 buckets by key % 1024, head insertion, deltas summed per key; read out
+  // bucket by bucket, chain head first, the merged pair skipped (bpe.cpp:297-313).
+  void to_changes(int32_t a, int32_t b, int32_t X) {
+    std::vector<const DeltaRecord*> ev(recs_.size());
+    for (size_t i = 0; i < recs_.size(); ++i) ev[i] = &recs_[i];
+    std::sort(ev.begin(), ev.end(), [](const DeltaRecord* x, const DeltaRecord* y) { return x->ft < y->ft; });
+    std::vector<std::vector<Selector::Change>> bucket(1024);
+    for (const DeltaRecord* r : ev) {
+      const uint32_t cat = r->key & 3u, slot = r->key >> 2;
+      const int32_t id = slot == 0 ? unk_ : (int32_t)(slot - 1);
+      const int32_t f = cat < 2u ? id : (cat == 2u ? b : X);
+      const int32_t g = cat == 0u ? a : (cat == 1u ? X : id);
+      const uint64_t hk = ((uint64_t)(int64_t)f << 32) | (uint64_t)(int64_t)g;
+      const int64_t d = (cat & 1u) ? (int64_t)r->sum : -(int64_t)r->sum;
+      std::vector<Selector::Change>& ch = bucket[hk % 1024];
+      bool found = false;
+      for (Selector::Change& c : ch)
+        if (c.hk == hk) {
+          c.delta += d;
+          found = true;
+          break;
+        }
+      if (!found) ch.insert(ch.begin(), Selector::Change{hk, d, r->ft});  // head insertion
+    }
+    chg_.clear();
+    const uint64_t kab = ((uint64_t)(int64_t)a << 32) | (uint64_t)(int64_t)b;
+    for (const auto& ch : bucket)
+      for (const Selector::Change& c : ch)
+        if (c.hk != kab) chg_.push_back(c);
+  }
+  bool fin_ = std::getenv("HH_FINALIZE") ? std::atoi(std::getenv("HH_FINALIZE")) != 0 : false;
+  bool changes_out_ = false;
+  std::vector<Selector::Change> chg_;
 
   // The oldest outstanding merge's records before it is collected (the emulated kernels ran at
   // launch time, so they are always ready): the Engine's apply helper reads them on its thread.
@@ -312,7 +353,10 @@ class EmuBackend : public Backend {
       const int32_t a = pair_first(bk), b = (int32_t)(uint32_t)bk, X = X0 + m;
       merge_one(a, b, X);
       const DeltaRecord* recs = nullptr;
+      const bool fin = fin_;
+      fin_ = false;  // the device selector folds the raw records into its table
       const size_t nr = collect(X, &recs);
+      fin_ = fin;
       for (size_t i = 0; i < nr; ++i) {
         const uint32_t sl = recs[i].key >> 2, cat = recs[i].key & 3u;
         const int32_t id = sl == 0 ? unk : (int32_t)(sl - 1);

@@ -81,6 +81,23 @@ def test_index_loop_matches_reference(name, case_corpus, tmp_path):
         assert st["resident_launches"] == 0
 
 
+@pytest.mark.parametrize("fin", [0, 8, 1024])
+@pytest.mark.parametrize("name", API_CASES)
+def test_index_loop_changes_on_device_match_reference(name, fin, case_corpus, tmp_path):
+    """K4 on the device (round 5): k_word_loop hands the host each merge's changes combined per
+    pair key and in the reference's application order (finalize_changes) for merges of at most
+    `finalize` records, raw records otherwise.  0: every merge raw (the host combines and orders);
+    8: both kinds within one run (<= 64 records: one wave, finalize_wave); 1024: the whole-workgroup
+    finalize_changes past 64 records; the default (0, off) runs in every other test.  Same bytes."""
+    case, corpus = case_corpus(name)
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, hybrid=0, finalize=fin))
+    if fin == 0:
+        assert st["index_finalized"] == 0
+    elif case["merges"] > 50:
+        assert 0 < st["index_finalized"] < st["index_merges"] + st["index_undos"], st
+
+
 @pytest.mark.parametrize("path", ["hybrid", "index", "resident", "launch", "stream"])
 @pytest.mark.parametrize("name", API_CASES)
 def test_argmax_verifier(name, path, case_corpus, tmp_path):

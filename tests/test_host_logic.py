@@ -289,3 +289,24 @@ def test_batch_after_tiebreak_device_train_rebuilds_the_heap(hh, case_corpus, tm
     assert out[0][0] == 25
     assert out[0] == out[1]
     assert len(out[0][1]) == 12 * (1000 - 256 + 25)
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_host_logic_with_device_ordered_changes(name, hh, case_corpus, tmp_path, monkeypatch):
+    """K4 on the device (round 5): the backend hands the host the merge's changes already combined
+    per pair key and in the reference's application order (Backend::records_are_changes; on the GPU
+    k_word_loop's finalize_changes).  The emulation builds them the reference's way (a 1024-bucket
+    FreqChangeMap fed in first-touch order); the host then only walks them
+    (Selector::apply_changes) and must still give the reference's bytes."""
+    monkeypatch.setenv("HH_FINALIZE", "1")
+    case, corpus = case_corpus(name)
+    merges, model, vocab, trace = _run(hh, case, corpus, tmp_path, "types")
+    assert (merges, trace, model, vocab) == (case["merges"], case["trace"], case["model_bytes"], case["vocab_bytes"])
+
+
+@pytest.mark.parametrize("name", seq_cases())
+def test_host_logic_call_sequences_with_device_ordered_changes(name, hh, seq_case, tmp_path, monkeypatch):
+    monkeypatch.setenv("HH_FINALIZE", "1")
+    case, ops = seq_case(name)
+    trace, outputs, returns = run_script_harness(hh, case, ops, tmp_path)
+    assert (returns, trace, outputs) == (case["returns"], case["trace"], case["outputs"])
