@@ -20,10 +20,12 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <sched.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -506,6 +508,37 @@ static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool
   return false;
 }
 
+// The allowed CPUs on the GPU's NUMA node (its PCI device's local_cpulist), empty when unknown:
+// the reader threads run there, so their pinned buffers and copies stay on the GPU's socket.
+static std::vector<int> gpu_local_cpus(int device) {
+  std::vector<int> out;
+  char bus[64] = {};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return out;
+  for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+  const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
+  FILE* f = std::fopen(path.c_str(), "r");
+  if (!f) return out;
+  char buf[4096] = {};
+  const size_t got = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[got] = 0;
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return out;
+  for (char* tok = std::strtok(buf, ",\n"); tok; tok = std::strtok(nullptr, ",\n")) {
+    int lo = 0, hi = 0;
+    if (std::sscanf(tok, "%d-%d", &lo, &hi) == 2) {
+    } else if (std::sscanf(tok, "%d", &lo) == 1) {
+      hi = lo;
+    } else {
+      continue;
+    }
+    for (int c = lo; c <= hi && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &allowed)) out.push_back(c);
+  }
+  return out;
+}
+
 static bool device_setup(int device, hipStream_t* st, int* cus, std::string* why) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
@@ -605,19 +638,29 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   uint8_t* db = static_cast<uint8_t*>(dd.p);
   LOAD_OK(hipMemsetAsync(db + n, ' ', kPadBytes, st));
   LOAD_OK(hipStreamSynchronize(st));
-  // The file straight into HBM: T reader threads, each with its own stream and two pinned
-  // buffers, pread() chunk c (c = t, t + T, ...) into one buffer while the other's DMA runs.  No
-  // mapping of the file: the page-ins of an mmap (one fault per 4 KiB page) and the runtime's
-  // pageable staging are what bound the mapped upload.  Overlap: the count runs on segments
-  // (whole tiles) as they land -- segment k once every chunk up to the end of segment k + 1 is
-  // in HBM (a word may run into the next segment; one running further is flagged and the whole
-  // count is repeated after the upload).
-  size_t chunk = (size_t)32 << 20;
+  // The file straight into HBM (round 5): a ring of NB pinned buffers of `chunk` bytes; T reader
+  // threads fill each chunk together (a slice each, pread) and one copy thread sends the full
+  // chunks, in order, over ONE stream.  Measured on the box (tools/h2d_probe.py): 32 MiB copies
+  // reach 44 GB/s on one stream but 29 GB/s spread over 8, and pread from the page cache scales
+  // to 52 GB/s at 8 threads -- round 4's reader-per-stream design sat at 12-14 GB/s.  No mapping of
+  // the file (the page-ins of an mmap and the runtime's pageable staging bound that).  Overlap:
+  // the count runs on segments (whole tiles) as they land -- segment k once every chunk up to the
+  // end of segment k + 1 is in HBM (a word may run into the next segment; one running further is
+  // flagged and the whole count is repeated after the upload).
+  size_t chunk = (size_t)64 << 20;
   if (const char* e = std::getenv("SHREDWORD_LOAD_CHUNK_MB")) chunk = std::max<size_t>(1, std::strtoull(e, nullptr, 10)) << 20;
   const size_t nchunks = (n + chunk - 1) / chunk;
   int T = 8;
-  if (const char* e = std::getenv("SHREDWORD_LOAD_READERS")) T = std::max(1, std::atoi(e));
-  T = (int)std::min<size_t>((size_t)T, nchunks);
+  if (const char* e = std::getenv("SHREDWORD_LOAD_READERS")) T = std::max(1, std::min(64, std::atoi(e)));
+  int NB = 4;  // chunks in flight: read, queued for DMA, in DMA
+  if (const char* e = std::getenv("SHREDWORD_LOAD_BUFS")) NB = std::max(2, std::min(16, std::atoi(e)));
+  NB = (int)std::min<size_t>((size_t)NB, nchunks);
+  // readers on the GPU's NUMA node (SHREDWORD_LOAD_NUMA=0: wherever the scheduler puts them)
+  std::vector<int> local;
+  {
+    const char* e = std::getenv("SHREDWORD_LOAD_NUMA");
+    if (!(e && e[0] == '0')) local = gpu_local_cpus(device);
+  }
   const CountShape shape = count_shape(n, cus);
   u64 seg_bytes = (u64)2 << 30;
   if (const char* e = std::getenv("SHREDWORD_LOAD_SEGMENT_MB")) seg_bytes = std::max<u64>(1, std::strtoull(e, nullptr, 10)) << 20;
@@ -642,44 +685,74 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
         if (e) (void)hipEventDestroy(e);
     }
   } eg{ev};
+  struct PinGuard {
+    std::vector<void*> v;
+    ~PinGuard() {
+      for (void* q : v)
+        if (q) (void)hipHostFree(q);
+    }
+  } pg;
+  pg.v.assign((size_t)NB, nullptr);
+  for (int k = 0; k < NB; ++k) LOAD_OK(hipHostMalloc(&pg.v[k], chunk, hipHostMallocDefault));
+  StreamGuard cs;
+  LOAD_OK(hipStreamCreateWithFlags(&cs.s, hipStreamNonBlocking));
+  // recorded[c]: 1 once chunk c's copy is queued behind ev[c] (2: failed); filled[c]: readers done
   std::unique_ptr<std::atomic<int>[]> recorded(new std::atomic<int>[nchunks]);
-  for (size_t c = 0; c < nchunks; ++c) recorded[c].store(0);
+  std::unique_ptr<std::atomic<int>[]> filled(new std::atomic<int>[nchunks]);
+  for (size_t c = 0; c < nchunks; ++c) {
+    recorded[c].store(0);
+    filled[c].store(0);
+  }
   std::vector<std::thread> pool;
   std::atomic<int> failed{0};
   std::atomic<uint64_t> read_ns{0};
+  const size_t slice = ((chunk + (size_t)T - 1) / (size_t)T + 4095) & ~(size_t)4095;
   for (int ti = 0; ti < T; ++ti)
     pool.emplace_back([&, ti] {
-      hipStream_t s = nullptr;
-      void* pin[2] = {nullptr, nullptr};
-      bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
-      for (int k = 0; k < 2 && ok; ++k) ok = hipHostMalloc(&pin[k], chunk, hipHostMallocDefault) == hipSuccess;
-      int k = 0;
-      size_t last[2] = {SIZE_MAX, SIZE_MAX};
-      for (size_t c = (size_t)ti; c < nchunks; c += (size_t)T, k ^= 1) {
-        if (ok && !failed.load(std::memory_order_relaxed)) {
-          if (last[k] != SIZE_MAX) ok = hipEventSynchronize(ev[last[k]]) == hipSuccess;  // buffer k is free again
-          const size_t off = c * chunk, len = std::min(chunk, n - off);
+      if (!local.empty()) {
+        cpu_set_t cpus;
+        CPU_ZERO(&cpus);
+        for (int c : local) CPU_SET(c, &cpus);
+        (void)sched_setaffinity(0, sizeof(cpus), &cpus);
+      }
+      bool ok = hipSetDevice(device) == hipSuccess;
+      for (size_t c = 0; c < nchunks; ++c) {
+        const size_t off = c * chunk, len = std::min(chunk, n - off);
+        const size_t s0 = std::min(len, (size_t)ti * slice), s1 = std::min(len, s0 + slice);
+        if (ok && !failed.load(std::memory_order_relaxed) && s1 > s0) {
+          if (c >= (size_t)NB) {  // the buffer is free once chunk c - NB's copy is done
+            int r;
+            while ((r = recorded[c - NB].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+            ok = r == 1 && hipEventSynchronize(ev[c - NB]) == hipSuccess;
+          }
+          uint8_t* dst = static_cast<uint8_t*>(pg.v[c % (size_t)NB]);
           const double tr = wall();
-          size_t got = 0;
-          while (ok && got < len) {
-            const ssize_t r = ::pread(fd, (uint8_t*)pin[k] + got, len - got, (off_t)(base + off + got));
+          size_t got = s0;
+          while (ok && got < s1) {
+            const ssize_t r = ::pread(fd, dst + got, s1 - got, (off_t)(base + off + got));
             if (r <= 0) ok = false;
             else got += (size_t)r;
           }
           read_ns.fetch_add((uint64_t)(1e9 * (wall() - tr)), std::memory_order_relaxed);
-          ok = ok && hipMemcpyAsync(db + off, pin[k], len, hipMemcpyHostToDevice, s) == hipSuccess &&
-               hipEventRecord(ev[c], s) == hipSuccess;
-          last[k] = c;
         }
         if (!ok) failed.store(1);
-        recorded[c].store(ok ? 1 : 2, std::memory_order_release);  // 2: failed (the counter stops)
+        filled[c].fetch_add(1, std::memory_order_acq_rel);
       }
-      if (s) ok = hipStreamSynchronize(s) == hipSuccess && ok;
-      for (int j = 0; j < 2; ++j)
-        if (pin[j]) (void)hipHostFree(pin[j]);
-      if (s) (void)hipStreamDestroy(s);
-      if (!ok) failed.store(1);
     });
+  // the copy thread: every full chunk, in order, on one stream
+  pool.emplace_back([&] {
+    bool ok = hipSetDevice(device) == hipSuccess;
+    for (size_t c = 0; c < nchunks; ++c) {
+      while (filled[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+      ok = ok && !failed.load(std::memory_order_relaxed);
+      const size_t off = c * chunk, len = std::min(chunk, n - off);
+      ok = ok && hipMemcpyAsync(db + off, pg.v[c % (size_t)NB], len, hipMemcpyHostToDevice, cs.s) == hipSuccess &&
+           hipEventRecord(ev[c], cs.s) == hipSuccess;
+      if (!ok) failed.store(1);
+      recorded[c].store(ok ? 1 : 2, std::memory_order_release);
+    }
+    if (hipStreamSynchronize(cs.s) != hipSuccess) failed.store(1);
+  });
   // the segmented count on this thread's stream, behind the chunks' events
   CountTable pre;
   bool pre_ok = false;
@@ -715,9 +788,10 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   }
   const double t1 = wall();
   if (report)
-    std::fprintf(stderr, "[LOAD] phase file_to_hbm %.1f ms (%d readers, %zu MiB chunks, pread %.1f ms summed over "
-                 "readers): %.1f GB/s%s\n", 1e3 * (t1 - t0), T, chunk >> 20, 1e-6 * (double)read_ns.load(),
-                 (double)n / (t1 - t0) / 1e9, overlap ? "; the count ran on segments meanwhile" : "");
+    std::fprintf(stderr, "[LOAD] phase file_to_hbm %.1f ms (%d readers, %d pinned %zu MiB chunks, one copy stream, readers "
+                 "on %zu GPU-local CPUs, pread %.1f ms summed over readers): %.1f GB/s%s\n", 1e3 * (t1 - t0), T, NB,
+                 chunk >> 20, local.size(), 1e-6 * (double)read_ns.load(), (double)n / (t1 - t0) / 1e9,
+                 overlap ? "; the count ran on segments meanwhile" : "");
   if (!count_on_device(db, n, st, cus, report, t0, t1, out, spell, nul, why, pre_ok ? &pre : nullptr, table_n))
     return false;
   if (base)
