@@ -61,13 +61,17 @@ constexpr int kTileStride = kChunkBytes + 4;  // LDS bytes per chunk: the lanes'
 //           occurrences at C3 by a host simulation of the table).
 constexpr int kNarrowThreads = 256, kNarrowSlots = 1536;
 constexpr int kWideThreads = 512, kWideSlots = 3072;
+// xwide (round 5): 768 threads, 48 KB tiles, the same 3072 slots (108 KB + 51 KB): 12 waves a CU
+// instead of 8, more HBM spill chains in flight (the count is bound by them, not by its bytes)
+constexpr int kXWideThreads = 768;
 constexpr int kLdsProbes = 8;
 constexpr int kSpell = 16;           // leading bytes of a word an LDS slot keeps
-constexpr size_t kPadBytes = (size_t)kChunkBytes * kWideThreads + 256;  // ' ' past the corpus: every tile load and word scan stays inside
+constexpr size_t kPadBytes = (size_t)kChunkBytes * kXWideThreads + 256;  // ' ' past the corpus: every tile load and word scan stays inside
 // HBM table probes before the table counts as too full (it is grown 4x and the count rerun); with
 // the 3/4 fill flag the usual probe run is a few slots
 constexpr u64 kTableProbes = 512;
-constexpr bool kLoadWideDefault = true;  // the wide shape (C3: PMC 87.8 -> 77.9 GB); SHREDWORD_LOAD_WIDE=0/1 overrides
+constexpr bool kLoadWideDefault = true;  // the wide shape (C3: PMC 87.8 -> 77.9 GB); SHREDWORD_LOAD_WIDE=0/1/2 overrides
+constexpr int kLoadShapeDefault = 2;  // xwide: C3 load 1.09-1.12 s -> 0.92-0.95 s (round 5 A/B on one box)
 
 __device__ __forceinline__ bool delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }
 __device__ __forceinline__ uint32_t has_zero(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
@@ -335,14 +339,18 @@ static double wall() {
 
 // The count kernel's geometry for n bytes: workgroup shape, tiles per workgroup.
 struct CountShape {
-  bool wide;
+  int kind;   // 0 narrow (256 threads, 2 a CU), 1 wide (512), 2 xwide (768)
+  bool wide;  // one workgroup a CU
+  int threads;
   u64 tile_bytes, ntiles, per;
 };
 static CountShape count_shape(size_t n, int cus) {
   const char* wenv = std::getenv("SHREDWORD_LOAD_WIDE");
   CountShape c;
-  c.wide = wenv ? std::atoi(wenv) != 0 : kLoadWideDefault;
-  c.tile_bytes = (u64)kChunkBytes * (c.wide ? kWideThreads : kNarrowThreads);
+  c.kind = wenv ? std::max(0, std::min(2, std::atoi(wenv))) : kLoadShapeDefault;
+  c.wide = c.kind != 0;
+  c.threads = c.kind == 2 ? kXWideThreads : c.kind == 1 ? kWideThreads : kNarrowThreads;
+  c.tile_bytes = (u64)kChunkBytes * (u64)c.threads;
   c.ntiles = (n + c.tile_bytes - 1) / c.tile_bytes;
   u64 grid = std::min<u64>(std::max<u64>(c.ntiles, 1), (u64)cus * (c.wide ? 1 : 2));
   c.per = (c.ntiles + grid - 1) / grid;
@@ -360,7 +368,10 @@ static void count_launch(const CountShape& c, const uint8_t* db, size_t n, const
   if (tile1 <= tile0) return;
   if (!per) per = c.per;
   const u64 grid = (tile1 - tile0 + per - 1) / per;
-  if (c.wide)
+  if (c.kind == 2)
+    k_word_count<kXWideThreads, kWideSlots><<<(unsigned)grid, kXWideThreads, 0, st>>>(db, n, t, seed, kmask, per, tile0,
+                                                                                      tile1, safe_end);
+  else if (c.wide)
     k_word_count<kWideThreads, kWideSlots><<<(unsigned)grid, kWideThreads, 0, st>>>(db, n, t, seed, kmask, per, tile0,
                                                                                     tile1, safe_end);
   else

@@ -502,14 +502,15 @@ def test_full_size_invariants(name, tmp_path, monkeypatch):
     assert freqs[-1] >= mpf
 
 
-@pytest.mark.parametrize("wide", ["0", "1"], ids=["narrow", "wide"])
+@pytest.mark.parametrize("wide", ["0", "1", "2"], ids=["narrow", "wide", "xwide"])
 @pytest.mark.parametrize("kind", ["medium", "adversarial_no_nul", "utf8"])
 def test_gpu_word_count_matches_host(kind, wide, medium_corpus, tmp_path, monkeypatch):
     """load_corpus counting words on the device (load_device.hip) against the host count: the
     same word table, so the same training bytes -- with both k_word_count workgroup shapes
     (256 threads / 1536 LDS slots, 512 / 3072; SHREDWORD_LOAD_WIDE).  The adversarial corpus (CR/TAB
     runs, 10 kB lines, a 10,333-byte word, no final newline) is taken without its NUL bytes,
-    which keep the host's fgets/strlen path."""
+    which keep the host's fgets/strlen path.  Shapes: 256 threads / 1536 slots, 512 / 3072, and
+    768 / 3072 (xwide, round 5)."""
     monkeypatch.setenv("SHREDWORD_GPU_LOAD_MIN", "1")
     monkeypatch.setenv("SHREDWORD_LOAD_WIDE", wide)
     if kind == "medium":
