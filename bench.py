@@ -652,6 +652,7 @@ def tiebreak_report(st, merges, elapsed, args, out_prefix):
         "launches": st["sel_launches"],
         "rebuilds": st["sel_rebuilds"], "rebuild_ms": st["sel_rebuild_ms"], "kernel_ms": st["sel_kernel_ms"],
         "device_select_us_per_merge": st["sel_select_us"] / n, "device_merge_us_per_merge": st["sel_merge_us"] / n,
+        "device_table_update_us_per_merge": st["sel_table_us"] / n,
         "table_pairs": st["sel_table_pairs"], "table_slots": st["sel_table_slots"],
         "operands_before_merge": bool((ops[:, :2] < ops[:, 2:3]).all()),
         "weighted_symbols": sym,

@@ -211,6 +211,7 @@ typedef struct ShredStats {
   double index_dev_out_us;     /* k_word_loop: Σ device time handing the records out (raw or finalized) */
   double index_dev_fin_us;     /*   of which: the finalized merges */
   uint64_t index_fin_records;  /*   their raw records */
+  double sel_table_us;         /* tiebreak=device: of sel_merge_us, the pair-table + frontier update */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

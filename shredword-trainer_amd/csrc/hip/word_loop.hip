@@ -115,15 +115,18 @@ struct SelParams {
   uint32_t* st;       // see kSel* below
   const u64* thr;     // threshold (count, key): every pair ranked at or above it is in the frontier
   u64* out;           // per merge: key, count
-  uint32_t* upd;      // scratch: slots of the pairs the current merge created
+  u64* log;           // the launch's pair-count changes (key, signed delta), applied to the table between launches
+  u64 log_cap;        //   entries
   int32_t X0;         // id of merge 0 of this training
   uint32_t n_max;     // merges wanted
   u64 min_freq;
   uint32_t fill_max;  // inserts allowed before the table counts as full
+  uint32_t probe;     // diagnostic (SHREDWORD_SEL_PROBE): 1 skips the table's HBM updates (timing only: wrong counts)
 };
 // st words
 constexpr int kSelM = 0, kSelNF = 1, kSelBuf = 2, kSelStatus = 3, kSelIns = 4, kSelErr = 5, kSelStats = 6;
-constexpr int kSelWords = kSelStats + 2 * 8;  // st: 6 words, then 8 u64 statistics
+constexpr int kSelWords = kSelStats + 2 * 12 + 2;  // st: 6 words, then 12 u64 statistics, then the log's length (u64)
+constexpr int kSelLogW = kSelStats + 2 * 12;
 // exit status: merges done (target reached / below min_pair_freq), frontier to rebuild, table full
 constexpr uint32_t kSelDone = 1, kSelRebuild = 2, kSelFull = 3;
 // The frontier lives in LDS for the whole launch: each entry's count follows the table's (the
@@ -137,14 +140,17 @@ constexpr int kPosShift = 48;
 template <bool kOn>
 struct SelLds {  // k_word_loop<false>: none
   u64 key[1], cnt[1];
-  uint32_t slot[1], n;
+  uint32_t idx[1], n;
 };
+// The frontier's LDS index (round 5): pair key -> position + 1 (16 bits, two to a word), so a
+// record finds its pair's LDS copy without a table round trip, and the table's count words carry
+// no positions (the table's atomics need no return value).
+constexpr uint32_t kSelIdx = 4096;
 template <>
 struct SelLds<true> {
   u64 key[kSelF], cnt[kSelF];
-  uint32_t slot[kSelF], n;
+  uint32_t idx[kSelIdx / 2], n;
 };
-
 struct WlParams {
   int32_t* wtok;
   const u64* weight;
@@ -180,6 +186,36 @@ __device__ __forceinline__ u64 mix64(u64 k) {
   return k;
 }
 __device__ __forceinline__ u64 pair_key(int32_t a, int32_t b) { return ((u64)(uint32_t)a << 32) | (uint32_t)b; }
+__device__ __forceinline__ uint32_t sel_idx_home(u64 k) { return (uint32_t)(mix64(k) >> 40) & (kSelIdx - 1); }
+// position of key in the frontier, or -1 (also for a dead entry never compacted: those are found
+// and their counts kept, harmlessly)
+__device__ __forceinline__ int sel_idx_find(const SelLds<true>& F, u64 k) {
+  uint32_t h = sel_idx_home(k);
+#pragma unroll 1
+  for (uint32_t probe = 0; probe < kSelIdx; ++probe) {
+    const uint32_t v = (F.idx[h >> 1] >> ((h & 1u) * 16u)) & 0xFFFFu;
+    if (v == 0) return -1;
+    if (F.key[v - 1u] == k) return (int)(v - 1u);
+    h = (h + 1u) & (kSelIdx - 1u);
+  }
+  return -1;
+}
+__device__ __forceinline__ bool sel_idx_insert(SelLds<true>& F, u64 k, uint32_t pos) {
+  uint32_t h = sel_idx_home(k);
+#pragma unroll 1
+  for (uint32_t probe = 0; probe < kSelIdx;) {
+    const uint32_t sh = (h & 1u) * 16u;
+    const uint32_t old = F.idx[h >> 1];
+    if (((old >> sh) & 0xFFFFu) == 0u) {
+      if (atomicCAS(&F.idx[h >> 1], old, old | ((pos + 1u) << sh)) == old) return true;
+      continue;  // the word changed under us: look again
+    }
+    h = (h + 1u) & (kSelIdx - 1u);
+    ++probe;
+  }
+  return false;
+}
+
 __device__ __forceinline__ uint32_t slot_of(int32_t id, uint32_t cap) {
   return (uint32_t)id < cap ? (uint32_t)id + 1u : 0u;
 }
@@ -219,29 +255,51 @@ __device__ __forceinline__ u64 sel_slot(const SelParams& q, u64 pk, uint32_t* in
   return ~0ull;
 }
 // One combined record of merge (a, b) -> X as a change of a pair's count (the reference's
-// FreqChangeMap entry, bpe.cpp:297-313, minus the pair merged and pairs holding unk).  New pairs
-// (categories 1 and 3: they hold X) are listed for the frontier.
-__device__ __forceinline__ void sel_apply(const SelParams& q, SelLds<true>& F, uint32_t* nnew, uint32_t* ins, uint32_t* err,
-                                          int32_t unk, uint32_t cap, uint32_t key, u64 sum, int32_t a, int32_t b,
-                                          int32_t X) {
+// FreqChangeMap entry, bpe.cpp:297-313, minus the pair merged and pairs holding unk).  The table
+// is only read between launches (the frontier's rebuild), so its change is logged (a coalesced
+// store, no round trip) and applied in bulk by k_sel_apply_log; a pair already in the frontier gets
+// it in LDS through the frontier's index.  Pairs holding X are new (their count was 0): their count
+// is the sum of their records' deltas, listed in LDS (nkey / ncnt) for the frontier -- (X, a) has
+// two records, NewRight(a) listed and OldLeft(X) summed into *dxa, added when it is appended.
+struct SelNew {
+  u64* key;
+  u64* cnt;
+  uint32_t* n;
+  uint32_t cap;
+  u64* dxa;
+  uint32_t* over;
+  u64* log;         // this merge's table changes go to log[0, *nlog)
+  uint32_t* nlog;
+};
+__device__ __forceinline__ void sel_record(const SelParams& q, SelLds<true>& F, const SelNew& nw, int32_t unk,
+                                           uint32_t key, u64 sum, int32_t a, int32_t b, int32_t X) {
   const uint32_t sl = key >> 2, cat = key & 3u;
   const int32_t id = sl == 0 ? unk : (int32_t)(sl - 1u);
   if (id == unk || sum == 0) return;
   const int32_t f = cat < 2u ? id : (cat == 2u ? b : X);
   const int32_t g = cat == 0u ? a : (cat == 1u ? X : id);
   if (f == a && g == b) return;
-  const u64 h = sel_slot(q, pair_key(f, g), ins, err);
-  if (h == ~0ull) return;
+  const u64 pk = pair_key(f, g);
   const u64 d = (cat & 1u) ? sum : (u64)(-(int64_t)sum);
-  // the count word's old value says where the LDS copy is.  A pair in the frontier holds no X, so
-  // it only falls and never below 0: its position bits are intact.  A new pair (holding X) is not
-  // in the frontier yet; a decrement landing before its increment may borrow through the
-  // position bits (reading as 0xFFFF, "not in the frontier") and the increment carries them back.
-  const u64 old = atomicAdd(q.tab + 2 * h + 1, d);
-  const uint32_t pos = (uint32_t)(old >> kPosShift) - 1u;
-  if (pos < kSelF) atomicAdd(reinterpret_cast<unsigned long long*>(&F.cnt[pos]), (unsigned long long)d);
-  if (cat & 1u) q.upd[atomicAdd(nnew, 1u)] = (uint32_t)h;
-  (void)cap;
+  if (!(q.probe & 1u)) {  // the table's change, applied between launches (k_sel_apply_log)
+    const uint32_t j = atomicAdd(nw.nlog, 1u);
+    nw.log[2 * (u64)j] = pk;
+    nw.log[2 * (u64)j + 1] = d;
+  }
+  if (f != X && g != X) {
+    const int pos = sel_idx_find(F, pk);
+    if (pos >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(&F.cnt[pos]), (unsigned long long)d);
+  } else if (cat == 0u) {  // OldLeft(X): (X, a)
+    atomicAdd(reinterpret_cast<unsigned long long*>(nw.dxa), (unsigned long long)d);
+  } else {
+    const uint32_t i = atomicAdd(nw.n, 1u);
+    if (i < nw.cap) {
+      nw.key[i] = pk;
+      nw.cnt[i] = d;
+    } else {
+      *nw.over = 1u;  // the frontier may miss a pair: rebuild
+    }
+  }
 }
 
 struct DeltaH {
@@ -458,7 +516,8 @@ struct LoopS {
   u64 t_wait, t_idle, t_undo;  // s_memrealtime: this command's wait began; idle / undo since the last flag
   // tiebreak=device
   uint32_t sm, snk, snew, status, sel_pos, sover, scompact, sins, serr;
-  u64 sel_slot;
+  u64 sel_cnt, dxa, t_rec, t_app, logn;
+  uint32_t lognew, newtot;
   u64 bc[kWlThreads / 64], bk[kWlThreads / 64];
   uint32_t bs[kWlThreads / 64];
 };
@@ -679,25 +738,28 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   uint32_t expect = p.seq0;
   uint32_t exit_op = kOpStop;
   const MergeCtx mc{&S.nspill, &S.nkeys};
-  if constexpr (kSelf) {  // the rebuilt frontier into LDS, each slot told its position
+  if constexpr (kSelf) {  // the rebuilt frontier into LDS, indexed by pair key
     const SelParams& q = p.sel;
     const uint32_t nf = min(ld_agent(q.st + kSelNF), kSelK);
+    for (uint32_t i = tid; i < kSelIdx / 2; i += kWlThreads) s_f.idx[i] = 0;
     for (uint32_t i = tid; i < nf; i += kWlThreads) {
       const uint32_t sl = ld_agent(q.fr[0] + i);
-      const u64 c = ld_agent64(q.tab + 2 * (u64)sl + 1) & kCntMask;
-      s_f.slot[i] = sl;
       s_f.key[i] = ld_agent64(q.tab + 2 * (u64)sl);
-      s_f.cnt[i] = c;
-      __hip_atomic_store(q.tab + 2 * (u64)sl + 1, c | ((u64)(i + 1u) << kPosShift), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      s_f.cnt[i] = ld_agent64(q.tab + 2 * (u64)sl + 1) & kCntMask;
     }
     if (tid == 0) {
       s_f.n = nf;
       S.scompact = 0;
       S.sins = ld_agent(q.st + kSelIns);  // the table's inserts so far (the host's and earlier launches')
       S.serr = 0;
+      S.sover = 0;
+      S.logn = 0;  // the host applied the previous launch's log
+      S.lognew = 0;
+      S.newtot = 0;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (uint32_t i = tid; i < nf; i += kWlThreads)
+      if (!sel_idx_insert(s_f, s_f.key[i], i)) S.sover = 1;
   }
   __syncthreads();
   for (;;) {
@@ -754,6 +816,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         const uint32_t m = S.sm;
         uint32_t status = 0;
         if (m >= q.n_max) status = kSelDone;
+        else if (S.logn + 4ull * ((u64)p.cap + 2u) > q.log_cap) status = kSelRebuild;  // the log must be applied first
+        // only pairs holding a new id are ever inserted: the table's fill is known without it
+        // (a merge inserts at most 2 (cap + 1) pairs: (p, X) and (X, n) for every neighbour id)
+        else if ((u64)S.sins + S.newtot + 2ull * ((u64)p.cap + 2u) > q.fill_max) status = kSelRebuild;
         else if (S.snk == 0) status = kSelRebuild;  // nothing at or above the threshold is left
         else if (bc < q.min_freq) status = kSelDone;
         S.cmd[0] = status ? kOpStop : kOpMerge;
@@ -768,7 +834,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           S.cmd[6] = 0;  // no list given: the loop looks it up
           S.cmd[7] = 0;
           S.sel_pos = bs;
-          S.sel_slot = s_f.slot[bs];
+          S.sel_cnt = bc;
           q.out[2 * (u64)m] = bk;
           q.out[2 * (u64)m + 1] = bc;
         }
@@ -1046,8 +1112,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     __syncthreads();
     const uint32_t nchg = append ? S.nchg : 0u;
     if constexpr (kSelf) {
-      // ---- tiebreak=device: the records change the pair table; the pairs this merge created
-      // that rank at or above the threshold join the frontier
+      // ---- tiebreak=device: the records change the pair table (atomics nobody waits for) and,
+      // through the frontier's LDS index, the frontier's counts; the pairs this merge created that
+      // rank at or above the threshold join the frontier -- their counts come from the records
+      // (they were 0 before), so nothing is read back from the table
       const SelParams& q = p.sel;
       const u64 t_tab = __builtin_amdgcn_s_memrealtime();
       if (tid == 0) {
@@ -1057,67 +1125,68 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           S.pool_top = top + nchg;
         }
         S.snew = 0;
+        S.dxa = 0;
       }
       __syncthreads();
+      constexpr uint32_t kNewCap = (uint32_t)kQ / 2;  // the new pairs' list in the merge queue's LDS (free now)
+      const SelNew nw{s_q, s_q + kNewCap, &S.snew, kNewCap, &S.dxa, &S.sover, q.log + 2 * S.logn, &S.lognew};
       for (int i = tid; i < kDh; i += kWlThreads) {
         const uint32_t key = s_h.key[i];
-        if (key != kEmpty32) sel_apply(q, s_f, &S.snew, &S.sins, &S.serr, p.unk, p.cap, key, s_h.sum[i], a, b, X);
+        if (key != kEmpty32) sel_record(q, s_f, nw, p.unk, key, s_h.sum[i], a, b, X);
       }
       const uint32_t nsp = S.nspill;
       for (uint32_t i = tid; i < nsp; i += kWlThreads) {
         const uint32_t key = p.dlist[i];
         const u64 sum = atomicExch(&p.dsum[key], 0ull);
         atomicExch(&p.dft[key], kEmpty64);
-        sel_apply(q, s_f, &S.snew, &S.sins, &S.serr, p.unk, p.cap, key, sum, a, b, X);
+        sel_record(q, s_f, nw, p.unk, key, sum, a, b, X);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {  // the merged pair: count 0 (it never occurs again), still at its LDS position
-        __hip_atomic_store(q.tab + 2 * S.sel_slot + 1, (u64)(S.sel_pos + 1u) << kPosShift, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        s_f.cnt[S.sel_pos] = 0;
-        S.sover = 0;
+      // LDS results only: the table's atomics stay in flight (a plain __syncthreads would drain them)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (tid == 0) S.t_rec = __builtin_amdgcn_s_memrealtime();
+      if (tid == 0) {  // the merged pair: count 0 (it never occurs again); in the table by its LDS
+        s_f.cnt[S.sel_pos] = 0;  // count's opposite, so the log's adds need no order
+        u64* lg = q.log + 2 * (S.logn + S.lognew);
+        lg[0] = pair_key(a, b);
+        lg[1] = (u64)(-(int64_t)S.sel_cnt);
+        S.logn += S.lognew + 1u;
+        S.lognew = 0;
+        S.newtot += S.snew;
       }
       const u64 tc = q.thr[0], tk = q.thr[1];
-      const uint32_t nnew = S.snew;
+      const uint32_t nnew = min(S.snew, kNewCap);
+      const u64 kxa = pair_key(X, a), dxa = S.dxa;
       for (uint32_t i = tid; i < nnew; i += kWlThreads) {
-        const uint32_t sl = q.upd[i];
-        const u64 k = ld_agent64(q.tab + 2 * (u64)sl), cv = ld_agent64(q.tab + 2 * (u64)sl + 1);
-        const u64 c = cv & kCntMask;
-        if ((cv >> kPosShift) == 0 && sel_at_least(c, k, tc, tk)) {
-          // a place first, then the claim (a pair listed twice claims once; the loser's place
-          // stays a dead entry)
+        const u64 k = nw.key[i];
+        const u64 c = nw.cnt[i] + (k == kxa ? dxa : 0ull);
+        if (sel_at_least(c, k, tc, tk)) {
           const uint32_t pos = atomicAdd(&s_f.n, 1u);
           if (pos < kSelF) {
-            const bool won = atomicCAS(q.tab + 2 * (u64)sl + 1, cv, c | ((u64)(pos + 1u) << kPosShift)) == cv;
-            s_f.slot[pos] = sl;
-            s_f.key[pos] = won ? k : kEmpty64;
-            s_f.cnt[pos] = won ? c : 0;
+            s_f.key[pos] = k;
+            s_f.cnt[pos] = c;
+            if (!sel_idx_insert(s_f, k, pos)) S.sover = 1;
           } else {
             S.sover = 1;  // the frontier lost an entry: rebuild
           }
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      // past kSelF - kSelRoom entries: the dead ones go (in place, order kept), the rest are told
-      // their new positions
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (tid == 0) S.t_app = __builtin_amdgcn_s_memrealtime();
+      // past kSelF - kSelRoom entries: the dead ones go (in place, order kept) and the index is
+      // rebuilt for the new positions
       if (!S.sover && s_f.n > kSelF - kSelSlack) {
         constexpr int kPer = (int)((kSelF + kWlThreads - 1) / kWlThreads);
         const uint32_t n0 = s_f.n;
         u64 ck[kPer], kk[kPer];
-        uint32_t sk[kPer];
         uint32_t mine = 0, keepm = 0;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {  // thread t holds entries kPer*t .. kPer*t + kPer-1
           const uint32_t i = (uint32_t)kPer * tid + (uint32_t)j;
           ck[j] = 0;
           kk[j] = kEmpty64;
-          sk[j] = 0;
           if (i < n0) {
             ck[j] = s_f.cnt[i];
             kk[j] = s_f.key[i];
-            sk[j] = s_f.slot[i];
             if (kk[j] != kEmpty64 && sel_at_least(ck[j], kk[j], tc, tk)) {
               keepm |= 1u << j;
               ++mine;
@@ -1126,29 +1195,26 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         }
         const uint32_t incl = wave_incl_add(mine);
         if (lane == 63) S.bs[wid] = incl;  // wave totals
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         uint32_t base = incl - mine;
         for (int w = 0; w < wid; ++w) base += S.bs[w];
         uint32_t tot = 0;
         for (int w = 0; w < kWlThreads / 64; ++w) tot += S.bs[w];
-        __syncthreads();  // every entry is in registers before any is moved
+        for (uint32_t i = tid; i < kSelIdx / 2; i += kWlThreads) s_f.idx[i] = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every entry is in registers before any is moved
+        const uint32_t b0 = base;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
           const uint32_t i = (uint32_t)kPer * tid + (uint32_t)j;
-          if (i >= n0) continue;
-          if ((keepm >> j) & 1u) {
-            s_f.cnt[base] = ck[j];
-            s_f.key[base] = kk[j];
-            s_f.slot[base] = sk[j];
-            __hip_atomic_store(q.tab + 2 * (u64)sk[j] + 1, ck[j] | ((u64)(base + 1u) << kPosShift), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            ++base;
-          } else if (kk[j] != kEmpty64) {  // (a dead place of a lost claim owns no slot)
-            __hip_atomic_store(q.tab + 2 * (u64)sk[j] + 1, ck[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
+          if (i >= n0 || !((keepm >> j) & 1u)) continue;
+          s_f.cnt[base] = ck[j];
+          s_f.key[base] = kk[j];
+          ++base;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (uint32_t i = b0; i < base; ++i)
+          if (!sel_idx_insert(s_f, s_f.key[i], i)) S.sover = 1;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (tid == 0) {
           s_f.n = tot;
           ++S.scompact;
@@ -1170,11 +1236,13 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         t64[5] += nnew;
         t64[6] += now - t_tab;  // of t64[1]: the table and frontier update
         t64[7] += S.scompact ? 1u : 0u;
+        t64[8] += S.t_rec - t_tab;    // records -> table + frontier counts + new-pair list
+        t64[9] += S.t_app - S.t_rec;  // merged pair, new pairs appended
+        t64[10] += now - S.t_app;     // compaction (when due), bookkeeping
         q.st[kSelBuf] = S.scompact;  // (statistic: LDS compactions of this launch)
         // after a complete merge: a frontier that lost an entry needs a rebuild, a table past its
         // fill bound must grow (the host stops)
-        const uint32_t full = S.sins > q.fill_max || S.serr != 0;
-        S.status = full ? kSelFull : (S.sover ? kSelRebuild : 0u);
+        S.status = S.sover ? kSelRebuild : 0u;  // (the table's fill is checked when its log is applied)
       }
       __syncthreads();
       if (S.status) {
@@ -1269,6 +1337,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     p.dstate[kStPoolTop] = S.pool_top;
     if constexpr (kSelf) {
       p.sel.st[kSelIns] = S.sins;
+      *reinterpret_cast<u64*>(p.sel.st + kSelLogW) = S.logn;
       p.sel.st[kSelErr] = S.serr;
       p.sel.st[kSelStatus] = exit_op;
       __threadfence_system();
@@ -1482,6 +1551,15 @@ __global__ void k_sel_insert(const PairCount* pc, uint64_t n, SelParams q) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const u64 h = sel_slot(q, pair_key(pc[i].a, pc[i].b), q.st + kSelIns, q.st + kSelErr);
     if (h != ~0ull) q.tab[2 * h + 1] = pc[i].count & kCntMask;
+  }
+}
+
+// The launch's logged changes into the table (whole chip, between launches): each a slot
+// (inserted when new) and an add; the adds commute, so their order is free.
+__global__ void k_sel_apply_log(const u64* log, u64 n, SelParams q) {
+  for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+    const u64 h = sel_slot(q, log[2 * i], q.st + kSelIns, q.st + kSelErr);
+    if (h != ~0ull) atomicAdd(q.tab + 2 * h + 1, log[2 * i + 1]);
   }
 }
 
@@ -2180,11 +2258,13 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
     sout_cap_ = 2ull * n_max;
     sout_ = wl_alloc<u64>(sout_cap_, &bytes_);
   }
-  const uint64_t need_upd = 4ull * ((uint64_t)cap_ + 1) + 64;  // records of one merge
-  if (need_upd > upd_cap_) {
+  // the table-change log: many merges' records between two applications (a launch ends early
+  // when one more merge might not fit)
+  const uint64_t need_log = std::max<uint64_t>(1ull << 22, 16ull * ((uint64_t)cap_ + 2));
+  if (need_log > upd_cap_) {
     if (upd_) WL_OK(hipFree(upd_));
-    upd_cap_ = need_upd;
-    upd_ = wl_alloc<uint32_t>(upd_cap_, &bytes_);
+    upd_cap_ = need_log;
+    upd_ = wl_alloc<uint32_t>(4 * upd_cap_, &bytes_);  // (key, delta) u64 pairs
   }
   WL_OK(hipMemsetAsync(sst_dev_, 0, kSelWords * sizeof(uint32_t), s));
   SelParams q{};
@@ -2204,11 +2284,13 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
     q.st = sst_dev_;
     q.thr = thr_;
     q.out = sout_;
-    q.upd = upd_;
+    q.log = reinterpret_cast<u64*>(upd_);
+    q.log_cap = upd_cap_;
     q.X0 = X0;
     q.n_max = n_max;
     q.min_freq = min_freq;
     q.fill_max = (uint32_t)std::min<uint64_t>(3 * pcap_ / 4, 0xFFFFFFF0ull);
+    if (const char* e = std::getenv("SHREDWORD_SEL_PROBE")) q.probe = (uint32_t)std::atoi(e);
     uint32_t zero = 0;
     WL_OK(hipMemcpyAsync(sst_dev_ + kSelIns, &zero, sizeof(zero), hipMemcpyHostToDevice, s));
     WL_OK(hipMemcpyAsync(sst_dev_ + kSelErr, &zero, sizeof(zero), hipMemcpyHostToDevice, s));
@@ -2217,6 +2299,9 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
       WL_OK(hipGetLastError());
     }
     WL_OK(hipStreamSynchronize(s));
+    uint32_t err = 0;  // a pair that found no slot within the probe bound would be a lost count
+    WL_OK(hipMemcpy(&err, sst_dev_ + kSelErr, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) fatal("tiebreak=device: the pair table's initial pairs overran the probe bound");
   };
   {
     size_t acc = 0;
@@ -2270,10 +2355,28 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
         std::fprintf(stderr, "[SELECT] launch %llu: merges %u..%u in %.3f ms (%.2f us/merge), status %u, table %u, "
                      "%u LDS compactions\n", (unsigned long long)sst_.launches, m, st[kSelM], ms,
                      st[kSelM] > m ? 1e3 * ms / (st[kSelM] - m) : 0.0, st[kSelStatus], st[kSelIns], st[kSelBuf]);
+      const bool progressed = st[kSelM] != m;
       m = st[kSelM];
+      // the launch's logged changes into the table
+      const u64 logn = *reinterpret_cast<const u64*>(st + kSelLogW);
+      if (logn) {
+        const double tl = now_seconds();
+        k_sel_apply_log<<<1024, 256, 0, s>>>(reinterpret_cast<const u64*>(upd_), logn, q);
+        WL_OK(hipGetLastError());
+        WL_OK(hipMemsetAsync(sst_dev_ + kSelLogW, 0, sizeof(u64), s));
+        WL_OK(hipMemcpyAsync(st + kSelIns, sst_dev_ + kSelIns, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        WL_OK(hipStreamSynchronize(s));
+        sst_.log_ms += 1e3 * (now_seconds() - tl);
+        sst_.log_entries += logn;
+      }
+      // a change whose pair found no table slot within the probe bound would be lost: the table
+      // would no longer be the corpus's count, so there is nothing exact to grow from
+      if (st[kSelErr]) fatal("tiebreak=device: a pair-table update overran the probe bound");
       const uint32_t status = st[kSelStatus];
       if (status == kSelDone) break;
-      if (status == kSelFull) {  // the table past 3/4 full (or a probe run past its bound): 4x, live pairs moved
+      // the table past 3/4 full, or without room for one more merge's new pairs (the launch then
+      // ended before merging anything): 4x, live pairs moved
+      if (st[kSelIns] > q.fill_max || (status == kSelRebuild && !progressed)) {
         size_t acc = 0;
         PairCount* dp = wl_alloc<PairCount>(pcap_, &acc);
         uint32_t* dn = wl_alloc<uint32_t>(1, &acc);
@@ -2310,10 +2413,14 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
     sst_.occurrences += t64[4];
     sst_.new_pairs += t64[5];
     sst_.table_us += 1e-2 * (double)t64[6];
+    sst_.rec_us += 1e-2 * (double)t64[8];
+    sst_.append_us += 1e-2 * (double)t64[9];
+    sst_.tail_us += 1e-2 * (double)t64[10];
     if (sel_report_ && m)
-      std::fprintf(stderr, "[SELECT] %u merges: device select %.2f us, merge %.2f us (of it table + frontier %.2f us) "
-                   "per merge; %llu LDS compactions, %llu listed / %llu changed words\n", m, 1e-2 * (double)t64[0] / m,
-                   1e-2 * (double)t64[1] / m, 1e-2 * (double)t64[6] / m, (unsigned long long)t64[7],
+      std::fprintf(stderr, "[SELECT] %u merges: device select %.2f us, merge %.2f us (of it table + frontier %.2f us: "
+                   "records %.2f, appends %.2f, tail %.2f) per merge; %llu LDS compactions, %llu listed / %llu changed "
+                   "words\n", m, 1e-2 * (double)t64[0] / m, 1e-2 * (double)t64[1] / m, 1e-2 * (double)t64[6] / m,
+                   1e-2 * (double)t64[8] / m, 1e-2 * (double)t64[9] / m, 1e-2 * (double)t64[10] / m, (unsigned long long)t64[7],
                    (unsigned long long)t64[2], (unsigned long long)t64[3]);
     sst_.table_pairs = st[kSelIns];
   }

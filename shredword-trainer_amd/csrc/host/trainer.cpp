@@ -520,6 +520,7 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
       s->sel_rebuild_ms = q.rebuild_ms;
       s->sel_select_us = q.select_us;
       s->sel_merge_us = q.merge_us;
+      s->sel_table_us = q.table_us;
       s->sel_table_pairs = q.table_pairs;
       s->sel_table_slots = q.table_slots;
       s->sel_table_grows = q.grows;

@@ -72,6 +72,9 @@ struct SelectStats {
   double kernel_ms = 0, rebuild_ms = 0;  // launches of k_word_loop<true>; frontier rebuilds (host wall)
   double select_us = 0, merge_us = 0;    // device time: selecting, merging + table update (s_memrealtime)
   double table_us = 0;                   // of merge_us: the pair table + frontier update
+  double rec_us = 0, append_us = 0, tail_us = 0;  // of table_us: records, appends, compaction + bookkeeping
+  double log_ms = 0;                     // the table-change logs applied between launches (host wall)
+  uint64_t log_entries = 0;
   uint64_t listed = 0, changed = 0, occurrences = 0, new_pairs = 0;
   uint64_t table_slots = 0, table_pairs = 0, frontier_max = 0;
   uint64_t grows = 0;  // pair tables grown 4x (past 3/4 full) between launches

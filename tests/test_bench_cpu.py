@@ -52,7 +52,8 @@ def test_merge_loop_report_accounting():
                          "index_run_ints_written", "index_changed", "index_records", "index_dev_us", "index_undos",
                          "index_launches", "index_occurrences", "index_dev_lookup_us", "index_dev_scan_us",
                          "index_wait_us", "index_switch_merge", "index_switch_ms", "merge_launches",
-                         "merge_kernel_ms", "merge_kernel_bytes", "resident_latency_us")}
+                         "merge_kernel_ms", "merge_kernel_bytes", "resident_latency_us", "index_raw_records",
+                         "index_finalized", "index_dev_out_us", "index_dev_fin_us", "index_fin_records")}
     st.update({f"host_{k}_seconds": 0.0 for k in ("select", "launch", "wait", "apply")})
     st.update(resident_merges=1000, resident_kernel_ms=80.0, resident_bytes=32e9, resident_launches=1,
               index_merges=30000, index_ms=500.0, index_candidates=30000 * 300, index_scanned=30000 * 100,
