@@ -1047,6 +1047,7 @@ struct ResParams {
   uint32_t w_global;         // 1: the weights stay in HBM (w_words = 0), read per matched occurrence
   uint32_t region_keys;      // a participant with more LDS delta keys adds them to the global tables
   uint32_t mt_dense;         // more matched tiles than this: the host index marks X in every tile
+  uint32_t mt_words;         // the matched tiles go to the host as a bitmap of this many u32 words
   ResSlot sl[Device::kResSlots];  // merge X uses sl[X % kResSlots]
   uint32_t* dbg;      // diagnostic (SHREDWORD_RESIDENT_DEBUG): per workgroup [phase, last seq, pi, T]
   u64* stamps;        // diagnostic: per participant [go seen, work done, loop cycles, -] (s_memrealtime)
@@ -1545,8 +1546,6 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
           uint32_t* dc = p.cmd + ((uint32_t)X % kResRing) * 8;
           __hip_atomic_store(reinterpret_cast<u64*>(dc + 6), (u64)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
-          if (p.stamps)  // diagnostic: the host times post -> dispatch (write-through)
-            __hip_atomic_store(p.status + 1, expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1843,10 +1842,32 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
       __syncthreads();
       n = s_nout;
       if (nm > p.mt_dense) nm = kAllTiles;  // X is in most tiles: the host marks it everywhere
-      for (uint32_t i = threadIdx.x; nm != kAllTiles && i < nm; i += kRT) {
-        const uint32_t o = owner(s_pmt, i);
-        sys_store(sl.hmlist + i,
-                  __hip_atomic_load(sl.rtile + (size_t)o * kResMaxTiles + (i - s_pmt[o]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (nm != kAllTiles) {
+        // the matched tiles as a bitmap over every tile, built in this workgroup's LDS (the
+        // gatherer owns no tiles: its dynamic area is free), so the host takes X's tile set as
+        // is instead of sorting a list of up to ntiles / 2 entries
+        uint32_t* s_bits = reinterpret_cast<uint32_t*>(s_dyn);
+        for (uint32_t i = threadIdx.x; i < p.mt_words; i += kRT) s_bits[i] = 0;
+        __syncthreads();
+        constexpr int kMB = 8;  // tile ids in flight per thread
+        for (uint32_t i0 = 0; i0 < nm; i0 += kRT * kMB) {
+          uint32_t t[kMB];
+#pragma unroll
+          for (int k = 0; k < kMB; ++k) {
+            const uint32_t i = i0 + k * kRT + threadIdx.x;
+            t[k] = kAllTiles;
+            if (i < nm) {
+              const uint32_t o = owner(s_pmt, i);
+              t[k] = __hip_atomic_load(sl.rtile + (size_t)o * kResMaxTiles + (i - s_pmt[o]), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < kMB; ++k)
+            if (t[k] != kAllTiles) atomicOr(&s_bits[t[k] >> 5], 1u << (t[k] & 31));
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < p.mt_words; i += kRT) sys_store(sl.hmlist + i, s_bits[i]);
       }
       if (s_nrec) {  // spilled deltas in the global tables: all of them follow the records
         __syncthreads();
@@ -1874,6 +1895,7 @@ __global__ __launch_bounds__(kLdsTok ? 256 : kResThreadsHbm) void k_resident(Res
       if (p.stamps) {  // diagnostic: the gatherer's phases, relative to the leader's dispatch
         for (int k = 0; k < 4; ++k) sys_store(&sl.hstats[3 + k], s_ts[k] - t_leader);
         sys_store(&sl.hstats[7], (u64)s_pre[T]);  // records before the combine
+        sys_store(&sl.hstats[8], t_leader);        // raw dispatch tick (the host's per-merge log)
       }
       sys_store(&sl.hcount[0], n);
       sys_store(&sl.hcount[2], nm);
@@ -4002,6 +4024,8 @@ void Device::plan_resident(const TiledStream& ts) {
     nr_max = w_global ? 0u : (nr_max + 1u) & ~1u;
     if (!lds_tok) tok_words = 0;
     shm = (size_t)tok_words * 4 + (size_t)nr_max * 8 + (size_t)nt_max * sw * 4;
+    shm = std::max(shm, 4 * ((T + 31) / 32));  // the gatherer's matched-tile bitmap
+    shm = (shm + 15) & ~(size_t)15;
     fit = (long)shm <= bud;
   }
   if (!fit) return;
@@ -4110,6 +4134,7 @@ void Device::start_resident() {
   rp.slot_cap = min_slot_cap();
   rp.region_keys = res_region_keys_;
   rp.mt_dense = (uint32_t)(ntiles_ / 2);
+  rp.mt_words = (uint32_t)((ntiles_ + 31) / 32);
   for (int k = 0; k < kResSlots; ++k) {
     MergeSlot& sl = slot_[k];
     ResSlot& r = rp.sl[k];
@@ -4235,6 +4260,7 @@ bool Device::wait_resident(const MergeSlot& sl, int32_t X) {
 
 size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   if (res_posted_.empty() || res_posted_.front().X != X) fatal("collect: merge X is not the oldest posted merge");
+  const double tw = now_seconds();
   if (!wait_resident(slot_[res_posted_.front().slot], X)) {  // not co-resident: nothing ran
     resident_abort_fallback();
     return collect(X, recs);
@@ -4242,15 +4268,10 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   const ResPost rp = res_posted_.front();
   res_posted_.erase(res_posted_.begin());
   MergeSlot& sl = slot_[rp.slot];
-  const double tw = now_seconds();
-  if (res_stamps_) {  // diagnostic: when the leader's dispatch of this merge becomes visible here
-    while ((int32_t)(__atomic_load_n(&res_status_[1], __ATOMIC_ACQUIRE) - rp.seq) < 0) __builtin_ia32_pause();
-    res_phase_[2] += 1e6 * (now_seconds() - rp.t_post);
-  }
-  wait_resident(sl, rp.X);
   {  // host clock: post -> flag seen, and the part of it spent waiting here
     const double t1 = now_seconds();
     res_post_flag_us_ += 1e6 * (t1 - rp.t_post);
+    res_post_flag_last_ = 1e6 * (t1 - rp.t_post);
     res_host_wait_ += 1e6 * (t1 - tw);
     res_parts_sum_ += rp.nparts;
   }
@@ -4258,9 +4279,13 @@ size_t Device::collect_resident(int32_t X, const DeltaRecord** recs) {
   const size_t n = sl.host_count[0];
   const uint32_t nm = sl.host_count[2];
   if (nm == kAllTiles) index_.set_all(X);
-  else index_.set_tiles(X, sl.host_mlist, nm);
+  else index_.set_tiles_bits(X, sl.host_mlist, nm);  // the gatherer's bitmap (k_resident)
   res_lat_us_ += 1e-2 * (double)hs[2];  // s_memrealtime: 100 MHz
   res_lat_n_ += 1;
+  if (res_stamps_ && merge_log_)  // diagnostic: host post / flag-seen clock beside the device's dispatch / flag
+    std::fprintf(merge_log_, "S %d %u %.2f %.2f %.2f %llu %llu %zu %u\n", X, rp.nparts, 1e6 * rp.t_post, 1e6 * tw,
+                 1e6 * (rp.t_post + 1e-6 * res_post_flag_last_), (unsigned long long)hs[8],
+                 (unsigned long long)(hs[8] + hs[2]), (size_t)sl.host_count[0], nm);
   if (res_stamps_) {
     for (int k = 0; k < 4; ++k) res_ph_[k] += 1e-2 * (double)hs[3 + k];
     res_phase_[4] += (double)hs[7];
@@ -4344,9 +4369,8 @@ void Device::park() {
                  (unsigned long long)res_merges_, ms, res_post_flag_us_ / n, res_host_wait_ / n, res_parts_sum_ / n);
     if (res_phase_n_)
       std::fprintf(stderr,
-                   " | host: post -> dispatch seen %.2f | device after dispatch: all published %.2f prefix %.2f loaded %.2f "
-                   "combined %.2f flag %.2f",
-                   res_phase_[2] / res_phase_n_, res_ph_[0] / res_phase_n_, res_ph_[1] / res_phase_n_,
+                   " | device after dispatch: all published %.2f prefix %.2f loaded %.2f combined %.2f flag %.2f",
+                   res_ph_[0] / res_phase_n_, res_ph_[1] / res_phase_n_,
                    res_ph_[2] / res_phase_n_, res_ph_[3] / res_phase_n_, res_phase_[3] / res_phase_n_);
     if (res_phase_n_) std::fprintf(stderr, " | records before combine %.1f", res_phase_[4] / res_phase_n_);
     std::fprintf(stderr, "\n");

@@ -70,7 +70,6 @@ constexpr size_t kPadBytes = (size_t)kChunkBytes * kXWideThreads + 256;  // ' ' 
 // HBM table probes before the table counts as too full (it is grown 4x and the count rerun); with
 // the 3/4 fill flag the usual probe run is a few slots
 constexpr u64 kTableProbes = 512;
-constexpr bool kLoadWideDefault = true;  // the wide shape (C3: PMC 87.8 -> 77.9 GB); SHREDWORD_LOAD_WIDE=0/1/2 overrides
 constexpr int kLoadShapeDefault = 2;  // xwide: C3 load 1.09-1.12 s -> 0.92-0.95 s (round 5 A/B on one box)
 
 __device__ __forceinline__ bool delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }

@@ -128,7 +128,7 @@ constexpr int kSelM = 0, kSelNF = 1, kSelBuf = 2, kSelStatus = 3, kSelIns = 4, k
 constexpr int kSelWords = kSelStats + 2 * 12 + 2;  // st: 6 words, then 12 u64 statistics, then the log's length (u64)
 constexpr int kSelLogW = kSelStats + 2 * 12;
 // exit status: merges done (target reached / below min_pair_freq), frontier to rebuild, table full
-constexpr uint32_t kSelDone = 1, kSelRebuild = 2, kSelFull = 3;
+constexpr uint32_t kSelDone = 1, kSelRebuild = 2;
 // The frontier lives in LDS for the whole launch: each entry's count follows the table's (the
 // merge's records add to both; inf[slot] = LDS position + 1), so a select is an LDS scan.  A
 // rebuild picks kSelK entries; merges append, and past kSelF - kSelSlack entries the dead ones

@@ -433,6 +433,7 @@ class Device : public Backend {
   double res_ph_[4] = {};  // diagnostic: the gatherer's phases
   uint64_t res_phase_n_ = 0;
   bool res_stamp_detail_ = false;
+  double res_post_flag_last_ = 0;      // the last collected merge's post -> flag seen (µs)
   double res_host_wait_ = 0, res_parts_sum_ = 0, res_post_flag_us_ = 0;
   uint32_t* res_status_ = nullptr;     // pinned host status
   void* res_status_dev_ = nullptr;

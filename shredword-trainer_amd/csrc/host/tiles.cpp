@@ -197,6 +197,25 @@ void TileIndex::set_tiles(int32_t id, const uint32_t* tiles, size_t n) {
   make(&ids_[id], std::move(v));
 }
 
+void TileIndex::set_tiles_bits(int32_t id, const uint32_t* words, size_t n) {
+  if (id < 0) return;
+  if ((size_t)id >= ids_.size()) ids_.resize(id + 1);
+  Set& s = ids_[id];
+  s.size = n;
+  s.list.clear();
+  s.bits.clear();
+  const size_t nw = (ntiles_ + 31) / 32;
+  if ((uint64_t)n * 32 > ntiles_) {  // dense: the bitmap as is (two u32 words per u64, low first)
+    s.bits.assign((ntiles_ + 63) / 64, 0);
+    for (size_t w = 0; w < nw; ++w) s.bits[w >> 1] |= (uint64_t)words[w] << (32 * (w & 1));
+  } else {
+    s.list.reserve(n);
+    for (size_t w = 0; w < nw; ++w)
+      for (uint32_t m = words[w]; m; m &= m - 1) s.list.push_back((uint32_t)(w * 32 + __builtin_ctz(m)));
+    s.size = s.list.size();
+  }
+}
+
 void TileIndex::set_all(int32_t id) {
   if (id < 0) return;
   if ((size_t)id >= ids_.size()) ids_.resize(id + 1);

@@ -59,6 +59,8 @@ class TileIndex {
   // ascending workgroup ids in *out.  Computed on tile bitmaps without listing the tiles.
   void owners(int32_t a, int32_t b, const std::vector<uint32_t>& first, std::vector<uint32_t>* out) const;
   void set_tiles(int32_t id, const uint32_t* tiles, size_t n);
+  // The same from a bitmap over the tiles ((ntiles + 31) / 32 words, bit t = tile t) of n bits.
+  void set_tiles_bits(int32_t id, const uint32_t* words, size_t n);
   void set_all(int32_t id);  // id may be in any tile
   size_t num_tiles() const { return ntiles_; }
 

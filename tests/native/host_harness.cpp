@@ -243,7 +243,16 @@ class EmuBackend : public Backend {
       pd.recs.resize(nb / sizeof(DeltaRecord));
       if (nb) std::memcpy(pd.recs.data(), all, nb);
     }
-    index_.set_tiles(X, pd.matched.data(), pd.matched.size());
+    if (X & 1) {  // odd merges take k_resident's bitmap form of the same tile set
+      std::vector<uint32_t> words((index_.num_tiles() + 31) / 32, 0);
+      std::vector<uint32_t> m(pd.matched);
+      std::sort(m.begin(), m.end());
+      m.erase(std::unique(m.begin(), m.end()), m.end());
+      for (uint32_t t : m) words[t >> 5] |= 1u << (t & 31);
+      index_.set_tiles_bits(X, words.data(), m.size());
+    } else {
+      index_.set_tiles(X, pd.matched.data(), pd.matched.size());
+    }
     if (rec_) {
       const int32_t hdr[4] = {pd.a, pd.b, X, (int32_t)pd.recs.size()};
       std::fwrite(hdr, 4, 4, rec_);
