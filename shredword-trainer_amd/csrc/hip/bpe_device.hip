@@ -2949,6 +2949,9 @@ Device::~Device() {
 }
 
 void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint64_t>& weights, int32_t max_id) {
+  const bool report = std::getenv("SHREDWORD_LOAD_REPORT") != nullptr;
+  double tph[8];
+  tph[0] = now_seconds();
   HIP_OK(hipSetDevice(ordinal_));
   park();
   HIP_OK(hipStreamSynchronize(S(stream_)));
@@ -2980,6 +2983,7 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
                             S(stream_)));
   }
   HIP_OK(hipStreamSynchronize(S(stream_)));
+  tph[1] = now_seconds();
   for (MergeSlot& s : slot_) {
     if (s.host_mlist) HIP_OK(hipHostFree(s.host_mlist));
     // one entry per (tile, chain merge) that matched
@@ -3004,7 +3008,9 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
   unmerge_pending_ = false;
   // per-tile pair signatures (built by reset_tokens)
   sig_ = dalloc<uint32_t>(std::max<size_t>(ntiles_, 1) * kSigWords, &bytes_alloc_);
+  tph[2] = now_seconds();
   index_.build(ts);
+  tph[3] = now_seconds();
   max_id_seen_ = max_id;
   max_id0_ = max_id;
   uploaded_ = true;
@@ -3022,8 +3028,16 @@ void Device::upload(const TiledStream& ts, Layout layout, const std::vector<uint
       wl_ = nullptr;
     }
   }
+  tph[4] = now_seconds();
   reset_tokens();
+  tph[5] = now_seconds();
   plan_resident(ts);
+  tph[6] = now_seconds();
+  if (report)
+    std::fprintf(stderr, "[LOAD] device upload: tables + copies %.1f ms, host-visible slots %.1f ms, tile index %.1f ms, "
+                 "word runs + index %.1f ms, reset %.1f ms, resident plan %.1f ms\n", 1e3 * (tph[1] - tph[0]),
+                 1e3 * (tph[2] - tph[1]), 1e3 * (tph[3] - tph[2]), 1e3 * (tph[4] - tph[3]), 1e3 * (tph[5] - tph[4]),
+                 1e3 * (tph[6] - tph[5]));
 }
 
 void Device::set_index(bool on) {

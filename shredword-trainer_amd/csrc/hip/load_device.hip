@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -331,6 +332,21 @@ struct DevBuf {
 };
 
 }  // namespace
+
+// The pinned host ring of the streamed load, kept for the process (a later load of the same
+// shape reuses it: pinning 4 x 64 MiB costs 50-90 ms on the box, unpinning as much again).  The
+// first load allocates it on a helper thread while the device buffer is being set up; the readers
+// wait per buffer (ready[k]: 0 pending, 1 ready, 2 failed).
+struct PinRing {
+  std::mutex mu;  // one streamed load at a time owns the ring
+  std::vector<void*> buf;
+  size_t chunk = 0;
+  std::unique_ptr<std::atomic<int>[]> ready;
+};
+static PinRing& pin_ring() {
+  static PinRing* r = new PinRing();  // never destroyed: the runtime may already be down at exit
+  return *r;
+}
 
 static double wall() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -639,6 +655,42 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
     if (why) *why = "corpus larger than 2^52 bytes";
     return false;
   }
+  size_t chunk = (size_t)64 << 20;
+  if (const char* e = std::getenv("SHREDWORD_LOAD_CHUNK_MB")) chunk = std::max<size_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+  const size_t nchunks = (n + chunk - 1) / chunk;
+  int NB = 4;  // chunks in flight: read, queued for DMA, in DMA
+  if (const char* e = std::getenv("SHREDWORD_LOAD_BUFS")) NB = std::max(2, std::min(16, std::atoi(e)));
+  NB = (int)std::min<size_t>((size_t)NB, nchunks);
+  // the pinned ring: reused, or (re)allocated on a helper thread meanwhile
+  PinRing& ring = pin_ring();
+  std::unique_lock<std::mutex> ring_lock(ring.mu);
+  std::thread pin_thread;
+  if (ring.chunk != chunk || ring.buf.size() < (size_t)NB) {
+    for (void* q : ring.buf)
+      if (q) (void)hipHostFree(q);
+    ring.buf.assign((size_t)NB, nullptr);
+    ring.chunk = chunk;
+    ring.ready.reset(new std::atomic<int>[(size_t)NB]);
+    for (int k = 0; k < NB; ++k) ring.ready[k].store(0);
+    pin_thread = std::thread([&ring, device, NB, chunk] {
+      bool ok = hipSetDevice(device) == hipSuccess;
+      for (int k = 0; k < NB; ++k) {
+        ok = ok && hipHostMalloc(&ring.buf[(size_t)k], chunk, hipHostMallocDefault) == hipSuccess;
+        if (!ok) ring.buf[(size_t)k] = nullptr;
+        ring.ready[k].store(ok ? 1 : 2, std::memory_order_release);
+      }
+    });
+  }
+  struct JoinGuard {
+    std::thread& t;
+    PinRing& r;
+    ~JoinGuard() {
+      if (!t.joinable()) return;
+      t.join();
+      for (size_t k = 0; k < r.buf.size(); ++k)  // a failed allocation: the next load starts over
+        if (r.ready[k].load() != 1) r.chunk = 0;
+    }
+  } pin_join{pin_thread, ring};
   StreamGuard sg;
   int cus = 256;
   if (!device_setup(device, &sg.s, &cus, why)) return false;
@@ -648,6 +700,7 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   uint8_t* db = static_cast<uint8_t*>(dd.p);
   LOAD_OK(hipMemsetAsync(db + n, ' ', kPadBytes, st));
   LOAD_OK(hipStreamSynchronize(st));
+  const double t_buf = wall();
   // The file straight into HBM (round 5): a ring of NB pinned buffers of `chunk` bytes; T reader
   // threads fill each chunk together (a slice each, pread) and one copy thread sends the full
   // chunks, in order, over ONE stream.  Measured on the box (tools/h2d_probe.py): 32 MiB copies
@@ -657,14 +710,8 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   // the count runs on segments (whole tiles) as they land -- segment k once every chunk up to the
   // end of segment k + 1 is in HBM (a word may run into the next segment; one running further is
   // flagged and the whole count is repeated after the upload).
-  size_t chunk = (size_t)64 << 20;
-  if (const char* e = std::getenv("SHREDWORD_LOAD_CHUNK_MB")) chunk = std::max<size_t>(1, std::strtoull(e, nullptr, 10)) << 20;
-  const size_t nchunks = (n + chunk - 1) / chunk;
   int T = 8;
   if (const char* e = std::getenv("SHREDWORD_LOAD_READERS")) T = std::max(1, std::min(64, std::atoi(e)));
-  int NB = 4;  // chunks in flight: read, queued for DMA, in DMA
-  if (const char* e = std::getenv("SHREDWORD_LOAD_BUFS")) NB = std::max(2, std::min(16, std::atoi(e)));
-  NB = (int)std::min<size_t>((size_t)NB, nchunks);
   // readers on the GPU's NUMA node (SHREDWORD_LOAD_NUMA=0: wherever the scheduler puts them)
   std::vector<int> local;
   {
@@ -695,17 +742,10 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
         if (e) (void)hipEventDestroy(e);
     }
   } eg{ev};
-  struct PinGuard {
-    std::vector<void*> v;
-    ~PinGuard() {
-      for (void* q : v)
-        if (q) (void)hipHostFree(q);
-    }
-  } pg;
-  pg.v.assign((size_t)NB, nullptr);
-  for (int k = 0; k < NB; ++k) LOAD_OK(hipHostMalloc(&pg.v[k], chunk, hipHostMallocDefault));
+  std::vector<void*>& pin = ring.buf;
   StreamGuard cs;
   LOAD_OK(hipStreamCreateWithFlags(&cs.s, hipStreamNonBlocking));
+  const double t_pin = wall();
   // recorded[c]: 1 once chunk c's copy is queued behind ev[c] (2: failed); filled[c]: readers done
   std::unique_ptr<std::atomic<int>[]> recorded(new std::atomic<int>[nchunks]);
   std::unique_ptr<std::atomic<int>[]> filled(new std::atomic<int>[nchunks]);
@@ -734,8 +774,12 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
             int r;
             while ((r = recorded[c - NB].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
             ok = r == 1 && hipEventSynchronize(ev[c - NB]) == hipSuccess;
+          } else {  // the buffer's first use: pinned yet?
+            int r;
+            while ((r = ring.ready[c].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+            ok = r == 1;
           }
-          uint8_t* dst = static_cast<uint8_t*>(pg.v[c % (size_t)NB]);
+          uint8_t* dst = static_cast<uint8_t*>(pin[c % (size_t)NB]);
           const double tr = wall();
           size_t got = s0;
           while (ok && got < s1) {
@@ -756,7 +800,7 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
       while (filled[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
       ok = ok && !failed.load(std::memory_order_relaxed);
       const size_t off = c * chunk, len = std::min(chunk, n - off);
-      ok = ok && hipMemcpyAsync(db + off, pg.v[c % (size_t)NB], len, hipMemcpyHostToDevice, cs.s) == hipSuccess &&
+      ok = ok && hipMemcpyAsync(db + off, pin[c % (size_t)NB], len, hipMemcpyHostToDevice, cs.s) == hipSuccess &&
            hipEventRecord(ev[c], cs.s) == hipSuccess;
       if (!ok) failed.store(1);
       recorded[c].store(ok ? 1 : 2, std::memory_order_release);
@@ -798,6 +842,10 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   }
   const double t1 = wall();
   if (report)
+    std::fprintf(stderr, "[LOAD] file_to_hbm setup: device + text buffer %.1f ms (the pinned ring meanwhile), events + copy stream "
+                 "%.1f ms\n",
+                 1e3 * (t_buf - t0), 1e3 * (t_pin - t_buf));
+  if (report)
     std::fprintf(stderr, "[LOAD] phase file_to_hbm %.1f ms (%d readers, %d pinned %zu MiB chunks, one copy stream, readers "
                  "on %zu GPU-local CPUs, pread %.1f ms summed over readers): %.1f GB/s%s\n", 1e3 * (t1 - t0), T, NB,
                  chunk >> 20, local.size(), 1e-6 * (double)read_ns.load(), (double)n / (t1 - t0) / 1e9,
@@ -806,6 +854,7 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
     return false;
   if (base)
     for (WordRec& w : *out) w.first += base;  // file offsets
+  if (report) std::fprintf(stderr, "[LOAD] file count done at %.1f ms (teardown follows)\n", 1e3 * (wall() - t0));
   return true;
 }
 

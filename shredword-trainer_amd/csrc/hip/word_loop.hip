@@ -24,6 +24,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <thread>
 #include <vector>
 
 #include "../host/common.h"
@@ -1652,43 +1654,91 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
   if (running_) stop();
   free_all();
   // the words of the tile stream in rank order (types layout: one entry per distinct word), each
-  // as a 16-B aligned run [length][tokens]
-  std::vector<uint32_t> woff, tfirst, tnw;
-  std::vector<int32_t> wtok;
-  woff.reserve(ts.entries + 1);
-  wtok.reserve(ts.live + 4 * ts.entries + 8);
-  tfirst.reserve(ts.num_tiles());
-  tnw.reserve(ts.num_tiles());
-  uint32_t expect_rank = 0;
-  uint64_t ntok = 0;
-  for (size_t t = 0; t < ts.num_tiles(); ++t) {
-    const int32_t* p = ts.tok.data() + ts.off[t];
-    tfirst.push_back((uint32_t)woff.size());
-    uint32_t nw = 0;
-    for (uint32_t i = 0; i < ts.len[t]; ++i) {
-      if (p[i] < kHeaderLimit) {
-        const uint32_t r = (uint32_t)(p[i] - kHeaderBase);
-        if (r != expect_rank) return false;  // not the whole table in rank order: not for this loop
-        ++expect_rank;
-        while (wtok.size() & 3) wtok.push_back(0);
-        if (wtok.size() >= 0xFFFFFF00ull) return false;  // offsets are 32-bit
-        woff.push_back((uint32_t)wtok.size());
-        wtok.push_back(0);  // the live length
-        ++nw;
-      } else {
-        if (woff.empty()) return false;
-        wtok.push_back(p[i]);
-        ++wtok[woff.back()];
-        ++ntok;
+  // as a 16-B aligned run [length][tokens] of round_up(1 + length, 4) ints.  Threads over tile
+  // ranges: a sizing pass (words and ints per tile, every header's rank checked against its
+  // position), a prefix over the tiles, then each range fills its part of the runs.
+  const size_t T = ts.num_tiles();
+  const int P = (int)std::max<size_t>(1, std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()),
+                                                          T / 64 + 1}));
+  auto par = [&](const std::function<void(int)>& f) {
+    if (P == 1) return f(0);
+    std::vector<std::thread> pool;
+    for (int k = 0; k < P; ++k) pool.emplace_back(f, k);
+    for (auto& th : pool) th.join();
+  };
+  auto range = [&](int k, size_t* t0, size_t* t1) {
+    *t0 = T * (size_t)k / (size_t)P;
+    *t1 = T * (size_t)(k + 1) / (size_t)P;
+  };
+  std::vector<uint32_t> tnw(T, 0), tfirst(T, 0);
+  std::vector<uint64_t> tints(T + 1, 0), ttok(T, 0);
+  std::vector<int32_t> tr0(T, -1);  // the rank of the tile's first word (-1: none)
+  std::vector<char> bad((size_t)P, 0);
+  par([&](int k) {
+    size_t t0, t1;
+    range(k, &t0, &t1);
+    for (size_t t = t0; t < t1 && !bad[(size_t)k]; ++t) {
+      const int32_t* p = ts.tok.data() + ts.off[t];
+      uint32_t nw = 0, wl = 0;
+      uint64_t ints = 0, ntk = 0;
+      for (uint32_t i = 0; i < ts.len[t]; ++i) {
+        if (p[i] < kHeaderLimit) {
+          const int32_t r = (int32_t)(uint32_t)(p[i] - kHeaderBase);
+          if (nw == 0) tr0[t] = r;
+          else if (r != tr0[t] + (int32_t)nw) bad[(size_t)k] = 1;  // ranks not consecutive
+          if (nw) ints += (1u + wl + 3u) & ~3u;
+          ++nw;
+          wl = 0;
+        } else {
+          if (nw == 0) bad[(size_t)k] = 1;  // tokens before any header
+          ++wl;
+          ++ntk;
+        }
+      }
+      if (nw) ints += (1u + wl + 3u) & ~3u;
+      tnw[t] = nw;
+      tints[t] = ints;
+      ttok[t] = ntk;
+    }
+  });
+  for (char b : bad)
+    if (b) return false;  // not the whole table in rank order: not for this loop
+  uint64_t words = 0, ints = 0, ntok = 0;
+  for (size_t t = 0; t < T; ++t) {
+    if (tnw[t] && tr0[t] != (int32_t)words) return false;
+    tfirst[t] = (uint32_t)words;
+    const uint64_t n = tints[t];
+    tints[t] = ints;
+    words += tnw[t];
+    ints += n;
+    ntok += ttok[t];
+  }
+  tints[T] = ints;
+  if (ints >= 0xFFFFFF00ull) return false;  // offsets are 32-bit
+  std::vector<uint32_t> woff(words + 1);
+  std::vector<int32_t> wtok(ints + kRunPad, 0);
+  par([&](int k) {
+    size_t t0, t1;
+    range(k, &t0, &t1);
+    for (size_t t = t0; t < t1; ++t) {
+      const int32_t* p = ts.tok.data() + ts.off[t];
+      uint64_t o = tints[t], w = tfirst[t];
+      int32_t* len = nullptr;
+      for (uint32_t i = 0; i < ts.len[t]; ++i) {
+        if (p[i] < kHeaderLimit) {
+          if (len) o = (o + 3u) & ~3ull;
+          woff[w++] = (uint32_t)o;
+          len = &wtok[o++];
+        } else {
+          wtok[o++] = p[i];
+          ++*len;
+        }
       }
     }
-    tnw.push_back(nw);
-  }
-  while (wtok.size() & 3) wtok.push_back(0);
-  if (wtok.size() >= 0xFFFFFF00ull) return false;
-  woff.push_back((uint32_t)wtok.size());
+  });
+  woff[words] = (uint32_t)ints;
   nwords_ = (uint32_t)(woff.size() - 1);
-  nint_ = wtok.size();
+  nint_ = ints;
   ntok_ = ntok;
   ntiles_ = (uint32_t)ts.num_tiles();
   if (nwords_ == 0 || nint_ >= (1ull << 31)) return false;  // hipcub sizes are int
@@ -1696,7 +1746,6 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
   if (3 * ntok_ + 4096 >= (1ull << 32)) return false;
   for (uint32_t w = 0; w < nwords_; ++w)
     if (wtok[woff[w]] == 0) return false;  // words are never empty (strtok)
-  wtok.resize(nint_ + kRunPad, 0);
   weight_ = reinterpret_cast<const unsigned long long*>(d_weight);
   woff_h_ = woff;
   wtok_ = wl_alloc<int32_t>(nint_ + kRunPad, &bytes_);

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <iterator>
 #include <thread>
 
@@ -147,43 +148,90 @@ void TileIndex::make(Set* s, std::vector<uint32_t>&& sorted) const {
 
 void TileIndex::build(const TiledStream& ts) {
   ntiles_ = (uint32_t)ts.num_tiles();
-  std::vector<std::vector<uint32_t>> tl(256);
-  std::vector<uint32_t> seen(256, UINT32_MAX);
-  for (uint32_t t = 0; t < ntiles_; ++t) {
-    const int32_t* p = ts.tok.data() + ts.off[t];
-    for (uint32_t i = 0; i < ts.len[t]; ++i) {
-      const int32_t id = p[i];
-      if (id < 0) continue;  // headers, negative unk
-      if ((size_t)id >= seen.size()) {
-        seen.resize(id + 1, UINT32_MAX);
-        tl.resize(id + 1);
-      }
-      if (seen[id] != t) {
-        seen[id] = t;
-        tl[id].push_back(t);
+  // Threads over contiguous tile ranges; each lists (key, tile) once per tile where the key occurs,
+  // in tile order, and a counting pass per key concatenates the ranges in order, so every key's
+  // tile list comes out sorted without a sort (C5 at 100 GB: 70 M tokens in 68,905 tiles).
+  //   ids: key = the token id (>= 0); pairs: key = x * 256 + y for adjacent ids x, y < 256
+  const size_t T = ntiles_;
+  const int P = (int)std::max<size_t>(1, std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()),
+                                                          T / 64 + 1}));
+  auto par = [&](const std::function<void(int)>& f) {
+    if (P == 1) return f(0);
+    std::vector<std::thread> pool;
+    for (int k = 0; k < P; ++k) pool.emplace_back(f, k);
+    for (auto& th : pool) th.join();
+  };
+  struct Part {
+    std::vector<uint64_t> ids, pairs;  // key << 32 | tile, in tile order
+    std::vector<uint32_t> nid, npair;  // entries per key
+  };
+  std::vector<Part> part((size_t)P);
+  par([&](int k) {
+    Part& pt = part[(size_t)k];
+    const size_t t0 = T * (size_t)k / (size_t)P, t1 = T * (size_t)(k + 1) / (size_t)P;
+    std::vector<uint32_t> seen(256, UINT32_MAX), last(256 * 256, UINT32_MAX);
+    pt.nid.assign(256, 0);
+    pt.npair.assign(256 * 256, 0);
+    for (size_t t = t0; t < t1; ++t) {
+      const int32_t* p = ts.tok.data() + ts.off[t];
+      const uint32_t len = ts.len[t];
+      for (uint32_t i = 0; i < len; ++i) {
+        const int32_t id = p[i];
+        if (id < 0) continue;  // headers, negative unk
+        if ((size_t)id >= seen.size()) {
+          seen.resize((size_t)id + 1, UINT32_MAX);
+          pt.nid.resize((size_t)id + 1, 0);
+        }
+        if (seen[id] != (uint32_t)t) {
+          seen[id] = (uint32_t)t;
+          pt.ids.push_back((uint64_t)id << 32 | t);
+          ++pt.nid[id];
+        }
+        if (i + 1 < len) {
+          const uint32_t x = (uint32_t)id, y = (uint32_t)p[i + 1];
+          if (x >= 256 || y >= 256) continue;  // headers, unk outside the byte range, merged ids
+          const uint32_t key = x * 256 + y;
+          if (last[key] != (uint32_t)t) {
+            last[key] = (uint32_t)t;
+            pt.pairs.push_back((uint64_t)key << 32 | t);
+            ++pt.npair[key];
+          }
+        }
       }
     }
-  }
-  ids_.assign(tl.size(), Set());
-  for (size_t id = 0; id < tl.size(); ++id) make(&ids_[id], std::move(tl[id]));
+  });
+  size_t nids = 256;
+  for (const Part& pt : part) nids = std::max(nids, pt.nid.size());
+  // per key: the ranges' entries back to back, range by range (so in tile order); then one Set each
+  auto gather = [&](size_t nkeys, std::vector<uint64_t> Part::*ent, std::vector<uint32_t> Part::*num,
+                    std::vector<Set>* out) {
+    std::vector<uint64_t> at((size_t)P * nkeys);  // [part][key]: where the part's entries of key go
+    std::vector<uint64_t> off(nkeys + 1, 0);
+    uint64_t run = 0;
+    for (size_t key = 0; key < nkeys; ++key) {
+      off[key] = run;
+      for (int k = 0; k < P; ++k) {
+        const std::vector<uint32_t>& n = part[(size_t)k].*num;
+        at[(size_t)k * nkeys + key] = run;
+        run += key < n.size() ? n[key] : 0;
+      }
+    }
+    off[nkeys] = run;
+    std::vector<uint32_t> flat(run);
+    par([&](int k) {
+      uint64_t* a = at.data() + (size_t)k * nkeys;
+      for (uint64_t e : part[(size_t)k].*ent) flat[a[(size_t)(e >> 32)]++] = (uint32_t)e;
+    });
+    out->assign(nkeys, Set());
+    par([&](int k) {
+      for (size_t key = nkeys * (size_t)k / (size_t)P; key < nkeys * (size_t)(k + 1) / (size_t)P; ++key)
+        if (off[key + 1] > off[key])
+          make(&(*out)[key], std::vector<uint32_t>(flat.begin() + (long)off[key], flat.begin() + (long)off[key + 1]));
+    });
+  };
+  gather(nids, &Part::ids, &Part::nid, &ids_);
   ids0_ = ids_;
-  // exact tiles of every adjacent pair of base ids
-  std::vector<std::vector<uint32_t>> pl(256 * 256);
-  std::vector<uint32_t> last(256 * 256, UINT32_MAX);
-  for (uint32_t t = 0; t < ntiles_; ++t) {
-    const int32_t* p = ts.tok.data() + ts.off[t];
-    for (uint32_t i = 0; i + 1 < ts.len[t]; ++i) {
-      const uint32_t x = (uint32_t)p[i], y = (uint32_t)p[i + 1];
-      if (x >= 256 || y >= 256) continue;  // headers, unk outside the byte range, merged ids
-      const uint32_t k = x * 256 + y;
-      if (last[k] != t) {
-        last[k] = t;
-        pl[k].push_back(t);
-      }
-    }
-  }
-  base_pairs_.assign(256 * 256, Set());
-  for (size_t k = 0; k < pl.size(); ++k) make(&base_pairs_[k], std::move(pl[k]));
+  gather(256 * 256, &Part::pairs, &Part::npair, &base_pairs_);
 }
 
 void TileIndex::reset() { ids_ = ids0_; }

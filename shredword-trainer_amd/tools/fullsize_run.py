@@ -116,6 +116,10 @@ def main():
            "sharded_load_ranges": env_shards}
     t = BPETrainer(vocab_size=cfg["vocab"], unk_id=cfg["unk"], character_coverage=cfg["cov"], min_pair_freq=cfg["mpf"])
     t.set_option("log", 0)
+    from shredword.cbase import lib
+    th = time.time()  # the HIP runtime comes up once per process, outside the load
+    lib.shred_device_count()
+    res["hip_init_s"] = time.time() - th
     t0 = time.time()
     t.load_corpus(path)
     res["load_s"] = time.time() - t0

@@ -27,6 +27,10 @@ def main():
     bench.ensure_corpus(cfg, path)
     t = BPETrainer(vocab_size=cfg["vocab"], min_pair_freq=cfg["mpf"])
     t.set_option("log", 0)
+    from shredword.cbase import lib
+    th = time.time()  # the HIP runtime comes up once per process, outside the load
+    lib.shred_device_count()
+    print(f"{args.config}: HIP runtime init {time.time() - th:.2f} s", flush=True)
     t0 = time.time()
     t.load_corpus(path)
     st = t.stats()
