@@ -71,6 +71,7 @@ constexpr size_t kPadBytes = (size_t)kChunkBytes * kXWideThreads + 256;  // ' ' 
 // HBM table probes before the table counts as too full (it is grown 4x and the count rerun); with
 // the 3/4 fill flag the usual probe run is a few slots
 constexpr u64 kTableProbes = 512;
+constexpr uint32_t kLoadEvictPctDefault = 0;  // LDS eviction off by default (A/B: SHREDWORD_LOAD_EVICT)
 constexpr int kLoadShapeDefault = 2;  // xwide: C3 load 1.09-1.12 s -> 0.92-0.95 s (round 5 A/B on one box)
 
 __device__ __forceinline__ bool delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }
@@ -92,6 +93,8 @@ struct Table {
   uint32_t* nkeys;
   uint32_t* flags;  // [0] table too full, [1] key collision, [2] a NUL byte in the text, [3] a word
                     // past a segment's landed bytes
+  u64* stats;       // [0] words, [1] counted straight in HBM (LDS table full / slot being made),
+                    // [2] words longer than the LDS spelling that hit an LDS slot, [3] LDS slots evicted
 };
 
 // kmask keeps all 64 bits (tests narrow it, SHREDWORD_LOAD_KEY_BITS, to force key collisions).
@@ -109,11 +112,35 @@ __device__ __forceinline__ uint32_t tile_byte(const uint8_t* s, const uint8_t* d
   return p < (uint32_t)kTileBytes ? s[(p / kChunkBytes) * kTileStride + (p % kChunkBytes)] : d[base + p];
 }
 
-// True when the words at d[a] and d[b] (a's length len) spell the same bytes.
+// True when the words at d[a] and d[b] (a's length len) spell the same bytes.  The bytes are
+// loaded 16 at a time, every load of a batch issued before the first compare (one HBM round trip
+// per 16 bytes instead of one per byte); reads past a word stay inside the text's ' ' padding.
 __device__ __forceinline__ bool same_global(const uint8_t* d, u64 a, u64 b, uint32_t len) {
   uint32_t diff = delim(d[b + len]) ? 0u : 1u;
-  for (uint32_t k = 0; k < len; ++k) diff |= d[a + k] ^ d[b + k];
+  for (uint32_t k = 0; k < len; k += 16) {
+    uint32_t x[16], y[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      x[j] = d[a + k + j];
+      y[j] = d[b + k + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) diff |= k + j < len ? x[j] ^ y[j] : 0u;
+  }
   return diff == 0;
+}
+// djb2 (32 bits) of the len bytes at d[a], 16 loads in flight at a time.
+__device__ __forceinline__ uint32_t djb2_global(const uint8_t* d, u64 a, uint32_t len) {
+  uint32_t dj = 5381u;
+  for (uint32_t k = 0; k < len; k += 16) {
+    uint32_t x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = d[a + k + j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (k + j < len) dj = dj * 33u + x[j];
+  }
+  return dj;
 }
 
 // Adds (cnt, first) to key's slot.  Exactness: every add but the slot's very first compares its
@@ -160,7 +187,8 @@ __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 
 // (djb2 & 4095) is computed at the flush, from the slot's first occurrence.
 template <int kLoadThreads, int kLdsSlots>
 __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u64 n, Table t, u64 seed, u64 kmask,
-                                                             u64 tiles_per_wg, u64 tile0, u64 tile1, u64 safe_end) {
+                                                             u64 tiles_per_wg, u64 tile0, u64 tile1, u64 safe_end,
+                                                             uint32_t evict_at) {
   constexpr int kTileBytes = kChunkBytes * kLoadThreads;
   __shared__ u64 s_key[kLdsSlots];
   __shared__ uint32_t s_first[kLdsSlots];
@@ -181,13 +209,42 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
   const u64 t0 = tile0 + (u64)blockIdx.x * tiles_per_wg;
   const u64 t1 = t0 + tiles_per_wg < tile1 ? t0 + tiles_per_wg : tile1;
   const u64 range = t0 * kTileBytes;  // LDS first offsets are relative to it (< 2^32: host-checked)
-  __shared__ uint32_t s_full, s_nul;
-  if (tid == 0) s_nul = 0;
+  __shared__ uint32_t s_full, s_nul, s_used, s_thr;
+  if (tid == 0) {
+    s_nul = 0;
+    s_used = 0;
+    s_thr = 1;
+  }
+  uint32_t n_words = 0, n_hbm = 0, n_long = 0, n_evict = 0;
   for (u64 tile = t0; tile < t1; ++tile) {
     const u64 base = tile * kTileBytes;
     if (tid == 0) s_full = __hip_atomic_load(&t.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();  // the previous tile's scans are done
     if (s_full) return;  // the table is too full: this count is rerun on a bigger one
+    // Eviction (evict_at > 0): once the LDS table holds more than evict_at slots, the words it met
+    // at most s_thr times go to the HBM table (counts, first offsets and links as at the final
+    // flush) and their slots are freed, so words that keep coming get slots instead of the rare
+    // words of the first tiles.  A key may then hold two slots (a probe run broken by a freed
+    // slot): both are flushed, and the HBM table adds them up.
+    if (evict_at && s_used > evict_at) {
+      uint32_t freed = 0;
+      for (int i = tid; i < kLdsSlots; i += kLoadThreads) {
+        if (!s_key[i] || s_cnt[i] > s_thr) continue;
+        const u64 first = range + s_first[i];
+        const uint32_t len = s_len[i];
+        table_add(d, t, s_key[i], djb2_global(d, first, len) & 4095u, len, s_cnt[i], first);
+        s_key[i] = 0;
+        s_first[i] = ~0u;
+        s_cnt[i] = 0;
+        s_len[i] = 0;
+        ++freed;
+      }
+      n_evict += freed;
+      if (freed) atomicSub(&s_used, freed);
+      __syncthreads();
+      if (tid == 0 && s_used > evict_at - evict_at / 4) s_thr = s_thr < (1u << 30) ? 2u * s_thr : s_thr;  // freed too little
+      __syncthreads();
+    }
     const int4* g = reinterpret_cast<const int4*>(d + base);
 #pragma unroll
     for (int j = 0; j < kTileBytes / 16 / kLoadThreads; ++j) {
@@ -237,6 +294,7 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
           k = atomicCAS(&s_key[s], 0ull, key);
           if (k == 0ull) {  // created: spelling and first offset, then the length publishes it
             mine = true;
+            if (evict_at) atomicAdd(&s_used, 1u);
             k = key;
             s_spell[s] = make_uint4(w[0], w[1], w[2], w[3]);
             atomicMin(&s_first[s], rel);
@@ -255,8 +313,16 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
           uint32_t link = s_first[s];
           if (rel < link) link = atomicMin(&s_first[s], rel);
           if (len > (uint32_t)kSpell && link != ~0u && !diff) {
+            ++n_long;
             const u64 rep = range + link;
-            for (uint32_t q = kSpell; q < len; ++q) diff |= tile_byte<kTileBytes>(s_tile, d, base, p + q) ^ d[rep + q];
+            for (uint32_t q = kSpell; q < len; q += 16) {  // the representative's bytes: 16 loads in flight
+              uint32_t r[16];
+#pragma unroll
+              for (int j = 0; j < 16; ++j) r[j] = d[rep + q + j];
+#pragma unroll
+              for (int j = 0; j < 16; ++j)
+                if (q + j < len) diff |= tile_byte<kTileBytes>(s_tile, d, base, p + q + j) ^ r[j];
+            }
           }
           if (diff) atomicOr(&t.flags[1], 1u);
           atomicAdd(&s_cnt[s], 1u);
@@ -265,7 +331,9 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
           s = s + 1 == (uint32_t)kLdsSlots ? 0u : s + 1;
         }
       }
+      ++n_words;
       if (!done) {
+        ++n_hbm;
         uint32_t dj = 5381u;  // djb2 in 32 bits: its & 4095 equals the reference's 64-bit value's
         for (uint32_t q = 0; q < len; ++q) dj = dj * 33u + tile_byte<kTileBytes>(s_tile, d, base, p + q);
         table_add(d, t, key, dj & 4095u, len, 1ull, off);
@@ -275,13 +343,15 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
   }
   __syncthreads();
   if (tid == 0 && s_nul) atomicOr(&t.flags[2], 1u);
+  if (n_words) atomicAdd(&t.stats[0], (u64)n_words);
+  if (n_hbm) atomicAdd(&t.stats[1], (u64)n_hbm);
+  if (n_long) atomicAdd(&t.stats[2], (u64)n_long);
+  if (n_evict) atomicAdd(&t.stats[3], (u64)n_evict);
   for (int i = tid; i < kLdsSlots; i += kLoadThreads) {
     if (!s_key[i]) continue;
     const u64 first = range + s_first[i];
     const uint32_t len = s_len[i];
-    uint32_t dj = 5381u;
-    for (uint32_t q = 0; q < len; ++q) dj = dj * 33u + d[first + q];
-    table_add(d, t, s_key[i], dj & 4095u, len, s_cnt[i], first);
+    table_add(d, t, s_key[i], djb2_global(d, first, len) & 4095u, len, s_cnt[i], first);
   }
 }
 
@@ -383,15 +453,20 @@ static void count_launch(const CountShape& c, const uint8_t* db, size_t n, const
   if (tile1 <= tile0) return;
   if (!per) per = c.per;
   const u64 grid = (tile1 - tile0 + per - 1) / per;
+  // LDS eviction trigger (slots in use); SHREDWORD_LOAD_EVICT=<percent of the slots>, 0 = off
+  uint32_t evict_pct = kLoadEvictPctDefault;
+  if (const char* e = std::getenv("SHREDWORD_LOAD_EVICT")) evict_pct = (uint32_t)std::max(0, std::min(100, std::atoi(e)));
+  const uint32_t slots = c.kind == 0 ? kNarrowSlots : kWideSlots;
+  const uint32_t evict_at = evict_pct ? std::max<uint32_t>(1, slots * evict_pct / 100) : 0u;
   if (c.kind == 2)
     k_word_count<kXWideThreads, kWideSlots><<<(unsigned)grid, kXWideThreads, 0, st>>>(db, n, t, seed, kmask, per, tile0,
-                                                                                      tile1, safe_end);
+                                                                                      tile1, safe_end, evict_at);
   else if (c.wide)
     k_word_count<kWideThreads, kWideSlots><<<(unsigned)grid, kWideThreads, 0, st>>>(db, n, t, seed, kmask, per, tile0,
-                                                                                    tile1, safe_end);
+                                                                                    tile1, safe_end, evict_at);
   else
     k_word_count<kNarrowThreads, kNarrowSlots><<<(unsigned)grid, kNarrowThreads, 0, st>>>(db, n, t, seed, kmask, per,
-                                                                                          tile0, tile1, safe_end);
+                                                                                          tile0, tile1, safe_end, evict_at);
 }
 static u64 count_table_slots(size_t n) {
   // a power of two >= 1 M and >= n / 8192 (grown 4x while it is over 3/4 full): a small table
@@ -437,6 +512,7 @@ static bool count_table_alloc(CountTable* ct, u64 cap, hipStream_t st, std::stri
   ct->t.mask = cap - 1;
   ct->t.nkeys = (uint32_t*)ct->meta.p;
   ct->t.flags = (uint32_t*)ct->meta.p + 4;
+  ct->t.stats = (u64*)ct->meta.p + 4;
   return true;
 }
 
@@ -473,6 +549,13 @@ static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool
       if (nul) *nul = true;
       if (why) *why = "the text holds NUL bytes";
       return false;
+    }
+    if (report) {
+      const u64* ms = reinterpret_cast<const u64*>(meta) + 4;
+      std::fprintf(stderr, "[LOAD] count attempt %d: %llu words, %.2f%% counted straight in HBM, %.2f%% long words "
+                   "compared in HBM, %llu LDS slots evicted\n", attempt, (unsigned long long)ms[0],
+                   100.0 * (double)ms[1] / (double)std::max<u64>(1, ms[0]),
+                   100.0 * (double)ms[2] / (double)std::max<u64>(1, ms[0]), (unsigned long long)ms[3]);
     }
     if (report && (meta[4] || meta[5] || meta[7]))
       std::fprintf(stderr, "[LOAD] count attempt %d over %zu bytes repeated:%s%s%s (%.1f ms)\n", attempt, n,
