@@ -24,9 +24,11 @@ def oracle_runs(case_corpus, oracle_bin, tmp_path_factory):
     def run(name, case, corpus):
         cfg = case["config"]
         model, vocab, trace = (str(out / f"{name}.{n}") for n in ("model", "vocab", "trace"))
+        # the deep cases split their O(S) scans over 4 threads (same output, oracle --threads)
+        threads = ["--threads", "4"] if case["merges"] > 20000 else []
         subprocess.run([oracle_bin, corpus, str(cfg["vocab_size"]), str(cfg["unk_id"]),
                         repr(cfg["character_coverage"]), str(cfg["min_pair_freq"]), model, vocab,
-                        "--trace", trace], check=True, stderr=subprocess.DEVNULL)
+                        "--trace", trace] + threads, check=True, stderr=subprocess.DEVNULL)
         return model, vocab, trace
 
     cases = {n: case_corpus(n) for n in golden_cases()}
