@@ -495,6 +495,27 @@ __device__ __forceinline__ uint32_t unmerge_run(int32_t* t, uint32_t L, int32_t 
   return L + nx;
 }
 
+// Inclusive wave max of a u64 on DPP row shifts and row broadcasts (identity 0; lane 63 holds
+// the wave's max): a few cycles a step instead of an LDS round trip per __shfl.
+template <int kCtrl, int kRowMask = 0xf, bool kBound = true>
+__device__ __forceinline__ u64 wl_dpp64(u64 x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, kCtrl, kRowMask, 0xf, kBound);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), kCtrl, kRowMask, 0xf, kBound);
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 wl_max64(u64 a, u64 b) { return a > b ? a : b; }
+__device__ __forceinline__ u64 wave_max64(u64 x) {
+  x = wl_max64(x, wl_dpp64<0x111>(x));
+  x = wl_max64(x, wl_dpp64<0x112>(x));
+  x = wl_max64(x, wl_dpp64<0x114>(x));
+  x = wl_max64(x, wl_dpp64<0x118>(x));
+  x = wl_max64(x, wl_dpp64<0x142, 0xa, false>(x));
+  x = wl_max64(x, wl_dpp64<0x143, 0xc, false>(x));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+  return ((u64)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -751,6 +772,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     }
     if (tid == 0) {
       s_f.n = nf;
+      S.sm = ld_agent(q.st + kSelM);  // merges so far (kept in LDS from here on)
       S.scompact = 0;
       S.sins = ld_agent(q.st + kSelIns);  // the table's inserts so far (the host's and earlier launches')
       S.serr = 0;
@@ -770,7 +792,6 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       // threshold) is the merge, by a scan of the LDS frontier
       const SelParams& q = p.sel;
       if (tid == 0) {
-        S.sm = ld_agent(q.st + kSelM);
         S.snk = 0;
         S.status = 0;
         S.t_wait = __builtin_amdgcn_s_memrealtime();
@@ -780,27 +801,36 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       const u64 tc = q.thr[0], tk = q.thr[1];
       u64 bc = 0, bk = kEmpty64;
       uint32_t bs = kEmpty32, live = 0;
-      for (uint32_t i = tid; i < nf; i += kWlThreads) {
-        const u64 c = s_f.cnt[i], k = s_f.key[i];
-        if (k != kEmpty64 && sel_at_least(c, k, tc, tk)) {
-          ++live;
-          if (sel_better(c, k, bc, bk)) {
-            bc = c;
-            bk = k;
-            bs = i;
+      {  // this thread's entries tid, tid + 256, ...: every load issued before the first compare
+        constexpr int kPerF = (int)((kSelF + kWlThreads - 1) / kWlThreads);
+        u64 fc[kPerF], fk[kPerF];
+#pragma unroll
+        for (int j = 0; j < kPerF; ++j) {
+          const uint32_t i = (uint32_t)j * kWlThreads + (uint32_t)tid;
+          fc[j] = i < nf ? s_f.cnt[i] : 0ull;
+          fk[j] = i < nf ? s_f.key[i] : kEmpty64;
+        }
+#pragma unroll
+        for (int j = 0; j < kPerF; ++j) {
+          if (fk[j] != kEmpty64 && sel_at_least(fc[j], fk[j], tc, tk)) {
+            ++live;
+            if (sel_better(fc[j], fk[j], bc, bk)) {
+              bc = fc[j];
+              bk = fk[j];
+              bs = (uint32_t)j * kWlThreads + (uint32_t)tid;
+            }
           }
         }
       }
       if (__ballot(live != 0) && lane == 0) atomicAdd(&S.snk, 1u);
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        const u64 c2 = __shfl_xor(bc, d, 64), k2 = __shfl_xor(bk, d, 64);
-        const uint32_t s2 = __shfl_xor(bs, d, 64);
-        if (sel_better(c2, k2, bc, bk)) {
-          bc = c2;
-          bk = k2;
-          bs = s2;
-        }
+      {  // the wave's best (count desc, key asc): the max count, then the least key holding it
+        const u64 wc = wave_max64(bc);
+        const u64 wk = ~wave_max64(bc == wc ? ~bk : 0ull);
+        const u64 who = __ballot(bc == wc && bk == wk);
+        const int src = who ? (int)__builtin_ctzll(who) : 0;
+        bs = (uint32_t)__builtin_amdgcn_readlane((int)bs, src);
+        bc = wc;
+        bk = wk;
       }
       if (lane == 0) {
         S.bc[wid] = bc;
@@ -1226,6 +1256,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       if (tid == 0) {
         q.st[kSelNF] = min(s_f.n, kSelF);
         q.st[kSelM] = S.sm + 1u;
+        ++S.sm;  // the merge count stays in LDS for the launch (this loop is its only writer)
         // statistics (st words 6..): select ticks, merge ticks (u64 each), listed / changed words,
         // occurrences (u64), new pairs
         u64* t64 = reinterpret_cast<u64*>(q.st + kSelStats);
@@ -2282,11 +2313,13 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
   if (n_max == 0) return 0;
   reserve(X0 + (int32_t)n_max);
   hipStream_t s = S(stream_);
-  // the table: room for the initial pairs and ~256 new pairs a merge, at most a quarter full
-  // (short probe runs: a table sized for the MALL, half full at C3's end, made the update slower,
-  // 6.9 -> 8.2 µs a merge); past 3/4 full it is grown 4x between launches
+  // the table: room for the initial pairs and ~64 new pairs a merge (C3 makes 62), 1.5x over;
+  // past 3/4 full it is grown 4x between launches.  Round 5, with the table updated from a log
+  // per launch: a smaller table is faster -- its rebuild histogram reads fewer slots and its
+  // updates stay in L2 / MALL (C3 A/B on one box: 33.5 M slots 57.4-57.5 k merges/s, 8.4 M
+  // 59.8-60.1 k, 4.2 M 60.3-60.4 k; profiles/r05_c3_tiebreak_table_ab.txt)
   uint64_t want = 1 << 16;
-  while (want < 4 * ((uint64_t)pairs.size() + 256ull * n_max)) want <<= 1;
+  while (want < 3 * ((uint64_t)pairs.size() + 64ull * n_max) / 2) want <<= 1;
   if (const char* e = std::getenv("SHREDWORD_SELECT_TABLE_SLOTS")) {  // tests: a table that must grow
     const uint64_t t = std::strtoull(e, nullptr, 10);
     if (t >= 1024) {  // never below what the initial pairs need (they must all fit)
