@@ -105,6 +105,17 @@ int loadVocab(void* trainer, const char* path);
  *                               merge on the GPU inside the indexed loop, with no host round trip per
  *                               merge: the pair of largest count, ties to the smaller (first, second)
  *                               key (env SHREDWORD_TIEBREAK; types layout, one GPU)
+ *   index = 0 | 1, hybrid = 0 | 1, switch_occ = <n>
+ *                               the indexed merge loop (k_word_loop) takes over from k_resident once
+ *                               a window of merges changed fewer than switch_occ entries (defaults
+ *                               1, 1, 4000; results are identical on every path)
+ *   early_guess = 0 | 1, early_max_records = <n>
+ *                               post the guess for merge X+2 once X is applied (default 0)
+ *   apply_helper = 0 | 1        a second host thread prepares the guessed merge's changes (default 0)
+ *   finalize = <n>              K4 on the device: merges with <= n delta records leave k_word_loop as
+ *                               changes combined per pair key in the reference's application order
+ *                               (default 0 = off; identical results)
+ *   trace_note = <text>         appends a line to the trace file
  *   verify_argmax = <n>         debug (K5 check): every n merges (0 = off, the default; env
  *                               SHREDWORD_VERIFY_ARGMAX) the device recounts the corpus's pairs
  *                               and reduces them (k_pair_max): the host heap's selected frequency
