@@ -738,7 +738,10 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
     if (why) *why = "corpus larger than 2^52 bytes";
     return false;
   }
-  size_t chunk = (size_t)64 << 20;
+  // 32 MiB chunks: the ring pins in half the time of 64 MiB ones and one stream still moves them
+  // at full rate (round 5 A/B, 3 loads each: C3 0.52-0.56 s against 0.53-0.63 s; C5 100 GB
+  // 2.85-2.90 against 2.84-2.85 s; profiles/r05_load_chunk_ab.txt)
+  size_t chunk = (size_t)32 << 20;
   if (const char* e = std::getenv("SHREDWORD_LOAD_CHUNK_MB")) chunk = std::max<size_t>(1, std::strtoull(e, nullptr, 10)) << 20;
   const size_t nchunks = (n + chunk - 1) / chunk;
   int NB = 4;  // chunks in flight: read, queued for DMA, in DMA
