@@ -175,6 +175,7 @@ struct WlParams {
   uint32_t seq0;
   uint32_t idle_polls;
   uint32_t fin_max;  // K4 on the device: merges with at most this many records leave as ordered changes (0: off)
+  uint32_t prefetch;  // 1: the poller wave reads the next command while the records go out (exact mode)
   WlSlotDev sl[WordLoop::kSlots];
   SelParams sel;  // k_word_loop<true> only
 };
@@ -537,6 +538,7 @@ struct LoopS {
   u64 need;   // filter bits the listed words must hold
   u64 occ, t[2];
   u64 t_wait, t_idle, t_undo;  // s_memrealtime: this command's wait began; idle / undo since the last flag
+  uint32_t t_rel;               // ticks of the last flag's system release (diagnostic)
   // tiebreak=device
   uint32_t sm, snk, snew, status, sel_pos, sover, scompact, sins, serr;
   u64 sel_cnt, dxa, t_rec, t_app, logn;
@@ -757,10 +759,19 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     S.pool_top = ld_agent(&p.dstate[kStPoolTop]);
     S.t_idle = 0;
     S.t_undo = 0;
+    S.t_rel = 0;
   }
   uint32_t expect = p.seq0;
   uint32_t exit_op = kOpStop;
   const MergeCtx mc{&S.nspill, &S.nkeys};
+  // command prefetch (p.prefetch, exact mode): the poller wave (wave 1) reads the next command's
+  // granules while the other waves write the current merge's records and its flag, so a command
+  // the host already posted is in registers when the loop comes round (a poll is a PCIe round
+  // trip, ≈ 1.6 µs, that late merges otherwise pay after every flag)
+  const bool pfon = !kSelf && p.prefetch != 0;
+  const int poll_wave = pfon ? 1 : 0;
+  u64 pre_v = 0;
+  bool pre_ok = false;
   if constexpr (kSelf) {  // the rebuilt frontier into LDS, indexed by pair key
     const SelParams& q = p.sel;
     const uint32_t nf = min(ld_agent(q.st + kSelNF), kSelK);
@@ -871,12 +882,15 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           q.out[2 * (u64)m + 1] = bc;
         }
       }
-    } else if (wid == 0) {
-      // ---- wave 0 waits for the next command (one round trip reads all four granules)
+    } else if (wid == poll_wave) {
+      // ---- the poller wave waits for the next command (one round trip reads all four granules;
+      // none when the prefetched granules already carry it)
       const u64* g = p.ring[expect % kRing].g;
       const u64 t_wait = __builtin_amdgcn_s_memrealtime();
       uint32_t op = 0, a = 0, b = 0, X = 0, idle = 0;
-      u64 v = lane < kCmdGranules ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+      u64 v = pre_ok ? pre_v
+                     : (lane < kCmdGranules ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull);
+      pre_ok = false;
       uint32_t loff = 0, lcnt1 = 0;
       for (;;) {
         const bool tagged = lane >= kCmdGranules || (uint32_t)v == expect;
@@ -1310,8 +1324,17 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     } else if (fin) {
       finalize_changes(p, s_h, S, s_q, reinterpret_cast<u64*>(s_strip), sd, a, b, X, nrec);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (pfon && wid == 1) {
+      // the poller wave: the next command's granules, in flight while the others write records
+      pre_v = lane < kCmdGranules
+                  ? __hip_atomic_load(p.ring[expect % kRing].g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                  : 0ull;
+      pre_ok = true;
     } else {
-      for (int i = tid; i < kDh; i += kWlThreads) {
+      // every wave but the poller (with the prefetch on) writes the records
+      const uint32_t rt = pfon ? (tid < 64u ? tid : tid - 64u) : tid;
+      const uint32_t rs = pfon ? (uint32_t)kWlThreads - 64u : (uint32_t)kWlThreads;
+      for (uint32_t i = rt; i < (uint32_t)kDh; i += rs) {
         const uint32_t key = s_h.key[i];
         if (key == kEmpty32) continue;
         const uint32_t r = atomicAdd(&S.nout, 1u);
@@ -1321,7 +1344,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         dst[2] = s_h.ft[i];
       }
       const uint32_t nsp = S.nspill;  // complete: every delta was added before the barrier above
-      for (uint32_t i = tid; i < nsp; i += kWlThreads) {
+      for (uint32_t i = rt; i < nsp; i += rs) {
         const uint32_t key = p.dlist[i];
         const u64 sum = atomicExch(&p.dsum[key], 0ull);
         const u64 ft = atomicExch(&p.dft[key], kEmpty64);
@@ -1333,7 +1356,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
+    // LDS only: the poller's prefetch stays in flight (every other wave drained its stores above)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (tid == 0) {
       sd.hdr[0] = fin ? S.nfin : S.nout;
       sd.hdr[22] = fin ? 1u : 0u;  // 1: ordered changes (finalize_changes), else raw records
@@ -1356,15 +1380,18 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       // device time outside merges since the previous flag: waiting for commands, undoing guesses
       sd.hdr[20] = (uint32_t)(S.t_idle + (t_cmd - S.t_wait));
       sd.hdr[21] = (uint32_t)S.t_undo;
+      sd.hdr[31] = S.t_rel;  // the previous flag's system release (L2 write-back + flag store), ticks
       h64[12] = S.lst_x;  // X's words-of list (0: none)
       h64[13] = t_cmd;    // diagnostic: absolute device clock at the command and at the wait's start
       h64[14] = S.t_wait;
       S.t_idle = 0;
       S.t_undo = 0;
       // one system-scope release (L2 write-back of the records and header, then the flag)
+      const u64 t_r0 = __builtin_amdgcn_s_memrealtime();
       __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      S.t_rel = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_r0);
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (the prefetch still in flight)
   }
   if (tid == 0) {
     p.dstate[kStPoolTop] = S.pool_top;
@@ -1642,6 +1669,7 @@ WordLoop::WordLoop(int ordinal, void* stream, int32_t unk_id) : ordinal_(ordinal
   // race the time-out against the posts
   if (const char* e = std::getenv("SHREDWORD_WL_IDLE_POLLS")) idle_polls_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_WL_FINALIZE")) fin_max_ = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char* e = std::getenv("SHREDWORD_WL_PREFETCH")) prefetch_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_SELECT_REPORT")) sel_report_ = std::atoi(e) != 0;
   for (auto& e : ev_) {
     hipEvent_t ev;
@@ -2027,6 +2055,7 @@ void WordLoop::launch(uint32_t seq0) {
   p.seq0 = seq0;
   p.idle_polls = idle_polls_;
   p.fin_max = fin_max_;
+  p.prefetch = prefetch_ ? 1u : 0u;
   for (int k = 0; k < kSlots; ++k) {
     p.sl[k].recs = static_cast<DeltaRecord*>(slot_[k].dev_recs);
     p.sl[k].hdr = static_cast<uint32_t*>(slot_[k].dev_hdr);
@@ -2122,6 +2151,7 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   st_.raw_records += h[22] ? h[23] : h[0];
   st_.finalized += h[22] ? 1u : 0u;
   st_.dev_out_us += 1e-2 * (double)h[30];
+  st_.dev_rel_us += 1e-2 * (double)h[31];
   if (h[22]) {
     st_.dev_fin_us += 1e-2 * (double)h[30];
     st_.fin_records += h[23];
@@ -2184,6 +2214,10 @@ void WordLoop::stop() {
   uint32_t ds[8];
   WL_OK(hipMemcpy(ds, dstate_, sizeof(ds), hipMemcpyDeviceToHost));
 
+  if (std::getenv("SHREDWORD_WL_REPORT") && st_.merges)
+    std::fprintf(stderr, "[WL] %llu merges: device %.2f us a merge, of it the flag's system release %.2f us, "
+                 "records out %.2f us\n", (unsigned long long)st_.merges, st_.dev_us / (double)st_.merges,
+                 st_.dev_rel_us / (double)st_.merges, st_.dev_out_us / (double)st_.merges);
   if (ds[kStError]) {
     static const char* what[] = {"", "index pool exhausted", "an undone merge had no word list", "",
                                  "a merged pair had no word list"};

@@ -62,6 +62,7 @@ struct WordLoopStats {
   uint64_t records = 0;           // Σ delta records handed to the host
   uint64_t raw_records = 0;       // Σ delta records of the merges (before the device's combine)
   uint64_t finalized = 0;         // merges whose records left as ordered changes
+  double dev_rel_us = 0;          // Σ device time of the flags' system release (L2 write-back), diagnostic
   double dev_out_us = 0;          // Σ device time handing the records out (raw, or gathered + finalized)
   double dev_fin_us = 0;          //   of which: the merges whose records were finalized
   uint64_t fin_records = 0;       //   their raw records
@@ -245,6 +246,9 @@ class WordLoop {
   // K4 on the device up to this many records (<= 64: one wave; up to kFinMax: the workgroup).  Off
   // by default: measured on C3 it costs the device more than it saves the host
   uint32_t fin_max_ = 0;
+  // the next command read while the records go out (SHREDWORD_WL_PREFETCH=0 turns it off): C3 A/B
+  // on one box, 2 rounds: 54.2-54.3 k off, 55.0-55.2 k on (profiles/r05_c3_command_prefetch_ab.txt)
+  bool prefetch_ = true;
   bool last_changes_ = false;
   std::vector<Post> posted_;
   // tiebreak=device: pair table, frontier, state (see word_loop.hip SelParams)
