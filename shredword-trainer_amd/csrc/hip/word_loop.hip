@@ -317,45 +317,49 @@ struct MergeCtx {
   uint32_t* nkeys;   // delta keys in the LDS hash
 };
 
-// One neighbour delta (reference freq_change_add, bpe.cpp:274-290): Σ weight and min first touch
+// Neighbour deltas (reference freq_change_add, bpe.cpp:274-290): Σ weight and min first touch
 // per key = slot * 4 + category, in the LDS hash; keys past it go to the global spill tables.
-__device__ __forceinline__ void delta_add(DeltaH& h, const WlParams& p, const MergeCtx& c, uint32_t key, u64 w,
-                                          u64 ft) {
-  uint32_t s = (key * 2654435761u) >> (32 - 11);
-#pragma unroll 1
-  for (int probe = 0; probe < 32; ++probe) {
-    const uint32_t prev = atomicCAS(&h.key[s], kEmpty32, key);
-    if (prev == kEmpty32 || prev == key) {
-      if (prev == kEmpty32) atomicAdd(c.nkeys, 1u);
-      atomicAdd(&h.sum[s], w);
-      atomicMin(&h.ft[s], ft);
-      return;
-    }
-    s = (s + 1) & (kDh - 1);
-  }
-  const u64 old = atomicAdd(&p.dsum[key], w);
-  atomicMin(&p.dft[key], ft);
-  if (old == 0) p.dlist[atomicAdd(c.nspill, 1u)] = key;  // weights are >= 1
-}
-
 // The four deltas of one occurrence (prev: the left neighbour after merging, X when just
 // produced, has_l false at the word's start; n: the original token after the pair, has_n false
-// at the word's end); returns its filter bits.
+// at the word's end); returns its filter bits.  The four keys are probed together, so their CAS
+// round trips overlap (one LDS latency a probe step instead of four), as delta_add would do
+// them one by one; a key still unplaced after 32 steps goes to the global spill tables.
 __device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const MergeCtx& c, bool has_l, int32_t prev,
                                           bool has_n, int32_t n, u64 wc, u64 ft) {
   u64 f = 0;
-  if (has_l) {
-    const uint32_t sl = slot_of(prev, p.cap) * 4u;
-    delta_add(h, p, c, sl + 0u, wc, ft | 0u);
-    delta_add(h, p, c, sl + 1u, wc, ft | 1u);
-    f |= nbit(prev, 0);
+  const uint32_t sl = slot_of(prev, p.cap) * 4u, sn = slot_of(n, p.cap) * 4u;
+  const uint32_t key[4] = {sl + 0u, sl + 1u, sn + 2u, sn + 3u};
+  bool pend[4] = {has_l, has_l, has_n, has_n};
+  uint32_t slot[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) slot[k] = (key[k] * 2654435761u) >> (32 - 11);
+#pragma unroll 1
+  for (int probe = 0; probe < 32 && (pend[0] | pend[1] | pend[2] | pend[3]); ++probe) {
+    uint32_t prv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) prv[k] = pend[k] ? atomicCAS(&h.key[slot[k]], kEmpty32, key[k]) : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!pend[k]) continue;
+      if (prv[k] == kEmpty32 || prv[k] == key[k]) {
+        if (prv[k] == kEmpty32) atomicAdd(c.nkeys, 1u);
+        atomicAdd(&h.sum[slot[k]], wc);
+        atomicMin(&h.ft[slot[k]], ft | (u64)k);
+        pend[k] = false;
+      } else {
+        slot[k] = (slot[k] + 1) & (kDh - 1);
+      }
+    }
   }
-  if (has_n) {
-    const uint32_t sn = slot_of(n, p.cap) * 4u;
-    delta_add(h, p, c, sn + 2u, wc, ft | 2u);
-    delta_add(h, p, c, sn + 3u, wc, ft | 3u);
-    f |= nbit(n, 1);
-  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (pend[k]) {  // the LDS hash is full around this key: the global tables take it
+      const u64 old = atomicAdd(&p.dsum[key[k]], wc);
+      atomicMin(&p.dft[key[k]], ft | (u64)k);
+      if (old == 0) p.dlist[atomicAdd(c.nspill, 1u)] = key[k];  // weights are >= 1
+    }
+  if (has_l) f |= nbit(prev, 0);
+  if (has_n) f |= nbit(n, 1);
   return f;
 }
 
@@ -1008,7 +1012,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.filter = need != 0;
         S.occ = 0;
         S.err = 0;
-        S.st[0] = S.st[1] = S.st[2] = 0;
+        S.st[0] = S.st[1] = S.st[2] = S.st[3] = 0;
         if (err) atomicMax(&p.dstate[kStError], undo ? kErrList : kErrLookup);
         if (!undo && (u64)S.pool_top + cnt > p.pool_cap) {
           S.err = 1;
@@ -1377,6 +1381,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       sd.hdr[16] = S.st[0];
       sd.hdr[17] = S.st[1];
       sd.hdr[18] = S.st[2];
+      sd.hdr[19] = S.st[3];
       // device time outside merges since the previous flag: waiting for commands, undoing guesses
       sd.hdr[20] = (uint32_t)(S.t_idle + (t_cmd - S.t_wait));
       sd.hdr[21] = (uint32_t)S.t_undo;
@@ -2165,7 +2170,7 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   if (timing_) {
     const uint32_t rec[kTraceFields] = {(uint32_t)X, h[2], h[12], h[3], (uint32_t)h64[2], (uint32_t)(10 * h64[3]),
                                         (uint32_t)(10 * h64[4]), (uint32_t)(10 * (h64[5] - h64[4])),
-                                        10 * h[16], 10 * h[17], 10 * h[18], 0u, 10 * h[20],
+                                        10 * h[16], 10 * h[17], 10 * h[18], 10 * h[19], 10 * h[20],
                                         10 * h[21], (uint32_t)(1e9 * (t_seen - pp.t_post)),
                                         // absolute clocks for a timeline: host 10 ns units since the
                                         // loop was made, device ticks (100 MHz), low 32 bits
