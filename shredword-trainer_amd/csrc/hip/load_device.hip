@@ -796,7 +796,10 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   // the count runs on segments (whole tiles) as they land -- segment k once every chunk up to the
   // end of segment k + 1 is in HBM (a word may run into the next segment; one running further is
   // flagged and the whole count is repeated after the upload).
-  int T = 8;
+  // 16 readers: the same rate as 8 once the file's pages are local (C3 0.51-0.55 s, C5 2.81-2.84 s
+  // either way), and 18% faster on the first read of freshly written tmpfs pages (C5 100 GB right
+  // after the generator: 4.99 s against 5.89 s; profiles/r05_load_readers_ab.txt)
+  int T = 16;
   if (const char* e = std::getenv("SHREDWORD_LOAD_READERS")) T = std::max(1, std::min(64, std::atoi(e)));
   // readers on the GPU's NUMA node (SHREDWORD_LOAD_NUMA=0: wherever the scheduler puts them)
   std::vector<int> local;
