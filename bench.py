@@ -710,6 +710,8 @@ def main():
                     help="merge selection: exact (the reference's heap replay, bit-exact files; default) or device "
                          "(opt-in K5 mode: every merge selected on the GPU, ties to the smaller pair key)")
     ap.add_argument("--bytes", type=int, default=0, help="override the corpus size (testing)")
+    ap.add_argument("--device-leg-steps", type=int, default=2,
+                    help="untimed leg after the timed steps: tiebreak=device trains on the same corpus (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--encode-reps", type=int, default=5, help="encoder leg repetitions (0 = skip)")
@@ -883,6 +885,35 @@ def main():
         tm = torch.tensor([merges], dtype=torch.int64)
         dist.all_reduce(tm, op=dist.ReduceOp.SUM)
         all_merges = int(tm.item())
+    st = t.stats()
+    tmpd = os.environ.get("TMPDIR", "/tmp")
+    t._save(t.trainer, os.path.join(tmpd, f"bench_r{rank}.model").encode(),
+            os.path.join(tmpd, f"bench_r{rank}.vocab").encode())
+    # untimed leg: the opt-in tiebreak=device mode on the same loaded corpus and box (not the
+    # reference's merge order, so never `value`): one warm train, then --device-leg-steps timed
+    device_leg = None
+    if (rank == 0 and world == 1 and args.tiebreak == "exact" and args.layout == "types"
+            and args.device_leg_steps > 0):
+        try:
+            t.set_option("tiebreak", "device")
+            train_step()
+            t.set_option("clear_stats", 1)
+            torch.cuda.synchronize()
+            d0 = time.perf_counter()
+            dm = 0
+            for _ in range(args.device_leg_steps):
+                dm += train_step()
+            torch.cuda.synchronize()
+            de = time.perf_counter() - d0
+            std = t.stats()
+            dpre = os.path.join(tmpd, f"bench_r{rank}_device")
+            t._save(t.trainer, (dpre + ".model").encode(), (dpre + ".vocab").encode())
+            device_leg = tiebreak_report(std, dm, de, args, dpre)
+            device_leg["steps"] = args.device_leg_steps
+            device_leg["exact_merges_per_s_same_run"] = merges / elapsed
+            device_leg["ratio_to_exact_same_run"] = (dm / de) / (merges / elapsed)
+        except Exception as e:  # the exact line stands on its own
+            device_leg = {"error": repr(e)}
     # the CPU baseline starts only now: the timed steps ran with the host to themselves
     cpu_h = None
     if world == 1 and not args.no_cpu_baseline:
@@ -890,10 +921,6 @@ def main():
             cpu_h = cpu_baseline_start(cfg, path, args.cpu_seconds)
         except Exception as e:  # the GPU number stands on its own
             cpu_h = {"error": repr(e)}
-    st = t.stats()
-    tmpd = os.environ.get("TMPDIR", "/tmp")
-    t._save(t.trainer, os.path.join(tmpd, f"bench_r{rank}.model").encode(),
-            os.path.join(tmpd, f"bench_r{rank}.vocab").encode())
     t.destroy()
 
     # K1 HBM leg (the metric's "pair-count HBM GB/s"): every rank counts its stream copy / shard
@@ -990,6 +1017,8 @@ def main():
                                if k1["avg_launch_us"] > 0 else None)
         if args.tiebreak == "device":
             result["tiebreak_device"] = tiebreak_report(st, merges, elapsed, args, os.path.join(tmpd, f"bench_r{rank}"))
+        if device_leg is not None:
+            result["tiebreak_device_leg"] = device_leg
         case = fullsize_case(case_name) if case_name else None
         if case and case["recipe"]["bytes"] == cfg["bytes"] and args.tiebreak == "exact":
             result["config"]["corpus_md5_expected"] = case["corpus_md5"]
