@@ -102,7 +102,12 @@ def corpus_path(cfg, name):
     return os.path.join(d, f"{name}_{cfg['script']}_{cfg['bytes']}_s{cfg['seed']}.txt")
 
 
-def ensure_corpus(cfg, path):
+def ensure_corpus(cfg, path, cpus=None):
+    """Generates the corpus file once.  cpus: the generator runs on these CPUs (the bench passes
+    the GPU's NUMA node), so the file's page-cache pages sit on the node whose threads read them,
+    as they would for a file the loader's own readers page in from disk (read right after a
+    generator on the other socket wrote them, 100 GB load at ~20 GB/s instead of ~50;
+    profiles/r05_c5_load_first_vs_later.txt)."""
     if os.path.exists(path) and os.path.getsize(path) == cfg["bytes"]:
         return 0.0
     gen = os.path.join(PKG, "bin", "gen_corpus")
@@ -111,8 +116,17 @@ def ensure_corpus(cfg, path):
     t0 = time.time()
     tmp = path + ".part"
     threads = str(min(16, os.cpu_count() or 8))
-    subprocess.run([gen, "--bytes", str(cfg["bytes"]), "--seed", str(cfg["seed"]), "--script", cfg["script"],
-                    "--out", tmp, "--threads", threads], check=True)
+    # the child inherits this process's affinity: set around the spawn, restored after
+    mine = set(os.sched_getaffinity(0))
+    near = mine & set(cpus) if cpus else set()
+    if near:
+        os.sched_setaffinity(0, near)
+    try:
+        subprocess.run([gen, "--bytes", str(cfg["bytes"]), "--seed", str(cfg["seed"]), "--script", cfg["script"],
+                        "--out", tmp, "--threads", threads], check=True)
+    finally:
+        if near:
+            os.sched_setaffinity(0, mine)
     os.replace(tmp, path)
     return time.time() - t0
 
@@ -786,7 +800,7 @@ def main():
             dist.barrier()
 
     path = corpus_path(cfg, args.config)
-    gen_s = ensure_corpus(cfg, path) if local == 0 else 0.0
+    gen_s = ensure_corpus(cfg, path, cpus=None if args.no_pin else gpu_numa_cpus(dev)) if local == 0 else 0.0
     barrier()
     # C4's corpus is 8 shards of one logical corpus: on one GPU the load counts the 8 byte ranges
     # in turn and merges their word lists, as 8 ranks of a sharded load would (corpus.cpp)
