@@ -176,6 +176,7 @@ struct WlParams {
   uint32_t idle_polls;
   uint32_t fin_max;  // K4 on the device: merges with at most this many records leave as ordered changes (0: off)
   uint32_t prefetch;  // 1: the poller wave reads the next command while the records go out (exact mode)
+  uint32_t drain;     // 1: the merge's barriers drain every wave's stores (0: only with spills or K4)
   WlSlotDev sl[WordLoop::kSlots];
   SelParams sel;  // k_word_loop<true> only
 };
@@ -776,6 +777,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   const int poll_wave = pfon ? 1 : 0;
   u64 pre_v = 0;
   bool pre_ok = false;
+  // the merge's word-run and pool stores need not land before the records go out: nothing reads
+  // them until the next command's barrier, which drains them; spilled deltas (read back by the
+  // records phase) and K4 (which reads the merged words) still drain at the merge's end
+  const bool drain = p.drain != 0 || p.fin_max != 0;
   if constexpr (kSelf) {  // the rebuilt frontier into LDS, indexed by pair key
     const SelParams& q = p.sel;
     const uint32_t nf = min(ld_agent(q.st + kSelNF), kSelK);
@@ -1151,15 +1156,17 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           }
         }
       }
-      __syncthreads();
+      if (drain) __syncthreads();
+      else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (tid == 0) S.qn = 0;
-      __syncthreads();
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     if (my_occ) atomicAdd(&S.occ, (u64)my_occ);
     if (my_scan) atomicAdd(&S.scan, my_scan);
     if (my_rd) atomicAdd(&S.rd, my_rd);
     if (my_wr) atomicAdd(&S.wr, my_wr);
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (drain || S.nspill) __syncthreads();  // (uniform: S.nspill is final after the barrier above)
     const uint32_t nchg = append ? S.nchg : 0u;
     if constexpr (kSelf) {
       // ---- tiebreak=device: the records change the pair table (atomics nobody waits for) and,
@@ -1675,6 +1682,7 @@ WordLoop::WordLoop(int ordinal, void* stream, int32_t unk_id) : ordinal_(ordinal
   if (const char* e = std::getenv("SHREDWORD_WL_IDLE_POLLS")) idle_polls_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_WL_FINALIZE")) fin_max_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_WL_PREFETCH")) prefetch_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SHREDWORD_WL_DRAIN")) drain_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_SELECT_REPORT")) sel_report_ = std::atoi(e) != 0;
   for (auto& e : ev_) {
     hipEvent_t ev;
@@ -2061,6 +2069,7 @@ void WordLoop::launch(uint32_t seq0) {
   p.idle_polls = idle_polls_;
   p.fin_max = fin_max_;
   p.prefetch = prefetch_ ? 1u : 0u;
+  p.drain = drain_ ? 1u : 0u;
   for (int k = 0; k < kSlots; ++k) {
     p.sl[k].recs = static_cast<DeltaRecord*>(slot_[k].dev_recs);
     p.sl[k].hdr = static_cast<uint32_t*>(slot_[k].dev_hdr);

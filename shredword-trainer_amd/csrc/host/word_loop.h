@@ -249,6 +249,8 @@ class WordLoop {
   // the next command read while the records go out (SHREDWORD_WL_PREFETCH=0 turns it off): C3 A/B
   // on one box, 2 rounds: 54.2-54.3 k off, 55.0-55.2 k on (profiles/r05_c3_command_prefetch_ab.txt)
   bool prefetch_ = true;
+  // SHREDWORD_WL_DRAIN=1: every merge barrier drains the stores (the round-4 barriers)
+  bool drain_ = false;
   bool last_changes_ = false;
   std::vector<Post> posted_;
   // tiebreak=device: pair table, frontier, state (see word_loop.hip SelParams)
