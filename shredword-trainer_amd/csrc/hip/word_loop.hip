@@ -177,6 +177,7 @@ struct WlParams {
   uint32_t fin_max;  // K4 on the device: merges with at most this many records leave as ordered changes (0: off)
   uint32_t prefetch;  // 1: the poller wave reads the next command while the records go out (exact mode)
   uint32_t drain;     // 1: the merge's barriers drain every wave's stores (0: only with spills or K4)
+  uint32_t probes;    // LDS delta hash probes before a key spills to HBM (32; tests force spills with 0)
   WlSlotDev sl[WordLoop::kSlots];
   SelParams sel;  // k_word_loop<true> only
 };
@@ -324,7 +325,7 @@ struct MergeCtx {
 // produced, has_l false at the word's start; n: the original token after the pair, has_n false
 // at the word's end); returns its filter bits.  The four keys are probed together, so their CAS
 // round trips overlap (one LDS latency a probe step instead of four), as delta_add would do
-// them one by one; a key still unplaced after 32 steps goes to the global spill tables.
+// them one by one; a key still unplaced after p.probes (32) steps goes to the global spill tables.
 __device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const MergeCtx& c, bool has_l, int32_t prev,
                                           bool has_n, int32_t n, u64 wc, u64 ft) {
   u64 f = 0;
@@ -335,7 +336,7 @@ __device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const Me
 #pragma unroll
   for (int k = 0; k < 4; ++k) slot[k] = (key[k] * 2654435761u) >> (32 - 11);
 #pragma unroll 1
-  for (int probe = 0; probe < 32 && (pend[0] | pend[1] | pend[2] | pend[3]); ++probe) {
+  for (uint32_t probe = 0; probe < p.probes && (pend[0] | pend[1] | pend[2] | pend[3]); ++probe) {
     uint32_t prv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) prv[k] = pend[k] ? atomicCAS(&h.key[slot[k]], kEmpty32, key[k]) : 0u;
@@ -1388,7 +1389,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       sd.hdr[16] = S.st[0];
       sd.hdr[17] = S.st[1];
       sd.hdr[18] = S.st[2];
-      sd.hdr[19] = S.st[3];
+      sd.hdr[19] = S.nspill;  // delta keys that spilled past the LDS hash to HBM
       // device time outside merges since the previous flag: waiting for commands, undoing guesses
       sd.hdr[20] = (uint32_t)(S.t_idle + (t_cmd - S.t_wait));
       sd.hdr[21] = (uint32_t)S.t_undo;
@@ -1683,6 +1684,7 @@ WordLoop::WordLoop(int ordinal, void* stream, int32_t unk_id) : ordinal_(ordinal
   if (const char* e = std::getenv("SHREDWORD_WL_FINALIZE")) fin_max_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_WL_PREFETCH")) prefetch_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_WL_DRAIN")) drain_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SHREDWORD_WL_PROBES")) probes_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_SELECT_REPORT")) sel_report_ = std::atoi(e) != 0;
   for (auto& e : ev_) {
     hipEvent_t ev;
@@ -2070,6 +2072,7 @@ void WordLoop::launch(uint32_t seq0) {
   p.fin_max = fin_max_;
   p.prefetch = prefetch_ ? 1u : 0u;
   p.drain = drain_ ? 1u : 0u;
+  p.probes = probes_;
   for (int k = 0; k < kSlots; ++k) {
     p.sl[k].recs = static_cast<DeltaRecord*>(slot_[k].dev_recs);
     p.sl[k].hdr = static_cast<uint32_t*>(slot_[k].dev_hdr);
@@ -2166,6 +2169,8 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   st_.finalized += h[22] ? 1u : 0u;
   st_.dev_out_us += 1e-2 * (double)h[30];
   st_.dev_rel_us += 1e-2 * (double)h[31];
+  st_.spill_merges += h[19] ? 1u : 0u;
+  st_.spill_keys += h[19];
   if (h[22]) {
     st_.dev_fin_us += 1e-2 * (double)h[30];
     st_.fin_records += h[23];
@@ -2179,7 +2184,7 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
   if (timing_) {
     const uint32_t rec[kTraceFields] = {(uint32_t)X, h[2], h[12], h[3], (uint32_t)h64[2], (uint32_t)(10 * h64[3]),
                                         (uint32_t)(10 * h64[4]), (uint32_t)(10 * (h64[5] - h64[4])),
-                                        10 * h[16], 10 * h[17], 10 * h[18], 10 * h[19], 10 * h[20],
+                                        10 * h[16], 10 * h[17], 10 * h[18], h[19], 10 * h[20],
                                         10 * h[21], (uint32_t)(1e9 * (t_seen - pp.t_post)),
                                         // absolute clocks for a timeline: host 10 ns units since the
                                         // loop was made, device ticks (100 MHz), low 32 bits
@@ -2230,8 +2235,10 @@ void WordLoop::stop() {
 
   if (std::getenv("SHREDWORD_WL_REPORT") && st_.merges)
     std::fprintf(stderr, "[WL] %llu merges: device %.2f us a merge, of it the flag's system release %.2f us, "
-                 "records out %.2f us\n", (unsigned long long)st_.merges, st_.dev_us / (double)st_.merges,
-                 st_.dev_rel_us / (double)st_.merges, st_.dev_out_us / (double)st_.merges);
+                 "records out %.2f us; %llu merges spilled %llu delta keys to HBM\n", (unsigned long long)st_.merges,
+                 st_.dev_us / (double)st_.merges, st_.dev_rel_us / (double)st_.merges,
+                 st_.dev_out_us / (double)st_.merges, (unsigned long long)st_.spill_merges,
+                 (unsigned long long)st_.spill_keys);
   if (ds[kStError]) {
     static const char* what[] = {"", "index pool exhausted", "an undone merge had no word list", "",
                                  "a merged pair had no word list"};
@@ -2461,6 +2468,7 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
     p.cap = cap_;
     p.unk = unk_;
     p.sel = q;
+    p.probes = probes_;
     dirty_ = true;
     for (;;) {
       p.seq0 = seq_ + 1;

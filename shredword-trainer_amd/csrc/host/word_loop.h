@@ -66,6 +66,8 @@ struct WordLoopStats {
   double dev_out_us = 0;          // Σ device time handing the records out (raw, or gathered + finalized)
   double dev_fin_us = 0;          //   of which: the merges whose records were finalized
   uint64_t fin_records = 0;       //   their raw records
+  uint64_t spill_merges = 0;      // merges whose delta keys overflowed the LDS hash (HBM spill tables)
+  uint64_t spill_keys = 0;        // Σ their spilled keys
 };
 
 struct SelectStats {
@@ -160,7 +162,7 @@ class WordLoop {
   // Per collected merge while timing is on, kTraceFields u32 each: X, listed words, scanned
   // words, changed words, occurrences, device ns command -> flag, of which lookup ns, scan ns;
   // then thread 0's stamps (ns after the command): pool entries loaded, first run loaded, first
-  // word merged; and ns spent building pair groups this merge needed first; then the device ns
+  // word merged; and the delta keys spilled past the LDS hash to HBM; then the device ns
   // outside merges since the previous merge's flag (waiting for commands; undoing guesses), and
   // the host ns from posting this merge to seeing its flag; then absolute clocks: host post and
   // flag seen (10 ns since the loop was made), device command seen and wait begun (100 MHz
@@ -251,6 +253,8 @@ class WordLoop {
   bool prefetch_ = true;
   // SHREDWORD_WL_DRAIN=1: every merge barrier drains the stores (the round-4 barriers)
   bool drain_ = false;
+  // SHREDWORD_WL_PROBES=<n>: LDS delta hash probes before a key spills to HBM (tests: 0 spills all)
+  uint32_t probes_ = 32;
   bool last_changes_ = false;
   std::vector<Post> posted_;
   // tiebreak=device: pair table, frontier, state (see word_loop.hip SelParams)
