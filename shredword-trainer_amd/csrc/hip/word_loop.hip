@@ -177,7 +177,6 @@ struct WlParams {
   uint32_t fin_max;  // K4 on the device: merges with at most this many records leave as ordered changes (0: off)
   uint32_t prefetch;  // 1: the poller wave reads the next command while the records go out (exact mode)
   uint32_t drain;     // 1: the merge's barriers drain every wave's stores (0: only with spills or K4)
-  uint32_t probes;    // LDS delta hash probes before a key spills to HBM (32; tests force spills with 0)
   WlSlotDev sl[WordLoop::kSlots];
   SelParams sel;  // k_word_loop<true> only
 };
@@ -325,7 +324,7 @@ struct MergeCtx {
 // produced, has_l false at the word's start; n: the original token after the pair, has_n false
 // at the word's end); returns its filter bits.  The four keys are probed together, so their CAS
 // round trips overlap (one LDS latency a probe step instead of four), as delta_add would do
-// them one by one; a key still unplaced after p.probes (32) steps goes to the global spill tables.
+// them one by one; a key still unplaced after 32 steps goes to the global spill tables.
 __device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const MergeCtx& c, bool has_l, int32_t prev,
                                           bool has_n, int32_t n, u64 wc, u64 ft) {
   u64 f = 0;
@@ -336,7 +335,7 @@ __device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const Me
 #pragma unroll
   for (int k = 0; k < 4; ++k) slot[k] = (key[k] * 2654435761u) >> (32 - 11);
 #pragma unroll 1
-  for (uint32_t probe = 0; probe < p.probes && (pend[0] | pend[1] | pend[2] | pend[3]); ++probe) {
+  for (int probe = 0; probe < 32 && (pend[0] | pend[1] | pend[2] | pend[3]); ++probe) {
     uint32_t prv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) prv[k] = pend[k] ? atomicCAS(&h.key[slot[k]], kEmpty32, key[k]) : 0u;
@@ -1684,7 +1683,6 @@ WordLoop::WordLoop(int ordinal, void* stream, int32_t unk_id) : ordinal_(ordinal
   if (const char* e = std::getenv("SHREDWORD_WL_FINALIZE")) fin_max_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_WL_PREFETCH")) prefetch_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_WL_DRAIN")) drain_ = std::atoi(e) != 0;
-  if (const char* e = std::getenv("SHREDWORD_WL_PROBES")) probes_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_SELECT_REPORT")) sel_report_ = std::atoi(e) != 0;
   for (auto& e : ev_) {
     hipEvent_t ev;
@@ -2072,7 +2070,6 @@ void WordLoop::launch(uint32_t seq0) {
   p.fin_max = fin_max_;
   p.prefetch = prefetch_ ? 1u : 0u;
   p.drain = drain_ ? 1u : 0u;
-  p.probes = probes_;
   for (int k = 0; k < kSlots; ++k) {
     p.sl[k].recs = static_cast<DeltaRecord*>(slot_[k].dev_recs);
     p.sl[k].hdr = static_cast<uint32_t*>(slot_[k].dev_hdr);
@@ -2468,7 +2465,6 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
     p.cap = cap_;
     p.unk = unk_;
     p.sel = q;
-    p.probes = probes_;
     dirty_ = true;
     for (;;) {
       p.seq0 = seq_ + 1;

@@ -253,8 +253,6 @@ class WordLoop {
   bool prefetch_ = true;
   // SHREDWORD_WL_DRAIN=1: every merge barrier drains the stores (the round-4 barriers)
   bool drain_ = false;
-  // SHREDWORD_WL_PROBES=<n>: LDS delta hash probes before a key spills to HBM (tests: 0 spills all)
-  uint32_t probes_ = 32;
   bool last_changes_ = false;
   std::vector<Post> posted_;
   // tiebreak=device: pair table, frontier, state (see word_loop.hip SelParams)

@@ -98,19 +98,6 @@ def test_index_loop_changes_on_device_match_reference(name, fin, case_corpus, tm
         assert 0 < st["index_finalized"] < st["index_merges"] + st["index_undos"], st
 
 
-@pytest.mark.parametrize("probes", [0, 1])
-@pytest.mark.parametrize("name", [n for n in API_CASES if n not in DEEP])
-def test_index_loop_spilled_deltas_match_reference(name, probes, case_corpus, tmp_path, monkeypatch):
-    """Delta keys pushed out of k_word_loop's LDS hash into the HBM spill tables
-    (SHREDWORD_WL_PROBES: 0 spills every key, 1 most of a busy merge's; the default 32 spills almost
-    none, once in C3's 29,000 indexed merges): the records phase reads them back after the merge's
-    store drain, which only spilling merges keep.  Same bytes."""
-    case, corpus = case_corpus(name)
-    monkeypatch.setenv("SHREDWORD_WL_PROBES", str(probes))
-    st = {}
-    _check(case, _train(case, corpus, tmp_path, "types", stats=st, hybrid=0))
-
-
 @pytest.mark.parametrize("path", ["hybrid", "index", "resident", "launch", "stream"])
 @pytest.mark.parametrize("name", API_CASES)
 def test_argmax_verifier(name, path, case_corpus, tmp_path):
