@@ -223,6 +223,8 @@ typedef struct ShredStats {
   double index_dev_fin_us;     /*   of which: the finalized merges */
   uint64_t index_fin_records;  /*   their raw records */
   double sel_table_us;         /* tiebreak=device: of sel_merge_us, the pair-table + frontier update */
+  uint64_t index_spill_merges; /* k_word_loop: merges whose delta keys overflowed the LDS hash into HBM */
+  uint64_t index_spill_keys;   /*   Σ their spilled keys */
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

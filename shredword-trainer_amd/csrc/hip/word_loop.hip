@@ -59,7 +59,15 @@ constexpr bool kWlPrefetch = false;     // (A/B builds) each word's run loaded i
 #else
 constexpr bool kWlPrefetch = true;      // the next word's run loads while this one merges
 #endif
-constexpr int kQ = kWlThreads * kB + kWlThreads;  // LDS queue of filtered entries (a round + a remainder)
+constexpr int kQ = kWlThreads * kB + kWlThreads;
+// Diagnostic builds (-DSHRED_WL_STAMPS, tools/build_variant.sh): per-merge phase stamps of the
+// indexed loop in header words [32, 44) (WordLoop::collect puts them in the trace)
+#ifdef SHRED_WL_STAMPS
+#define WL_ST(...) __VA_ARGS__
+#else
+#define WL_ST(...)
+#endif
+constexpr int kXs = 12;  // LDS queue of filtered entries (a round + a remainder)
 constexpr uint32_t kDeltaBucketsDev = 1024;  // the reference's FREQ_CHANGE_BUCKETS (bpe.cpp:16)
 constexpr uint32_t kRing = 64;          // command ring entries
 constexpr uint32_t kOpMerge = 1, kOpStop = 2, kOpTimeout = 3, kOpUnmerge = 4;
@@ -130,7 +138,8 @@ constexpr int kSelM = 0, kSelNF = 1, kSelBuf = 2, kSelStatus = 3, kSelIns = 4, k
 constexpr int kSelWords = kSelStats + 2 * 12 + 2;  // st: 6 words, then 12 u64 statistics, then the log's length (u64)
 constexpr int kSelLogW = kSelStats + 2 * 12;
 // exit status: merges done (target reached / below min_pair_freq), frontier to rebuild, table full
-constexpr uint32_t kSelDone = 1, kSelRebuild = 2;
+// (the in-kernel fill bound: one more merge's new pairs might not fit; the host grows the table)
+constexpr uint32_t kSelDone = 1, kSelRebuild = 2, kSelFull = 3;
 // The frontier lives in LDS for the whole launch: each entry's count follows the table's (the
 // merge's records add to both; inf[slot] = LDS position + 1), so a select is an LDS scan.  A
 // rebuild picks kSelK entries; merges append, and past kSelF - kSelSlack entries the dead ones
@@ -176,7 +185,14 @@ struct WlParams {
   uint32_t idle_polls;
   uint32_t fin_max;  // K4 on the device: merges with at most this many records leave as ordered changes (0: off)
   uint32_t prefetch;  // 1: the poller wave reads the next command while the records go out (exact mode)
-  uint32_t drain;     // 1: the merge's barriers drain every wave's stores (0: only with spills or K4)
+  // 1: the merge's barriers drain every wave's stores (0: only with spills or K4).  With 0 the
+  // word-run (wtok), pool and lst stores of a merge may still be in flight when its flag is raised;
+  // that is sound only because nothing reads them before the next command's __syncthreads, which
+  // drains them, and the host never reads them while the loop runs.  Any new reader of wtok, pool
+  // or lst inside a merge's records phase, or on the host after a flag, needs drain = 1 (K4 sets
+  // it: finalize reads the merged words).  tests/test_gpu_parity.py runs both modes.
+  uint32_t drain;
+  uint32_t fast;      // 1: merges listing <= kWlThreads words take the small-merge path (exact mode)
   WlSlotDev sl[WordLoop::kSlots];
   SelParams sel;  // k_word_loop<true> only
 };
@@ -316,6 +332,7 @@ struct DeltaH {
 struct MergeCtx {
   uint32_t* nspill;  // delta keys spilled past the LDS hash
   uint32_t* nkeys;   // delta keys in the LDS hash
+  uint16_t* klist;   // their slots, in insertion order (the small-merge path's records and clear)
 };
 
 // Neighbour deltas (reference freq_change_add, bpe.cpp:274-290): Σ weight and min first touch
@@ -324,7 +341,27 @@ struct MergeCtx {
 // produced, has_l false at the word's start; n: the original token after the pair, has_n false
 // at the word's end); returns its filter bits.  The four keys are probed together, so their CAS
 // round trips overlap (one LDS latency a probe step instead of four), as delta_add would do
-// them one by one; a key still unplaced after 32 steps goes to the global spill tables.
+// them one by one; a key still unplaced after kProbes steps goes to the global spill tables.
+// kProbes is a template argument so that the tests can force the spill path (kProbes 0: every key
+// spills, 1: most of a busy merge's) with no cost to the default kernel (32; C3 spills one or two
+// keys in 29,000 indexed merges).
+constexpr int kProbesDefault = 32;
+
+// Sum of a u32 over the wave by DPP row shifts and row broadcasts (lane 63 holds it), read back
+// as a scalar.  Call it with every lane active (0 from lanes that add nothing).  A per-lane
+// atomicAdd on one LDS word instead compiles to a loop over the active lanes (the compiler's
+// iterative atomic combine: ~7 scalar instructions a lane), microseconds a merge at 64 lanes.
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+template <int kProbes>
 __device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const MergeCtx& c, bool has_l, int32_t prev,
                                           bool has_n, int32_t n, u64 wc, u64 ft) {
   u64 f = 0;
@@ -335,15 +372,25 @@ __device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const Me
 #pragma unroll
   for (int k = 0; k < 4; ++k) slot[k] = (key[k] * 2654435761u) >> (32 - 11);
 #pragma unroll 1
-  for (int probe = 0; probe < 32 && (pend[0] | pend[1] | pend[2] | pend[3]); ++probe) {
+  for (int probe = 0; probe < kProbes && (pend[0] | pend[1] | pend[2] | pend[3]); ++probe) {
     uint32_t prv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) prv[k] = pend[k] ? atomicCAS(&h.key[slot[k]], kEmpty32, key[k]) : 0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      {  // a key new to the hash joins the key list: one counter add per wave (ballot + rank)
+        const bool fresh = pend[k] && prv[k] == kEmpty32;
+        const u64 fm = __ballot(fresh);
+        if (fm) {
+          const int lead = __ffsll((long long)fm) - 1;
+          uint32_t base = 0;
+          if ((int)(threadIdx.x & 63) == lead) base = atomicAdd(c.nkeys, (uint32_t)__popcll(fm));
+          base = (uint32_t)__builtin_amdgcn_readlane((int)base, lead);
+          if (fresh) c.klist[base + (uint32_t)__popcll(fm & ((1ull << (threadIdx.x & 63)) - 1ull))] = (uint16_t)slot[k];
+        }
+      }
       if (!pend[k]) continue;
       if (prv[k] == kEmpty32 || prv[k] == key[k]) {
-        if (prv[k] == kEmpty32) atomicAdd(c.nkeys, 1u);
         atomicAdd(&h.sum[slot[k]], wc);
         atomicMin(&h.ft[slot[k]], ft | (u64)k);
         pend[k] = false;
@@ -368,6 +415,7 @@ __device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const Me
 // as the reference's chain walk (the path of words longer than the strip); returns the
 // occurrences merged, the new length in *len and the filter bits in *sig.  First touch =
 // (rank << 32) | (input position << 2) | category.
+template <int kProbes>
 __device__ __forceinline__ uint32_t merge_run(const WlParams& p, DeltaH& h, const MergeCtx& c, int32_t* t, uint32_t L,
                                               u64 e, u64 wc, int32_t a, int32_t b, int32_t X, uint32_t* len,
                                               u64* sig) {
@@ -382,7 +430,7 @@ __device__ __forceinline__ uint32_t merge_run(const WlParams& p, DeltaH& h, cons
       const bool has_n = j + 2 < L;
       const int32_t n = has_n ? t[j + 2] : 0;  // the original next token (bpe.cpp:283-289)
       const int32_t n2 = j + 3 < L ? t[j + 3] : 0;
-      f |= occurrence(p, h, c, k > 0, prev, has_n, n, wc, rank | ((u64)j << 2));
+      f |= occurrence<kProbes>(p, h, c, k > 0, prev, has_n, n, wc, rank | ((u64)j << 2));
       t[k] = X;
       prev = X;
       ++k;
@@ -429,6 +477,7 @@ __device__ __forceinline__ int32_t run_at(const Run& x, int i) {
 // out[k - 1] (X when just produced), right neighbour the original token after the pair
 // (out[k + 1], or a where that is the next occurrence's X); input position of occurrence o at
 // output k: k + o.  The changed run is written back with 16-B stores.  Same results as merge_run.
+template <int kProbes>
 __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, const MergeCtx& c, int32_t* s,
                                                int32_t* r, const Run& x, uint32_t L, u64 e, u64 wc, int32_t a,
                                                int32_t b, int32_t X, uint32_t* len, u64* sig) {
@@ -462,7 +511,7 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
       const int32_t prev = ko > 0 ? s[ko * kWlThreads] : 0;  // out[ko - 1]
       const bool has_n = jo + 2 < L;
       const int32_t nx = has_n ? s[(2 + ko) * kWlThreads] : 0;  // out[ko + 1]
-      f |= occurrence(p, h, c, ko > 0, prev, has_n, nx == X ? a : nx, wc, rank | ((u64)jo << 2));
+      f |= occurrence<kProbes>(p, h, c, ko > 0, prev, has_n, nx == X ? a : nx, wc, rank | ((u64)jo << 2));
     }
   }
   *sig = f;
@@ -538,12 +587,15 @@ struct LoopS {
   uint32_t nout, nchg, pool_top, err, scan, filter, nspill, qn, nkeys, nfin;
   uint32_t rd, wr;  // run ints read (length + tokens of every scanned word) / written back (changed words)
   u64 lst_x;        // the words-of list written for X (offset | (count + 1) << 32), for the host
+  u64 last_lst;     // the last merge's X and its words-of list (offset | count << 32), kept in LDS so
+  int32_t last_x;   //   that a merge of the pair the loop just made skips the list lookup (-1: none)
   uint32_t st[4];
   u64 lk[2];  // word list: pool offset, count
   u64 need;   // filter bits the listed words must hold
   u64 occ, t[2];
   u64 t_wait, t_idle, t_undo;  // s_memrealtime: this command's wait began; idle / undo since the last flag
   uint32_t t_rel;               // ticks of the last flag's system release (diagnostic)
+  uint32_t xs[kXs];             // SHRED_WL_STAMPS: phase stamps (ticks after the command) and counts
   // tiebreak=device
   uint32_t sm, snk, snew, status, sel_pos, sover, scompact, sins, serr;
   u64 sel_cnt, dxa, t_rec, t_app, logn;
@@ -750,13 +802,15 @@ __device__ uint32_t finalize_changes(const WlParams& p, DeltaH& h, LoopS& S, u64
 // The merge loop (see the file comment).  One workgroup; command numbers start at p.seq0.
 // kSelf (tiebreak=device): no host commands; the loop selects each merge from the device pair
 // table's frontier (p.sel) and folds the merge's records back into the table.
-template <bool kSelf>
+// kProbes: the LDS delta hash's probe bound (kProbesDefault; 0 and 1 force the HBM spill path).
+template <bool kSelf, int kProbes>
 __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   __shared__ int32_t s_strip[kStrip * kWlThreads];  // [position][lane]: conflict-free per wave
   __shared__ DeltaH s_h;
   __shared__ LoopS S;
   __shared__ u64 s_q[kQ];  // the listed entries that pass the filter, merged densely
   __shared__ SelLds<kSelf> s_f;
+  __shared__ uint16_t s_klist[kDh];  // the merge's delta keys (their hash slots), insertion order
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t tid = threadIdx.x;
   int32_t* const mys = s_strip + tid;
@@ -765,10 +819,23 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     S.t_idle = 0;
     S.t_undo = 0;
     S.t_rel = 0;
+    S.last_x = -1;
+    S.last_lst = 0;
+  }
+  // The delta hash is clean between merges: cleared once here, then every merge clears what it
+  // used once its records are out (the small-merge path only its own slots, by the key list)
+  for (int i = tid; i < kDh; i += kWlThreads) {
+    s_h.key[i] = kEmpty32;
+    s_h.sum[i] = 0;
+    s_h.ft[i] = kEmpty64;
   }
   uint32_t expect = p.seq0;
   uint32_t exit_op = kOpStop;
-  const MergeCtx mc{&S.nspill, &S.nkeys};
+  const MergeCtx mc{&S.nspill, &S.nkeys, s_klist};
+  // the small-merge path (p.fast, exact mode): the last wave writes the records and raises the flag;
+  // it merges words only when a merge lists more than kWlThreads - 64 of them
+  const bool fast = !kSelf && p.fast != 0 && p.fin_max == 0;
+  constexpr int kFlagWave = kWlThreads / 64 - 1;
   // command prefetch (p.prefetch, exact mode): the poller wave (wave 1) reads the next command's
   // granules while the other waves write the current merge's records and its flag, so a command
   // the host already posted is in registers when the loop comes round (a poll is a PCIe round
@@ -871,7 +938,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         else if (S.logn + 4ull * ((u64)p.cap + 2u) > q.log_cap) status = kSelRebuild;  // the log must be applied first
         // only pairs holding a new id are ever inserted: the table's fill is known without it
         // (a merge inserts at most 2 (cap + 1) pairs: (p, X) and (X, n) for every neighbour id)
-        else if ((u64)S.sins + S.newtot + 2ull * ((u64)p.cap + 2u) > q.fill_max) status = kSelRebuild;
+        else if ((u64)S.sins + S.newtot + 2ull * ((u64)p.cap + 2u) > q.fill_max) status = kSelFull;
         else if (S.snk == 0) status = kSelRebuild;  // nothing at or above the threshold is left
         else if (bc < q.min_freq) status = kSelDone;
         S.cmd[0] = status ? kOpStop : kOpMerge;
@@ -950,7 +1017,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     if (wid == 0) {
       const bool undo = op == kOpUnmerge;
       const int32_t M = undo ? X : (a > b ? a : b);
-      const uint32_t given = undo ? 0u : S.cmd[6];  // the host sent M's words-of list: no lookup
+      // the host sent M's words-of list, or M is the loop's last merge (its list in LDS): no lookup
+      const bool recent = !undo && M == S.last_x;
+      const uint32_t given = undo ? 0u : (S.cmd[6] ? S.cmd[6] : recent ? (uint32_t)(S.last_lst >> 32) + 1u : 0u);
+      const uint32_t goff = S.cmd[6] ? S.cmd[7] : (uint32_t)S.last_lst;
       u64 lv64 = 0;
       bool lv = false;
       if (!given && (lane == 16 || lane == 17) && M >= 0 && (uint32_t)M < p.id_cap) {
@@ -965,7 +1035,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         dv = p.dval[(h + (u64)lane) & p.dir_mask];
       }
       const bool has_list = given || ((__ballot(lv) >> 16) & 1ull);
-      const u64 wl = given ? ((u64)S.cmd[7] | ((u64)(given - 1u) << 32)) : __shfl(lv64, 17, 64);
+      const u64 wl = given ? ((u64)goff | ((u64)(given - 1u) << 32)) : __shfl(lv64, 17, 64);
       u64 off = 0, cnt = 0, need = 0;
       bool err = false;
       if (has_list) {
@@ -1018,6 +1088,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.occ = 0;
         S.err = 0;
         S.st[0] = S.st[1] = S.st[2] = S.st[3] = 0;
+        WL_ST(for (int i = 0; i < kXs; ++i) S.xs[i] = 0; S.xs[8] = given ? 1u : 0u;)
         if (err) atomicMax(&p.dstate[kStError], undo ? kErrList : kErrLookup);
         if (!undo && (u64)S.pool_top + cnt > p.pool_cap) {
           S.err = 1;
@@ -1026,13 +1097,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.t[0] = __builtin_amdgcn_s_memrealtime() - t_cmd;
       }
     }
-    if (op == kOpMerge)
-      for (int i = tid; i < kDh; i += kWlThreads) {
-        s_h.key[i] = kEmpty32;
-        s_h.sum[i] = 0;
-        s_h.ft[i] = kEmpty64;
-      }
     __syncthreads();
+    WL_ST(if (tid == 0) S.xs[0] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
     const u64 off = S.lk[0], cnt = S.lk[1];
     const uint32_t top = S.pool_top;
     if (op == kOpUnmerge) {
@@ -1047,6 +1113,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       if (tid == 0 && X >= 0 && (uint32_t)X < p.id_cap) {
         if (off + cnt == (u64)S.pool_top) S.pool_top = (uint32_t)off;  // the guess's list was the last one
         p.lseq[X] = kNoList;
+        if (S.last_x == X) S.last_x = -1;
       }
       if (tid == 0) {
         S.t_idle += t_cmd - S.t_wait;
@@ -1054,6 +1121,151 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       }
       __syncthreads();
       continue;
+    }
+    if (fast && op == kOpMerge && cnt <= (u64)kWlThreads) {
+      // ---- the small-merge path (every late merge: a few hundred listed words, tens changed).  A
+      // lane per listed entry, no queue and no barrier before the merge: entry tid's filter decides
+      // and a passing lane loads its word's run and weight right away (the only hop after the
+      // entry), merges it in registers (merge_regs) and stores it back.  The delta keys are listed
+      // as they enter the LDS hash, so the records phase reads (and clears) only those.  The last
+      // wave writes the records and raises the flag: it issued no word stores (unless more than
+      // kWlThreads - 64 words are listed), so its drain and release wait for the records alone --
+      // the other waves' word-run and pool stores drain at the next command's barrier (the rule
+      // at WlParams::drain; with drain = 1 they drain here).
+      const bool append = S.err == 0;
+      const u64 need = S.need;
+      u64 e = kEmpty64;
+      bool pass = false;
+      if (tid < cnt) {
+        const WEnt v = p.pool[off + tid];
+        e = v.e;
+        pass = (v.sig & need) == need;
+      }
+      uint32_t occ = 0, L = 0, nl = 0;
+      u64 nsig = 0;
+      if (pass) {
+        int32_t* r = p.wtok + (uint32_t)(e >> 32);
+        const Run x = load_run(r);
+        const u64 wc = p.weight[(uint32_t)e];
+        L = (uint32_t)x.v[0].x;
+        nl = L;
+        WL_ST(atomicMax(&S.xs[2], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd)); atomicMax(&S.xs[6], L);
+              if (L > kStripTok) atomicAdd(&S.xs[5], 1u);)
+        if (L >= 2) {
+          if (L <= kStripTok) {
+            occ = merge_regs<kProbes>(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig);
+          } else {
+            occ = merge_run<kProbes>(p, s_h, mc, r + 1, L, e, wc, a, b, X, &nl, &nsig);
+            if (occ) r[0] = (int32_t)nl;
+          }
+        }
+        WL_ST(atomicMax(&S.xs[3], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd)); atomicMax(&S.xs[7], occ);)
+      }
+      const u64 chg = __ballot(occ != 0);
+      if (chg) {  // the changed words become the words of X
+        const int lead = __ffsll((long long)chg) - 1;
+        uint32_t nb = 0;
+        if (lane == lead) nb = atomicAdd(&S.nchg, (uint32_t)__popcll(chg));
+        nb = __shfl(nb, lead, 64);
+        if (occ && append) {
+          WEnt ne;
+          ne.e = e;
+          ne.sig = nsig;
+          p.pool[(u64)top + nb + (uint32_t)__popcll(chg & ((1ull << lane) - 1ull))] = ne;
+        }
+      }
+      if (const u64 sm = __ballot(pass)) {  // statistics: wave sums, one LDS add each per wave
+        const uint32_t w_occ = wave_sum32(occ), w_rd = wave_sum32(pass ? 1u + L : 0u);
+        const uint32_t w_wr = wave_sum32(occ ? 1u + nl : 0u);
+        if (lane == 0) {
+          atomicAdd(&S.occ, (u64)w_occ);
+          atomicAdd(&S.scan, (uint32_t)__popcll(sm));
+          atomicAdd(&S.rd, w_rd);
+          atomicAdd(&S.wr, w_wr);
+        }
+      }
+      // read before the barrier: past it the poller wave may already be waiting for the next command
+      // (it writes S.t_wait there); the flag wave has not written the header yet
+      const u64 t_wait = S.t_wait;
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every delta is in the hash
+      if (drain || S.nspill) __syncthreads();  // spilled deltas' HBM atomics complete (S.nspill is final)
+      WL_ST(if (tid == 0) S.xs[4] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
+      const uint32_t nchg = append ? S.nchg : 0u;
+      if (wid == 0 && lane == 0 && X >= 0 && (uint32_t)X < p.id_cap) {
+        p.lst[X] = (u64)top | ((u64)nchg << 32);
+        p.lseq[X] = seq;
+      }
+      if (wid == kFlagWave) {
+        const WlSlotDev& sd = p.sl[slot & (WordLoop::kSlots - 1)];
+        const u64 t_out = __builtin_amdgcn_s_memrealtime();
+        const uint32_t nk = S.nkeys, nsp = S.nspill;
+        for (uint32_t i = (uint32_t)lane; i < nk; i += 64u) {  // the records, their slots cleared
+          const uint32_t h = s_klist[i];
+          u64* dst = reinterpret_cast<u64*>(sd.recs + i);
+          dst[0] = (u64)s_h.key[h];
+          dst[1] = s_h.sum[h];
+          dst[2] = s_h.ft[h];
+          s_h.key[h] = kEmpty32;
+          s_h.sum[h] = 0;
+          s_h.ft[h] = kEmpty64;
+        }
+        for (uint32_t i = (uint32_t)lane; i < nsp; i += 64u) {  // then the keys spilled to HBM
+          const uint32_t key = p.dlist[i];
+          const u64 sum = atomicExch(&p.dsum[key], 0ull);
+          const u64 ft = atomicExch(&p.dft[key], kEmpty64);
+          u64* dst = reinterpret_cast<u64*>(sd.recs + nk + i);
+          dst[0] = (u64)key;
+          dst[1] = sum;
+          dst[2] = ft;
+        }
+        WL_ST(if (lane == 0) S.xs[10] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
+        if (lane == 0) {
+          S.lst_x = 0;
+          S.last_x = -1;
+          if (X >= 0 && (uint32_t)X < p.id_cap) {
+            S.pool_top = top + nchg;
+            S.lst_x = (u64)top | ((u64)(nchg + 1u) << 32);  // for the host: offset, count + 1
+            S.last_x = X;
+            S.last_lst = (u64)top | ((u64)nchg << 32);
+          }
+          sd.hdr[0] = nk + nsp;
+          sd.hdr[22] = 0u;
+          sd.hdr[23] = nk + nsp;
+          sd.hdr[30] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_out);
+          sd.hdr[2] = (uint32_t)cnt;
+          sd.hdr[3] = S.nchg;
+          u64* h64 = reinterpret_cast<u64*>(sd.hdr);
+          h64[2] = S.occ;
+          h64[3] = (u64)__builtin_amdgcn_s_memrealtime() - t_cmd;
+          h64[4] = S.t[0];
+          h64[5] = t_out - t_cmd;
+          sd.hdr[12] = S.scan;
+          sd.hdr[13] = S.filter;
+          sd.hdr[14] = S.rd;
+          sd.hdr[15] = S.wr;
+          sd.hdr[16] = sd.hdr[17] = sd.hdr[18] = 0u;  // (the queued path's stamps)
+          sd.hdr[19] = nsp;
+          sd.hdr[20] = (uint32_t)(S.t_idle + (t_cmd - t_wait));
+          sd.hdr[21] = (uint32_t)S.t_undo;
+          sd.hdr[31] = S.t_rel;
+          h64[12] = S.lst_x;
+          h64[13] = t_cmd;
+          h64[14] = t_wait;
+          S.t_idle = 0;
+          S.t_undo = 0;
+          const u64 t_r0 = __builtin_amdgcn_s_memrealtime();
+          WL_ST(S.xs[11] = (uint32_t)(t_r0 - t_cmd); for (int i = 0; i < kXs; ++i) sd.hdr[32 + i] = S.xs[i];)
+          // one system-scope release: this wave's record and header stores, then the flag
+          __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          S.t_rel = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_r0);
+        }
+      } else if (pfon && wid == poll_wave) {  // the next command's granules, in flight meanwhile
+        pre_v = lane < kCmdGranules
+                    ? __hip_atomic_load(p.ring[expect % kRing].g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                    : 0ull;
+        pre_ok = true;
+      }
+      continue;  // (the next command's barrier orders the flag wave's LDS writes before any use)
     }
     // ---- the merge over the listed words; changed words become the words of X.  Each round a
     // lane loads kB pool entries (coalesced) and queues in LDS those whose filter holds the
@@ -1097,6 +1309,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       __syncthreads();  // every thread has read qn before the next round queues more
       const bool last = base + (u64)kWlThreads * kB >= cnt;
       if (qn < (uint32_t)kWlThreads && !last) continue;
+      WL_ST(if (tid == 0) { if (!S.xs[1]) S.xs[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd); ++S.xs[9]; })
       // A lane's words one after another, the next word's run and weight loading while this one
       // merges (the compiler's waits count the loads; big merges queue up to 9 words a lane)
       const uint32_t qend = ((qn + kWlThreads - 1) / kWlThreads) * kWlThreads;
@@ -1126,16 +1339,19 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           int32_t* r = p.wtok + (uint32_t)(e >> 32);
           const uint32_t L = (uint32_t)x.v[0].x;
           uint32_t nl = L;
+          WL_ST(atomicMax(&S.xs[2], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd)); atomicMax(&S.xs[6], L);
+                if (L > kStripTok) atomicAdd(&S.xs[5], 1u);)
           if (qi == 0 && base == 0) S.st[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
           ++my_scan;
           if (L >= 2) {
             if (L <= kStripTok) {
-              occ = merge_regs(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig);
+              occ = merge_regs<kProbes>(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig);
             } else {
-              occ = merge_run(p, s_h, mc, r + 1, L, e, wc, a, b, X, &nl, &nsig);
+              occ = merge_run<kProbes>(p, s_h, mc, r + 1, L, e, wc, a, b, X, &nl, &nsig);
               if (occ) r[0] = (int32_t)nl;
             }
           }
+          WL_ST(atomicMax(&S.xs[3], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd)); atomicMax(&S.xs[7], occ);)
           my_occ += occ;
           my_rd += 1u + L;
           my_wr += occ ? 1u + nl : 0u;
@@ -1161,12 +1377,19 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       if (tid == 0) S.qn = 0;
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    if (my_occ) atomicAdd(&S.occ, (u64)my_occ);
-    if (my_scan) atomicAdd(&S.scan, my_scan);
-    if (my_rd) atomicAdd(&S.rd, my_rd);
-    if (my_wr) atomicAdd(&S.wr, my_wr);
+    {  // statistics: wave sums, one LDS add each per wave
+      const uint32_t w_occ = wave_sum32(my_occ), w_scan = wave_sum32(my_scan);
+      const uint32_t w_rd = wave_sum32(my_rd), w_wr = wave_sum32(my_wr);
+      if (lane == 0 && w_scan) {
+        atomicAdd(&S.occ, (u64)w_occ);
+        atomicAdd(&S.scan, w_scan);
+        atomicAdd(&S.rd, w_rd);
+        atomicAdd(&S.wr, w_wr);
+      }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (drain || S.nspill) __syncthreads();  // (uniform: S.nspill is final after the barrier above)
+    WL_ST(if (tid == 0) S.xs[4] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
     const uint32_t nchg = append ? S.nchg : 0u;
     if constexpr (kSelf) {
       // ---- tiebreak=device: the records change the pair table (atomics nobody waits for) and,
@@ -1176,10 +1399,13 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       const SelParams& q = p.sel;
       const u64 t_tab = __builtin_amdgcn_s_memrealtime();
       if (tid == 0) {
+        S.last_x = -1;
         if (X >= 0 && (uint32_t)X < p.id_cap) {
           p.lst[X] = (u64)top | ((u64)nchg << 32);
           p.lseq[X] = seq;
           S.pool_top = top + nchg;
+          S.last_x = X;
+          S.last_lst = (u64)top | ((u64)nchg << 32);
         }
         S.snew = 0;
         S.dxa = 0;
@@ -1189,7 +1415,12 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       const SelNew nw{s_q, s_q + kNewCap, &S.snew, kNewCap, &S.dxa, &S.sover, q.log + 2 * S.logn, &S.lognew};
       for (int i = tid; i < kDh; i += kWlThreads) {
         const uint32_t key = s_h.key[i];
-        if (key != kEmpty32) sel_record(q, s_f, nw, p.unk, key, s_h.sum[i], a, b, X);
+        if (key != kEmpty32) {
+          sel_record(q, s_f, nw, p.unk, key, s_h.sum[i], a, b, X);
+          s_h.key[i] = kEmpty32;  // the hash is clean between merges
+          s_h.sum[i] = 0;
+          s_h.ft[i] = kEmpty64;
+        }
       }
       const uint32_t nsp = S.nspill;
       for (uint32_t i = tid; i < nsp; i += kWlThreads) {
@@ -1320,6 +1551,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.pool_top = top + nchg;
         S.lst_x = (u64)top | ((u64)(nchg + 1u) << 32);  // for the host: offset, count + 1
       }
+      S.last_x = S.lst_x ? X : -1;
+      S.last_lst = (u64)top | ((u64)nchg << 32);
     }
     const uint32_t nrec = S.nkeys + S.nspill;
     const bool fin = p.fin_max != 0 && nrec <= p.fin_max && nrec <= kFinMax;
@@ -1353,6 +1586,9 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         dst[0] = (u64)key;
         dst[1] = s_h.sum[i];
         dst[2] = s_h.ft[i];
+        s_h.key[i] = kEmpty32;  // the hash is clean between merges
+        s_h.sum[i] = 0;
+        s_h.ft[i] = kEmpty64;
       }
       const uint32_t nsp = S.nspill;  // complete: every delta was added before the barrier above
       for (uint32_t i = rt; i < nsp; i += rs) {
@@ -1369,6 +1605,13 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     }
     // LDS only: the poller's prefetch stays in flight (every other wave drained its stores above)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    WL_ST(if (tid == 0) S.xs[10] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
+    if (fin)  // K4 used the hash keys as bucket counters: clean it whole (ordered by the next barrier)
+      for (int i = tid; i < kDh; i += kWlThreads) {
+        s_h.key[i] = kEmpty32;
+        s_h.sum[i] = 0;
+        s_h.ft[i] = kEmpty64;
+      }
     if (tid == 0) {
       sd.hdr[0] = fin ? S.nfin : S.nout;
       sd.hdr[22] = fin ? 1u : 0u;  // 1: ordered changes (finalize_changes), else raw records
@@ -1400,6 +1643,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       S.t_undo = 0;
       // one system-scope release (L2 write-back of the records and header, then the flag)
       const u64 t_r0 = __builtin_amdgcn_s_memrealtime();
+      WL_ST(S.xs[11] = (uint32_t)(t_r0 - t_cmd); for (int i = 0; i < kXs; ++i) sd.hdr[32 + i] = S.xs[i];)
       __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       S.t_rel = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_r0);
     }
@@ -1683,6 +1927,8 @@ WordLoop::WordLoop(int ordinal, void* stream, int32_t unk_id) : ordinal_(ordinal
   if (const char* e = std::getenv("SHREDWORD_WL_FINALIZE")) fin_max_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_WL_PREFETCH")) prefetch_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_WL_DRAIN")) drain_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SHREDWORD_WL_PROBES")) probes_ = std::atoi(e);
+  if (const char* e = std::getenv("SHREDWORD_WL_FAST")) fast_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_SELECT_REPORT")) sel_report_ = std::atoi(e) != 0;
   for (auto& e : ev_) {
     hipEvent_t ev;
@@ -1995,8 +2241,8 @@ void WordLoop::ensure_slots(uint32_t cap) {
     WL_OK(hipHostMalloc((void**)&sl.host_recs, (size_t)rec_cap * sizeof(DeltaRecord), pin));
     WL_OK(hipHostGetDevicePointer(&sl.dev_recs, sl.host_recs, 0));
     if (!sl.host_hdr) {
-      WL_OK(hipHostMalloc((void**)&sl.host_hdr, 128, pin));
-      std::memset(sl.host_hdr, 0, 128);
+      WL_OK(hipHostMalloc((void**)&sl.host_hdr, 256, pin));
+      std::memset(sl.host_hdr, 0, 256);
       WL_OK(hipHostGetDevicePointer(&sl.dev_hdr, sl.host_hdr, 0));
     }
     sl.rec_cap = rec_cap;
@@ -2070,6 +2316,7 @@ void WordLoop::launch(uint32_t seq0) {
   p.fin_max = fin_max_;
   p.prefetch = prefetch_ ? 1u : 0u;
   p.drain = drain_ ? 1u : 0u;
+  p.fast = fast_ ? 1u : 0u;
   for (int k = 0; k < kSlots; ++k) {
     p.sl[k].recs = static_cast<DeltaRecord*>(slot_[k].dev_recs);
     p.sl[k].hdr = static_cast<uint32_t*>(slot_[k].dev_hdr);
@@ -2077,7 +2324,11 @@ void WordLoop::launch(uint32_t seq0) {
   }
   status_[0] = 0;
   WL_OK(hipEventRecord((hipEvent_t)ev_[0], S(stream_)));
-  k_word_loop<false><<<1, kWlThreads, 0, S(stream_)>>>(p);
+  switch (probes_) {  // SHREDWORD_WL_PROBES (tests): 0 / 1 force the delta hash's HBM spill path
+    case 0: k_word_loop<false, 0><<<1, kWlThreads, 0, S(stream_)>>>(p); break;
+    case 1: k_word_loop<false, 1><<<1, kWlThreads, 0, S(stream_)>>>(p); break;
+    default: k_word_loop<false, kProbesDefault><<<1, kWlThreads, 0, S(stream_)>>>(p); break;
+  }
   WL_OK(hipGetLastError());
   WL_OK(hipEventRecord((hipEvent_t)ev_[1], S(stream_)));
   running_ = true;
@@ -2186,7 +2437,10 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
                                         // absolute clocks for a timeline: host 10 ns units since the
                                         // loop was made, device ticks (100 MHz), low 32 bits
                                         (uint32_t)(1e8 * (pp.t_post - t_epoch_)), (uint32_t)(1e8 * (t_seen - t_epoch_)),
-                                        (uint32_t)h64[13], (uint32_t)h64[14]};
+                                        (uint32_t)h64[13], (uint32_t)h64[14],
+                                        // SHRED_WL_STAMPS builds: phase stamps and counts (0 otherwise)
+                                        h[32], h[33], h[34], h[35], h[36], h[37], h[38], h[39], h[40], h[41],
+                                        h[42], h[43]};
     trace_.insert(trace_.end(), rec, rec + kTraceFields);
   }
   if (n > sl.rec_cap) fatal("k_word_loop: record overflow");
@@ -2466,10 +2720,15 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
     p.unk = unk_;
     p.sel = q;
     dirty_ = true;
+    int stalls = 0;
     for (;;) {
       p.seq0 = seq_ + 1;
       WL_OK(hipEventRecord((hipEvent_t)ev_[0], s));
-      k_word_loop<true><<<1, kWlThreads, 0, s>>>(p);
+      switch (probes_) {
+        case 0: k_word_loop<true, 0><<<1, kWlThreads, 0, s>>>(p); break;
+        case 1: k_word_loop<true, 1><<<1, kWlThreads, 0, s>>>(p); break;
+        default: k_word_loop<true, kProbesDefault><<<1, kWlThreads, 0, s>>>(p); break;
+      }
       WL_OK(hipGetLastError());
       WL_OK(hipEventRecord((hipEvent_t)ev_[1], s));
       WL_OK(hipStreamSynchronize(s));
@@ -2508,9 +2767,16 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
       if (st[kSelErr]) fatal("tiebreak=device: a pair-table update overran the probe bound");
       const uint32_t status = st[kSelStatus];
       if (status == kSelDone) break;
-      // the table past 3/4 full, or without room for one more merge's new pairs (the launch then
-      // ended before merging anything): 4x, live pairs moved
-      if (st[kSelIns] > q.fill_max || (status == kSelRebuild && !progressed)) {
+      // a rebuild that merged nothing is not a full table: only kSelFull and the
+      // inserts past the bound grow it.  Right after a rebuild the frontier holds entries at or
+      // above the threshold, so two such launches in a row would be a loop that cannot progress.
+      if (status == kSelRebuild && !progressed) {
+        if (++stalls > 1) fatal("tiebreak=device: two launches in a row ended for a rebuild without a merge");
+      } else {
+        stalls = 0;
+      }
+      // the table past 3/4 full, or without room for one more merge's new pairs: 4x, live pairs moved
+      if (st[kSelIns] > q.fill_max || status == kSelFull) {
         size_t acc = 0;
         PairCount* dp = wl_alloc<PairCount>(pcap_, &acc);
         uint32_t* dn = wl_alloc<uint32_t>(1, &acc);

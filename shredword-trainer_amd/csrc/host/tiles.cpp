@@ -255,7 +255,12 @@ void TileIndex::set_tiles_bits(int32_t id, const uint32_t* words, size_t n) {
   const size_t nw = (ntiles_ + 31) / 32;
   if ((uint64_t)n * 32 > ntiles_) {  // dense: the bitmap as is (two u32 words per u64, low first)
     s.bits.assign((ntiles_ + 63) / 64, 0);
-    for (size_t w = 0; w < nw; ++w) s.bits[w >> 1] |= (uint64_t)words[w] << (32 * (w & 1));
+    size_t pop = 0;  // the set's size is the bitmap's popcount, not the caller's entry count
+    for (size_t w = 0; w < nw; ++w) {
+      s.bits[w >> 1] |= (uint64_t)words[w] << (32 * (w & 1));
+      pop += (size_t)__builtin_popcount(words[w]);
+    }
+    s.size = pop;
   } else {
     s.list.reserve(n);
     for (size_t w = 0; w < nw; ++w)

@@ -510,6 +510,8 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
       s->index_dev_out_us = w.dev_out_us;
       s->index_dev_fin_us = w.dev_fin_us;
       s->index_fin_records = w.fin_records;
+      s->index_spill_merges = w.spill_merges;
+      s->index_spill_keys = w.spill_keys;
       s->index_switch_merge = t->dev->switch_merge();
       s->index_switch_ms = t->dev->switch_ms();
       const SelectStats& q = wl->select_stats();

@@ -167,7 +167,7 @@ class WordLoop {
   // the host ns from posting this merge to seeing its flag; then absolute clocks: host post and
   // flag seen (10 ns since the loop was made), device command seen and wait begun (100 MHz
   // ticks), low 32 bits each.
-  static constexpr int kTraceFields = 19;
+  static constexpr int kTraceFields = 31;
   const std::vector<uint32_t>& trace() const { return trace_; }
   void set_timing(bool on) { timing_ = on; }
   size_t device_bytes() const { return bytes_; }
@@ -253,6 +253,11 @@ class WordLoop {
   bool prefetch_ = true;
   // SHREDWORD_WL_DRAIN=1: every merge barrier drains the stores (the round-4 barriers)
   bool drain_ = false;
+  // SHREDWORD_WL_PROBES=0 / 1 (tests): the kernel instance whose LDS delta hash spills every key /
+  // most keys to the HBM tables (a template argument: the default kernel pays nothing for it)
+  int probes_ = 32;
+  // the small-merge path for merges listing <= 512 words (SHREDWORD_WL_FAST=0: the queued path only)
+  bool fast_ = true;
   bool last_changes_ = false;
   std::vector<Post> posted_;
   // tiebreak=device: pair table, frontier, state (see word_loop.hip SelParams)

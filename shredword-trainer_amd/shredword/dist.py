@@ -44,7 +44,10 @@ def host_load_gather(group=None, fallback=None, state=None):
     default gloo group) is used when the collective on `group` raises on ANY rank: after every
     attempt the ranks agree over `fallback` (all_reduce MAX of a failure flag) and fall back all
     together, for the rest of the load (state["fell_back"] = the error, when a dict is given).
-    The returned callback
+    Before the first attempt the ranks also agree over `fallback` on whether `group` came up on
+    every rank, so a rank whose group is missing never leaves the others blocked inside its
+    collective.  Not covered: a collective on `group` that hangs after it started on every rank
+    (that waits for the process group's own timeout).  The returned callback
     keeps its last result alive until its next call, as the C ABI requires."""
     import torch.distributed as dist
 
@@ -66,6 +69,20 @@ def host_load_gather(group=None, fallback=None, state=None):
         try:
             mine = ctypes.string_at(send, nbytes) if nbytes else b""
             parts = None
+            if fallback is not None and "checked" not in keep:
+                keep["checked"] = True
+                try:  # the group exists here and spans the same ranks as the fallback
+                    up = dist.get_world_size(group) == dist.get_world_size(fallback)
+                except Exception:  # noqa: BLE001
+                    up = False
+                if agree_failed(not up):
+                    import sys
+                    why = "the gather's group did not come up on every rank"
+                    print(f"[WARNING]\t host_load_gather: {why}; every rank gathers over the fallback group",
+                          file=sys.stderr)
+                    keep["fell_back"] = True
+                    if state is not None:
+                        state["fell_back"] = why
             if not keep.get("fell_back"):
                 err = None
                 try:

@@ -58,6 +58,17 @@ def main():
                      "stamps_us_mean": [float(v[s].mean() / 1e3) for v in (s0, s1, s2, s3)],
                      "dev_idle_us_mean": float(idle[s].mean() / 1e3), "dev_undo_us_mean": float(undo[s].mean() / 1e3),
                      "host_post_to_flag_us_mean": float(hflag[s].mean() / 1e3)})
+        if tr.shape[1] >= 31 and tr[s, 19:31].any():  # a -DSHRED_WL_STAMPS build
+            xs = tr[s, 19:31]
+            names = ["hash_cleared", "queue_ready", "last_run_landed", "last_word_merged", "merge_phase_end",
+                     "long_words", "max_len", "max_occ", "list_given", "queue_rounds", "records_stored",
+                     "before_release"]
+            ticks = {0, 1, 2, 3, 4, 10, 11}
+            rows[-1]["stamps"] = {nm: (float(xs[:, i].mean() / 100.0) if i in ticks else float(xs[:, i].mean()))
+                                  for i, nm in enumerate(names)}
+            rows[-1]["stamps_p50"] = {nm: float(np.median(xs[:, i]) / 100.0) for i, nm in enumerate(names)
+                                      if i in ticks}
+            rows[-1]["release_us_mean"] = float((dev[s] / 1e3 - xs[:, 11] / 100.0).mean())
     print(json.dumps({"config": args.config, "merges": int(n), "train_s": st["train_seconds"],
                       "merges_per_s": n / st["train_seconds"], "dev_s_total": float(dev.sum() / 1e9),
                       "host": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},

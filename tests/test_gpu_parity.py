@@ -98,6 +98,36 @@ def test_index_loop_changes_on_device_match_reference(name, fin, case_corpus, tm
         assert 0 < st["index_finalized"] < st["index_merges"] + st["index_undos"], st
 
 
+@pytest.mark.parametrize("probes", [0, 1])
+@pytest.mark.parametrize("name", [n for n in API_CASES if n not in DEEP])
+def test_index_loop_spilled_deltas_match_reference(name, probes, case_corpus, tmp_path, monkeypatch):
+    """Delta keys pushed out of k_word_loop's LDS hash into the HBM spill tables: the kernel
+    instance with the LDS probe bound 0 (every key spills) or 1 (most of a busy merge's) -- a
+    template argument (SHREDWORD_WL_PROBES selects the instance), so the default kernel (32, which
+    spills one or two keys in C3's 29,000 indexed merges) pays nothing for it.  The records phase
+    reads the spilled keys back after the merge's store drain, which only spilling merges keep
+    (word_loop.hip: `drain || S.nspill`).  Same bytes."""
+    case, corpus = case_corpus(name)
+    monkeypatch.setenv("SHREDWORD_WL_PROBES", str(probes))
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, hybrid=0))
+    if probes == 0 and case["merges"] > 0:
+        assert st["index_spill_keys"] > 0 and st["index_spill_merges"] > 0, st
+
+
+@pytest.mark.parametrize("drain", [0, 1])
+@pytest.mark.parametrize("name", ["small_v300", "adv_unk3_cov09", "ascii1m_v3000_mpf2", "mixed2m_v4000"])
+def test_index_loop_store_drain_modes_match_reference(name, drain, case_corpus, tmp_path, monkeypatch):
+    """k_word_loop's merge-end barriers: with SHREDWORD_WL_DRAIN=0 (the default) they wait on LDS
+    only and the word-run / pool stores drain at the next command's barrier, which is sound only
+    because nothing reads wtok, pool or lst before it (see WlParams::drain); =1 drains every
+    wave's stores at the merge's end (the round-4 barriers).  Both give the reference's bytes
+    (ADVICE r05)."""
+    case, corpus = case_corpus(name)
+    monkeypatch.setenv("SHREDWORD_WL_DRAIN", str(drain))
+    _check(case, _train(case, corpus, tmp_path, "types", hybrid=0))
+
+
 @pytest.mark.parametrize("path", ["hybrid", "index", "resident", "launch", "stream"])
 @pytest.mark.parametrize("name", API_CASES)
 def test_argmax_verifier(name, path, case_corpus, tmp_path):

@@ -135,3 +135,16 @@ def test_tiebreak_device_pair_table_grows(name, case_corpus, tmp_path, monkeypat
     n2, m2, v2, t2, st2 = _train(case, corpus, tmp_path, "small")
     assert (n1, m1, v1, t1) == (n2, m2, v2, t2)
     assert st2["sel_table_grows"] >= 1 and st1["sel_table_grows"] == 0
+
+
+@pytest.mark.parametrize("probes", [0, 1])
+@pytest.mark.parametrize("name", ["adv_unk3_cov09", "ascii1m_v3000_mpf2", "mixed2m_v4000"])
+def test_tiebreak_device_spilled_deltas(name, probes, case_corpus, tmp_path, monkeypatch):
+    """Delta keys pushed out of k_word_loop<true>'s LDS hash into the HBM spill tables (the
+    kernel instance with probe bound 0 or 1, SHREDWORD_WL_PROBES): the table and frontier updates
+    read them back after the merge's drain; the same files as the default instance."""
+    case, corpus = case_corpus(name)
+    n1, m1, v1, t1, _ = _train(case, corpus, tmp_path, "lds")
+    monkeypatch.setenv("SHREDWORD_WL_PROBES", str(probes))
+    n2, m2, v2, t2, _ = _train(case, corpus, tmp_path, "spill")
+    assert (n1, m1, v1, t1) == (n2, m2, v2, t2)
