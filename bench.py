@@ -415,35 +415,61 @@ PMC_NOTE = ("HBM bytes per k_merge launch from rocprofv3 --pmc FETCH_SIZE / WRIT
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def pmc_source(cfg_name, layout, kernel):
-    """The committed PMC summary pmc_traffic() reads for this kernel (newest round first)."""
+def _pmc_files(cfg_name):
+    """The committed PMC summaries of this config, newest first: the round number of the file name
+    (rNN_...), then the name (r05_final_c3 before r05_c3).  A summary holds every kernel of its
+    profiled bench run (both layouts: the K1 stream leg runs in the same command)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(HERE, "profiles", f"*_{cfg_name}_{layout}*_pmc_traffic.json")), reverse=True):
-        try:
-            if kernel in json.load(open(path))["kernels"]:
-                return ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (FETCH doubled for gfx950 16-B reads): "
-                        + os.path.relpath(path, HERE))
-        except (OSError, ValueError, KeyError):
-            continue
-    return None
+    import re
+    out = []
+    for path in glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")):
+        name = os.path.basename(path)
+        m = re.match(r"r(\d+)_", name)
+        if m and f"_{cfg_name}_" in name:
+            out.append((int(m.group(1)), name, path))
+    return [p for _r, _n, p in sorted(out, reverse=True)]
 
 
-def pmc_traffic(cfg_name, layout, kernel=None, all_launches=False):
-    """Measured HBM bytes per launch of `kernel` (default k_merge) for this workload, from the
-    committed PMC summaries (profiles/*_<config>_<layout>*_pmc_traffic.json).  all_launches: the
-    sum over the profiled run's launches (the load's segmented count: one load = all of them)."""
-    import glob
-    if kernel is None:
-        kernel = "k_merge<true>" if layout == "types" else "k_merge<false>"
-    for path in sorted(glob.glob(os.path.join(HERE, "profiles", f"*_{cfg_name}_{layout}*_pmc_traffic.json")), reverse=True):
+def _pmc_entry(cfg_name, kernel):
+    """(summary path, kernel entry) of the newest summary holding `kernel` (a name or a tuple of
+    names, first match wins within a file), or (None, None)."""
+    names = (kernel,) if isinstance(kernel, str) else tuple(kernel)
+    for path in _pmc_files(cfg_name):
         try:
             k = json.load(open(path))["kernels"]
-            ent = k.get(kernel)
-            if ent:
-                return ent["hbm_bytes_per_launch"] * (ent.get("launches", 1) if all_launches else 1)
         except (OSError, ValueError, KeyError):
             continue
-    return None
+        for n in names:
+            if n.endswith("*"):  # any template instance (one per profiled run)
+                hit = [v for kk, v in sorted(k.items()) if kk.startswith(n[:-1]) and v]
+                if hit:
+                    return path, hit[0]
+            elif k.get(n):
+                return path, k[n]
+    return None, None
+
+
+def pmc_source(cfg_name, layout, kernel):
+    """The committed PMC summary pmc_traffic() reads for this kernel (the newest holding it)."""
+    path, _ent = _pmc_entry(cfg_name, kernel)
+    if path is None:
+        return None
+    return ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (FETCH doubled for gfx950 16-B reads): "
+            + os.path.relpath(path, HERE))
+
+
+def pmc_traffic(cfg_name, layout, kernel=None, all_launches=False, raw=False):
+    """Measured HBM bytes per launch of `kernel` (default k_merge) for this workload, from the
+    newest committed PMC summary holding it (profiles/rNN_*<config>*_pmc_traffic.json).
+    all_launches: the sum over the profiled run's launches (the load's segmented count: one load =
+    all of them).  raw: FETCH_SIZE as counted (no x2), the lower bound for probe/atomic reads."""
+    if kernel is None:
+        kernel = "k_merge<true>" if layout == "types" else "k_merge<false>"
+    _path, ent = _pmc_entry(cfg_name, kernel)
+    if not ent:
+        return None
+    v = ent["hbm_bytes_per_launch_fetch_raw"] if raw else ent["hbm_bytes_per_launch"]
+    return v * (ent.get("launches", 1) if all_launches else 1)
 
 
 def pair_count_leg(cfg, path, reps, device=0, layout="stream", dist=None, shard=False):
@@ -580,10 +606,8 @@ def merge_loop_report(st, merges, elapsed, args):
             # K3: the dirty tiles a merge rewrites, read + written (4 B a token each way)
             "k3_dirty_tile_bytes_per_merge": st.get("resident_k3_bytes", 0.0) / res_n,
             "achieved_GBps": gbps, "frac_of_hbm_peak": gbps / HBM_PEAK_GBS if gbps else None,
-            "traffic_bytes_per_launch": (pmc_traffic(args.config, args.layout, "k_resident<true>")
-                                         or pmc_traffic(args.config, args.layout, "k_resident")),
-            "traffic_source": (pmc_source(args.config, args.layout, "k_resident<true>")
-                               or pmc_source(args.config, args.layout, "k_resident")),
+            "traffic_bytes_per_launch": pmc_traffic(args.config, args.layout, "k_resident*"),
+            "traffic_source": pmc_source(args.config, args.layout, "k_resident*"),
             "dispatch_to_flag_us": st.get("resident_latency_us"),
         }
     if idx_n:
@@ -593,6 +617,10 @@ def merge_loop_report(st, merges, elapsed, args):
         ms = st["index_ms"]
         gbps = b / (ms * 1e-3) / 1e9 if ms > 0 else None
         busy = st["index_dev_us"]
+        wl_names = ("k_word_loop<false, 32>", "k_word_loop<false>")
+        wl_traffic = pmc_traffic(args.config, args.layout, wl_names)
+        wl_raw = pmc_traffic(args.config, args.layout, wl_names, raw=True)
+        per_launch_alg = b / max(1, st["index_launches"])
         out["index"] = {
             "kernel": "k_word_loop (indexed persistent loop, one workgroup: word lists, filter, register merge, "
                       "neighbour deltas, in-place compaction)",
@@ -606,6 +634,12 @@ def merge_loop_report(st, merges, elapsed, args):
                 "pool_entries_appended": 16.0 * st["index_changed"] / idx_n,
                 "records_to_host": 24.0 * st["index_records"] / idx_n},
             "achieved_GBps": gbps, "frac_of_hbm_peak": gbps / HBM_PEAK_GBS if gbps else None,
+            # PMC of the profiled run's k_word_loop launch (one launch per train()), against this
+            # step's algorithmic bytes per launch; the doubled FETCH is the upper bound, raw the lower
+            "traffic_bytes_per_launch": wl_traffic, "traffic_bytes_per_launch_fetch_raw": wl_raw,
+            "traffic_x_algorithmic": (wl_traffic / per_launch_alg) if wl_traffic else None,
+            "traffic_x_algorithmic_fetch_raw": (wl_raw / per_launch_alg) if wl_raw else None,
+            "traffic_source": pmc_source(args.config, args.layout, wl_names),
             "device_busy_us_per_merge": busy / idx_n,
             "achieved_GBps_while_busy": b / (busy * 1e-6) / 1e9 if busy > 0 else None,
             "words_listed_per_merge": st["index_candidates"] / idx_n,
@@ -928,6 +962,17 @@ def main():
             device_leg["ratio_to_exact_same_run"] = (dm / de) / (merges / elapsed)
         except Exception as e:  # the exact line stands on its own
             device_leg = {"error": repr(e)}
+    # a second load of the same file (untimed, one rank): the step's load above is the first of this
+    # process -- the first after the corpus was generated when gen_s > 0, with the file's page-cache
+    # pages fresh -- and later loads (the pinned ring kept, pages warm) are faster
+    later_load_s = None
+    if world == 1:
+        try:
+            t1 = time.time()
+            t.load_corpus(path)
+            later_load_s = time.time() - t1
+        except Exception:  # noqa: BLE001 (the line stands without it)
+            later_load_s = None
     # the CPU baseline starts only now: the timed steps ran with the host to themselves
     cpu_h = None
     if world == 1 and not args.no_cpu_baseline:
@@ -1006,6 +1051,8 @@ def main():
             "load": {"kernel": "k_word_count (one pass, LDS-staged tiles, byte-exact in-pass verification)",
                      "algorithmic_bytes": cfg["bytes"],
                      "load_s_max_over_ranks": load_s_max, "load_s_rank0": load_s,
+                     "first_load_s": load_s, "first_load_after_generation": gen_s > 0,
+                     "later_load_s": later_load_s,
                      "bytes_per_rank": cfg["bytes"] / world if one_job else cfg["bytes"],
                      "traffic_bytes": pmc_traffic(args.config, args.layout, "k_word_count", all_launches=True),
                      "traffic_source": pmc_source(args.config, args.layout, "k_word_count"),

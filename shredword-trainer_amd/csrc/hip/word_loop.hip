@@ -67,7 +67,16 @@ constexpr int kQ = kWlThreads * kB + kWlThreads;
 #else
 #define WL_ST(...)
 #endif
-constexpr int kXs = 12;  // LDS queue of filtered entries (a round + a remainder)
+constexpr int kXs = 12;
+// stamps build: wave 0's clock (ticks after t0) into xs[i], written by its first active lane (a
+// scalar clock read and one LDS store: no per-lane atomics, which would cost more than the stamped work)
+__device__ __forceinline__ void wl_stamp(uint32_t* xs, int i, unsigned long long t0) {
+#ifdef SHRED_WL_STAMPS
+  const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x >> 6) == 0 && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1))
+    xs[i] = (uint32_t)(now - t0);
+#endif
+}  // LDS queue of filtered entries (a round + a remainder)
 constexpr uint32_t kDeltaBucketsDev = 1024;  // the reference's FREQ_CHANGE_BUCKETS (bpe.cpp:16)
 constexpr uint32_t kRing = 64;          // command ring entries
 constexpr uint32_t kOpMerge = 1, kOpStop = 2, kOpTimeout = 3, kOpUnmerge = 4;
@@ -332,7 +341,7 @@ struct DeltaH {
 struct MergeCtx {
   uint32_t* nspill;  // delta keys spilled past the LDS hash
   uint32_t* nkeys;   // delta keys in the LDS hash
-  uint16_t* klist;   // their slots, in insertion order (the small-merge path's records and clear)
+  uint32_t* kbits;   // their slots as a bitmap (kDh bits: the small-merge path's records and clear)
 };
 
 // Neighbour deltas (reference freq_change_add, bpe.cpp:274-290): Σ weight and min first touch
@@ -351,6 +360,16 @@ constexpr int kProbesDefault = 32;
 // as a scalar.  Call it with every lane active (0 from lanes that add nothing).  A per-lane
 // atomicAdd on one LDS word instead compiles to a loop over the active lanes (the compiler's
 // iterative atomic combine: ~7 scalar instructions a lane), microseconds a merge at 64 lanes.
+// Inclusive prefix sum of a u32 over the wave (same DPP steps; every lane active).
+__device__ __forceinline__ uint32_t wave_scan32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
+}
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
@@ -378,16 +397,9 @@ __device__ __forceinline__ u64 occurrence(const WlParams& p, DeltaH& h, const Me
     for (int k = 0; k < 4; ++k) prv[k] = pend[k] ? atomicCAS(&h.key[slot[k]], kEmpty32, key[k]) : 0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      {  // a key new to the hash joins the key list: one counter add per wave (ballot + rank)
-        const bool fresh = pend[k] && prv[k] == kEmpty32;
-        const u64 fm = __ballot(fresh);
-        if (fm) {
-          const int lead = __ffsll((long long)fm) - 1;
-          uint32_t base = 0;
-          if ((int)(threadIdx.x & 63) == lead) base = atomicAdd(c.nkeys, (uint32_t)__popcll(fm));
-          base = (uint32_t)__builtin_amdgcn_readlane((int)base, lead);
-          if (fresh) c.klist[base + (uint32_t)__popcll(fm & ((1ull << (threadIdx.x & 63)) - 1ull))] = (uint16_t)slot[k];
-        }
+      if (pend[k] && prv[k] == kEmpty32) {  // a key new to the hash: its slot's bit (no return values)
+        atomicOr(&c.kbits[slot[k] >> 5], 1u << (slot[k] & 31u));
+        atomicAdd(c.nkeys, 1u);
       }
       if (!pend[k]) continue;
       if (prv[k] == kEmpty32 || prv[k] == key[k]) {
@@ -480,7 +492,8 @@ __device__ __forceinline__ int32_t run_at(const Run& x, int i) {
 template <int kProbes>
 __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, const MergeCtx& c, int32_t* s,
                                                int32_t* r, const Run& x, uint32_t L, u64 e, u64 wc, int32_t a,
-                                               int32_t b, int32_t X, uint32_t* len, u64* sig) {
+                                               int32_t b, int32_t X, uint32_t* len, u64* sig, uint32_t* xs = nullptr,
+                                               u64 t0 = 0) {
   uint32_t k = 0, xm = 0;
   bool skip = false;
 #pragma unroll
@@ -495,6 +508,7 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
     k += emit ? 1u : 0u;
     skip = m;
   }
+  if (xs) wl_stamp(xs, 4, t0);  // (stamps build) the walk done
   *len = k;
   *sig = 0;
   if (!xm) return 0;
@@ -514,20 +528,24 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
       f |= occurrence<kProbes>(p, h, c, ko > 0, prev, has_n, nx == X ? a : nx, wc, rank | ((u64)jo << 2));
     }
   }
+  if (xs) wl_stamp(xs, 5, t0);  // the occurrences' deltas issued
   *sig = f;
   // the run [length][k tokens] from the first 16-B group that changed
   s[0] = (int32_t)k;
   int4* r4 = reinterpret_cast<int4*>(r);
   const uint32_t q0 = (uint32_t)__ffs(xm) >> 2;  // (1 + first X position) / 4
-  for (uint32_t q = 0; q <= (k >> 2); ++q) {
-    if (q != 0 && q < q0) continue;
-    int4 v;
-    v.x = s[(4 * q + 0) * kWlThreads];
-    v.y = s[(4 * q + 1) * kWlThreads];
-    v.z = s[(4 * q + 2) * kWlThreads];
-    v.w = s[(4 * q + 3) * kWlThreads];
-    r4[q] = v;
+  int4 v[kStripV];  // every group read at once (one LDS wait), the changed ones stored
+#pragma unroll
+  for (int q = 0; q < kStripV; ++q) {
+    v[q].x = s[(4 * q + 0) * kWlThreads];
+    v[q].y = s[(4 * q + 1) * kWlThreads];
+    v[q].z = s[(4 * q + 2) * kWlThreads];
+    v[q].w = s[(4 * q + 3) * kWlThreads];
   }
+#pragma unroll
+  for (int q = 0; q < kStripV; ++q)
+    if ((uint32_t)q <= (k >> 2) && (q == 0 || (uint32_t)q >= q0)) r4[q] = v[q];
+  if (xs) wl_stamp(xs, 6, t0);  // the write-back issued
   return occ;
 }
 
@@ -583,6 +601,7 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
 
 // The loop's state in LDS.
 struct LoopS {
+  alignas(16) uint32_t hs[32];  // the small-merge path's header, staged for 16-B stores (word 1 = 0: not the flag)
   uint32_t cmd[8];
   uint32_t nout, nchg, pool_top, err, scan, filter, nspill, qn, nkeys, nfin;
   uint32_t rd, wr;  // run ints read (length + tokens of every scanned word) / written back (changed words)
@@ -810,7 +829,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   __shared__ LoopS S;
   __shared__ u64 s_q[kQ];  // the listed entries that pass the filter, merged densely
   __shared__ SelLds<kSelf> s_f;
-  __shared__ uint16_t s_klist[kDh];  // the merge's delta keys (their hash slots), insertion order
+  __shared__ uint32_t s_kbits[kDh / 32];  // the merge's delta keys: a bit per hash slot in use
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t tid = threadIdx.x;
   int32_t* const mys = s_strip + tid;
@@ -829,9 +848,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     s_h.sum[i] = 0;
     s_h.ft[i] = kEmpty64;
   }
+  if (tid < kDh / 32) s_kbits[tid] = 0;
   uint32_t expect = p.seq0;
   uint32_t exit_op = kOpStop;
-  const MergeCtx mc{&S.nspill, &S.nkeys, s_klist};
+  const MergeCtx mc{&S.nspill, &S.nkeys, s_kbits};
   // the small-merge path (p.fast, exact mode): the last wave writes the records and raises the flag;
   // it merges words only when a merge lists more than kWlThreads - 64 of them
   const bool fast = !kSelf && p.fast != 0 && p.fin_max == 0;
@@ -1014,6 +1034,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     // word that held the pair when the index was built, exact).  Undo: the words of X, exactly.
     // Wave 0 reads the id tables and 16 directory slots in one round trip.
     const u64 t_cmd = __builtin_amdgcn_s_memrealtime();
+    WL_ST(const u64 c_cmd = __builtin_amdgcn_s_memtime();)
     if (wid == 0) {
       const bool undo = op == kOpUnmerge;
       const int32_t M = undo ? X : (a > b ? a : b);
@@ -1141,6 +1162,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         e = v.e;
         pass = (v.sig & need) == need;
       }
+      WL_ST(if (pass) wl_stamp(S.xs, 2, t_cmd);)
       uint32_t occ = 0, L = 0, nl = 0;
       u64 nsig = 0;
       if (pass) {
@@ -1149,17 +1171,16 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         const u64 wc = p.weight[(uint32_t)e];
         L = (uint32_t)x.v[0].x;
         nl = L;
-        WL_ST(atomicMax(&S.xs[2], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd)); atomicMax(&S.xs[6], L);
-              if (L > kStripTok) atomicAdd(&S.xs[5], 1u);)
+        WL_ST(wl_stamp(S.xs, 3, t_cmd);)
         if (L >= 2) {
           if (L <= kStripTok) {
-            occ = merge_regs<kProbes>(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig);
+            occ = merge_regs<kProbes>(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig
+                                      WL_ST(, S.xs, t_cmd));
           } else {
             occ = merge_run<kProbes>(p, s_h, mc, r + 1, L, e, wc, a, b, X, &nl, &nsig);
             if (occ) r[0] = (int32_t)nl;
           }
         }
-        WL_ST(atomicMax(&S.xs[3], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd)); atomicMax(&S.xs[7], occ);)
       }
       const u64 chg = __ballot(occ != 0);
       if (chg) {  // the changed words become the words of X
@@ -1184,12 +1205,13 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           atomicAdd(&S.wr, w_wr);
         }
       }
+      WL_ST(wl_stamp(S.xs, 7, t_cmd);)
       // read before the barrier: past it the poller wave may already be waiting for the next command
       // (it writes S.t_wait there); the flag wave has not written the header yet
       const u64 t_wait = S.t_wait;
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every delta is in the hash
       if (drain || S.nspill) __syncthreads();  // spilled deltas' HBM atomics complete (S.nspill is final)
-      WL_ST(if (tid == 0) S.xs[4] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
+      WL_ST(wl_stamp(S.xs, 9, t_cmd);)
       const uint32_t nchg = append ? S.nchg : 0u;
       if (wid == 0 && lane == 0 && X >= 0 && (uint32_t)X < p.id_cap) {
         p.lst[X] = (u64)top | ((u64)nchg << 32);
@@ -1198,10 +1220,18 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       if (wid == kFlagWave) {
         const WlSlotDev& sd = p.sl[slot & (WordLoop::kSlots - 1)];
         const u64 t_out = __builtin_amdgcn_s_memrealtime();
-        const uint32_t nk = S.nkeys, nsp = S.nspill;
-        for (uint32_t i = (uint32_t)lane; i < nk; i += 64u) {  // the records, their slots cleared
-          const uint32_t h = s_klist[i];
-          u64* dst = reinterpret_cast<u64*>(sd.recs + i);
+        // the records: lane l takes the slots of bitmap word l (32 slots), placed by a wave scan
+        // of the words' popcounts; the slots are cleared as they are read
+        const uint32_t nsp = S.nspill;
+        uint32_t bw = s_kbits[lane];
+        s_kbits[lane] = 0;
+        const uint32_t nb = (uint32_t)__popc(bw);
+        const uint32_t incl = wave_scan32(nb);
+        const uint32_t nk = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        uint32_t ri = incl - nb;
+        for (; bw; bw &= bw - 1u, ++ri) {
+          const uint32_t h = (uint32_t)lane * 32u + (uint32_t)__builtin_ctz(bw);
+          u64* dst = reinterpret_cast<u64*>(sd.recs + ri);
           dst[0] = (u64)s_h.key[h];
           dst[1] = s_h.sum[h];
           dst[2] = s_h.ft[h];
@@ -1228,33 +1258,43 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
             S.last_x = X;
             S.last_lst = (u64)top | ((u64)nchg << 32);
           }
-          sd.hdr[0] = nk + nsp;
-          sd.hdr[22] = 0u;
-          sd.hdr[23] = nk + nsp;
-          sd.hdr[30] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_out);
-          sd.hdr[2] = (uint32_t)cnt;
-          sd.hdr[3] = S.nchg;
-          u64* h64 = reinterpret_cast<u64*>(sd.hdr);
-          h64[2] = S.occ;
-          h64[3] = (u64)__builtin_amdgcn_s_memrealtime() - t_cmd;
-          h64[4] = S.t[0];
-          h64[5] = t_out - t_cmd;
-          sd.hdr[12] = S.scan;
-          sd.hdr[13] = S.filter;
-          sd.hdr[14] = S.rd;
-          sd.hdr[15] = S.wr;
-          sd.hdr[16] = sd.hdr[17] = sd.hdr[18] = 0u;  // (the queued path's stamps)
-          sd.hdr[19] = nsp;
-          sd.hdr[20] = (uint32_t)(S.t_idle + (t_cmd - t_wait));
-          sd.hdr[21] = (uint32_t)S.t_undo;
-          sd.hdr[31] = S.t_rel;
-          h64[12] = S.lst_x;
-          h64[13] = t_cmd;
-          h64[14] = t_wait;
+          // the header, staged in LDS and written by 8 lanes with one 16-B store each
+          uint32_t* hs = S.hs;
+          u64* hs64 = reinterpret_cast<u64*>(hs);
+          const u64 now = __builtin_amdgcn_s_memrealtime();
+          hs[0] = nk + nsp;
+          hs[1] = 0u;  // (the flag word: written last, by the release)
+          hs[2] = (uint32_t)cnt;
+          hs[3] = S.nchg;
+          hs64[2] = S.occ;
+          hs64[3] = now - t_cmd;
+          hs64[4] = S.t[0];
+          hs64[5] = t_out - t_cmd;
+          hs[12] = S.scan;
+          hs[13] = S.filter;
+          hs[14] = S.rd;
+          hs[15] = S.wr;
+          hs[16] = hs[17] = hs[18] = 0u;  // (the queued path's stamps)
+          hs[19] = nsp;
+          hs[20] = (uint32_t)(S.t_idle + (t_cmd - t_wait));
+          hs[21] = (uint32_t)S.t_undo;
+          hs[22] = 0u;
+          hs[23] = nk + nsp;
+          hs64[12] = S.lst_x;
+          hs64[13] = t_cmd;
+          hs64[14] = t_wait;
+          hs[30] = (uint32_t)(now - t_out);
+          hs[31] = S.t_rel;
           S.t_idle = 0;
           S.t_undo = 0;
+        }
+        if (lane < 8) reinterpret_cast<int4*>(sd.hdr)[lane] = reinterpret_cast<const int4*>(S.hs)[lane];
+        if (lane == 0) {
           const u64 t_r0 = __builtin_amdgcn_s_memrealtime();
-          WL_ST(S.xs[11] = (uint32_t)(t_r0 - t_cmd); for (int i = 0; i < kXs; ++i) sd.hdr[32 + i] = S.xs[i];)
+          // stamps build: [1] the shader clock (MHz) over the merge, [9] cycles of one s_memrealtime
+          WL_ST(const u64 c_now = __builtin_amdgcn_s_memtime(); const u64 t_now = __builtin_amdgcn_s_memrealtime();
+                S.xs[1] = (uint32_t)((c_now - c_cmd) * 100ull / (t_now - t_cmd + 1ull));
+                S.xs[11] = (uint32_t)(t_r0 - t_cmd); for (int i = 0; i < kXs; ++i) sd.hdr[32 + i] = S.xs[i];)
           // one system-scope release: this wave's record and header stores, then the flag
           __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
           S.t_rel = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_r0);
@@ -1391,6 +1431,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     if (drain || S.nspill) __syncthreads();  // (uniform: S.nspill is final after the barrier above)
     WL_ST(if (tid == 0) S.xs[4] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
     const uint32_t nchg = append ? S.nchg : 0u;
+    if (tid < kDh / 32) s_kbits[tid] = 0;  // (this path reads the whole hash; the next barrier orders it)
     if constexpr (kSelf) {
       // ---- tiebreak=device: the records change the pair table (atomics nobody waits for) and,
       // through the frontier's LDS index, the frontier's counts; the pairs this merge created that

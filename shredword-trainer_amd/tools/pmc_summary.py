@@ -15,7 +15,7 @@ def per_kernel(path):
     out = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        m = re.search(r"(k_[a-z_]+)(<(true|false)>)?", name)
+        m = re.search(r"(k_[a-z_0-9]+)(<[^<>()]*>)?", name)
         key = (m.group(1) + (m.group(2) or "")) if m else name.split("(")[0]
         out[key].append(float(r["Counter_Value"]))
     return out
