@@ -67,7 +67,17 @@ constexpr int kQ = kWlThreads * kB + kWlThreads;
 #else
 #define WL_ST(...)
 #endif
-constexpr int kXs = 12;
+constexpr int kXs = 16;
+// A/B builds (-DSHRED_WL_NT_WORDS): the word-run write-backs and pool appends as nontemporal stores
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16(void* dst, int4 v) {
+#ifdef SHRED_WL_NT_WORDS
+  v4i_t x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<v4i_t*>(dst));
+#else
+  *reinterpret_cast<int4*>(dst) = v;
+#endif
+}
 // stamps build: wave 0's clock (ticks after t0) into xs[i], written by its first active lane (a
 // scalar clock read and one LDS store: no per-lane atomics, which would cost more than the stamped work)
 __device__ __forceinline__ void wl_stamp(uint32_t* xs, int i, unsigned long long t0) {
@@ -193,6 +203,7 @@ struct WlParams {
   uint32_t seq0;
   uint32_t idle_polls;
   uint32_t fin_max;  // K4 on the device: merges with at most this many records leave as ordered changes (0: off)
+  uint32_t fin_min;  //   and at least this many (> 0: the small-merge path stays on; its merges leave raw)
   uint32_t prefetch;  // 1: the poller wave reads the next command while the records go out (exact mode)
   // 1: the merge's barriers drain every wave's stores (0: only with spills or K4).  With 0 the
   // word-run (wtok), pool and lst stores of a merge may still be in flight when its flag is raised;
@@ -544,7 +555,7 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
   }
 #pragma unroll
   for (int q = 0; q < kStripV; ++q)
-    if ((uint32_t)q <= (k >> 2) && (q == 0 || (uint32_t)q >= q0)) r4[q] = v[q];
+    if ((uint32_t)q <= (k >> 2) && (q == 0 || (uint32_t)q >= q0)) st16(&r4[q], v[q]);
   if (xs) wl_stamp(xs, 6, t0);  // the write-back issued
   return occ;
 }
@@ -613,6 +624,7 @@ struct LoopS {
   u64 need;   // filter bits the listed words must hold
   u64 occ, t[2];
   u64 t_wait, t_idle, t_undo;  // s_memrealtime: this command's wait began; idle / undo since the last flag
+  u64 t_seen;                   // (stamps build) the poller saw the command's granules tagged
   uint32_t t_rel;               // ticks of the last flag's system release (diagnostic)
   uint32_t xs[kXs];             // SHRED_WL_STAMPS: phase stamps (ticks after the command) and counts
   // tiebreak=device
@@ -854,7 +866,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   const MergeCtx mc{&S.nspill, &S.nkeys, s_kbits};
   // the small-merge path (p.fast, exact mode): the last wave writes the records and raises the flag;
   // it merges words only when a merge lists more than kWlThreads - 64 of them
-  const bool fast = !kSelf && p.fast != 0 && p.fin_max == 0;
+  const bool fast = !kSelf && p.fast != 0 && (p.fin_max == 0 || p.fin_min != 0);
   constexpr int kFlagWave = kWlThreads / 64 - 1;
   // command prefetch (p.prefetch, exact mode): the poller wave (wave 1) reads the next command's
   // granules while the other waves write the current merge's records and its flag, so a command
@@ -991,6 +1003,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       for (;;) {
         const bool tagged = lane >= kCmdGranules || (uint32_t)v == expect;
         if (__all(tagged)) {
+          WL_ST(if (lane == 0) S.t_seen = __builtin_amdgcn_s_memrealtime();)
           const uint32_t val = (uint32_t)(v >> 32);
           op = __shfl(val, 0, 64);
           a = __shfl(val, 1, 64);
@@ -1143,7 +1156,9 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       __syncthreads();
       continue;
     }
-    if (fast && op == kOpMerge && cnt <= (u64)kWlThreads) {
+    const bool append = S.err == 0;
+    const u64 need = S.need;
+    if ((fast || (kSelf && p.fast != 0)) && op == kOpMerge && cnt <= (u64)kWlThreads) {
       // ---- the small-merge path (every late merge: a few hundred listed words, tens changed).  A
       // lane per listed entry, no queue and no barrier before the merge: entry tid's filter decides
       // and a passing lane loads its word's run and weight right away (the only hop after the
@@ -1152,9 +1167,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       // wave writes the records and raises the flag: it issued no word stores (unless more than
       // kWlThreads - 64 words are listed), so its drain and release wait for the records alone --
       // the other waves' word-run and pool stores drain at the next command's barrier (the rule
-      // at WlParams::drain; with drain = 1 they drain here).
-      const bool append = S.err == 0;
-      const u64 need = S.need;
+      // at WlParams::drain; with drain = 1 they drain here).  tiebreak=device (kSelf) merges the
+      // same way and then takes the common tail below (pair table + frontier, no host records).
       u64 e = kEmpty64;
       bool pass = false;
       if (tid < cnt) {
@@ -1192,7 +1206,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           WEnt ne;
           ne.e = e;
           ne.sig = nsig;
-          p.pool[(u64)top + nb + (uint32_t)__popcll(chg & ((1ull << lane) - 1ull))] = ne;
+          st16(&p.pool[(u64)top + nb + (uint32_t)__popcll(chg & ((1ull << lane) - 1ull))],
+               make_int4((int)(uint32_t)ne.e, (int)(uint32_t)(ne.e >> 32), (int)(uint32_t)ne.sig, (int)(uint32_t)(ne.sig >> 32)));
         }
       }
       if (const u64 sm = __ballot(pass)) {  // statistics: wave sums, one LDS add each per wave
@@ -1209,110 +1224,117 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       // read before the barrier: past it the poller wave may already be waiting for the next command
       // (it writes S.t_wait there); the flag wave has not written the header yet
       const u64 t_wait = S.t_wait;
+      WL_ST(const u64 t_seen_m = S.t_seen;)
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every delta is in the hash
-      if (drain || S.nspill) __syncthreads();  // spilled deltas' HBM atomics complete (S.nspill is final)
+      // spilled deltas' HBM atomics complete (S.nspill is final); K4 never runs here, so only the
+      // drain option itself drains
+      if (p.drain != 0 || S.nspill) __syncthreads();
       WL_ST(wl_stamp(S.xs, 9, t_cmd);)
-      const uint32_t nchg = append ? S.nchg : 0u;
-      if (wid == 0 && lane == 0 && X >= 0 && (uint32_t)X < p.id_cap) {
-        p.lst[X] = (u64)top | ((u64)nchg << 32);
-        p.lseq[X] = seq;
-      }
-      if (wid == kFlagWave) {
-        const WlSlotDev& sd = p.sl[slot & (WordLoop::kSlots - 1)];
-        const u64 t_out = __builtin_amdgcn_s_memrealtime();
-        // the records: lane l takes the slots of bitmap word l (32 slots), placed by a wave scan
-        // of the words' popcounts; the slots are cleared as they are read
-        const uint32_t nsp = S.nspill;
-        uint32_t bw = s_kbits[lane];
-        s_kbits[lane] = 0;
-        const uint32_t nb = (uint32_t)__popc(bw);
-        const uint32_t incl = wave_scan32(nb);
-        const uint32_t nk = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        uint32_t ri = incl - nb;
-        for (; bw; bw &= bw - 1u, ++ri) {
-          const uint32_t h = (uint32_t)lane * 32u + (uint32_t)__builtin_ctz(bw);
-          u64* dst = reinterpret_cast<u64*>(sd.recs + ri);
-          dst[0] = (u64)s_h.key[h];
-          dst[1] = s_h.sum[h];
-          dst[2] = s_h.ft[h];
-          s_h.key[h] = kEmpty32;
-          s_h.sum[h] = 0;
-          s_h.ft[h] = kEmpty64;
+      if constexpr (!kSelf) {
+        const uint32_t nchg = append ? S.nchg : 0u;
+        if (wid == 0 && lane == 0 && X >= 0 && (uint32_t)X < p.id_cap) {
+          p.lst[X] = (u64)top | ((u64)nchg << 32);
+          p.lseq[X] = seq;
         }
-        for (uint32_t i = (uint32_t)lane; i < nsp; i += 64u) {  // then the keys spilled to HBM
-          const uint32_t key = p.dlist[i];
-          const u64 sum = atomicExch(&p.dsum[key], 0ull);
-          const u64 ft = atomicExch(&p.dft[key], kEmpty64);
-          u64* dst = reinterpret_cast<u64*>(sd.recs + nk + i);
-          dst[0] = (u64)key;
-          dst[1] = sum;
-          dst[2] = ft;
-        }
-        WL_ST(if (lane == 0) S.xs[10] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
-        if (lane == 0) {
-          S.lst_x = 0;
-          S.last_x = -1;
-          if (X >= 0 && (uint32_t)X < p.id_cap) {
-            S.pool_top = top + nchg;
-            S.lst_x = (u64)top | ((u64)(nchg + 1u) << 32);  // for the host: offset, count + 1
-            S.last_x = X;
-            S.last_lst = (u64)top | ((u64)nchg << 32);
+        if (wid == kFlagWave) {
+          const WlSlotDev& sd = p.sl[slot & (WordLoop::kSlots - 1)];
+          const u64 t_out = __builtin_amdgcn_s_memrealtime();
+          WL_ST(if (lane == 0) S.xs[12] = (uint32_t)(t_out - t_cmd);)
+          // the records: lane l takes the slots of bitmap word l (32 slots), placed by a wave scan
+          // of the words' popcounts; the slots are cleared as they are read
+          const uint32_t nsp = S.nspill;
+          uint32_t bw = s_kbits[lane];
+          s_kbits[lane] = 0;
+          const uint32_t nb = (uint32_t)__popc(bw);
+          const uint32_t incl = wave_scan32(nb);
+          const uint32_t nk = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+          uint32_t ri = incl - nb;
+          WL_ST(if (lane == 0) S.xs[13] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
+          for (; bw; bw &= bw - 1u, ++ri) {
+            const uint32_t h = (uint32_t)lane * 32u + (uint32_t)__builtin_ctz(bw);
+            u64* dst = reinterpret_cast<u64*>(sd.recs + ri);
+            dst[0] = (u64)s_h.key[h];
+            dst[1] = s_h.sum[h];
+            dst[2] = s_h.ft[h];
+            s_h.key[h] = kEmpty32;
+            s_h.sum[h] = 0;
+            s_h.ft[h] = kEmpty64;
           }
-          // the header, staged in LDS and written by 8 lanes with one 16-B store each
-          uint32_t* hs = S.hs;
-          u64* hs64 = reinterpret_cast<u64*>(hs);
-          const u64 now = __builtin_amdgcn_s_memrealtime();
-          hs[0] = nk + nsp;
-          hs[1] = 0u;  // (the flag word: written last, by the release)
-          hs[2] = (uint32_t)cnt;
-          hs[3] = S.nchg;
-          hs64[2] = S.occ;
-          hs64[3] = now - t_cmd;
-          hs64[4] = S.t[0];
-          hs64[5] = t_out - t_cmd;
-          hs[12] = S.scan;
-          hs[13] = S.filter;
-          hs[14] = S.rd;
-          hs[15] = S.wr;
-          hs[16] = hs[17] = hs[18] = 0u;  // (the queued path's stamps)
-          hs[19] = nsp;
-          hs[20] = (uint32_t)(S.t_idle + (t_cmd - t_wait));
-          hs[21] = (uint32_t)S.t_undo;
-          hs[22] = 0u;
-          hs[23] = nk + nsp;
-          hs64[12] = S.lst_x;
-          hs64[13] = t_cmd;
-          hs64[14] = t_wait;
-          hs[30] = (uint32_t)(now - t_out);
-          hs[31] = S.t_rel;
-          S.t_idle = 0;
-          S.t_undo = 0;
+          WL_ST(if (lane == 0) S.xs[14] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
+          for (uint32_t i = (uint32_t)lane; i < nsp; i += 64u) {  // then the keys spilled to HBM
+            const uint32_t key = p.dlist[i];
+            const u64 sum = atomicExch(&p.dsum[key], 0ull);
+            const u64 ft = atomicExch(&p.dft[key], kEmpty64);
+            u64* dst = reinterpret_cast<u64*>(sd.recs + nk + i);
+            dst[0] = (u64)key;
+            dst[1] = sum;
+            dst[2] = ft;
+          }
+          WL_ST(if (lane == 0) S.xs[10] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
+          if (lane == 0) {
+            S.lst_x = 0;
+            S.last_x = -1;
+            if (X >= 0 && (uint32_t)X < p.id_cap) {
+              S.pool_top = top + nchg;
+              S.lst_x = (u64)top | ((u64)(nchg + 1u) << 32);  // for the host: offset, count + 1
+              S.last_x = X;
+              S.last_lst = (u64)top | ((u64)nchg << 32);
+            }
+            // the header, staged in LDS and written by 8 lanes with one 16-B store each
+            uint32_t* hs = S.hs;
+            u64* hs64 = reinterpret_cast<u64*>(hs);
+            const u64 now = __builtin_amdgcn_s_memrealtime();
+            hs[0] = nk + nsp;
+            hs[1] = 0u;  // (the flag word: written last, by the release)
+            hs[2] = (uint32_t)cnt;
+            hs[3] = S.nchg;
+            hs64[2] = S.occ;
+            hs64[3] = now - t_cmd;
+            hs64[4] = S.t[0];
+            hs64[5] = t_out - t_cmd;
+            hs[12] = S.scan;
+            hs[13] = S.filter;
+            hs[14] = S.rd;
+            hs[15] = S.wr;
+            hs[16] = hs[17] = hs[18] = 0u;  // (the queued path's stamps)
+            hs[19] = nsp;
+            hs[20] = (uint32_t)(S.t_idle + (t_cmd - t_wait));
+            hs[21] = (uint32_t)S.t_undo;
+            hs[22] = 0u;
+            hs[23] = nk + nsp;
+            hs64[12] = S.lst_x;
+            hs64[13] = t_cmd;
+            hs64[14] = t_wait;
+            hs[30] = (uint32_t)(now - t_out);
+            hs[31] = S.t_rel;
+            S.t_idle = 0;
+            S.t_undo = 0;
+          }
+          if (lane < 8) reinterpret_cast<int4*>(sd.hdr)[lane] = reinterpret_cast<const int4*>(S.hs)[lane];
+          if (lane == 0) {
+            const u64 t_r0 = __builtin_amdgcn_s_memrealtime();
+            // stamps build: [1] the shader clock (MHz) over the merge, [9] cycles of one s_memrealtime
+            WL_ST(sd.hdr[48] = (uint32_t)t_seen_m;
+                const u64 c_now = __builtin_amdgcn_s_memtime(); const u64 t_now = __builtin_amdgcn_s_memrealtime();
+                  S.xs[1] = (uint32_t)((c_now - c_cmd) * 100ull / (t_now - t_cmd + 1ull));
+                  S.xs[11] = (uint32_t)(t_r0 - t_cmd); for (int i = 0; i < kXs; ++i) sd.hdr[32 + i] = S.xs[i];)
+            // one system-scope release: this wave's record and header stores, then the flag
+            __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            S.t_rel = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_r0);
+          }
+        } else if (pfon && wid == poll_wave) {  // the next command's granules, in flight meanwhile
+          pre_v = lane < kCmdGranules
+                      ? __hip_atomic_load(p.ring[expect % kRing].g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                      : 0ull;
+          pre_ok = true;
         }
-        if (lane < 8) reinterpret_cast<int4*>(sd.hdr)[lane] = reinterpret_cast<const int4*>(S.hs)[lane];
-        if (lane == 0) {
-          const u64 t_r0 = __builtin_amdgcn_s_memrealtime();
-          // stamps build: [1] the shader clock (MHz) over the merge, [9] cycles of one s_memrealtime
-          WL_ST(const u64 c_now = __builtin_amdgcn_s_memtime(); const u64 t_now = __builtin_amdgcn_s_memrealtime();
-                S.xs[1] = (uint32_t)((c_now - c_cmd) * 100ull / (t_now - t_cmd + 1ull));
-                S.xs[11] = (uint32_t)(t_r0 - t_cmd); for (int i = 0; i < kXs; ++i) sd.hdr[32 + i] = S.xs[i];)
-          // one system-scope release: this wave's record and header stores, then the flag
-          __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-          S.t_rel = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_r0);
-        }
-      } else if (pfon && wid == poll_wave) {  // the next command's granules, in flight meanwhile
-        pre_v = lane < kCmdGranules
-                    ? __hip_atomic_load(p.ring[expect % kRing].g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                    : 0ull;
-        pre_ok = true;
+        continue;  // (the next command's barrier orders the flag wave's LDS writes before any use)
       }
-      continue;  // (the next command's barrier orders the flag wave's LDS writes before any use)
-    }
+    } else {
     // ---- the merge over the listed words; changed words become the words of X.  Each round a
     // lane loads kB pool entries (coalesced) and queues in LDS those whose filter holds the
     // pair's bit; once a workgroup's worth is queued (and at the end) the queue is merged
     // densely, a lane per word: the run in one round trip, the walk in registers.
-    const bool append = S.err == 0;
-    const u64 need = S.need;
     uint32_t my_occ = 0, my_scan = 0, my_rd = 0, my_wr = 0;
     if (tid == 0) S.qn = 0;
     for (u64 base = 0; base < cnt; base += (u64)kWlThreads * kB) {
@@ -1430,6 +1452,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (drain || S.nspill) __syncthreads();  // (uniform: S.nspill is final after the barrier above)
     WL_ST(if (tid == 0) S.xs[4] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
+    }
     const uint32_t nchg = append ? S.nchg : 0u;
     if (tid < kDh / 32) s_kbits[tid] = 0;  // (this path reads the whole hash; the next barrier orders it)
     if constexpr (kSelf) {
@@ -1596,7 +1619,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       S.last_lst = (u64)top | ((u64)nchg << 32);
     }
     const uint32_t nrec = S.nkeys + S.nspill;
-    const bool fin = p.fin_max != 0 && nrec <= p.fin_max && nrec <= kFinMax;
+    const bool fin = p.fin_max != 0 && nrec <= p.fin_max && nrec <= kFinMax && nrec >= p.fin_min;
     const u64 t_fin = __builtin_amdgcn_s_memrealtime();
     if (fin && nrec <= 64u) {  // one wave combines and orders them
       fin_gather(p, s_h, S, s_q, a, b, X);
@@ -1966,6 +1989,7 @@ WordLoop::WordLoop(int ordinal, void* stream, int32_t unk_id) : ordinal_(ordinal
   // race the time-out against the posts
   if (const char* e = std::getenv("SHREDWORD_WL_IDLE_POLLS")) idle_polls_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_WL_FINALIZE")) fin_max_ = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char* e = std::getenv("SHREDWORD_WL_FIN_MIN")) fin_min_ = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("SHREDWORD_WL_PREFETCH")) prefetch_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_WL_DRAIN")) drain_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("SHREDWORD_WL_PROBES")) probes_ = std::atoi(e);
@@ -2355,6 +2379,7 @@ void WordLoop::launch(uint32_t seq0) {
   p.seq0 = seq0;
   p.idle_polls = idle_polls_;
   p.fin_max = fin_max_;
+  p.fin_min = fin_min_;
   p.prefetch = prefetch_ ? 1u : 0u;
   p.drain = drain_ ? 1u : 0u;
   p.fast = fast_ ? 1u : 0u;
@@ -2481,7 +2506,9 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
                                         (uint32_t)h64[13], (uint32_t)h64[14],
                                         // SHRED_WL_STAMPS builds: phase stamps and counts (0 otherwise)
                                         h[32], h[33], h[34], h[35], h[36], h[37], h[38], h[39], h[40], h[41],
-                                        h[42], h[43]};
+                                        h[42], h[43], h[44], h[45], h[46], h[47],
+                                        // the previous flag's release ticks; (stamps) the poller saw the command
+                                        h[31], h[48]};
     trace_.insert(trace_.end(), rec, rec + kTraceFields);
   }
   if (n > sl.rec_cap) fatal("k_word_loop: record overflow");
@@ -2759,6 +2786,7 @@ int WordLoop::run_select(const std::vector<PairCount>& pairs, int32_t X0, uint32
     p.dstate = dstate_;
     p.cap = cap_;
     p.unk = unk_;
+    p.fast = fast_ ? 1u : 0u;  // small merges through the small-merge body (then the pair-table tail)
     p.sel = q;
     dirty_ = true;
     int stalls = 0;

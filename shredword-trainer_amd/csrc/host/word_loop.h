@@ -167,7 +167,7 @@ class WordLoop {
   // the host ns from posting this merge to seeing its flag; then absolute clocks: host post and
   // flag seen (10 ns since the loop was made), device command seen and wait begun (100 MHz
   // ticks), low 32 bits each.
-  static constexpr int kTraceFields = 31;
+  static constexpr int kTraceFields = 37;
   const std::vector<uint32_t>& trace() const { return trace_; }
   void set_timing(bool on) { timing_ = on; }
   size_t device_bytes() const { return bytes_; }
@@ -248,6 +248,9 @@ class WordLoop {
   // K4 on the device up to this many records (<= 64: one wave; up to kFinMax: the workgroup).  Off
   // by default: measured on C3 it costs the device more than it saves the host
   uint32_t fin_max_ = 0;
+  // SHREDWORD_WL_FIN_MIN: K4 only for merges of at least this many records (the large ones; the
+  // small-merge path then stays on for the rest)
+  uint32_t fin_min_ = 0;
   // the next command read while the records go out (SHREDWORD_WL_PREFETCH=0 turns it off): C3 A/B
   // on one box, 2 rounds: 54.2-54.3 k off, 55.0-55.2 k on (profiles/r05_c3_command_prefetch_ab.txt)
   bool prefetch_ = true;

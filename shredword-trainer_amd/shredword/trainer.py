@@ -76,20 +76,21 @@ class BPETrainer:
 
     def index_trace(self):
         """Per-merge trace of the indexed merge loop (diagnostic, recorded while the 'timing'
-        option is on): numpy uint32 array (merges, 31) of X, listed words, scanned words, changed
+        option is on): numpy uint32 array (merges, 37) of X, listed words, scanned words, changed
         words, occurrences, device ns command -> flag, lookup ns, scan ns, wave 0's stamps
         (ns after the command: pool entries loaded, first run loaded, first word merged, unused),
         device ns since the previous flag spent waiting for commands and undoing guesses, host ns
         from post to flag, then absolute clocks (low 32 bits): host post and flag seen (10 ns
-        units), device command seen and wait begun (100 MHz ticks); then 12 phase stamps and counts that only
-        a -DSHRED_WL_STAMPS build fills in (word_loop.hip, zeros otherwise)."""
+        units), device command seen and wait begun (100 MHz ticks); then 16 phase stamps and counts that only
+        a -DSHRED_WL_STAMPS build fills in (word_loop.hip, zeros otherwise); then the previous flag's
+        release ticks and (stamps build) the device clock when the poller saw the command."""
         import numpy as np
         n = lib.shred_index_trace(self.trainer, None, 0)
         if n < 0:
             raise RuntimeError("no device")
         out = np.empty(n, dtype=np.uint32)
         lib.shred_index_trace(self.trainer, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n)
-        return out.reshape(-1, 31)
+        return out.reshape(-1, 37)
 
     def stats(self) -> dict:
         s = ShredStats()

@@ -58,14 +58,15 @@ def main():
                      "stamps_us_mean": [float(v[s].mean() / 1e3) for v in (s0, s1, s2, s3)],
                      "dev_idle_us_mean": float(idle[s].mean() / 1e3), "dev_undo_us_mean": float(undo[s].mean() / 1e3),
                      "host_post_to_flag_us_mean": float(hflag[s].mean() / 1e3)})
-        if tr.shape[1] >= 31 and tr[s, 19:31].any():  # a -DSHRED_WL_STAMPS build
-            xs = tr[s, 19:31]
+        if tr.shape[1] >= 35 and tr[s, 19:35].any():  # a -DSHRED_WL_STAMPS build
+            xs = tr[s, 19:35]
             # the small-merge path's stamps (word_loop.hip, SHRED_WL_STAMPS): wave 0's clock after the
             # command at each point; [1] is the shader clock in MHz, [8] 1 when the list needed no lookup
             names = ["lookup_done", "clock_MHz_x0.01", "w0_entry_landed", "w0_run_landed", "w0_walk_done",
                      "w0_deltas_issued", "w0_writeback_issued", "w0_appended", "list_given", "merge_barrier",
-                     "records_stored", "before_release"]
-            ticks = {0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11}
+                     "records_stored", "before_release", "fw_start", "fw_scanned", "fw_records_issued",
+                     "unused"]
+            ticks = {0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12, 13, 14}
             rows[-1]["stamps"] = {nm: (float(xs[:, i].mean() / 100.0) if i in ticks else float(xs[:, i].mean()))
                                   for i, nm in enumerate(names)}
             rows[-1]["stamps_p50"] = {nm: float(np.median(xs[:, i]) / 100.0) for i, nm in enumerate(names)

@@ -32,6 +32,13 @@ def main():
     cmd_h = dcmd - off
     wait_h = dwait - off
     fence_h = cmd_h + dev
+    # the release (L2 write-back + flag store) of merge i, reported in merge i + 1's header
+    rel = np.zeros(len(tr))
+    if tr.shape[1] >= 37:
+        rel[:-1] = tr[1:, 35] * 1e-2
+    released_h = fence_h + rel
+    seen_dev = (np.unwrap(tr[:, 36].astype(np.float64), period=2.0**32) * 1e-2 - off) if (
+        tr.shape[1] >= 37 and tr[:, 36].any()) else None
     rows = []
     edges = [0, 256, 1024, 4096, 8192, 16384, 24576, len(tr)]
     for lo, hi in zip(edges[:-1], edges[1:]):
@@ -45,6 +52,10 @@ def main():
             "post_to_cmd_us": float(np.mean(cmd_h[s] - post[s])),
             "cmd_to_header_us": float(np.mean(dev[s])),
             "header_to_seen_us": float(np.mean(seen[s] - fence_h[s])),
+            "release_us": float(np.mean(rel[s])),
+            "released_to_seen_us": float(np.mean(seen[s] - released_h[s])),
+            "post_to_poller_saw_us": float(np.mean(seen_dev[s] - post[s])) if seen_dev is not None else None,
+            "poller_saw_to_cmd_us": float(np.mean(cmd_h[s] - seen_dev[s])) if seen_dev is not None else None,
             "prev_seen_to_post_us": float(np.mean(post[s] - prev_seen)),
             "prev_header_to_cmd_us": float(np.mean(cmd_h[s] - prev_fence)),
             "wait_start_to_cmd_us": float(np.mean(cmd_h[s] - wait_h[s])),

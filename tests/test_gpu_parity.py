@@ -98,6 +98,17 @@ def test_index_loop_changes_on_device_match_reference(name, fin, case_corpus, tm
         assert 0 < st["index_finalized"] < st["index_merges"] + st["index_undos"], st
 
 
+@pytest.mark.parametrize("name", API_CASES)
+def test_large_merges_changes_on_device_match_reference(name, case_corpus, tmp_path, monkeypatch):
+    """K4 on the device for the large merges only (SHREDWORD_WL_FIN_MIN=32, finalize=1024): merges of
+    32..1024 records through the queued path leave as ordered changes, while the small-merge path
+    (a lane per listed word) stays on for the rest and hands raw records.  Same bytes."""
+    case, corpus = case_corpus(name)
+    monkeypatch.setenv("SHREDWORD_WL_FIN_MIN", "32")
+    st = {}
+    _check(case, _train(case, corpus, tmp_path, "types", stats=st, finalize=1024))
+
+
 @pytest.mark.parametrize("probes", [0, 1])
 @pytest.mark.parametrize("name", [n for n in API_CASES if n not in DEEP])
 def test_index_loop_spilled_deltas_match_reference(name, probes, case_corpus, tmp_path, monkeypatch):
