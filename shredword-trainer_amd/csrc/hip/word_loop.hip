@@ -50,9 +50,21 @@ typedef unsigned long long u64;
 
 constexpr int kWlThreads = 512;
 constexpr int kDh = 2048;               // LDS delta hash slots
-constexpr int kStripV = 6;              // 16-B loads per word run: [length][23 tokens]
+constexpr int kStripV = 7;              // 16-B loads per word run: [length][weight lo, hi][25 tokens]
 constexpr int kStrip = 4 * kStripV;     // ints per lane in the LDS strip
-constexpr uint32_t kStripTok = kStrip - 1;
+// A run's header: its live length, then the word's weight (u64, the count of the word) inline, so
+// that the run's loads bring it and a scanned word costs no separate weight line (round 6: a third
+// of the loop's HBM read requests were those lines)
+constexpr uint32_t kRunHdr = 3;
+constexpr uint32_t kStripTok = kStrip - kRunHdr;
+// Runs are 16-B aligned with a capacity of whole 16-B groups.  (Round 6 measured 128-B aligned
+// runs: one L2 line per run load, HBM reads of the loop -30%, but the table grew 2.5x, past what
+// the MALL keeps, and the loop got slower; the groups a word needs ride in its pool entries
+// instead, see WEnt.)
+constexpr uint32_t kRunAlign = 4;  // ints
+__host__ __device__ constexpr uint32_t run_cap(uint32_t len) {
+  return (kRunHdr + len + kRunAlign - 1u) & ~(kRunAlign - 1u);
+}
 constexpr int kB = 8;                   // pool entries per lane per scan round (one load batch)
 #ifdef SHRED_WL_NO_PREFETCH
 constexpr bool kWlPrefetch = false;     // (A/B builds) each word's run loaded in its own iteration
@@ -60,6 +72,14 @@ constexpr bool kWlPrefetch = false;     // (A/B builds) each word's run loaded i
 constexpr bool kWlPrefetch = true;      // the next word's run loads while this one merges
 #endif
 constexpr int kQ = kWlThreads * kB + kWlThreads;
+// tiebreak=device (k_word_loop<true>) holds its LDS frontier beside the loop's arrays: it queues
+// 6 entries a lane per round so that everything fits the 160 KB of LDS
+constexpr int kBSelf = 6;
+template <bool kSelf>
+struct QueueShape {
+  static constexpr int kBatch = kSelf ? kBSelf : kB;
+  static constexpr int kCap = kWlThreads * kBatch + kWlThreads;
+};
 // Diagnostic builds (-DSHRED_WL_STAMPS, tools/build_variant.sh): per-merge phase stamps of the
 // indexed loop in header words [32, 44) (WordLoop::collect puts them in the trace)
 #ifdef SHRED_WL_STAMPS
@@ -124,9 +144,13 @@ struct WlSlotDev {
 // (c, M) / (M, d) the word holds later it held right after merge M: a word holding the pair
 // now has its bit.  Initial-index entries (exact lists) hold all ones.
 struct WEnt {
-  u64 e;    // run offset << 32 | word id
+  u64 e;    // run offset << 32 | groups << 28 | word id (groups: the 16-B groups of the word's run
+            // capacity, at most kStripV: a word's run load issues only those, round 6)
   u64 sig;
 };
+constexpr int kGroupShift = 28;
+constexpr u64 kWordMask = (1ull << kGroupShift) - 1;
+__host__ __device__ __forceinline__ uint32_t ent_groups(u64 e) { return (uint32_t)(e >> kGroupShift) & 0xFu; }
 
 // tiebreak=device (K5 as the selector, WordLoop::run_select): the loop picks its own merges from
 // a pair table on the device.  Table: open addressing on the pair key, 16 B a slot -- the key,
@@ -442,7 +466,7 @@ template <int kProbes>
 __device__ __forceinline__ uint32_t merge_run(const WlParams& p, DeltaH& h, const MergeCtx& c, int32_t* t, uint32_t L,
                                               u64 e, u64 wc, int32_t a, int32_t b, int32_t X, uint32_t* len,
                                               u64* sig) {
-  const u64 rank = (e & 0xFFFFFFFFull) << 32;
+  const u64 rank = (e & kWordMask) << 32;
   uint32_t j = 0, k = 0, occ = 0;
   u64 f = 0;
   int32_t prev = 0;
@@ -479,12 +503,15 @@ __device__ __forceinline__ uint32_t merge_run(const WlParams& p, DeltaH& h, cons
 struct Run {
   int4 v[kStripV];
 };
-__device__ __forceinline__ Run load_run(const int32_t* r) {
+__device__ __forceinline__ Run load_run(const int32_t* r, uint32_t groups = kStripV) {
   Run x;
   const int4* r4 = reinterpret_cast<const int4*>(r);
 #pragma unroll
-  for (int q = 0; q < kStripV; ++q) x.v[q] = r4[q];
+  for (int q = 0; q < kStripV; ++q) x.v[q] = (uint32_t)q < groups ? r4[q] : make_int4(0, 0, 0, 0);
   return x;
+}
+__device__ __forceinline__ u64 run_weight(const Run& x) {
+  return (u64)(uint32_t)x.v[0].y | ((u64)(uint32_t)x.v[0].z << 32);
 }
 __device__ __forceinline__ int32_t run_at(const Run& x, int i) {
   const int4 q = x.v[i >> 2];
@@ -510,11 +537,11 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
 #pragma unroll
   for (int j = 0; j < (int)kStripTok; ++j) {
     if ((j & 3) == 0 && !__any((uint32_t)j < L)) break;  // every lane's word has ended
-    const int32_t t0 = run_at(x, 1 + j);
-    const int32_t t1 = j + 1 < (int)kStripTok ? run_at(x, 2 + j) : 0;
+    const int32_t t0 = run_at(x, (int)kRunHdr + j);
+    const int32_t t1 = j + 1 < (int)kStripTok ? run_at(x, (int)kRunHdr + 1 + j) : 0;
     const bool emit = (uint32_t)j < L && !skip;
     const bool m = emit && (uint32_t)(j + 1) < L && t0 == a && t1 == b;
-    s[(emit ? 1u + k : 0u) * kWlThreads] = m ? X : t0;
+    s[(emit ? kRunHdr + k : 0u) * kWlThreads] = m ? X : t0;
     xm |= (m ? 1u : 0u) << k;
     k += emit ? 1u : 0u;
     skip = m;
@@ -524,7 +551,7 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
   *sig = 0;
   if (!xm) return 0;
   const uint32_t occ = (uint32_t)__popc(xm);
-  const u64 rank = (e & 0xFFFFFFFFull) << 32;
+  const u64 rank = (e & kWordMask) << 32;
   uint32_t m = xm, o = 0;
   u64 f = 0;
   while (__ballot(m != 0u)) {
@@ -533,18 +560,18 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
       m &= m - 1u;
       const uint32_t jo = ko + o;
       ++o;
-      const int32_t prev = ko > 0 ? s[ko * kWlThreads] : 0;  // out[ko - 1]
+      const int32_t prev = ko > 0 ? s[(kRunHdr - 1u + ko) * kWlThreads] : 0;  // out[ko - 1]
       const bool has_n = jo + 2 < L;
-      const int32_t nx = has_n ? s[(2 + ko) * kWlThreads] : 0;  // out[ko + 1]
+      const int32_t nx = has_n ? s[(kRunHdr + 1u + ko) * kWlThreads] : 0;  // out[ko + 1]
       f |= occurrence<kProbes>(p, h, c, ko > 0, prev, has_n, nx == X ? a : nx, wc, rank | ((u64)jo << 2));
     }
   }
   if (xs) wl_stamp(xs, 5, t0);  // the occurrences' deltas issued
   *sig = f;
-  // the run [length][k tokens] from the first 16-B group that changed
+  // the run [length][weight][k tokens] from the first 16-B group that changed
   s[0] = (int32_t)k;
   int4* r4 = reinterpret_cast<int4*>(r);
-  const uint32_t q0 = (uint32_t)__ffs(xm) >> 2;  // (1 + first X position) / 4
+  const uint32_t q0 = ((uint32_t)__ffs(xm) + kRunHdr - 1u) >> 2;  // (kRunHdr + first X position) / 4
   int4 v[kStripV];  // every group read at once (one LDS wait), the changed ones stored
 #pragma unroll
   for (int q = 0; q < kStripV; ++q) {
@@ -553,9 +580,11 @@ __device__ __forceinline__ uint32_t merge_regs(const WlParams& p, DeltaH& h, con
     v[q].z = s[(4 * q + 2) * kWlThreads];
     v[q].w = s[(4 * q + 3) * kWlThreads];
   }
+  v[0].y = x.v[0].y;  // the weight, as it was
+  v[0].z = x.v[0].z;
 #pragma unroll
   for (int q = 0; q < kStripV; ++q)
-    if ((uint32_t)q <= (k >> 2) && (q == 0 || (uint32_t)q >= q0)) st16(&r4[q], v[q]);
+    if ((uint32_t)q <= ((k + kRunHdr - 1u) >> 2) && (q == 0 || (uint32_t)q >= q0)) st16(&r4[q], v[q]);
   if (xs) wl_stamp(xs, 6, t0);  // the write-back issued
   return occ;
 }
@@ -839,7 +868,9 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
   __shared__ int32_t s_strip[kStrip * kWlThreads];  // [position][lane]: conflict-free per wave
   __shared__ DeltaH s_h;
   __shared__ LoopS S;
-  __shared__ u64 s_q[kQ];  // the listed entries that pass the filter, merged densely
+  constexpr int kBq = QueueShape<kSelf>::kBatch;
+  constexpr int kQs = QueueShape<kSelf>::kCap;
+  __shared__ u64 s_q[kQs];  // the listed entries that pass the filter, merged densely
   __shared__ SelLds<kSelf> s_f;
   __shared__ uint32_t s_kbits[kDh / 32];  // the merge's delta keys: a bit per hash slot in use
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1140,7 +1171,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         const u64 e = p.pool[off + i].e;
         int32_t* r = p.wtok + (uint32_t)(e >> 32);
         const uint32_t L = (uint32_t)r[0];
-        const uint32_t nl = unmerge_run(r + 1, L, a, b, X);
+        const uint32_t nl = unmerge_run(r + kRunHdr, L, a, b, X);
         if (nl != L) r[0] = (int32_t)nl;
       }
       __syncthreads();
@@ -1181,8 +1212,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       u64 nsig = 0;
       if (pass) {
         int32_t* r = p.wtok + (uint32_t)(e >> 32);
-        const Run x = load_run(r);
-        const u64 wc = p.weight[(uint32_t)e];
+        const Run x = load_run(r, ent_groups(e));
+        const u64 wc = run_weight(x);
         L = (uint32_t)x.v[0].x;
         nl = L;
         WL_ST(wl_stamp(S.xs, 3, t_cmd);)
@@ -1191,7 +1222,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
             occ = merge_regs<kProbes>(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig
                                       WL_ST(, S.xs, t_cmd));
           } else {
-            occ = merge_run<kProbes>(p, s_h, mc, r + 1, L, e, wc, a, b, X, &nl, &nsig);
+            occ = merge_run<kProbes>(p, s_h, mc, r + kRunHdr, L, e, wc, a, b, X, &nl, &nsig);
             if (occ) r[0] = (int32_t)nl;
           }
         }
@@ -1337,10 +1368,10 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
     // densely, a lane per word: the run in one round trip, the walk in registers.
     uint32_t my_occ = 0, my_scan = 0, my_rd = 0, my_wr = 0;
     if (tid == 0) S.qn = 0;
-    for (u64 base = 0; base < cnt; base += (u64)kWlThreads * kB) {
-      u64 ex[kB], sx[kB];
+    for (u64 base = 0; base < cnt; base += (u64)kWlThreads * kBq) {
+      u64 ex[kBq], sx[kBq];
 #pragma unroll
-      for (int q = 0; q < kB; ++q) {
+      for (int q = 0; q < kBq; ++q) {
         const u64 i = base + (u64)q * kWlThreads + tid;
         ex[q] = kEmpty64;
         sx[q] = 0;
@@ -1355,7 +1386,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.st[0] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);
       }
 #pragma unroll
-      for (int q = 0; q < kB; ++q) {
+      for (int q = 0; q < kBq; ++q) {
         const bool pass = ex[q] != kEmpty64 && (sx[q] & need) == need;
         const u64 bl = __ballot(pass);
         if (bl) {
@@ -1369,31 +1400,29 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
       __syncthreads();
       const uint32_t qn = S.qn;
       __syncthreads();  // every thread has read qn before the next round queues more
-      const bool last = base + (u64)kWlThreads * kB >= cnt;
+      const bool last = base + (u64)kWlThreads * kBq >= cnt;
       if (qn < (uint32_t)kWlThreads && !last) continue;
       WL_ST(if (tid == 0) { if (!S.xs[1]) S.xs[1] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd); ++S.xs[9]; })
       // A lane's words one after another, the next word's run and weight loading while this one
       // merges (the compiler's waits count the loads; big merges queue up to 9 words a lane)
       const uint32_t qend = ((qn + kWlThreads - 1) / kWlThreads) * kWlThreads;
-      u64 e_n = kEmpty64, wc_n = 0;
+      u64 e_n = kEmpty64;
       Run x_n{};
       if (kWlPrefetch && tid < qn) {
         e_n = s_q[tid];
-        x_n = load_run(p.wtok + (uint32_t)(e_n >> 32));
-        wc_n = p.weight[(uint32_t)e_n];
+        x_n = load_run(p.wtok + (uint32_t)(e_n >> 32), ent_groups(e_n));
       }
       for (uint32_t qi = tid; qi < qend; qi += kWlThreads) {
         if (!kWlPrefetch && qi < qn) {
           e_n = s_q[qi];
-          x_n = load_run(p.wtok + (uint32_t)(e_n >> 32));
-          wc_n = p.weight[(uint32_t)e_n];
+          x_n = load_run(p.wtok + (uint32_t)(e_n >> 32), ent_groups(e_n));
         }
-        const u64 e = e_n, wc = wc_n;
+        const u64 e = e_n;
         const Run x = x_n;
+        const u64 wc = run_weight(x);
         if (kWlPrefetch && qi + kWlThreads < qn) {
           e_n = s_q[qi + kWlThreads];
-          x_n = load_run(p.wtok + (uint32_t)(e_n >> 32));
-          wc_n = p.weight[(uint32_t)e_n];
+          x_n = load_run(p.wtok + (uint32_t)(e_n >> 32), ent_groups(e_n));
         }
         uint32_t occ = 0;
         u64 nsig = 0;
@@ -1409,7 +1438,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
             if (L <= kStripTok) {
               occ = merge_regs<kProbes>(p, s_h, mc, mys, r, x, L, e, wc, a, b, X, &nl, &nsig);
             } else {
-              occ = merge_run<kProbes>(p, s_h, mc, r + 1, L, e, wc, a, b, X, &nl, &nsig);
+              occ = merge_run<kProbes>(p, s_h, mc, r + kRunHdr, L, e, wc, a, b, X, &nl, &nsig);
               if (occ) r[0] = (int32_t)nl;
             }
           }
@@ -1475,7 +1504,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
         S.dxa = 0;
       }
       __syncthreads();
-      constexpr uint32_t kNewCap = (uint32_t)kQ / 2;  // the new pairs' list in the merge queue's LDS (free now)
+      constexpr uint32_t kNewCap = (uint32_t)kQs / 2;  // the new pairs' list in the merge queue's LDS (free now)
       const SelNew nw{s_q, s_q + kNewCap, &S.snew, kNewCap, &S.dxa, &S.sover, q.log + 2 * S.logn, &S.lognew};
       for (int i = tid; i < kDh; i += kWlThreads) {
         const uint32_t key = s_h.key[i];
@@ -1731,22 +1760,24 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
 
 namespace {
 
-// Initial index: entry woff[w] + j holds pair j of word w (tokens j, j + 1); pairs holding unk,
-// pairs past the live length and the run's length/padding slots emit EMPTY.
-__global__ void k_wl_emit_pairs(const int32_t* wtok, const uint32_t* woff, uint32_t W, int32_t unk, u64* key,
-                                uint32_t* val) {
+// Initial index, compact (round 6: the sort no longer spans the runs' padding): word w's
+// adjacent pairs go to entries base[w] .. base[w] + L - 2 (base: exclusive sum of the words' pair
+// counts, k_wl_pair_counts); pairs holding unk emit EMPTY.
+__global__ void k_wl_pair_counts(const int32_t* wtok, const uint32_t* woff, uint32_t W, uint32_t* cnt) {
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w <= W; w += gridDim.x * blockDim.x) {
+    const uint32_t L = w < W ? (uint32_t)wtok[woff[w]] : 0u;
+    cnt[w] = L >= 2 ? L - 1 : 0u;
+  }
+}
+__global__ void k_wl_emit_pairs(const int32_t* wtok, const uint32_t* woff, const uint32_t* base, uint32_t W,
+                                int32_t unk, u64* key, uint32_t* val) {
   for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < W; w += gridDim.x * blockDim.x) {
-    const uint32_t o = woff[w], span = woff[w + 1] - o;
-    const uint32_t L = (uint32_t)wtok[o];
-    const int32_t* t = wtok + o + 1;
-    for (uint32_t j = 0; j < span; ++j) {
-      u64 k = kEmpty64;
-      if (j + 1 < L) {
-        const int32_t x = t[j], y = t[j + 1];
-        if (x != unk && y != unk) k = pair_key(x, y);
-      }
-      key[o + j] = k;
-      val[o + j] = w;
+    const uint32_t o = woff[w], b = base[w], np = base[w + 1] - b;
+    const int32_t* t = wtok + o + kRunHdr;
+    for (uint32_t j = 0; j < np; ++j) {
+      const int32_t x = t[j], y = t[j + 1];
+      key[b + j] = (x != unk && y != unk) ? pair_key(x, y) : kEmpty64;
+      val[b + j] = w;
     }
   }
 }
@@ -1769,7 +1800,8 @@ __global__ void k_wl_scatter(const u64* key, const uint32_t* val, uint64_t n, co
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     if (keep[i]) {
       WEnt ent;
-      ent.e = ((u64)woff[val[i]] << 32) | val[i];
+      const uint32_t w = val[i], cap4 = (woff[w + 1] - woff[w]) >> 2;  // the run's 16-B groups
+      ent.e = ((u64)woff[w] << 32) | ((u64)min(cap4, (uint32_t)kStripV) << kGroupShift) | w;
       ent.sig = ~0ull;  // an exact list: no filter
       pool[pos[i]] = ent;
     }
@@ -1804,6 +1836,15 @@ __global__ void k_wl_dir_init(const u64* ikey, const u64* ival, uint64_t nk, u64
   }
 }
 
+// Each run's header gets its word's weight (ints 1-2), after a host upload of the runs.
+__global__ void k_wl_set_weights(int32_t* wtok, const uint32_t* woff, uint32_t W, const u64* weight) {
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < W; w += gridDim.x * blockDim.x) {
+    const u64 c = weight[w];
+    wtok[woff[w] + 1] = (int32_t)(uint32_t)c;
+    wtok[woff[w] + 2] = (int32_t)(uint32_t)(c >> 32);
+  }
+}
+
 // Words -> tiles: a wave per tile writes [header][tokens] for its words in rank order and the
 // tile's live length; the old tail up to the previous length becomes padding.
 __global__ void k_words_to_tiles(const int32_t* wtok, const uint32_t* woff, const uint32_t* tile_first,
@@ -1825,7 +1866,7 @@ __global__ void k_words_to_tiles(const int32_t* wtok, const uint32_t* woff, cons
       if (on) {
         int32_t* d = dst + base + incl - need;
         d[0] = (int32_t)((uint32_t)kHeaderBase + w);
-        for (uint32_t j = 0; j < len; ++j) d[1 + j] = s[1 + j];
+        for (uint32_t j = 0; j < len; ++j) d[1 + j] = s[kRunHdr + j];
       }
       base += __shfl(incl, 63, 64);
     }
@@ -1852,7 +1893,7 @@ __global__ void k_tiles_to_words(const int32_t* tok, const uint64_t* tile_off, c
         run = wtok + woff[w];
         len = 0;
       } else if (run) {
-        run[1 + len++] = v;
+        run[kRunHdr + len++] = v;
       }
     }
     if (run) run[0] = (int32_t)len;
@@ -2069,7 +2110,7 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
           const int32_t r = (int32_t)(uint32_t)(p[i] - kHeaderBase);
           if (nw == 0) tr0[t] = r;
           else if (r != tr0[t] + (int32_t)nw) bad[(size_t)k] = 1;  // ranks not consecutive
-          if (nw) ints += (1u + wl + 3u) & ~3u;
+          if (nw) ints += run_cap(wl);
           ++nw;
           wl = 0;
         } else {
@@ -2078,7 +2119,7 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
           ++ntk;
         }
       }
-      if (nw) ints += (1u + wl + 3u) & ~3u;
+      if (nw) ints += run_cap(wl);
       tnw[t] = nw;
       tints[t] = ints;
       ttok[t] = ntk;
@@ -2109,9 +2150,10 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
       int32_t* len = nullptr;
       for (uint32_t i = 0; i < ts.len[t]; ++i) {
         if (p[i] < kHeaderLimit) {
-          if (len) o = (o + 3u) & ~3ull;
+          if (len) o = (o + kRunAlign - 1u) & ~(uint64_t)(kRunAlign - 1u);
           woff[w++] = (uint32_t)o;
-          len = &wtok[o++];
+          len = &wtok[o];
+          o += kRunHdr;  // (the weight ints are filled on the device: k_wl_set_weights)
         } else {
           wtok[o++] = p[i];
           ++*len;
@@ -2125,6 +2167,7 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
   ntok_ = ntok;
   ntiles_ = (uint32_t)ts.num_tiles();
   if (nwords_ == 0 || nint_ >= (1ull << 31)) return false;  // hipcub sizes are int
+  if (nwords_ > kWordMask) return false;  // word ids share the pool entry with the run's groups
   // the pool (below) is addressed with 32-bit offsets (pool top, lst_, directory values)
   if (3 * ntok_ + 4096 >= (1ull << 32)) return false;
   for (uint32_t w = 0; w < nwords_; ++w)
@@ -2139,6 +2182,8 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
   hipStream_t s = S(stream_);
   WL_OK(hipMemcpyAsync(wtok0_, wtok.data(), (nint_ + kRunPad) * sizeof(int32_t), hipMemcpyHostToDevice, s));
   WL_OK(hipMemcpyAsync(woff_, woff.data(), woff.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  k_wl_set_weights<<<(int)std::min<uint32_t>((nwords_ + 255) / 256, 4096), 256, 0, s>>>(wtok0_, woff_, nwords_, weight_);
+  WL_OK(hipGetLastError());
   WL_OK(hipMemcpyAsync(tile_first_, tfirst.data(), ntiles_ * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   WL_OK(hipMemcpyAsync(tile_nw_, tnw.data(), ntiles_ * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   WL_OK(hipMemcpyAsync(wtok_, wtok0_, (nint_ + kRunPad) * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
@@ -2161,8 +2206,23 @@ bool WordLoop::upload(const TiledStream& ts, const uint64_t* d_weight) {
 // The index of the current words: every (pair, word) once, grouped by pair.
 void WordLoop::build_index() {
   hipStream_t s = S(stream_);
-  const uint64_t n = nint_;
   size_t acc = 0;
+  // the pairs of the current words, compactly: per-word counts, their exclusive sum
+  uint32_t* pbase = wl_alloc<uint32_t>((size_t)nwords_ + 2, &acc);
+  uint32_t* pcnt = wl_alloc<uint32_t>((size_t)nwords_ + 2, &acc);
+  k_wl_pair_counts<<<(int)std::min<uint32_t>((nwords_ + 256) / 256, 4096), 256, 0, s>>>(wtok_, woff_, nwords_, pcnt);
+  WL_OK(hipGetLastError());
+  {
+    size_t tb = 0;
+    WL_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, pcnt, pbase, (int)nwords_ + 1, s));
+    void* t0 = wl_alloc<uint8_t>(tb, &acc);
+    WL_OK(hipcub::DeviceScan::ExclusiveSum(t0, tb, pcnt, pbase, (int)nwords_ + 1, s));
+    WL_OK(hipStreamSynchronize(s));
+    WL_OK(hipFree(t0));
+  }
+  uint32_t npairs = 0;
+  WL_OK(hipMemcpy(&npairs, pbase + nwords_, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  const uint64_t n = std::max<uint64_t>(npairs, 1);
   u64* kin = wl_alloc<u64>(n, &acc);
   u64* kout = wl_alloc<u64>(n, &acc);
   uint32_t* vin = wl_alloc<uint32_t>(n, &acc);
@@ -2172,7 +2232,11 @@ void WordLoop::build_index() {
   uint32_t* pos = wl_alloc<uint32_t>(n + 1, &acc);
   uint32_t* kidx = wl_alloc<uint32_t>(n + 1, &acc);
   const int grid = 2048;
-  k_wl_emit_pairs<<<grid, 256, 0, s>>>(wtok_, woff_, nwords_, unk_, kin, vin);
+  if (npairs == 0) {
+    WL_OK(hipMemsetAsync(kin, 0xFF, sizeof(u64), s));
+    WL_OK(hipMemsetAsync(vin, 0, sizeof(uint32_t), s));
+  }
+  k_wl_emit_pairs<<<grid, 256, 0, s>>>(wtok_, woff_, pbase, nwords_, unk_, kin, vin);
   WL_OK(hipGetLastError());
   size_t tmp_bytes = 0, tb2 = 0;
   WL_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, vout, (int)n, 0, 64, s));
@@ -2204,7 +2268,7 @@ void WordLoop::build_index() {
   WL_OK(hipGetLastError());
   WL_OK(hipStreamSynchronize(s));
   for (void* p : {(void*)kin, (void*)kout, (void*)vin, (void*)vout, (void*)keep, (void*)head, (void*)pos, (void*)kidx,
-                  tmp})
+                  tmp, (void*)pbase, (void*)pcnt})
     WL_OK(hipFree(p));
   // the directory: at most half full
   uint64_t want = 1024;
@@ -2251,8 +2315,8 @@ bool WordLoop::load_current(const TiledStream& ts) {
       } else {
         if (!open) return false;
         int32_t& len = wtok[woff_h_[w]];
-        if (1u + (uint32_t)len >= woff_h_[w + 1] - woff_h_[w]) return false;  // past the run
-        wtok[woff_h_[w] + 1 + (uint32_t)len] = p[i];
+        if (kRunHdr + (uint32_t)len >= woff_h_[w + 1] - woff_h_[w]) return false;  // past the run
+        wtok[woff_h_[w] + kRunHdr + (uint32_t)len] = p[i];
         ++len;
       }
     }
@@ -2260,6 +2324,8 @@ bool WordLoop::load_current(const TiledStream& ts) {
   if (!open || w + 1 != nwords_) return false;
   hipStream_t s = S(stream_);
   WL_OK(hipMemcpyAsync(wtok_, wtok.data(), wtok.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  k_wl_set_weights<<<(int)std::min<uint32_t>((nwords_ + 255) / 256, 4096), 256, 0, s>>>(wtok_, woff_, nwords_, weight_);
+  WL_OK(hipGetLastError());
   WL_OK(hipStreamSynchronize(s));
   build_index();
   dirty_ = false;
