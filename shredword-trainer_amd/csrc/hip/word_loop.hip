@@ -148,6 +148,14 @@ struct WEnt {
             // capacity, at most kStripV: a word's run load issues only those, round 6)
   u64 sig;
 };
+// The small-merge path hands its records over without ordering them before the flag (round 6):
+// the records, the header and two tagged checksum granules go out back to back behind one release
+// fence, and the host accepts them once both granules carry the command's tag and the checksum of
+// header words 0..31 and the records matches (so a record still in flight is never read).  The
+// checksum weighs word i by an odd constant of its position, so records swapped between positions
+// or a stale block do not cancel out.
+__host__ __device__ __forceinline__ u64 hand_weight(uint32_t i) { return 0x9E3779B97F4A7C15ull + 2ull * i; }
+constexpr int kCksWord = 30;  // header u64 words 30, 31: seq << 32 | checksum low / high half
 constexpr int kGroupShift = 28;
 constexpr u64 kWordMask = (1ull << kGroupShift) - 1;
 __host__ __device__ __forceinline__ uint32_t ent_groups(u64 e) { return (uint32_t)(e >> kGroupShift) & 0xFu; }
@@ -1281,12 +1289,15 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
           const uint32_t nk = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
           uint32_t ri = incl - nb;
           WL_ST(if (lane == 0) S.xs[13] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
+          u64 cks = 0;  // this lane's share of the hand-off checksum
           for (; bw; bw &= bw - 1u, ++ri) {
             const uint32_t h = (uint32_t)lane * 32u + (uint32_t)__builtin_ctz(bw);
             u64* dst = reinterpret_cast<u64*>(sd.recs + ri);
-            dst[0] = (u64)s_h.key[h];
-            dst[1] = s_h.sum[h];
-            dst[2] = s_h.ft[h];
+            const u64 w0 = (u64)s_h.key[h], w1 = s_h.sum[h], w2 = s_h.ft[h];
+            dst[0] = w0;
+            dst[1] = w1;
+            dst[2] = w2;
+            cks += w0 * hand_weight(16u + 3u * ri) + w1 * hand_weight(17u + 3u * ri) + w2 * hand_weight(18u + 3u * ri);
             s_h.key[h] = kEmpty32;
             s_h.sum[h] = 0;
             s_h.ft[h] = kEmpty64;
@@ -1300,6 +1311,8 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
             dst[0] = (u64)key;
             dst[1] = sum;
             dst[2] = ft;
+            const uint32_t r = nk + i;
+            cks += (u64)key * hand_weight(16u + 3u * r) + sum * hand_weight(17u + 3u * r) + ft * hand_weight(18u + 3u * r);
           }
           WL_ST(if (lane == 0) S.xs[10] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_cmd);)
           if (lane == 0) {
@@ -1316,7 +1329,7 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
             u64* hs64 = reinterpret_cast<u64*>(hs);
             const u64 now = __builtin_amdgcn_s_memrealtime();
             hs[0] = nk + nsp;
-            hs[1] = 0u;  // (the flag word: written last, by the release)
+            hs[1] = 0u;  // (the flag word: the ordered paths' flag; this path's are the checksum granules)
             hs[2] = (uint32_t)cnt;
             hs[3] = S.nchg;
             hs64[2] = S.occ;
@@ -1341,7 +1354,21 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
             S.t_idle = 0;
             S.t_undo = 0;
           }
-          if (lane < 8) reinterpret_cast<int4*>(sd.hdr)[lane] = reinterpret_cast<const int4*>(S.hs)[lane];
+          if (lane < 8) {
+            const int4 hv = reinterpret_cast<const int4*>(S.hs)[lane];
+            reinterpret_cast<int4*>(sd.hdr)[lane] = hv;
+            const u64 lo = (u64)(uint32_t)hv.x | ((u64)(uint32_t)hv.y << 32), hi = (u64)(uint32_t)hv.z | ((u64)(uint32_t)hv.w << 32);
+            cks += lo * hand_weight(2u * lane) + hi * hand_weight(2u * lane + 1u);
+          }
+          {  // the wave's sum (DPP row shifts and broadcasts, lane 63), then the tagged granules
+            cks += wl_dpp64<0x111>(cks);
+            cks += wl_dpp64<0x112>(cks);
+            cks += wl_dpp64<0x114>(cks);
+            cks += wl_dpp64<0x118>(cks);
+            cks += wl_dpp64<0x142, 0xa, false>(cks);
+            cks += wl_dpp64<0x143, 0xc, false>(cks);
+            cks = rl64(cks, 63);
+          }
           if (lane == 0) {
             const u64 t_r0 = __builtin_amdgcn_s_memrealtime();
             // stamps build: [1] the shader clock (MHz) over the merge, [9] cycles of one s_memrealtime
@@ -1349,8 +1376,12 @@ __global__ __launch_bounds__(kWlThreads) void k_word_loop(WlParams p) {
                 const u64 c_now = __builtin_amdgcn_s_memtime(); const u64 t_now = __builtin_amdgcn_s_memrealtime();
                   S.xs[1] = (uint32_t)((c_now - c_cmd) * 100ull / (t_now - t_cmd + 1ull));
                   S.xs[11] = (uint32_t)(t_r0 - t_cmd); for (int i = 0; i < kXs; ++i) sd.hdr[32 + i] = S.xs[i];)
-            // one system-scope release: this wave's record and header stores, then the flag
-            __hip_atomic_store(sd.hdr + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the checksum granules right behind the records and the header (no drain between), then
+            // one system-scope release fence: the L2 write-back that sends them all out promptly
+            u64* h64w = reinterpret_cast<u64*>(sd.hdr);
+            h64w[kCksWord] = ((u64)seq << 32) | (cks & 0xFFFFFFFFull);
+            h64w[kCksWord + 1] = ((u64)seq << 32) | (cks >> 32);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             S.t_rel = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_r0);
           }
         } else if (pfon && wid == poll_wave) {  // the next command's granules, in flight meanwhile
@@ -2366,7 +2397,10 @@ void WordLoop::reset() {
 
 void WordLoop::ensure_slots(uint32_t cap) {
   const uint32_t rec_cap = 4 * (cap + 1) + 64;
-  const unsigned pin = hipHostMallocMapped | hipHostMallocCoherent;
+  // records and headers: non-coherent pinned memory (the device's L2 holds the stores until the
+  // release fence writes them back in one go; tools/rec_probe.hip: post -> every record seen
+  // 3.1 us coherent + ordered flag, 2.3 us non-coherent + checksummed, round 6)
+  const unsigned pin = hipHostMallocMapped | hipHostMallocNonCoherent;
   for (Slot& sl : slot_) {
     if (sl.host_recs) WL_OK(hipHostFree(sl.host_recs));
     WL_OK(hipHostMalloc((void**)&sl.host_recs, (size_t)rec_cap * sizeof(DeltaRecord), pin));
@@ -2507,11 +2541,30 @@ void WordLoop::post_merge(int32_t a, int32_t b, int32_t X) {
   dirty_ = true;
 }
 
+// The small-merge path's hand-off (see hand_weight): both granules tagged with seq, then the
+// checksum of header words 0..31 and the header's record count of records.
+bool WordLoop::handed_over(const Slot& sl, uint32_t seq) const {
+  const uint64_t* h64 = reinterpret_cast<const uint64_t*>(sl.host_hdr);
+  const uint64_t g0 = __atomic_load_n(&h64[kCksWord], __ATOMIC_ACQUIRE), g1 = __atomic_load_n(&h64[kCksWord + 1], __ATOMIC_ACQUIRE);
+  if ((uint32_t)(g0 >> 32) != seq || (uint32_t)(g1 >> 32) != seq) return false;
+  const uint64_t want = (g0 & 0xFFFFFFFFull) | (g1 << 32);
+  const uint32_t n = __atomic_load_n(&sl.host_hdr[0], __ATOMIC_ACQUIRE);
+  if (n > sl.rec_cap) return false;
+  uint64_t c = 0;
+  for (uint32_t i = 0; i < 16; ++i) c += __atomic_load_n(&h64[i], __ATOMIC_RELAXED) * hand_weight(i);
+  const uint64_t* r = reinterpret_cast<const uint64_t*>(sl.host_recs);
+  for (uint32_t i = 0; i < 3 * n; ++i) c += __atomic_load_n(&r[i], __ATOMIC_RELAXED) * hand_weight(16u + i);
+  return c == want;
+}
+
 void WordLoop::wait_flag(const Slot& sl, uint32_t seq) {
   volatile uint32_t* flag = sl.host_hdr + 1;
+  const uint64_t* h64 = reinterpret_cast<const uint64_t*>(sl.host_hdr);
   const double t0 = now_seconds();
   unsigned spins = 0;
-  while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+  for (;;) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;  // the ordered paths' flag
+    if ((uint32_t)(__atomic_load_n(&h64[kCksWord + 1], __ATOMIC_ACQUIRE) >> 32) == seq && handed_over(sl, seq)) break;
     __builtin_ia32_pause();
     if (++spins % 4096 != 0) continue;
     const uint32_t st = __atomic_load_n(&status_[0], __ATOMIC_ACQUIRE);
@@ -2586,7 +2639,9 @@ size_t WordLoop::collect(int32_t X, const DeltaRecord** recs) {
 bool WordLoop::peek(int32_t X, const DeltaRecord** recs, size_t* n) const {
   if (posted_.empty() || posted_.front().X != X) return false;
   const Slot& sl = slot_[(uint32_t)X & (kSlots - 1)];
-  if (__atomic_load_n(sl.host_hdr + 1, __ATOMIC_ACQUIRE) != posted_.front().seq) return false;
+  if (__atomic_load_n(sl.host_hdr + 1, __ATOMIC_ACQUIRE) != posted_.front().seq &&
+      !handed_over(sl, posted_.front().seq))
+    return false;
   if (sl.host_hdr[22]) return false;  // ordered changes already: nothing for the apply helper to prepare
   const size_t k = sl.host_hdr[0];
   if (k > sl.rec_cap) return false;  // collect() reports it

@@ -196,6 +196,7 @@ class WordLoop {
   // Writes one command; (loff, lcnt1): the words-of list of max(a, b) if known (count + 1; 0: none).
   uint32_t post(uint32_t op, int32_t a, int32_t b, int32_t X, uint32_t loff = 0, uint32_t lcnt1 = 0);
   void wait_flag(const Slot& s, uint32_t seq);
+  bool handed_over(const Slot& s, uint32_t seq) const;  // the small-merge path's checksummed hand-off
   void ensure_slots(uint32_t cap);
 
   int ordinal_ = 0;
