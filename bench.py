@@ -842,7 +842,22 @@ def main():
     if sim_shards:
         os.environ.setdefault("SHREDWORD_LOAD_SIM_SHARDS", str(sim_shards))
 
+    allowed0 = set(os.sched_getaffinity(0))
     pinned = None if args.no_pin else pin_host_loop(local, dev)
+    # The pin is for the merge loop (the host replay's tables in one L3).  A load runs on the
+    # process's whole CPU share: its 16 readers confined to one 8-core domain measured 0.65 s for
+    # C3 against 0.47-0.50 s on the GPU's NUMA node (profiles/r06_load_pin_ab.json);
+    # SHREDWORD_BENCH_LOAD_PIN=1 keeps the load on the domain too.
+    load_unpinned = pinned is not None and os.environ.get("SHREDWORD_BENCH_LOAD_PIN", "0") != "1"
+
+    def load(p):
+        if load_unpinned:
+            os.sched_setaffinity(0, allowed0)
+        try:
+            t.load_corpus(p)
+        finally:
+            if load_unpinned:
+                os.sched_setaffinity(0, set(pinned))
     from shredword import dist as sdist
     from shredword.cbase import lib
     from shredword.trainer import BPETrainer
@@ -889,7 +904,7 @@ def main():
             t.set_option("resident", 0)  # ranks share one GPU: a whole-chip persistent loop per rank would not be co-resident
     barrier()
     t0 = time.time()
-    t.load_corpus(path)
+    load(path)
     load_s = time.time() - t0
     load_s_max = load_s
     if gather_state.get("fell_back"):
@@ -969,7 +984,7 @@ def main():
     if world == 1:
         try:
             t1 = time.time()
-            t.load_corpus(path)
+            load(path)
             later_load_s = time.time() - t1
         except Exception:  # noqa: BLE001 (the line stands without it)
             later_load_s = None
@@ -1065,10 +1080,13 @@ def main():
                           if pinned
                           else "not pinned"),
             "host_breakdown_s": {k: st[f"host_{k}_seconds"] for k in ("select", "launch", "wait", "apply")},
+            "host_apply_split_s": {k: st[f"host_apply_{k}_seconds"]
+                                   for k in ("combine", "correct", "finish", "early", "offer")},
             "init_s_last_step": st["init_seconds"],
             "selector_last_step": {k: st[k] for k in ("heap_pops", "heap_stale_pops", "heap_pushes", "delta_records",
                                                       "apply_cycles_combine", "apply_cycles_order",
-                                                      "apply_cycles_walk")},
+                                                      "apply_cycles_walk", "apply_cycles_push",
+                                                      "helper_adopted")},
             "tiles_visited_per_merge": st["tiles_visited"] / max(1, merges),
             "speculation": {"hits": st["spec_hits"], "misses": st["spec_misses"],
                             "hit_rate": st["spec_hits"] / max(1, st["spec_hits"] + st["spec_misses"])},

@@ -225,6 +225,13 @@ typedef struct ShredStats {
   double sel_table_us;         /* tiebreak=device: of sel_merge_us, the pair-table + frontier update */
   uint64_t index_spill_merges; /* k_word_loop: merges whose delta keys overflowed the LDS hash into HBM */
   uint64_t index_spill_keys;   /*   Σ their spilled keys */
+  /* host_apply_seconds split (round 6): the records' combine + order on the main thread (merges
+   * whose combine ran on the helper thread: helper_adopted), the late correction, the pair-info
+   * walk + heap pushes (apply_cycles_walk / apply_cycles_push TSC cycles of it), the early guess,
+   * the helper hand-over */
+  double host_apply_combine_seconds, host_apply_correct_seconds, host_apply_finish_seconds;
+  double host_apply_early_seconds, host_apply_offer_seconds;
+  uint64_t helper_adopted, apply_cycles_push;
 } ShredStats;
 int shred_get_stats(const Trainer* trainer, ShredStats* out);
 

@@ -50,6 +50,12 @@ void Engine::count_bigrams(Backend& be) {
   std::vector<PairCount> pairs;
   be.count_pairs(unk_, &pairs);
   const size_t unique = pairs.size();
+  if (capture_) {  // SHREDWORD_APPLY_CAPTURE: the counts the selector starts from
+    const uint64_t n = pairs.size();
+    std::fwrite("P", 1, 1, capture_);
+    std::fwrite(&n, 8, 1, capture_);
+    std::fwrite(pairs.data(), sizeof(PairCount), n, capture_);
+  }
   sel_.add_counts(std::move(pairs));
   check_exact(be);
   if (log_ >= 1)
@@ -245,12 +251,21 @@ bool Engine::merge_one(Backend& be, int remaining) {
   }
   const size_t n = adopted ? 0 : be.collect(X, &recs);
   const double t3 = now_seconds();
+  if (capture_ && !adopted && !be.records_are_changes()) {  // one merge's records, for host replays
+    const int32_t h[3] = {a, b, X};
+    const uint64_t nn = n;
+    std::fwrite("M", 1, 1, capture_);
+    std::fwrite(h, 4, 3, capture_);
+    std::fwrite(&nn, 8, 1, capture_);
+    std::fwrite(recs, sizeof(DeltaRecord), n, capture_);
+  }
   if (!adopted) {
     if (be.records_are_changes())
       sel_.apply_changes(a, b, X, reinterpret_cast<const Selector::Change*>(recs), n);
     else
       sel_.apply_combine(a, b, X, recs, n);
   }
+  const double ta = now_seconds();
   // Late correction: with (a, b)'s changes known, a new pair holding X that is strictly more
   // frequent than the guess in flight (made before them; its own count is unchanged by this
   // merge) replaces it now, so the device undoes and redoes the guess while this merge is
@@ -272,7 +287,9 @@ bool Engine::merge_one(Backend& be, int remaining) {
       be.post_guess(pa, pb, X + 1);
     }
   }
+  const double tb = now_seconds();
   sel_.apply_finish(a, b, X);
+  const double tc = now_seconds();
   // Early guess: with X applied, the guess for X+2 is made now, on the heap the coming selects
   // will pop (the guess for X+1 and every pair sharing its tokens counted as changing), and posted
   // at once, so the device has X+2 queued before it finishes X+1.  The selects of X+1 happen after
@@ -290,6 +307,7 @@ bool Engine::merge_one(Backend& be, int remaining) {
       be.post_guess(g.a, g.b, g.X);
     }
   }
+  const double td = now_seconds();
   if (spec) helper_offer(be);  // X+1's records, if they have landed
   times_.launch_s += t2 - t1;
   times_.wait_s += t3 - t2;
@@ -302,6 +320,11 @@ bool Engine::merge_one(Backend& be, int remaining) {
   }
   const double t4 = now_seconds();
   times_.apply_s += t4 - t3;
+  times_.combine_s += ta - t3;
+  times_.correct_s += tb - ta;
+  times_.finish_s += tc - tb;
+  times_.early_s += td - tc;
+  times_.offer_s += t4 - td;
   if (mtrace_on_)
     mtrace_.push_back(MergeTime{(float)(1e6 * (t1 - t0)), (float)(1e6 * (t2 - t1)), (float)(1e6 * (t3 - t2)),
                                 (float)(1e6 * (t4 - t3)), (uint32_t)n, (uint8_t)(launched ? 1 : 0)});
@@ -529,6 +552,16 @@ int Engine::train(Backend& be) {
   selector_stale_ = false;
   sel_.reset(unk_, min_freq_);  // bpe_init (bpe.cpp:98-108)
   mtrace_on_ = std::getenv("SHREDWORD_ENGINE_TRACE") != nullptr;
+  // Diagnostic: the selector's inputs of this train() (the initial counts, every merge's records)
+  // to a file, so the host half can be replayed and timed without a device (tools/apply_replay.cpp)
+  if (const char* cp = std::getenv("SHREDWORD_APPLY_CAPTURE")) {
+    capture_ = std::fopen(cp, "wb");
+    if (capture_) {
+      const int64_t h[2] = {unk_, (int64_t)min_freq_};
+      std::fwrite("R", 1, 1, capture_);
+      std::fwrite(h, 8, 2, capture_);
+    }
+  }
   if (const char* e = std::getenv("SHREDWORD_SIM_SELECT")) sel_.set_simulate_pops(std::atoi(e) != 0);
   mtrace_.clear();
   count_bigrams(be);
@@ -563,6 +596,10 @@ int Engine::train(Backend& be) {
   }
   finish_speculation(be);
   helper_stop();
+  if (capture_) {
+    std::fclose(capture_);
+    capture_ = nullptr;
+  }
   be.quiesce();
   if (trace_) std::fflush(trace_);
   times_.train_s += now_seconds() - t0;

@@ -103,6 +103,9 @@ struct EngineTimes {
   double select_s = 0, launch_s = 0, wait_s = 0, apply_s = 0;
   double wait_hit_s = 0, wait_miss_s = 0;  // wait_s of merges whose guess ran / had to be posted
   uint64_t n_hit = 0, n_miss = 0;
+  // apply_s split: the records' combine on this thread, the late correction, the info walk and
+  // heap pushes, the early guess, the helper hand-over
+  double combine_s = 0, correct_s = 0, finish_s = 0, early_s = 0, offer_s = 0;
 };
 
 class Engine {
@@ -194,6 +197,7 @@ class Engine {
   uint64_t min_freq_ = 2000;
   int log_ = 1;
   FILE* trace_ = nullptr;
+  FILE* capture_ = nullptr;  // SHREDWORD_APPLY_CAPTURE (train(): counts + records)
   Selector sel_;
   std::vector<int32_t> merge_a_, merge_b_;
   EngineTimes times_;

@@ -462,6 +462,11 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
   s->host_launch_seconds = et.launch_s;
   s->host_wait_seconds = et.wait_s;
   s->host_apply_seconds = et.apply_s;
+  s->host_apply_combine_seconds = et.combine_s;
+  s->host_apply_correct_seconds = et.correct_s;
+  s->host_apply_finish_seconds = et.finish_s;
+  s->host_apply_early_seconds = et.early_s;
+  s->host_apply_offer_seconds = et.offer_s;
   if (t->dev) {
     const KernelTimes& k = t->dev->times();
     s->merge_kernel_ms = k.merge_ms;
@@ -545,6 +550,8 @@ int shred_get_stats(const Trainer* tc, ShredStats* s) {
   s->apply_cycles_combine = c.cyc_combine;
   s->apply_cycles_order = c.cyc_order;
   s->apply_cycles_walk = c.cyc_walk;
+  s->apply_cycles_push = c.cyc_push;
+  s->helper_adopted = t->engine.helper_used();
   if (t->dev) s->tiles_visited = t->dev->visited_tiles();
   if (t->dev) s->exchange_overflows = t->dev->exchange_overflows();
   s->spec_hits = t->engine.spec_hits();

@@ -84,7 +84,11 @@ class ShredStats(Structure):
                 ("sel_host_merges", c_uint64), ("sel_table_grows", c_uint64),
                 ("index_raw_records", c_uint64), ("index_finalized", c_uint64),
                 ("index_dev_out_us", c_double), ("index_dev_fin_us", c_double), ("index_fin_records", c_uint64),
-                ("sel_table_us", c_double), ("index_spill_merges", c_uint64), ("index_spill_keys", c_uint64)]
+                ("sel_table_us", c_double), ("index_spill_merges", c_uint64), ("index_spill_keys", c_uint64),
+                ("host_apply_combine_seconds", c_double), ("host_apply_correct_seconds", c_double),
+                ("host_apply_finish_seconds", c_double), ("host_apply_early_seconds", c_double),
+                ("host_apply_offer_seconds", c_double), ("helper_adopted", c_uint64),
+                ("apply_cycles_push", c_uint64)]
 
 
 Trainer = c_void_p
