@@ -87,7 +87,7 @@ struct Slot {
   u64 key;     // 0 = empty; else mix(hash, len, seed) | 1
   u64 cnt;
   u64 nfirst;  // ~(min first offset): 0 = none yet, so the table clears with one memset
-  u64 coff;    // the creator's occurrence (bytes past kSpell are compared with it)
+  u64 coff;    // the creator's occurrence + 1 (bytes past kSpell are compared with it)
   uint4 spell;   // the creator's first kSpell bytes, zero-padded
   uint32_t len;  // 0 until the creator has published coff / bkt / spell
   uint32_t bkt;  // djb2 & 4095
@@ -168,12 +168,16 @@ __device__ __forceinline__ bool same_tail(const uint8_t* d, u64 a, u64 b, uint32
 }
 
 // Adds (cnt, first) to key's slot; w: the word's first kSpell bytes, packed and zero-padded.
-// Exactness: the slot's creator publishes its length, spelling and occurrence (release, then the
-// length), and every other add compares its length and first kSpell bytes with the slot's and,
-// past kSpell, its bytes with the creator's occurrence -- so every occurrence behind one key
-// equals the creator's word, or flags[1] is raised (a 64-bit key collision: the count is repeated
-// with another seed).  An add that finds the slot still unpublished is appended to t.defer and
-// compared after the count (k_word_verify); a full list raises flags[1] too.
+// Exactness: the slot's creator publishes its spelling, occurrence (+ 1) and length, and every
+// other add compares its length and first kSpell bytes with the slot's and, past kSpell, its bytes
+// with the creator's occurrence; an add that does not see a match -- the slot not yet published,
+// a partly published one, or a different word behind the same 64-bit key -- is appended to
+// t.defer and compared after the count (k_word_verify), which raises flags[1] on a real mismatch
+// (the count is then repeated with another seed); a full list raises flags[1] too.  So every
+// occurrence behind one key equals the creator's word.  The fields are agent-scope relaxed atomics
+// and no add fences: a stale read can only fail the compare (a word has a non-zero first byte)
+// and send the add to the checked list, and no L2 is written back or invalidated per add (round
+// 6's first version fenced each add: 2x the count's traffic).
 __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 key, uint32_t len, u64 cnt, u64 first,
                                           const uint32_t (&w)[kSpell / 4]) {
   u64 s = key & t.mask;
@@ -183,10 +187,12 @@ __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 
     if (prev == 0ull) {
       prev = atomicCAS(&e.key, 0ull, key);
       if (prev == 0ull) {  // created: publish, then count
-        e.coff = first;
-        e.bkt = (len <= (uint32_t)kSpell ? djb2_spell(w, len) : djb2_global(d, first, len)) & 4095u;
-        e.spell = make_uint4(w[0], w[1], w[2], w[3]);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&e.coff, first + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&e.bkt, (len <= (uint32_t)kSpell ? djb2_spell(w, len) : djb2_global(d, first, len)) & 4095u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        u64* sp64 = reinterpret_cast<u64*>(&e.spell);
+        __hip_atomic_store(sp64, (u64)w[0] | ((u64)w[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sp64 + 1, (u64)w[2] | ((u64)w[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&e.len, len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (atomicAdd(t.nkeys, 1u) > (uint32_t)((t.mask + 1) / 4 * 3)) atomicOr(&t.flags[0], 1u);
         atomicAdd(&e.cnt, cnt);
@@ -198,17 +204,19 @@ __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 
       atomicAdd(&e.cnt, cnt);
       atomicMax(&e.nfirst, ~first);
       const uint32_t sl = __hip_atomic_load(&e.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (sl == 0u) {
+      const u64* sp64 = reinterpret_cast<const u64*>(&e.spell);
+      const u64 s0 = __hip_atomic_load(sp64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const u64 s1 = __hip_atomic_load(sp64 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bool same = sl == len && s0 == ((u64)w[0] | ((u64)w[1] << 32)) && s1 == ((u64)w[2] | ((u64)w[3] << 32));
+      if (same && len > (uint32_t)kSpell) {
+        const u64 c = __hip_atomic_load(&e.coff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        same = c != 0ull && same_tail(d, first, c - 1ull, len);
+      }
+      if (!same) {
         const uint32_t i = atomicAdd(t.ndefer, 1u);
         if (i < kDeferCap) t.defer[i] = Deferred{first, (uint32_t)s, len};
         else atomicOr(&t.flags[1], 1u);
-        return;
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const uint4 sp = e.spell;
-      bool same = sl == len && sp.x == w[0] && sp.y == w[1] && sp.z == w[2] && sp.w == w[3];
-      if (same && len > (uint32_t)kSpell) same = same_tail(d, first, e.coff, len);
-      if (!same) atomicOr(&t.flags[1], 1u);
       return;
     }
     s = (s + 1) & t.mask;
@@ -407,7 +415,7 @@ __global__ void k_word_verify(const uint8_t* d, Table t) {
     uint32_t w[kSpell / 4] = {0, 0, 0, 0};
     for (uint32_t k = 0; k < q.len && k < (uint32_t)kSpell; ++k) w[k / 4] |= (uint32_t)d[q.first + k] << (8 * (k % 4));
     bool same = e.len == q.len && e.spell.x == w[0] && e.spell.y == w[1] && e.spell.z == w[2] && e.spell.w == w[3];
-    if (same && q.len > (uint32_t)kSpell) same = same_tail(d, q.first, e.coff, q.len);
+    if (same && q.len > (uint32_t)kSpell) same = e.coff != 0ull && same_tail(d, q.first, e.coff - 1ull, q.len);
     if (!same) atomicOr(&t.flags[1], 1u);
   }
 }
