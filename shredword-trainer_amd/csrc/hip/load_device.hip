@@ -7,11 +7,10 @@
 //                  (maximal runs of bytes outside "\t\r\n "), hashes each (64-bit FNV-1a + length
 //                  mix) with its djb2 & 4095 (the reference StrMap bucket), and counts it in a
 //                  per-workgroup LDS table (count, min first offset) that spills to, and is
-//                  flushed into, one open-addressing HBM table of 64-byte slots with 64-bit
-//                  atomics.  Every occurrence is compared byte for byte with the word that
-//                  created its key's slot (its first 16 bytes kept in the slot), so a 64-bit key
-//                  collision is detected (the count is then repeated with another seed) and the
-//                  table is exact;
+//                  flushed into, one open-addressing HBM table with 64-bit atomics.  Every
+//                  occurrence is compared byte for byte with an earlier occurrence of its key
+//                  (the one atomicMin hands back), so a 64-bit key collision is detected (the
+//                  count is then repeated with another seed) and the table is exact;
 //   k_word_compact entries -> (bucket << 52 | first offset) keys, radix-sorted (hipCUB): the
 //                  reference word order, since first offsets are distinct;
 //   k_word_gather  rank -> {first, count, length} records for the host.
@@ -78,36 +77,19 @@ constexpr int kLoadShapeDefault = 2;  // xwide: C3 load 1.09-1.12 s -> 0.92-0.95
 __device__ __forceinline__ bool delim(uint32_t c) { return c == 9u || c == 13u || c == 10u || c == 32u; }
 __device__ __forceinline__ uint32_t has_zero(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
 
-// One 64-byte HBM slot per distinct word: a probe, its atomics and (for words of up to kSpell
-// bytes) its exactness check touch one cache line.  Round 6: the creator's spelling lives in the
-// slot, so an add compares with it in place; round 5's 32-byte slot compared every add with an
-// earlier occurrence in the text (a second random line per add: k_word_count moved 4.8x its
-// bytes).
+// One 32-byte HBM slot per distinct word (a probe and its atomics touch one cache line).
 struct Slot {
   u64 key;     // 0 = empty; else mix(hash, len, seed) | 1
   u64 cnt;
   u64 nfirst;  // ~(min first offset): 0 = none yet, so the table clears with one memset
-  u64 coff;    // the creator's occurrence + 1 (bytes past kSpell are compared with it)
-  uint4 spell;   // the creator's first kSpell bytes, zero-padded
-  uint32_t len;  // 0 until the creator has published coff / bkt / spell
+  uint32_t len;
   uint32_t bkt;  // djb2 & 4095
-  u64 pad;
 };
-static_assert(sizeof(Slot) == 64, "slot layout");
-
-// An add that finds its slot not yet published by the creator (a race of a few hundred cycles):
-// checked after the count by k_word_verify instead of waiting (no wave ever spins on another).
-struct Deferred {
-  u64 first;
-  uint32_t slot, len;
-};
-constexpr uint32_t kDeferCap = 1u << 20;
+static_assert(sizeof(Slot) == 32, "slot layout");
 
 struct Table {
   Slot* slot;
   u64 mask;         // capacity - 1
-  Deferred* defer;  // kDeferCap entries
-  uint32_t* ndefer;
   uint32_t* nkeys;
   uint32_t* flags;  // [0] table too full, [1] key collision, [2] a NUL byte in the text, [3] a word
                     // past a segment's landed bytes
@@ -130,6 +112,23 @@ __device__ __forceinline__ uint32_t tile_byte(const uint8_t* s, const uint8_t* d
   return p < (uint32_t)kTileBytes ? s[(p / kChunkBytes) * kTileStride + (p % kChunkBytes)] : d[base + p];
 }
 
+// True when the words at d[a] and d[b] (a's length len) spell the same bytes.  The bytes are
+// loaded 16 at a time, every load of a batch issued before the first compare (one HBM round trip
+// per 16 bytes instead of one per byte); reads past a word stay inside the text's ' ' padding.
+__device__ __forceinline__ bool same_global(const uint8_t* d, u64 a, u64 b, uint32_t len) {
+  uint32_t diff = delim(d[b + len]) ? 0u : 1u;
+  for (uint32_t k = 0; k < len; k += 16) {
+    uint32_t x[16], y[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      x[j] = d[a + k + j];
+      y[j] = d[b + k + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) diff |= k + j < len ? x[j] ^ y[j] : 0u;
+  }
+  return diff == 0;
+}
 // djb2 (32 bits) of the len bytes at d[a], 16 loads in flight at a time.
 __device__ __forceinline__ uint32_t djb2_global(const uint8_t* d, u64 a, uint32_t len) {
   uint32_t dj = 5381u;
@@ -144,79 +143,29 @@ __device__ __forceinline__ uint32_t djb2_global(const uint8_t* d, u64 a, uint32_
   return dj;
 }
 
-// djb2 of a word of up to kSpell bytes from its packed spelling.
-__device__ __forceinline__ uint32_t djb2_spell(const uint32_t (&w)[kSpell / 4], uint32_t len) {
-  uint32_t dj = 5381u;
-  for (uint32_t k = 0; k < len; ++k) dj = dj * 33u + ((w[k / 4] >> (8 * (k % 4))) & 0xFFu);
-  return dj;
-}
-// True when bytes [kSpell, len) of the words at d[a] and d[b] are equal (their first kSpell
-// bytes and lengths already compared); 16 loads in flight at a time.
-__device__ __forceinline__ bool same_tail(const uint8_t* d, u64 a, u64 b, uint32_t len) {
-  uint32_t diff = 0;
-  for (uint32_t k = kSpell; k < len; k += 16) {
-    uint32_t x[16], y[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      x[j] = d[a + k + j];
-      y[j] = d[b + k + j];
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) diff |= k + j < len ? x[j] ^ y[j] : 0u;
-  }
-  return diff == 0;
-}
-
-// Adds (cnt, first) to key's slot; w: the word's first kSpell bytes, packed and zero-padded.
-// Exactness: the slot's creator publishes its spelling, occurrence (+ 1) and length, and every
-// other add compares its length and first kSpell bytes with the slot's and, past kSpell, its bytes
-// with the creator's occurrence; an add that does not see a match -- the slot not yet published,
-// a partly published one, or a different word behind the same 64-bit key -- is appended to
-// t.defer and compared after the count (k_word_verify), which raises flags[1] on a real mismatch
-// (the count is then repeated with another seed); a full list raises flags[1] too.  So every
-// occurrence behind one key equals the creator's word.  The fields are agent-scope relaxed atomics
-// and no add fences: a stale read can only fail the compare (a word has a non-zero first byte)
-// and send the add to the checked list, and no L2 is written back or invalidated per add (round
-// 6's first version fenced each add: 2x the count's traffic).
-__device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 key, uint32_t len, u64 cnt, u64 first,
-                                          const uint32_t (&w)[kSpell / 4]) {
+// Adds (cnt, first) to key's slot.  Exactness: every add but the slot's very first compares its
+// occurrence with the offset the atomic hands back — an occurrence some earlier add stored — so
+// all the occurrences behind one key are linked by byte-equal pairs, or flags[1] is raised (a
+// 64-bit key collision: the count is repeated with another seed).
+__device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 key, uint32_t bkt, uint32_t len,
+                                          u64 cnt, u64 first) {
   u64 s = key & t.mask;
   for (u64 probe = 0; probe < kTableProbes; ++probe) {
     Slot& e = t.slot[s];
-    u64 prev = __hip_atomic_load(&e.key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    u64 prev = e.key;
     if (prev == 0ull) {
       prev = atomicCAS(&e.key, 0ull, key);
-      if (prev == 0ull) {  // created: publish, then count
-        __hip_atomic_store(&e.coff, first + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&e.bkt, (len <= (uint32_t)kSpell ? djb2_spell(w, len) : djb2_global(d, first, len)) & 4095u,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        u64* sp64 = reinterpret_cast<u64*>(&e.spell);
-        __hip_atomic_store(sp64, (u64)w[0] | ((u64)w[1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sp64 + 1, (u64)w[2] | ((u64)w[3] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&e.len, len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == 0ull) {
+        e.len = len;
+        e.bkt = bkt;
         if (atomicAdd(t.nkeys, 1u) > (uint32_t)((t.mask + 1) / 4 * 3)) atomicOr(&t.flags[0], 1u);
-        atomicAdd(&e.cnt, cnt);
-        atomicMax(&e.nfirst, ~first);
-        return;
+        prev = key;
       }
     }
     if (prev == key) {
       atomicAdd(&e.cnt, cnt);
-      atomicMax(&e.nfirst, ~first);
-      const uint32_t sl = __hip_atomic_load(&e.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const u64* sp64 = reinterpret_cast<const u64*>(&e.spell);
-      const u64 s0 = __hip_atomic_load(sp64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const u64 s1 = __hip_atomic_load(sp64 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      bool same = sl == len && s0 == ((u64)w[0] | ((u64)w[1] << 32)) && s1 == ((u64)w[2] | ((u64)w[3] << 32));
-      if (same && len > (uint32_t)kSpell) {
-        const u64 c = __hip_atomic_load(&e.coff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        same = c != 0ull && same_tail(d, first, c - 1ull, len);
-      }
-      if (!same) {
-        const uint32_t i = atomicAdd(t.ndefer, 1u);
-        if (i < kDeferCap) t.defer[i] = Deferred{first, (uint32_t)s, len};
-        else atomicOr(&t.flags[1], 1u);
-      }
+      const u64 link = ~atomicMax(&e.nfirst, ~first);  // ~0: none yet (this is the key's first add)
+      if (link != ~0ull && !same_global(d, first, link, len)) atomicOr(&t.flags[1], 1u);
       return;
     }
     s = (s + 1) & t.mask;
@@ -232,8 +181,8 @@ __device__ __forceinline__ void table_add(const uint8_t* d, const Table& t, u64 
 // spills to, and at the end is flushed into, one open-addressing HBM table.
 // Exactness without a second pass: an LDS hit compares its bytes with the slot's kSpell-byte
 // spelling (LDS) and its length with the slot's; bytes past kSpell with the occurrence the
-// slot's atomicMin hands back (every occurrence is linked to the LDS creator's by byte-equal
-// pairs), and the flush and every spill compare with the HBM slot's creator (table_add).  A slot is used once its length is published
+// slot's atomicMin hands back (the same linking argument as table_add), and the flush and every
+// spill compare with the HBM slot's occurrence.  A slot is used once its length is published
 // (0 = being created: the occurrence then goes to HBM directly).  The reference StrMap bucket
 // (djb2 & 4095) is computed at the flush, from the slot's first occurrence.
 template <int kLoadThreads, int kLdsSlots>
@@ -282,9 +231,8 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
       for (int i = tid; i < kLdsSlots; i += kLoadThreads) {
         if (!s_key[i] || s_cnt[i] > s_thr) continue;
         const u64 first = range + s_first[i];
-        const uint4 sp = s_spell[i];
-        const uint32_t w[kSpell / 4] = {sp.x, sp.y, sp.z, sp.w};
-        table_add(d, t, s_key[i], s_len[i], s_cnt[i], first, w);
+        const uint32_t len = s_len[i];
+        table_add(d, t, s_key[i], djb2_global(d, first, len) & 4095u, len, s_cnt[i], first);
         s_key[i] = 0;
         s_first[i] = ~0u;
         s_cnt[i] = 0;
@@ -386,7 +334,9 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
       ++n_words;
       if (!done) {
         ++n_hbm;
-        table_add(d, t, key, len, 1ull, off, w);
+        uint32_t dj = 5381u;  // djb2 in 32 bits: its & 4095 equals the reference's 64-bit value's
+        for (uint32_t q = 0; q < len; ++q) dj = dj * 33u + tile_byte<kTileBytes>(s_tile, d, base, p + q);
+        table_add(d, t, key, dj & 4095u, len, 1ull, off);
       }
       p += len;
     }
@@ -400,23 +350,8 @@ __global__ __launch_bounds__(kLoadThreads) void k_word_count(const uint8_t* d, u
   for (int i = tid; i < kLdsSlots; i += kLoadThreads) {
     if (!s_key[i]) continue;
     const u64 first = range + s_first[i];
-    const uint4 sp = s_spell[i];
-    const uint32_t w[kSpell / 4] = {sp.x, sp.y, sp.z, sp.w};
-    table_add(d, t, s_key[i], s_len[i], s_cnt[i], first, w);
-  }
-}
-
-// The deferred adds of a count (table_add), against their slots' creators, after every add.
-__global__ void k_word_verify(const uint8_t* d, Table t) {
-  const uint32_t n = min(*t.ndefer, kDeferCap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const Deferred q = t.defer[i];
-    const Slot& e = t.slot[q.slot];
-    uint32_t w[kSpell / 4] = {0, 0, 0, 0};
-    for (uint32_t k = 0; k < q.len && k < (uint32_t)kSpell; ++k) w[k / 4] |= (uint32_t)d[q.first + k] << (8 * (k % 4));
-    bool same = e.len == q.len && e.spell.x == w[0] && e.spell.y == w[1] && e.spell.z == w[2] && e.spell.w == w[3];
-    if (same && q.len > (uint32_t)kSpell) same = e.coff != 0ull && same_tail(d, q.first, e.coff - 1ull, q.len);
-    if (!same) atomicOr(&t.flags[1], 1u);
+    const uint32_t len = s_len[i];
+    table_add(d, t, s_key[i], djb2_global(d, first, len) & 4095u, len, s_cnt[i], first);
   }
 }
 
@@ -560,14 +495,13 @@ static u64 count_seed(int attempt) { return 0x51ED270B27A1F4A3ull * (u64)(attemp
 // A count's device table (slots + meta) that outlives one attempt (the segmented count of
 // gpu_count_file hands its table to count_on_device).
 struct CountTable {
-  DevBuf slot, meta, defer;
+  DevBuf slot, meta;
   u64 cap = 0;
   Table t{};
 };
 static bool count_table_alloc(CountTable* ct, u64 cap, hipStream_t st, std::string* why) {
   if (ct->slot.p) (void)hipFree(ct->slot.p);
   if (ct->meta.p) (void)hipFree(ct->meta.p);
-  if (!ct->defer.p) LOAD_OK(hipMalloc(&ct->defer.p, (size_t)kDeferCap * sizeof(Deferred)));
   ct->slot.p = ct->meta.p = nullptr;
   LOAD_OK(hipMalloc(&ct->slot.p, cap * sizeof(Slot)));
   LOAD_OK(hipMalloc(&ct->meta.p, 64));
@@ -577,8 +511,6 @@ static bool count_table_alloc(CountTable* ct, u64 cap, hipStream_t st, std::stri
   ct->t.slot = (Slot*)ct->slot.p;
   ct->t.mask = cap - 1;
   ct->t.nkeys = (uint32_t*)ct->meta.p;
-  ct->t.ndefer = (uint32_t*)ct->meta.p + 1;
-  ct->t.defer = (Deferred*)ct->defer.p;
   ct->t.flags = (uint32_t*)ct->meta.p + 4;
   ct->t.stats = (u64*)ct->meta.p + 4;
   return true;
@@ -608,8 +540,6 @@ static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool
       LOAD_OK(hipGetLastError());
     }
     const Table& t = ct->t;
-    k_word_verify<<<cus, 256, 0, st>>>(db, t);
-    LOAD_OK(hipGetLastError());
     uint32_t meta[16];
     LOAD_OK(hipMemcpyAsync(meta, ct->meta.p, 64, hipMemcpyDeviceToHost, st));
     LOAD_OK(hipStreamSynchronize(st));
@@ -623,9 +553,9 @@ static bool count_on_device(uint8_t* db, size_t n, hipStream_t st, int cus, bool
     if (report) {
       const u64* ms = reinterpret_cast<const u64*>(meta) + 4;
       std::fprintf(stderr, "[LOAD] count attempt %d: %llu words, %.2f%% counted straight in HBM, %.2f%% long words "
-                   "compared in HBM, %llu LDS slots evicted, %u adds verified after the count\n", attempt,
-                   (unsigned long long)ms[0], 100.0 * (double)ms[1] / (double)std::max<u64>(1, ms[0]),
-                   100.0 * (double)ms[2] / (double)std::max<u64>(1, ms[0]), (unsigned long long)ms[3], meta[1]);
+                   "compared in HBM, %llu LDS slots evicted\n", attempt, (unsigned long long)ms[0],
+                   100.0 * (double)ms[1] / (double)std::max<u64>(1, ms[0]),
+                   100.0 * (double)ms[2] / (double)std::max<u64>(1, ms[0]), (unsigned long long)ms[3]);
     }
     if (report && (meta[4] || meta[5] || meta[7]))
       std::fprintf(stderr, "[LOAD] count attempt %d over %zu bytes repeated:%s%s%s (%.1f ms)\n", attempt, n,
@@ -879,7 +809,9 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   }
   const CountShape shape = count_shape(n, cus);
   // 512 MiB segments (round 6; 2 GiB before): the count of the last segment is what follows the
-  // upload, 73-112 ms -> 18-49 ms at C3 (profiles/r06_load_ab.json)
+  // upload, 73-112 ms -> 18-49 ms at C3 (profiles/r06_load_ab.json).  (Round 6 also tried the
+  // word's spelling in 64-B HBM slots, compared in place instead of at a linked occurrence: 14%
+  // more count traffic, profiles/r06_count_pmc_ab.json; not kept.)
   u64 seg_bytes = (u64)512 << 20;
   if (const char* e = std::getenv("SHREDWORD_LOAD_SEGMENT_MB")) seg_bytes = std::max<u64>(1, std::strtoull(e, nullptr, 10)) << 20;
   const char* oenv = std::getenv("SHREDWORD_LOAD_OVERLAP");
