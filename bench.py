@@ -472,6 +472,14 @@ def pmc_traffic(cfg_name, layout, kernel=None, all_launches=False, raw=False):
     return v * (ent.get("launches", 1) if all_launches else 1)
 
 
+def _per_load(per_launch, nbytes):
+    """k_word_count bytes of one load: the per-launch PMC figure x the load's segment launches."""
+    if per_launch is None:
+        return None
+    seg = max(1, int(os.environ.get("SHREDWORD_LOAD_SEGMENT_MB", "512"))) << 20
+    return per_launch * -(-int(nbytes) // seg)
+
+
 def pair_count_leg(cfg, path, reps, device=0, layout="stream", dist=None, shard=False):
     """K1 at HBM scale: the same corpus in the stream layout (every occurrence as int32 tokens,
     the north-star data layout), `reps` x (reset + bpe_init).  k_pair_hist counts the bulk of the
@@ -1069,8 +1077,11 @@ def main():
                      "first_load_s": load_s, "first_load_after_generation": gen_s > 0,
                      "later_load_s": later_load_s,
                      "bytes_per_rank": cfg["bytes"] / world if one_job else cfg["bytes"],
-                     "traffic_bytes": pmc_traffic(args.config, args.layout, "k_word_count", all_launches=True),
-                     "traffic_source": pmc_source(args.config, args.layout, "k_word_count"),
+                     # one load = one k_word_count launch per 512 MiB segment (the profiled run holds two loads)
+                     "traffic_bytes": _per_load(pmc_traffic(args.config, args.layout, "k_word_count*"), cfg["bytes"]),
+                     "traffic_bytes_fetch_raw": _per_load(pmc_traffic(args.config, args.layout, "k_word_count*", raw=True),
+                                                          cfg["bytes"]),
+                     "traffic_source": pmc_source(args.config, args.layout, "k_word_count*"),
                      "note": ("load_corpus: page-in + PCIe upload + device word count + host table; outside the timed "
                               "step" + ("; each rank counts its byte range, the word lists are all-gathered and "
                                         "merged on every rank" if one_job else ""))},
@@ -1117,6 +1128,7 @@ def main():
                 result["roofline"] = {k: pair_count[k] for k in ("kernel", "bound", "achieved", "peak", "unit", "frac",
                                                                  "traffic")}
                 result["roofline"]["traffic_unit"] = "HBM bytes per launch (PMC)"
+                result["roofline"]["traffic_source"] = pair_count.get("traffic_source")
                 result["roofline"]["algorithmic_bytes_per_launch"] = pair_count["bytes_per_launch"]
                 result["roofline"]["avg_launch_us"] = pair_count["avg_launch_us"]
                 result["roofline"]["note"] = ("K1, the pair-count scan the north star sets the HBM-roofline target on; "

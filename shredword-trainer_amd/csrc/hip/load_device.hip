@@ -810,7 +810,7 @@ bool gpu_count_file(int device, int fd, uint64_t base, size_t n, std::vector<Wor
   const CountShape shape = count_shape(n, cus);
   // 512 MiB segments (round 6; 2 GiB before): the count of the last segment is what follows the
   // upload, 73-112 ms -> 18-49 ms at C3 (profiles/r06_load_ab.json).  (Round 6 also tried the
-  // word's spelling in 64-B HBM slots, compared in place instead of at a linked occurrence: 14%
+  // word's spelling in 64-B HBM slots, compared in place instead of at a linked occurrence: 12-16%
   // more count traffic, profiles/r06_count_pmc_ab.json; not kept.)
   u64 seg_bytes = (u64)512 << 20;
   if (const char* e = std::getenv("SHREDWORD_LOAD_SEGMENT_MB")) seg_bytes = std::max<u64>(1, std::strtoull(e, nullptr, 10)) << 20;
