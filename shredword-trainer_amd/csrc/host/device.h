@@ -367,7 +367,11 @@ class Device : public Backend {
   bool hybrid_ = true;             // option (SHREDWORD_HYBRID / set_option hybrid)
   bool idx_phase_ = false;         // hybrid: the indexed loop has taken over this train()
   bool switch_pending_ = false;    // hybrid: a resident merge changed < switch_occ_ occurrences
-  uint64_t switch_occ_ = 4000;     // option (SHREDWORD_SWITCH_OCC / set_option switch_occ)
+  // option (SHREDWORD_SWITCH_OCC / set_option switch_occ); 2000 since round 6 (the small-merge word
+  // loop made the late merges cheaper, the queued path's mid merges stay better on k_resident a
+  // little longer: C3 A/Bs +0.5..+1.3% on three boxes, C5 10 GB within noise;
+  // profiles/r06_c3_switch_ab.json)
+  uint64_t switch_occ_ = 2000;
   static constexpr int kSwitchWindow = 64;
   uint64_t sw_win_[kSwitchWindow] = {};  // entries merged by the last resident merges
   uint64_t sw_n_ = 0;
