@@ -1,11 +1,53 @@
 // Exact merge selection: see selector.h for the rules and reference citations.
 #include "selector.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
+#include <cstring>
 
 #include "common.h"
 
 namespace shred {
+
+namespace {
+// First touch descending for one bucket's changes (the reference applies a bucket's chain head
+// first: the latest first touch).  Buckets above a few entries (a merge's (p, a) and (p, X)
+// changes share a's and X's buckets: about a quarter of its changes each) are radix-sorted on the
+// bits of ft that vary inside the bucket (pext), inverted, with the change's index below them --
+// no compare branches; first touches are distinct, so the order is the comparison sort's.
+__attribute__((target("bmi2"))) bool sort_ft_desc_radix(Selector::Change* c, size_t m, std::vector<uint64_t>& ka,
+                                                        std::vector<uint64_t>& kb, std::vector<Selector::Change>& tmp) {
+  uint64_t orv = 0, andv = ~0ull;
+  for (size_t i = 0; i < m; ++i) {
+    orv |= c[i].ft;
+    andv &= c[i].ft;
+  }
+  const uint64_t live = orv & ~andv;
+  const int bits = __builtin_popcountll(live);
+  const int ib = 64 - __builtin_clzll((uint64_t)m);
+  if (bits + ib > 64) return false;
+  const uint64_t fm = bits == 64 ? ~0ull : (1ull << bits) - 1;
+  ka.resize(m);
+  kb.resize(m);
+  for (size_t i = 0; i < m; ++i) ka[i] = ((~_pext_u64(c[i].ft, live) & fm) << ib) | i;
+  uint64_t* src = ka.data();
+  uint64_t* dst = kb.data();
+  for (int sh = ib; sh < ib + bits; sh += 8) {
+    uint32_t cnt[257];
+    std::memset(cnt, 0, sizeof cnt);
+    for (size_t i = 0; i < m; ++i) cnt[((src[i] >> sh) & 255u) + 1]++;
+    for (int k = 0; k < 256; ++k) cnt[k + 1] += cnt[k];
+    for (size_t i = 0; i < m; ++i) dst[cnt[(src[i] >> sh) & 255u]++] = src[i];
+    std::swap(src, dst);
+  }
+  tmp.assign(c, c + m);
+  const uint64_t im = (1ull << ib) - 1;
+  for (size_t i = 0; i < m; ++i) c[i] = tmp[src[i] & im];
+  return true;
+}
+const bool kHaveBmi2 = __builtin_cpu_supports("bmi2");
+}  // namespace
 
 namespace {
 inline uint64_t mix64(uint64_t k) {
@@ -481,6 +523,14 @@ void Selector::prepare(int32_t a, int32_t b, int32_t X, const DeltaRecord* recs,
     const uint64_t bk = ordered[i].hk % kDeltaBuckets;
     size_t e = i + 1;
     while (e < nc && ordered[e].hk % kDeltaBuckets == bk) ++e;
+    if (e - i > 16 && kHaveBmi2) {
+      static thread_local std::vector<uint64_t> ka, kb;
+      static thread_local std::vector<Change> tmp;
+      if (sort_ft_desc_radix(ordered.data() + i, e - i, ka, kb, tmp)) {
+        i = e;
+        continue;
+      }
+    }
     if (e - i > 1) std::sort(ordered.begin() + i, ordered.begin() + e, [](const Change& x, const Change& y) { return x.ft > y.ft; });
     i = e;
   }
